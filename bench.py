@@ -1,0 +1,230 @@
+#!/usr/bin/env python3
+"""Device-resident Internet-checksum throughput (BASELINE.json metric).
+
+One "step" = one ics_checksum_batch pass (InternetChecksum{pseudo}.add(seg).value(),
+util/tools/checksum.h:17-41 with the TCP pseudo-header seed of
+util/ipv4_header/ipv4_header.cpp:103-110) over one resident batch.  At N=1 the
+workload is the north-star configuration: 1 M x 1500 B segments (1.57 GB, far
+larger than the 256 MiB Infinity Cache, so every step streams from HBM).
+At N>1 (torchrun, one process per GPU) every rank owns its own 1 M-segment
+shard of one global spec stream — weak scaling, no data-path collective; the
+only collectives are the timing barrier and the max-over-ranks reduction.
+
+Prints ONE JSON line (rank 0) with `roofline` (HIP-event kernel time vs the
+8 TB/s HBM peak; PMC traffic from a rocprofv3 child pass) and `cpu_baseline`
+(the reference's own InternetChecksum, compiled from /root/reference into
+oracle/_ref/, on a bounded sample of the same bytes, all host threads).
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "device-resident GiB/s, Internet checksum over segment batch, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level parameters)
+KERNEL_PREFIX = "k_checksum"
+
+WORKLOADS = {
+    # name: (segments per rank, segment bytes, seed) — DESIGN.md §Workload spec
+    "ns_1Mx1500": (1 << 20, 1500, 0x10710000),
+    "tcp_1Mx64": (1 << 20, 64, 0x10710003),
+    "jumbo_1Mx9000": (1 << 20, 9000, 0x10710005),
+}
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--workload", default="ns_1Mx1500", choices=sorted(WORKLOADS))
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU-baseline budget (0 = skip)")
+    ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC child pass")
+    ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    return ap.parse_args()
+
+
+# ------------------------------------------------------------ PMC traffic --
+def pmc_traffic(args):
+    """HBM bytes per launch of the checksum kernel from FETCH_SIZE, in a child
+    `rocprofv3 --pmc FETCH_SIZE` run of this same workload (its own pass, no
+    tracing domains).  gfx950: FETCH_SIZE (KiB) reads 1/2 of a wide coalesced
+    stream (MI355X_MICROARCH.md §HBM), so bytes = 2 * 1024 * FETCH_SIZE."""
+    rocprof = shutil.which("rocprofv3")
+    if not rocprof:
+        return None, "rocprofv3 not found"
+    out = tempfile.mkdtemp(prefix="icsum_pmc_", dir=os.environ.get("TMPDIR", "/tmp"))
+    cmd = [rocprof, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
+           sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
+           "--workload", args.workload, "--cpu-seconds", "0", "--no-pmc"]
+    try:
+        subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                       cwd=out)
+        rows = []
+        for f in glob.glob(os.path.join(out, "**", "*counter_collection*.csv"), recursive=True):
+            with open(f) as fh:
+                rows += [r for r in csv.DictReader(fh) if KERNEL_PREFIX in r.get("Kernel_Name", "")]
+        vals = [float(r["Counter_Value"]) for r in rows if r.get("Counter_Name") == "FETCH_SIZE"]
+        if not vals:
+            return None, "no FETCH_SIZE rows"
+        vals = vals[1:] if len(vals) > 1 else vals  # drop the first (cold) launch
+        return 2.0 * 1024.0 * sum(vals) / len(vals), "rocprofv3 --pmc FETCH_SIZE x2 (gfx950 correction)"
+    except Exception as e:  # reported, never fatal
+        return None, f"pmc pass failed: {type(e).__name__}"
+    finally:
+        shutil.rmtree(out, ignore_errors=True)
+
+
+# ------------------------------------------------------------ CPU baseline -
+def cpu_baseline(n_total, seg, seed, budget_s, gpu_out_head):
+    """Reference InternetChecksum (oracle/_ref) — or the oracle port if the
+    reference build is absent — on the first `sample` segments of the same
+    byte stream, repeated until `budget_s` of wall time; all host threads."""
+    import numpy as np
+
+    from oracle import oracle as orc
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    sample = min(n_total, max(threads * 4096, (256 << 20) // seg))
+    data = orc.fill_bytes(seed, 0, sample * seg)
+    init = np.array([orc.pseudo_init(seed, i, seg) for i in range(sample)], dtype=np.uint32)
+    out = np.empty(sample, dtype=np.uint16)
+    ref = orc.ref_lib()
+    kind = "reference" if ref is not None else "port"
+
+    def run():
+        if ref is not None:
+            ref.ref_checksum_batch(data.ctypes.data, None, seg, seg, init.ctypes.data, out.ctypes.data,
+                                   sample, threads)
+        else:
+            out[:] = orc.checksum_batch(data, sample, stride=seg, seg_len=seg, init=init, threads=threads)
+
+    run()  # warm
+    passes, t0 = 0, time.perf_counter()
+    while True:
+        run()
+        passes += 1
+        el = time.perf_counter() - t0
+        if el >= budget_s:
+            break
+    gib = passes * sample * seg / el / 2**30
+    match = bool((out[: len(gpu_out_head)] == gpu_out_head).all())
+    return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "sample": f"first {sample} segments x {seg} B of the same batch, {passes} passes "
+                      f"in {el:.1f} s; outputs bit-identical to the GPU: {match}"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    n, seg, seed = WORKLOADS[args.workload]
+
+    # the PMC child pass runs before this process touches the GPU
+    traffic, traffic_src = (None, "skipped")
+    if not args.pmc_child and not args.no_pmc and world == 1:
+        traffic, traffic_src = pmc_traffic(args)
+
+    import numpy as np
+    import torch
+
+    from tcpip_network_protocol_stack_amd.engine import Engine
+
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=dev)
+    eng = Engine(local)
+    # rank r owns global segments [r*n, (r+1)*n) of one spec stream
+    data = torch.empty(n * seg, dtype=torch.uint8, device=dev)
+    eng.fill_bytes(data, seed, pos0=rank * n * seg)
+    init = eng.pseudo_inits(n, seed, seg_len=seg, index0=rank * n)
+    out = torch.empty(n, dtype=torch.int16, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        eng.checksum_batch(data, n=n, stride=seg, seg_len=seg, init=init, out=out, stream=stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if args.pmc_child:
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize(dev)
+        return
+
+    # per-launch kernel time: HIP events on the stream the kernel runs on
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for a, b in ev:
+        a.record(stream)
+        step()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    kern_ms = [a.elapsed_time(b) for a, b in ev]
+    kern_s = sum(kern_ms) / len(kern_ms) / 1e3
+
+    bytes_step = n * seg  # algorithmic bytes per rank per step (each byte read once)
+    value = world * bytes_step * args.steps / elapsed / 2**30
+    achieved = bytes_step / kern_s / 1e9  # GB/s, decimal like the 8 TB/s peak
+
+    head = out[:4096].cpu().numpy().view(np.uint16).copy()
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(n, seg, seed, args.cpu_seconds, head)
+
+    if rank == 0:
+        line = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (seeded splitmix64 spec, DESIGN.md §Workload spec)",
+            "config": {"workload": args.workload, "segments_per_gpu": n, "segment_bytes": seg,
+                       "bytes_per_step_per_gpu": bytes_step, "inits": "IPv4 pseudo-header sums",
+                       "entry": "ics_checksum_batch", "parallelism": f"shard{world}"},
+            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                         "traffic": None if traffic is None else round(traffic),
+                         "kernel_ms": round(kern_s * 1e3, 4),
+                         "traffic_source": traffic_src},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,161 @@
+/*
+ * icsum.h — C-ABI of the MI355X Internet-checksum engine (libicsum.so).
+ *
+ * This is the drop-in boundary for the one per-byte transform the reference
+ * stack (qmmzzdx/tcpip_network_protocol_stack) implements itself: the RFC-1071
+ * one's-complement 16-bit sum over IPv4 headers and TCP segments.  Every entry
+ * point below replaces a batch of calls to a reference C++ routine; the
+ * reference has no C ABI of its own (its "interface" is the C++ header surface,
+ * SURVEY.md §8b), so each declaration cites the reference function whose
+ * semantics it reproduces bit for bit.
+ *
+ * Conventions
+ *   - All functions return ICS_OK (0) or a negative ICS_ERR_* code.  No C++
+ *     exception ever crosses this boundary; the message of the last failure on
+ *     the calling thread is available from ics_last_error().
+ *   - d_* pointers are device (HBM) pointers on the context's GPU; h_* pointers
+ *     are host pointers.  `stream` is a hipStream_t (NULL = the legacy default
+ *     stream of the context's device).  Device-pointer calls are asynchronous
+ *     with respect to the host: they enqueue on `stream` and return.
+ *   - Segment addressing (used by every batch call):
+ *       d_offsets != NULL : segment i = bytes[d_offsets[i], d_offsets[i+1])
+ *                           (n+1 monotone uint64 offsets; starts may be odd /
+ *                           unaligned — byte roles are relative to each start)
+ *       d_offsets == NULL : segment i = bytes[i*stride, i*stride + seg_len)
+ *   - A context is bound to one device and may be used from several host
+ *     threads (launch calls are thread-safe; the host-memory *_host calls
+ *     serialise on an internal staging lock).
+ */
+#ifndef ICSUM_H
+#define ICSUM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ICS_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define ICS_OK 0
+#define ICS_ERR_INVALID (-1)     /* bad argument (null pointer, bad mode, ...) */
+#define ICS_ERR_HIP (-2)         /* HIP runtime error (message has details) */
+#define ICS_ERR_NOMEM (-3)       /* device / pinned allocation failed */
+#define ICS_ERR_NODEVICE (-4)    /* no GPU / device index out of range */
+
+/* ---- per-datagram status bits written by ics_ipv4_tcp_batch ------------ */
+/* IPv4Header::parse success: ver==4, hlen>=5, recomputed == given
+ * (util/ipv4_header/ipv4_header.cpp:9-59).  In COMPUTE/PATCH mode: ver==4 &&
+ * hlen>=5 only (nothing to compare). */
+#define ICS_ST_IPV4_OK 0x01u
+/* TCP checksum: VERIFY = InternetChecksum{pseudo}.add(all bytes after the IPv4
+ * header).value()==0 (util/tcp_segment/tcp_segment.cpp:11-18);
+ * COMPUTE/PATCH = the TCP checksum field lies inside the datagram (patchable). */
+#define ICS_ST_TCP_CKSUM_OK 0x02u
+/* TCP header parse: >=20 bytes after the IPv4 header and data offset >= 5
+ * (tcp_segment.cpp:25-65). */
+#define ICS_ST_TCP_HDR_OK 0x04u
+/* proto == IPv4Header::PROTO_TCP (util/tcp_over_ip/tcp_over_ip.cpp:26-29). */
+#define ICS_ST_PROTO_TCP 0x08u
+/* all of the above: the datagram would pass unwrap_tcp_in_ip's parse steps. */
+#define ICS_ST_ACCEPT 0x0Fu
+
+/* ---- modes of ics_ipv4_tcp_batch ---------------------------------------- */
+#define ICS_MODE_COMPUTE 0 /* IPv4Header::compute_checksum + TCPSegment::compute_checksum */
+#define ICS_MODE_VERIFY 1  /* IPv4Header::parse + TCPSegment::parse checksum checks */
+#define ICS_MODE_PATCH 2   /* COMPUTE, then write both checksum fields in place */
+
+typedef struct ics_ctx ics_ctx;
+
+/* ---- lifecycle ---------------------------------------------------------- */
+const char* ics_version(void);
+int ics_abi_version(void);
+int ics_device_count(int* count);
+/* One context per GPU.  Allocates the context's staging resources lazily. */
+int ics_create(int device, ics_ctx** out);
+int ics_destroy(ics_ctx* ctx);
+int ics_device_of(const ics_ctx* ctx, int* device);
+/* Message of the last failing call made by this thread ("" if none). */
+const char* ics_last_error(void);
+
+/* ---- a1-a4: InternetChecksum over a batch of segments ------------------ */
+/* d_out[i] = InternetChecksum{init_i}.add(segment_i).value()
+ *   replaces util/tools/checksum.h:17 (ctor), :20-28 (add), :31-41 (value);
+ *   the TCP use is util/tcp_segment/tcp_segment.cpp:109-118 with init_i =
+ *   IPv4Header::pseudo_checksum() (ipv4_header.cpp:103-110).
+ * d_init == NULL means init_i = 0.  Bit-exact for every length, including the
+ * reference's uint32 wrap above 131074 bytes of 0xFF. */
+int ics_checksum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets,
+                       uint64_t stride, uint64_t seg_len, const uint32_t* d_init,
+                       uint16_t* d_out, uint64_t n, void* stream);
+
+/* Unfolded running sum, for multi-piece add() chains (checksum.h:44-59, parity
+ * carried across pieces): d_sum[i] = sum_ after InternetChecksum{init_i} has
+ * had add(segment_i) applied with parity_ = d_odd[i] (0/1; NULL = all 0).
+ * Chain pieces by feeding d_sum back as d_init and (len & 1) ^ odd as d_odd;
+ * fold with ics_fold_batch or on the host. */
+int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets,
+                  uint64_t stride, uint64_t seg_len, const uint32_t* d_init,
+                  const uint8_t* d_odd, uint32_t* d_sum, uint64_t n, void* stream);
+
+/* d_out[i] = InternetChecksum::value() of a raw sum (checksum.h:31-41). */
+int ics_fold_batch(ics_ctx* ctx, const uint32_t* d_sum, uint16_t* d_out, uint64_t n,
+                   void* stream);
+
+/* ---- a7/a8/a10/a11/a13: fused IPv4 + TCP over raw datagrams ------------- */
+/* Each segment is one raw IPv4 datagram (wire bytes, header first).  Per
+ * datagram, in one pass over its bytes:
+ *   ip_ck  = IPv4Header::compute_checksum() of the parsed fields
+ *            (ipv4_header.cpp:113-123: 20 serialized bytes, cksum=0, flag bit
+ *            0x8000 dropped, options never summed)
+ *   pseudo = IPv4Header::pseudo_checksum() (ipv4_header.cpp:103-110)
+ *   tcp_ck = COMPUTE/PATCH: TCPSegment::compute_checksum(pseudo) over the bytes
+ *            after the IPv4 header with the TCP checksum field read as 0
+ *            (tcp_segment.cpp:109-118)
+ *            VERIFY: InternetChecksum{pseudo}.add(all bytes after the IPv4
+ *            header).value() (tcp_segment.cpp:11-18; 0 means valid)
+ *   status = ICS_ST_* bits above.
+ * PATCH additionally stores ip_ck / tcp_ck big-endian into the datagram
+ * (the checksum fields wrap_tcp_in_ip fills, tcp_over_ip.cpp:69-88).
+ * Datagrams shorter than 20 bytes get ip_ck = tcp_ck = status = 0.
+ * Any of d_ip_ck / d_tcp_ck / d_status may be NULL. */
+int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets,
+                       uint64_t stride, uint64_t dgram_len, uint64_t n, int mode,
+                       uint16_t* d_ip_ck, uint16_t* d_tcp_ck, uint8_t* d_status,
+                       void* stream);
+
+/* ---- router forwarding batch (src/router/router.cpp:43-50) -------------- */
+/* For each raw datagram whose IPv4 header parses (ver 4, hlen>=5, checksum
+ * valid): if ttl <= 1 the datagram is dropped (d_status[i] = 0, bytes
+ * untouched); else ttl-- and the header checksum is recomputed with
+ * IPv4Header::compute_checksum() semantics and written in place
+ * (d_status[i] = 1).  Unparseable datagrams get d_status[i] = 0. */
+int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets,
+                         uint64_t stride, uint64_t dgram_len, uint64_t n,
+                         uint8_t* d_status, void* stream);
+
+/* ---- host-memory variants (PCIe-inclusive path) ------------------------ */
+/* Same semantics as ics_checksum_batch on host buffers.  The engine stages
+ * through pinned memory in chunks and pipelines H2D / kernel / D2H on two
+ * streams; returns when h_out is complete. */
+int ics_checksum_batch_host(ics_ctx* ctx, const void* h_bytes, const uint64_t* h_offsets,
+                            uint64_t stride, uint64_t seg_len, const uint32_t* h_init,
+                            uint16_t* h_out, uint64_t n);
+int ics_ipv4_tcp_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offsets,
+                            uint64_t stride, uint64_t dgram_len, uint64_t n, int mode,
+                            uint16_t* h_ip_ck, uint16_t* h_tcp_ck, uint8_t* h_status);
+
+/* ---- device memory helpers for FFI callers without an allocator -------- */
+int ics_malloc(ics_ctx* ctx, void** d_ptr, size_t bytes);
+int ics_free(ics_ctx* ctx, void* d_ptr);
+int ics_memcpy_htod(ics_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, void* stream);
+int ics_memcpy_dtoh(ics_ctx* ctx, void* h_dst, const void* d_src, size_t bytes, void* stream);
+int ics_stream_synchronize(ics_ctx* ctx, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* ICSUM_H */

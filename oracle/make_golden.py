@@ -1,0 +1,93 @@
+#!/usr/bin/env python3
+"""TEST INFRASTRUCTURE ONLY — regenerate tests/golden/ from the real reference.
+
+Builds oracle/ref (the reference's own checksum path compiled in place from
+/root/reference, outputs in oracle/_ref/), runs its golden_gen and writes:
+
+  tests/golden/checksum_kat.json   InternetChecksum KATs (checksum.h:9-60)
+  tests/golden/ipv4_cases.json     IPv4Header parse/compute/pseudo (ipv4_header.cpp:9-123)
+  tests/golden/tcp_wrap.json       wrap/unwrap + TCPSegment::parse (tcp_over_ip.cpp, tcp_segment.cpp)
+  tests/golden/router_cases.json   Router ttl--/recompute (router.cpp:43-50)
+  tests/golden/configs.json        per BASELINE config: sha256 + head of the
+                                   reference's output arrays at FULL size
+
+Only needs /root/reference; run here, never on the GPU box:
+    python oracle/make_golden.py [--skip-configs]
+"""
+import argparse
+import hashlib
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GOLD = os.path.join(ROOT, "tests", "golden")
+GEN = os.path.join(ROOT, "oracle", "_ref", "golden_gen")
+
+# BASELINE.json configs; k=0 is the north-star workload.
+CONFIGS = {
+    0: dict(name="ns_1Mx1500", n=1 << 20, stride=1500, seg_len=1500, inits="pseudo"),
+    2: dict(name="ipv4_64Kix1500", n=1 << 16, stride=1500, seg_len=1500, inits="ipv4"),
+    3: dict(name="tcp_1Mx64", n=1 << 20, stride=64, seg_len=64, inits="pseudo"),
+    4: dict(name="mixed_1M_64B_64KiB", n=1 << 20, stride=0, seg_len=0, inits="pseudo", mixed=True),
+    5: dict(name="jumbo_8Mx9000", n=8 << 20, stride=9000, seg_len=9000, inits="pseudo"),
+}
+
+
+def sha(path):
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 24), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--skip-configs", action="store_true")
+    ap.add_argument("--configs", default="0,2,3,4,5")
+    args = ap.parse_args()
+    if not os.path.isdir("/root/reference"):
+        sys.exit("make_golden.py needs /root/reference (run it in the build container)")
+    subprocess.check_call(["make", "-s", "-C", os.path.join(ROOT, "oracle", "ref")])
+    os.makedirs(GOLD, exist_ok=True)
+    subprocess.check_call([GEN, "kat", GOLD])
+    if args.skip_configs:
+        return
+    out = {}
+    path = os.path.join(GOLD, "configs.json")
+    if os.path.exists(path):
+        out = json.load(open(path))
+    tmp = tempfile.mkdtemp(prefix="golden_")
+    try:
+        for k in [int(x) for x in args.configs.split(",")]:
+            spec = dict(CONFIGS[k])
+            subprocess.check_call([GEN, "config", str(k), tmp])
+            ent = dict(spec, seed=0x10710000 + k)
+            if k == 2:
+                for nm in ("ipck", "tcpck"):
+                    f = os.path.join(tmp, f"cfg2_{nm}.bin")
+                    ent[f"{nm}_sha256"] = sha(f)
+                    ent[f"{nm}_head"] = np.fromfile(f, dtype="<u2")[:64].tolist()
+                ent["patched_sha256"] = sha(os.path.join(tmp, "cfg2_patched.bin"))
+            else:
+                f = os.path.join(tmp, f"cfg{k}_out.bin")
+                ent["out_sha256"] = sha(f)
+                ent["out_head"] = np.fromfile(f, dtype="<u2")[:64].tolist()
+            out[str(k)] = ent
+            print("config", k, "done", flush=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    with open(path, "w") as f:
+        json.dump({"source": "reference InternetChecksum / IPv4Header / TCPSegment at full "
+                             "BASELINE sizes (oracle/ref/golden_gen.cpp)",
+                   **{k: v for k, v in out.items() if k != "source"}}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,525 @@
+// golden_gen.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// Golden-vector generator linked against the REAL reference, compiled in place
+// from /root/reference (recipe: oracle/ref/Makefile, outputs in oracle/_ref/).
+// It only calls the reference's own types:
+//   InternetChecksum            util/tools/checksum.h:9-60
+//   IPv4Header / IPv4Datagram   util/ipv4_header/ipv4_header.cpp, util/tools/ipv4_datagram.h
+//   TCPSegment                  util/tcp_segment/tcp_segment.cpp
+//   TCPOverIPv4Adapter          util/tcp_over_ip/tcp_over_ip.cpp
+//   serialize<T> / parse<T>     util/tools/parser.h:275-289
+// and writes fixtures (inputs + the reference's outputs) for tests/golden/.
+// Inputs come from an independent splitmix64 written here (not the oracle's)
+// following the DESIGN.md workload spec, so the oracle is checked, not trusted.
+//
+// usage: golden_gen kat DIR          small known-answer fixtures (JSON)
+//        golden_gen config K DIR     raw reference outputs of BASELINE config K
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <sstream>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "checksum.h"
+#include "ipv4_datagram.h"
+#include "ipv4_header.h"
+#include "parser.h"
+#include "tcp_over_ip.h"
+#include "tcp_segment.h"
+
+namespace {
+
+// ---- independent workload-spec implementation (DESIGN.md §Workload spec) --
+constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
+uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+uint64_t word(uint64_t seed, uint64_t c) { return mix64(seed + (c + 1) * kGolden); }
+uint8_t sbyte(uint64_t seed, uint64_t p) { return uint8_t(word(seed, p >> 3) >> (8 * (p & 7))); }
+void fill(uint64_t seed, uint64_t p0, uint64_t n, char* out) {
+  uint64_t p = p0, e = p0 + n;
+  while (p < e && (p & 7)) *out++ = char(sbyte(seed, p++));
+  while (p + 8 <= e) {
+    uint64_t w = word(seed, p >> 3);
+    std::memcpy(out, &w, 8);  // little-endian host: byte k = (w >> 8k)
+    out += 8;
+    p += 8;
+  }
+  while (p < e) *out++ = char(sbyte(seed, p++));
+}
+uint64_t meta(uint64_t seed, uint64_t i) { return word(seed ^ 0xA5A5A5A5A5A5A5A5ull, i); }
+uint32_t src_of(uint64_t seed, uint64_t i) { return 0x0A000000u | uint32_t(meta(seed, i) & 0xFFFFFFu); }
+uint32_t dst_of(uint64_t seed, uint64_t i) {
+  return 0x0A000000u | uint32_t((meta(seed, i) >> 24) & 0xFFFFFFu);
+}
+uint64_t mixed_len(uint64_t seed, uint64_t i) {
+  uint64_t m = word(seed ^ 0x3C3C3C3C3C3C3C3Cull, i);
+  unsigned e = 6u + unsigned(m % 10u);
+  return (1ull << e) + ((m >> 8) & ((1ull << e) - 1));
+}
+// the reference's own pseudo-header sum for a TCP segment of length L
+uint32_t ref_pseudo(uint64_t seed, uint64_t i, uint64_t L) {
+  IPv4Header h;
+  h.src = src_of(seed, i);
+  h.dst = dst_of(seed, i);
+  h.proto = IPv4Header::PROTO_TCP;
+  h.hlen = 5;
+  h.len = uint16_t(20 + L);  // payload_length() == L (mod 2^16)
+  return h.pseudo_checksum();
+}
+
+// raw value of a Wrap32 (the member is protected, wrapping_integers.h:40)
+struct WrapRaw : Wrap32 {
+  explicit WrapRaw(Wrap32 w) : Wrap32(w) {}
+  uint32_t raw() const { return raw_value_; }
+};
+uint32_t Wrap32Probe(Wrap32 w) { return WrapRaw{w}.raw(); }
+
+// ---- tiny JSON helpers --------------------------------------------------
+std::string hex(const std::string& s) {
+  static const char* d = "0123456789abcdef";
+  std::string r;
+  r.reserve(s.size() * 2);
+  for (unsigned char c : s) {
+    r.push_back(d[c >> 4]);
+    r.push_back(d[c & 15]);
+  }
+  return r;
+}
+std::string joined(const std::vector<std::string>& v) {
+  std::string r;
+  for (auto& s : v) r += s;
+  return r;
+}
+
+struct Rng {  // splitmix64 sequence for fixture case construction
+  uint64_t s;
+  uint64_t next() { return mix64(s += kGolden); }
+  uint64_t below(uint64_t n) { return n ? next() % n : 0; }
+  std::string bytes(size_t n) {
+    std::string r(n, '\0');
+    for (auto& c : r) c = char(next());
+    return r;
+  }
+};
+
+uint16_t ref_value(uint32_t init, const std::vector<std::string>& pieces) {
+  InternetChecksum c{init};
+  c.add(pieces);
+  return c.value();
+}
+
+// ---------------------------------------------------------------- KATs ---
+void kat_checksum(const std::string& dir) {
+  std::ofstream o(dir + "/checksum_kat.json");
+  o << "{\"source\": \"reference InternetChecksum (util/tools/checksum.h:9-60)\",\n \"cases\": [\n";
+  bool first = true;
+  auto emit = [&](uint32_t init, const std::vector<std::string>& pieces, const char* tag) {
+    // both add(vector<string>) and add(vector<string_view>) must agree
+    std::vector<std::string_view> views(pieces.begin(), pieces.end());
+    InternetChecksum cv{init};
+    cv.add(views);
+    const uint16_t v = ref_value(init, pieces);
+    if (cv.value() != v) {
+      std::fprintf(stderr, "string/string_view disagree\n");
+      std::exit(2);
+    }
+    o << (first ? "  " : ",\n  ") << "{\"tag\": \"" << tag << "\", \"init\": " << init << ", \"pieces\": [";
+    for (size_t k = 0; k < pieces.size(); ++k) o << (k ? ", " : "") << "\"" << hex(pieces[k]) << "\"";
+    o << "], \"value\": " << v << "}";
+    first = false;
+  };
+  auto emit_fill = [&](uint32_t init, int byte, size_t len) {
+    std::string s(len, char(byte));
+    o << (first ? "  " : ",\n  ") << "{\"tag\": \"fill\", \"init\": " << init << ", \"fill\": " << byte
+      << ", \"len\": " << len << ", \"value\": " << ref_value(init, {s}) << "}";
+    first = false;
+  };
+  // RFC 1071 §3 example (independent anchor: expected 0x220d)
+  emit(0, {std::string("\x00\x01\xf2\x03\xf4\xf5\xf6\xf7", 8)}, "rfc1071");
+  Rng r{0x1071'0001ull};
+  const uint32_t inits_all[] = {0u, 1u, 0xFFFFu, 0x10000u, 0x5FFFAu, 0xFFFFFFFFu, 0x12345678u};
+  for (uint32_t init : {0u, 0x5FFFAu})
+    for (size_t len = 0; len <= 257; ++len) emit(init, {r.bytes(len)}, "len");
+  for (uint32_t init : inits_all)
+    for (size_t len : {0, 1, 2, 3, 20, 63, 64, 65, 1500}) emit(init, {r.bytes(len)}, "init");
+  for (uint32_t init : {0u, 0xFFFFFFFFu, 0x5FFFAu})
+    for (int byte : {0x00, 0xFF})
+      for (size_t len : {1, 2, 3, 4, 255, 256, 257, 1500, 9000, 65535, 131072, 131073, 131074,
+                         131075, 131076, 131077, 200000, 262147})
+        emit_fill(init, byte, len);
+  // chunk-split invariance: the same bytes split into 2-4 pieces (parity is
+  // carried across pieces, checksum.h:44-59), including empty pieces and odd cuts
+  for (int t = 0; t < 48; ++t) {
+    const size_t len = 1 + r.below(96);
+    const std::string s = r.bytes(len);
+    const uint32_t init = uint32_t(r.next());
+    const size_t np = 2 + r.below(3);
+    std::vector<size_t> cuts;
+    for (size_t k = 0; k + 1 < np; ++k) cuts.push_back(r.below(len + 1));
+    std::sort(cuts.begin(), cuts.end());
+    std::vector<std::string> pieces;
+    size_t prev = 0;
+    for (size_t c : cuts) {
+      pieces.push_back(s.substr(prev, c - prev));
+      prev = c;
+    }
+    pieces.push_back(s.substr(prev));
+    emit(init, pieces, "split");
+    emit(init, {s}, "whole");
+  }
+  o << "\n ]}\n";
+}
+
+// IPv4 header cases: reference parse (verify) + compute + pseudo_checksum
+void kat_ipv4(const std::string& dir) {
+  std::ofstream o(dir + "/ipv4_cases.json");
+  o << "{\"source\": \"reference IPv4Header::parse/compute_checksum/pseudo_checksum "
+       "(util/ipv4_header/ipv4_header.cpp:9-123)\",\n \"cases\": [\n";
+  bool first = true;
+  auto emit = [&](const std::string& wire, const char* tag) {
+    IPv4Header h;
+    const bool ok = parse(h, std::vector<std::string>{wire});
+    o << (first ? "  " : ",\n  ") << "{\"tag\": \"" << tag << "\", \"bytes\": \"" << hex(wire)
+      << "\", \"parse_ok\": " << (ok ? "true" : "false");
+    if (wire.size() >= 20 && h.ver == 4) {
+      IPv4Header c = h;  // after a full parse cksum == computed; recompute explicitly
+      c.compute_checksum();
+      o << ", \"computed\": " << c.cksum << ", \"pseudo\": " << c.pseudo_checksum()
+        << ", \"payload_length\": " << c.payload_length();
+    }
+    o << "}";
+    first = false;
+  };
+  Rng r{0x1071'0002ull};
+  auto make = [&](bool df, bool mf, uint8_t ttl) {
+    IPv4Header h;
+    h.tos = uint8_t(r.next());
+    h.len = uint16_t(20 + r.below(1480));
+    h.id = uint16_t(r.next());
+    h.df = df;
+    h.mf = mf;
+    h.offset = uint16_t(r.next() & 0x1fff);
+    h.ttl = ttl;
+    h.proto = uint8_t(r.below(3) == 0 ? r.next() : 6);
+    h.src = uint32_t(r.next());
+    h.dst = uint32_t(r.next());
+    h.compute_checksum();
+    return h;
+  };
+  for (int t = 0; t < 64; ++t) {
+    IPv4Header h = make(r.below(2), r.below(2), uint8_t(r.next()));
+    emit(joined(serialize(h)), "valid");
+    std::string w = joined(serialize(h));
+    const size_t bit = r.below(160);
+    w[bit / 8] = char(w[bit / 8] ^ (1 << (bit % 8)));
+    emit(w, "bitflip");
+  }
+  // quirk: reserved flag bit 0x8000 with an RFC-valid checksum over the wire
+  for (int t = 0; t < 4; ++t) {
+    IPv4Header h = make(true, false, 64);
+    std::string w = joined(serialize(h));
+    w[6] = char(w[6] | 0x80);
+    w[10] = w[11] = 0;
+    InternetChecksum c;
+    c.add(w);
+    const uint16_t v = c.value();
+    w[10] = char(v >> 8);
+    w[11] = char(v & 0xff);
+    emit(w, "rfc_valid_reserved_bit");
+    // and the reference-consistent one (checksum computed without the bit)
+    std::string w2 = joined(serialize(h));
+    w2[6] = char(w2[6] | 0x80);
+    emit(w2, "reserved_bit_ref_cksum");
+  }
+  // quirk: options (hlen=6) with an RFC-valid checksum over all 24 bytes
+  for (int t = 0; t < 4; ++t) {
+    IPv4Header h = make(true, false, 64);
+    h.hlen = 6;
+    h.compute_checksum();  // reference: sums the 20 serialized bytes only
+    std::string w = joined(serialize(h)) + r.bytes(4);
+    emit(w, "options_ref_cksum");
+    w[10] = w[11] = 0;
+    InternetChecksum c;
+    c.add(w);
+    const uint16_t v = c.value();
+    w[10] = char(v >> 8);
+    w[11] = char(v & 0xff);
+    emit(w, "options_rfc_cksum");
+  }
+  // quirk: computed 0x0000 vs wire 0xFFFF (one's-complement -0): search the
+  // id field for a header whose checksum is exactly 0x0000
+  {
+    IPv4Header h = make(true, false, 64);
+    for (uint32_t id = 0; id <= 0xFFFF; ++id) {
+      h.id = uint16_t(id);
+      h.compute_checksum();
+      if (h.cksum == 0) {
+        emit(joined(serialize(h)), "cksum_zero");
+        std::string w = joined(serialize(h));
+        w[10] = w[11] = char(0xff);
+        emit(w, "cksum_minus_zero");
+        break;
+      }
+    }
+  }
+  {
+    IPv4Header h = make(true, false, 64);
+    h.ver = 4;
+    std::string w = joined(serialize(h));
+    w[0] = char(0x65);
+    emit(w, "ver6");
+    w = joined(serialize(h));
+    w[0] = char(0x44);
+    emit(w, "hlen4");
+    emit(joined(serialize(h)).substr(0, 19), "short19");
+    emit(joined(serialize(h)) + r.bytes(33), "trailing_bytes");
+  }
+  o << "\n ]}\n";
+}
+
+// TCP-over-IPv4 wrap/unwrap through the reference adapter
+void kat_tcp(const std::string& dir) {
+  std::ofstream o(dir + "/tcp_wrap.json");
+  o << "{\"source\": \"reference TCPOverIPv4Adapter::wrap_tcp_in_ip/unwrap_tcp_in_ip, "
+       "TCPSegment::parse (util/tcp_over_ip/tcp_over_ip.cpp:10-88, "
+       "util/tcp_segment/tcp_segment.cpp:9-118)\",\n \"cases\": [\n";
+  bool first = true;
+  Rng r{0x1071'0003ull};
+  auto ipstr = [](uint32_t a) {
+    return std::to_string(a >> 24) + "." + std::to_string((a >> 16) & 255) + "." +
+           std::to_string((a >> 8) & 255) + "." + std::to_string(a & 255);
+  };
+  // reference verification of raw wire bytes, as unwrap would see them
+  auto verify = [&](const std::string& wire, std::ostream& out) {
+    IPv4Datagram dg;
+    const bool ip_ok = parse(dg, std::vector<std::string>{wire});
+    out << ", \"ip_parse_ok\": " << (ip_ok ? "true" : "false");
+    if (wire.size() >= 20 && dg.header.ver == 4 && dg.header.hlen >= 5) {
+      TCPSegment seg;
+      const uint32_t pseudo = dg.header.pseudo_checksum();
+      const bool tcp_ok = parse(seg, dg.payload, pseudo);
+      InternetChecksum c{pseudo};
+      c.add(dg.payload);
+      out << ", \"proto\": " << unsigned(dg.header.proto) << ", \"tcp_parse_ok\": "
+          << (tcp_ok ? "true" : "false") << ", \"tcp_value\": " << c.value()
+          << ", \"ip_computed\": " << dg.header.cksum;
+    }
+  };
+  for (int t = 0; t < 160; ++t) {
+    const uint32_t a_ip = 0x0A000000u | uint32_t(r.next() & 0xFFFFFF);
+    const uint32_t b_ip = 0x0A000000u | uint32_t(r.next() & 0xFFFFFF);
+    const uint16_t a_port = uint16_t(1 + r.below(65535));
+    const uint16_t b_port = uint16_t(1 + r.below(65535));
+    TCPOverIPv4Adapter A, B;
+    A.config_mut().source = Address{ipstr(a_ip), a_port};
+    A.config_mut().destination = Address{ipstr(b_ip), b_port};
+    B.config_mut().source = Address{ipstr(b_ip), b_port};
+    B.config_mut().destination = Address{ipstr(a_ip), a_port};
+    TCPMessage m;
+    m.sender.seqno = Wrap32{uint32_t(r.next())};
+    m.sender.SYN = r.below(4) == 0;
+    m.sender.FIN = r.below(4) == 0;
+    m.sender.RST = r.below(16) == 0;
+    const size_t plen = (t < 8) ? size_t(t) : size_t(r.below(1001));
+    m.sender.payload = r.bytes(plen);
+    if (r.below(4)) m.receiver.ackno = Wrap32{uint32_t(r.next())};
+    m.receiver.window_size = uint16_t(r.next());
+    m.receiver.RST = r.below(32) == 0;
+    const InternetDatagram dg = A.wrap_tcp_in_ip(m);
+    const std::string wire = joined(serialize(dg));
+    const auto back = B.unwrap_tcp_in_ip(dg);
+    o << (first ? "  " : ",\n  ") << "{\"tag\": \"wrap\", \"src\": " << a_ip << ", \"dst\": " << b_ip
+      << ", \"sport\": " << a_port << ", \"dport\": " << b_port << ", \"seqno\": "
+      << Wrap32Probe(m.sender.seqno) << ", \"syn\": " << m.sender.SYN << ", \"fin\": " << m.sender.FIN
+      << ", \"rst\": " << (m.sender.RST || m.receiver.RST) << ", \"has_ack\": " << m.receiver.ackno.has_value()
+      << ", \"ackno\": " << (m.receiver.ackno ? Wrap32Probe(*m.receiver.ackno) : 0u)
+      << ", \"window\": " << m.receiver.window_size << ", \"payload_len\": " << m.sender.payload.size()
+      << ", \"wire\": \"" << hex(wire) << "\", \"ip_cksum\": " << dg.header.cksum
+      << ", \"unwrap_ok\": " << (back.has_value() ? "true" : "false");
+    verify(wire, o);
+    o << "}";
+    first = false;
+    // corrupted variants: one bit flip anywhere in the datagram
+    std::string bad = wire;
+    const size_t bit = r.below(bad.size() * 8);
+    bad[bit / 8] = char(bad[bit / 8] ^ (1 << (bit % 8)));
+    o << ",\n  {\"tag\": \"bitflip\", \"bit\": " << bit << ", \"wire\": \"" << hex(bad) << "\"";
+    verify(bad, o);
+    o << "}";
+    if (t % 16 == 0) {
+      // trailing bytes past ip.len: the TCP check covers ALL remaining bytes
+      o << ",\n  {\"tag\": \"trailing_zero2\", \"wire\": \"" << hex(wire + std::string(2, '\0')) << "\"";
+      verify(wire + std::string(2, '\0'), o);
+      o << "}";
+      const std::string junk = wire + r.bytes(3);
+      o << ",\n  {\"tag\": \"trailing_junk\", \"wire\": \"" << hex(junk) << "\"";
+      verify(junk, o);
+      o << "}";
+      const std::string cut = wire.substr(0, 20 + r.below(20));
+      o << ",\n  {\"tag\": \"truncated\", \"wire\": \"" << hex(cut) << "\"";
+      verify(cut, o);
+      o << "}";
+    }
+  }
+  o << "\n ]}\n";
+}
+
+// router: parse (verify), ttl <= 1 drop, else ttl-- + compute_checksum
+void kat_router(const std::string& dir) {
+  std::ofstream o(dir + "/router_cases.json");
+  o << "{\"source\": \"reference IPv4Datagram parse + Router::route ttl/checksum step "
+       "(src/router/router.cpp:43-50)\",\n \"cases\": [\n";
+  bool first = true;
+  Rng r{0x1071'0004ull};
+  for (int t = 0; t < 96; ++t) {
+    IPv4Header h;
+    h.len = uint16_t(20 + r.below(100));
+    h.id = uint16_t(r.next());
+    h.ttl = uint8_t(t < 8 ? t : r.next());
+    h.src = uint32_t(r.next());
+    h.dst = uint32_t(r.next());
+    h.proto = uint8_t(r.next());
+    h.compute_checksum();
+    std::string wire = joined(serialize(h)) + r.bytes(h.len - 20);
+    if (t % 8 == 7) wire[2 + r.below(18)] ^= char(1 << r.below(8));  // corrupt some
+    IPv4Datagram dg;
+    const bool ok = parse(dg, std::vector<std::string>{wire});
+    bool fwd = false;
+    std::string out = wire;
+    if (ok && dg.header.ttl > 1) {
+      dg.header.ttl--;
+      dg.header.compute_checksum();
+      out = joined(serialize(dg));
+      fwd = true;
+    }
+    o << (first ? "  " : ",\n  ") << "{\"wire\": \"" << hex(wire) << "\", \"forwarded\": "
+      << (fwd ? "true" : "false") << ", \"out\": \"" << hex(out) << "\"}";
+    first = false;
+  }
+  o << "\n ]}\n";
+}
+
+// ------------------------------------------------------------- configs ---
+void write_bin(const std::string& path, const void* p, size_t n) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f || std::fwrite(p, 1, n, f) != n) {
+    std::fprintf(stderr, "write %s failed\n", path.c_str());
+    std::exit(2);
+  }
+  std::fclose(f);
+}
+
+// fixed-stride / offset segment configs: out[i] = InternetChecksum{pseudo}.add(seg).value()
+void config_bytes(int k, uint64_t n, uint64_t stride, bool mixed, const std::string& dir) {
+  const uint64_t seed = 0x10710000ull + uint64_t(k);
+  std::vector<uint16_t> out(n);
+  unsigned nt = std::max(1u, std::thread::hardware_concurrency());
+  std::vector<std::thread> th;
+  std::vector<uint64_t> offs;
+  if (mixed) {
+    offs.resize(n + 1);
+    offs[0] = 0;
+    for (uint64_t i = 0; i < n; ++i) offs[i + 1] = offs[i] + mixed_len(seed, i);
+  }
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      std::string buf;
+      for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+        const uint64_t b = mixed ? offs[i] : i * stride;
+        const uint64_t L = mixed ? offs[i + 1] - offs[i] : stride;
+        buf.resize(L);
+        fill(seed, b, L, buf.data());
+        InternetChecksum c{ref_pseudo(seed, i, L)};
+        c.add(std::string_view{buf});
+        out[i] = c.value();
+      }
+    });
+  for (auto& x : th) x.join();
+  write_bin(dir + "/cfg" + std::to_string(k) + "_out.bin", out.data(), n * 2);
+  uint64_t total = mixed ? offs[n] : n * stride;
+  std::printf("config %d: n=%llu bytes=%llu\n", k, (unsigned long long)n, (unsigned long long)total);
+}
+
+// config 2: IPv4 datagrams — build each through the reference types exactly
+// as wrap_tcp_in_ip does (tcp_over_ip.cpp:69-88), from fields the spec puts on
+// the wire; outputs: ip/tcp checksums and the patched (serialized) batch.
+void config_ipv4(uint64_t n, uint64_t stride, const std::string& dir) {
+  const uint64_t seed = 0x10710002ull;
+  std::vector<uint16_t> ipc(n), tcpc(n);
+  std::vector<char> patched(n * stride);
+  std::string raw(stride, '\0');
+  for (uint64_t i = 0; i < n; ++i) {
+    fill(seed, i * stride, stride, raw.data());
+    auto u8 = [&](size_t k) { return uint8_t(raw[k]); };
+    auto be16 = [&](size_t k) { return uint16_t((u8(k) << 8) | u8(k + 1)); };
+    auto be32 = [&](size_t k) { return uint32_t((be16(k) << 16) | be16(k + 2)); };
+    TCPSegment seg;
+    seg.udinfo.src_port = be16(20);
+    seg.udinfo.dst_port = be16(22);
+    seg.message.sender.seqno = Wrap32{be32(24)};
+    seg.message.receiver.ackno = Wrap32{be32(28)};  // flags = ACK (0x10)
+    seg.message.receiver.window_size = be16(34);
+    seg.message.sender.payload = raw.substr(40);
+    IPv4Header h;  // defaults: ver 4, hlen 5, df, proto TCP
+    h.len = uint16_t(stride);
+    h.id = uint16_t(i);
+    h.ttl = 64;
+    h.src = src_of(seed, i);
+    h.dst = dst_of(seed, i);
+    seg.compute_checksum(h.pseudo_checksum());
+    h.compute_checksum();
+    IPv4Datagram dg{h, serialize(seg)};
+    const std::string wire = joined(serialize(dg));
+    if (wire.size() != stride) std::exit(3);
+    std::memcpy(patched.data() + i * stride, wire.data(), stride);
+    ipc[i] = h.cksum;
+    tcpc[i] = seg.udinfo.cksum;
+    if (i < 64) {  // the batch must verify through the reference parse path
+      IPv4Datagram back;
+      TCPSegment s2;
+      if (!parse(back, std::vector<std::string>{wire}) ||
+          !parse(s2, back.payload, back.header.pseudo_checksum())) {
+        std::fprintf(stderr, "reference rejects its own datagram %llu\n", (unsigned long long)i);
+        std::exit(3);
+      }
+    }
+  }
+  write_bin(dir + "/cfg2_ipck.bin", ipc.data(), n * 2);
+  write_bin(dir + "/cfg2_tcpck.bin", tcpc.data(), n * 2);
+  write_bin(dir + "/cfg2_patched.bin", patched.data(), patched.size());
+  std::printf("config 2: n=%llu bytes=%llu\n", (unsigned long long)n, (unsigned long long)(n * stride));
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc >= 3 && std::string(argv[1]) == "kat") {
+    kat_checksum(argv[2]);
+    kat_ipv4(argv[2]);
+    kat_tcp(argv[2]);
+    kat_router(argv[2]);
+    return 0;
+  }
+  if (argc >= 4 && std::string(argv[1]) == "config") {
+    const int k = std::atoi(argv[2]);
+    const std::string dir = argv[3];
+    switch (k) {
+      case 0: config_bytes(0, 1ull << 20, 1500, false, dir); return 0;   // north star
+      case 2: config_ipv4(1ull << 16, 1500, dir); return 0;
+      case 3: config_bytes(3, 1ull << 20, 64, false, dir); return 0;
+      case 4: config_bytes(4, 1ull << 20, 0, true, dir); return 0;
+      case 5: config_bytes(5, 8ull << 20, 9000, false, dir); return 0;
+      default: break;
+    }
+  }
+  std::fprintf(stderr, "usage: golden_gen kat DIR | golden_gen config {0,2,3,4,5} DIR\n");
+  return 1;
+}

@@ -1,0 +1,83 @@
+"""ctypes binding of libicsum.so (the C-ABI declared in include/icsum.h).
+
+This is the same binding a maintainer would add to call the engine from any
+FFI.  Loading fails loudly: there is no Python or CPU
+fallback for the checksum path.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libicsum.so")
+
+ICS_OK = 0
+ICS_MODE_COMPUTE, ICS_MODE_VERIFY, ICS_MODE_PATCH = 0, 1, 2
+ICS_ST_IPV4_OK, ICS_ST_TCP_CKSUM_OK, ICS_ST_TCP_HDR_OK, ICS_ST_PROTO_TCP = 0x01, 0x02, 0x04, 0x08
+ICS_ST_ACCEPT = 0x0F
+
+_p = ctypes.c_void_p
+_u64 = ctypes.c_uint64
+_int = ctypes.c_int
+
+# name -> (restype, argtypes); every symbol include/icsum.h and
+# include/icsum_workload.h declare
+SIGNATURES = {
+    "ics_version": (ctypes.c_char_p, []),
+    "ics_abi_version": (_int, []),
+    "ics_device_count": (_int, [ctypes.POINTER(_int)]),
+    "ics_create": (_int, [_int, ctypes.POINTER(_p)]),
+    "ics_destroy": (_int, [_p]),
+    "ics_device_of": (_int, [_p, ctypes.POINTER(_int)]),
+    "ics_last_error": (ctypes.c_char_p, []),
+    "ics_checksum_batch": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _u64, _p]),
+    "ics_sum_batch": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _p, _u64, _p]),
+    "ics_fold_batch": (_int, [_p, _p, _p, _u64, _p]),
+    "ics_ipv4_tcp_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p, _p]),
+    "ics_router_ttl_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p]),
+    "ics_checksum_batch_host": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _u64]),
+    "ics_ipv4_tcp_batch_host": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p]),
+    "ics_malloc": (_int, [_p, ctypes.POINTER(_p), ctypes.c_size_t]),
+    "ics_free": (_int, [_p, _p]),
+    "ics_memcpy_htod": (_int, [_p, _p, _p, ctypes.c_size_t, _p]),
+    "ics_memcpy_dtoh": (_int, [_p, _p, _p, ctypes.c_size_t, _p]),
+    "ics_stream_synchronize": (_int, [_p, _p]),
+    "icsw_fill_bytes": (_int, [_p, _p, _u64, _u64, _u64, _p]),
+    "icsw_pseudo_inits": (_int, [_p, _p, _p, _u64, _u64, _u64, _u64, _p]),
+    "icsw_ipv4_tcp_headers": (_int, [_p, _p, _u64, _u64, _u64, _u64, _u64, _p]),
+    "icsw_mixed_len": (_u64, [_u64, _u64]),
+    "icsw_mixed_offsets": (_int, [_p, _u64, _u64]),
+}
+
+
+class IcsumError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load():
+    """Load libicsum.so (built by __graft_entry__.build()); raise if absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise IcsumError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            "(the checksum engine has no CPU fallback)")
+    # torch (if imported) already holds the process's libamdhip64.so.7; the
+    # engine binds to the same runtime by soname.
+    lib = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(rc):
+    if rc != ICS_OK:
+        msg = load().ics_last_error().decode(errors="replace")
+        raise IcsumError(f"icsum error {rc}: {msg}")
+    return rc

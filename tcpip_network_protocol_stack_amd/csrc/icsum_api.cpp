@@ -1,0 +1,446 @@
+// icsum_api.cpp — the C-ABI of libicsum.so (declared in include/icsum.h).
+//
+// Thin, exception-free layer: argument validation, device binding, error
+// strings, geometry choice, and the host-memory (PCIe-inclusive) pipeline.
+// All arithmetic happens in the HIP kernels (kernels/icsum_kernels.hip); there
+// is no CPU fallback — without a usable GPU every call returns an error.
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+
+#include "icsum.h"
+#include "icsum_workload.h"
+#include "kernels/icsum_launch.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(e == hipErrorOutOfMemory ? ICS_ERR_NOMEM : ICS_ERR_HIP, "%s: %s (%d)", what,
+              hipGetErrorString(e), int(e));
+}
+
+#define ICS_HIP(call)                                 \
+  do {                                                \
+    hipError_t e_ = (call);                           \
+    if (e_ != hipSuccess) return hip_fail(e_, #call); \
+  } while (0)
+
+uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* v = std::getenv(name);
+  return v && *v ? uint32_t(std::strtoul(v, nullptr, 0)) : dflt;
+}
+
+}  // namespace
+
+// One engine context per GPU.  Staging for the host-memory path is created
+// on first use and guarded by `mu`.
+struct ics_ctx {
+  int device = 0;
+  uint32_t max_blocks = 0;  // 0 = one lane group per segment (no grid-stride cap)
+  int force_lps = 0, force_unroll = 0;
+  std::mutex mu;
+  // host path: two slots, each with pinned in/out staging and device buffers
+  static constexpr size_t kSlotBytes = size_t(64) << 20;
+  static constexpr size_t kSlotSegs = size_t(1) << 20;
+  bool staged = false;
+  hipStream_t st[2] = {nullptr, nullptr};
+  hipEvent_t ev[2] = {nullptr, nullptr};
+  uint8_t* h_in[2] = {nullptr, nullptr};
+  uint8_t* d_in[2] = {nullptr, nullptr};
+  uint64_t* h_off[2] = {nullptr, nullptr};
+  uint64_t* d_off[2] = {nullptr, nullptr};
+  uint32_t* h_init[2] = {nullptr, nullptr};
+  uint32_t* d_init[2] = {nullptr, nullptr};
+  uint8_t* h_out[2] = {nullptr, nullptr};   // u16 outputs or 5-byte ipv4 results
+  uint8_t* d_out[2] = {nullptr, nullptr};
+};
+
+namespace {
+
+int bind(ics_ctx* ctx) {
+  if (!ctx) return fail(ICS_ERR_INVALID, "null context");
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess || cur != ctx->device) ICS_HIP(hipSetDevice(ctx->device));
+  return ICS_OK;
+}
+
+icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
+  icsum::Geometry g = icsum::pick_geometry(avg_len);
+  if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll};
+  return g;
+}
+
+// average segment length for the geometry choice without reading d_offsets
+uint64_t avg_len_hint(const uint64_t* offsets, uint64_t seg_len, uint64_t n, uint64_t total_hint) {
+  if (!offsets) return seg_len;
+  return total_hint && n ? total_hint / n : 4096;
+}
+
+int ensure_staging(ics_ctx* ctx) {
+  if (ctx->staged) return ICS_OK;
+  for (int k = 0; k < 2; ++k) {
+    ICS_HIP(hipStreamCreateWithFlags(&ctx->st[k], hipStreamNonBlocking));
+    ICS_HIP(hipEventCreateWithFlags(&ctx->ev[k], hipEventDisableTiming));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_in[k]), ics_ctx::kSlotBytes, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_in[k]), ics_ctx::kSlotBytes));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_off[k]), (ics_ctx::kSlotSegs + 1) * 8, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_off[k]), (ics_ctx::kSlotSegs + 1) * 8));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_init[k]), ics_ctx::kSlotSegs * 4, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_init[k]), ics_ctx::kSlotSegs * 4));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_out[k]), ics_ctx::kSlotSegs * 5, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_out[k]), ics_ctx::kSlotSegs * 5));
+  }
+  ctx->staged = true;
+  return ICS_OK;
+}
+
+void free_staging(ics_ctx* ctx) {
+  for (int k = 0; k < 2; ++k) {
+    if (ctx->st[k]) (void)hipStreamSynchronize(ctx->st[k]);
+    if (ctx->h_in[k]) (void)hipHostFree(ctx->h_in[k]);
+    if (ctx->d_in[k]) (void)hipFree(ctx->d_in[k]);
+    if (ctx->h_off[k]) (void)hipHostFree(ctx->h_off[k]);
+    if (ctx->d_off[k]) (void)hipFree(ctx->d_off[k]);
+    if (ctx->h_init[k]) (void)hipHostFree(ctx->h_init[k]);
+    if (ctx->d_init[k]) (void)hipFree(ctx->d_init[k]);
+    if (ctx->h_out[k]) (void)hipHostFree(ctx->h_out[k]);
+    if (ctx->d_out[k]) (void)hipFree(ctx->d_out[k]);
+    if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
+    if (ctx->st[k]) (void)hipStreamDestroy(ctx->st[k]);
+  }
+  ctx->staged = false;
+}
+
+// One staged chunk of segments [i0, i1) covering bytes [b0, b1).
+struct Chunk {
+  uint64_t i0, i1, b0, b1;
+};
+
+// Next chunk starting at segment i0 that fits the slot (a single segment
+// larger than a slot is an error for the host path).
+int next_chunk(const uint64_t* offsets, uint64_t stride, uint64_t seg_len, uint64_t n, uint64_t i0,
+               Chunk* c) {
+  const uint64_t cap_b = ics_ctx::kSlotBytes, cap_n = ics_ctx::kSlotSegs;
+  if (!offsets) {
+    const uint64_t per = std::max<uint64_t>(stride, seg_len);
+    uint64_t k = per ? cap_b / per : cap_n;
+    if (k == 0) return fail(ICS_ERR_INVALID, "segment of %llu bytes exceeds the %zu-byte staging slot",
+                            (unsigned long long)per, ics_ctx::kSlotBytes);
+    k = std::min<uint64_t>({k, cap_n, n - i0});
+    *c = {i0, i0 + k, i0 * stride, (i0 + k - 1) * stride + seg_len};
+    return ICS_OK;
+  }
+  const uint64_t b0 = offsets[i0];
+  uint64_t i1 = i0;
+  while (i1 < n && i1 - i0 < cap_n && offsets[i1 + 1] - b0 <= cap_b) ++i1;
+  if (i1 == i0)
+    return fail(ICS_ERR_INVALID, "segment %llu (%llu bytes) exceeds the staging slot",
+                (unsigned long long)i0, (unsigned long long)(offsets[i0 + 1] - offsets[i0]));
+  *c = {i0, i1, b0, offsets[i1]};
+  return ICS_OK;
+}
+
+// kind 0: checksum batch (u16 out); kind 1: ipv4_tcp batch (ip u16, tcp u16, status u8)
+int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets,
+                  uint64_t stride, uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode,
+                  uint16_t* out_a, uint16_t* out_b, uint8_t* out_c) {
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (int rc = ensure_staging(ctx)) return rc;
+  Chunk pending[2];
+  bool busy[2] = {false, false};
+  auto retire = [&](int k) -> int {
+    if (!busy[k]) return ICS_OK;
+    ICS_HIP(hipEventSynchronize(ctx->ev[k]));
+    const Chunk& c = pending[k];
+    const uint64_t m = c.i1 - c.i0;
+    if (kind == 0) {
+      std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
+    } else {
+      if (out_a) std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
+      if (out_b) std::memcpy(out_b + c.i0, ctx->h_out[k] + m * 2, m * 2);
+      if (out_c) std::memcpy(out_c + c.i0, ctx->h_out[k] + m * 4, m);
+      if (mode == ICS_MODE_PATCH)
+        std::memcpy(static_cast<uint8_t*>(h_bytes) + c.b0, ctx->h_in[k], c.b1 - c.b0);
+    }
+    busy[k] = false;
+    return ICS_OK;
+  };
+  uint64_t i0 = 0;
+  int slot = 0;
+  while (i0 < n) {
+    Chunk c;
+    if (int rc = next_chunk(h_offsets, stride, seg_len, n, i0, &c)) return rc;
+    if (int rc = retire(slot)) return rc;
+    const uint64_t m = c.i1 - c.i0, nb = c.b1 - c.b0;
+    std::memcpy(ctx->h_in[slot], static_cast<const uint8_t*>(h_bytes) + c.b0, nb);
+    hipStream_t st = ctx->st[slot];
+    ICS_HIP(hipMemcpyAsync(ctx->d_in[slot], ctx->h_in[slot], nb, hipMemcpyHostToDevice, st));
+    const uint64_t* d_off = nullptr;
+    if (h_offsets) {
+      for (uint64_t j = 0; j <= m; ++j) ctx->h_off[slot][j] = h_offsets[c.i0 + j] - c.b0;
+      ICS_HIP(hipMemcpyAsync(ctx->d_off[slot], ctx->h_off[slot], (m + 1) * 8, hipMemcpyHostToDevice, st));
+      d_off = ctx->d_off[slot];
+    }
+    const icsum::SegSpec sp{ctx->d_in[slot], d_off, stride, seg_len, m};
+    const uint64_t avg = h_offsets ? nb / m : seg_len;
+    const icsum::Geometry g = geometry_for(ctx, avg);
+    if (kind == 0) {
+      const uint32_t* d_init = nullptr;
+      if (h_init) {
+        std::memcpy(ctx->h_init[slot], h_init + c.i0, m * 4);
+        ICS_HIP(hipMemcpyAsync(ctx->d_init[slot], ctx->h_init[slot], m * 4, hipMemcpyHostToDevice, st));
+        d_init = ctx->d_init[slot];
+      }
+      ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, ctx->d_out[slot], 0, g, ctx->max_blocks, st));
+      ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 2, hipMemcpyDeviceToHost, st));
+    } else {
+      uint16_t* a = reinterpret_cast<uint16_t*>(ctx->d_out[slot]);
+      uint16_t* b = a + m;
+      uint8_t* s = ctx->d_out[slot] + m * 4;
+      ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, a, b, s, g, ctx->max_blocks, st));
+      ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 5, hipMemcpyDeviceToHost, st));
+      if (mode == ICS_MODE_PATCH)
+        ICS_HIP(hipMemcpyAsync(ctx->h_in[slot], ctx->d_in[slot], nb, hipMemcpyDeviceToHost, st));
+    }
+    ICS_HIP(hipEventRecord(ctx->ev[slot], st));
+    pending[slot] = c;
+    busy[slot] = true;
+    i0 = c.i1;
+    slot ^= 1;
+  }
+  if (int rc = retire(slot)) return rc;
+  if (int rc = retire(slot ^ 1)) return rc;
+  return ICS_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* ics_version(void) { return "icsum 0.1.0 (gfx950)"; }
+int ics_abi_version(void) { return ICS_ABI_VERSION; }
+const char* ics_last_error(void) { return g_err.c_str(); }
+
+int ics_device_count(int* count) {
+  if (!count) return fail(ICS_ERR_INVALID, "null count");
+  *count = 0;
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e == hipErrorNoDevice || (e == hipSuccess && c == 0)) return ICS_OK;
+  ICS_HIP(e);
+  *count = c;
+  return ICS_OK;
+}
+
+int ics_create(int device, ics_ctx** out) {
+  if (!out) return fail(ICS_ERR_INVALID, "null output pointer");
+  *out = nullptr;
+  int c = 0;
+  hipError_t e = hipGetDeviceCount(&c);
+  if (e != hipSuccess || c == 0) return fail(ICS_ERR_NODEVICE, "no GPU available (%s)", hipGetErrorString(e));
+  if (device < 0 || device >= c) return fail(ICS_ERR_NODEVICE, "device %d out of range [0,%d)", device, c);
+  ICS_HIP(hipSetDevice(device));
+  ics_ctx* ctx = new (std::nothrow) ics_ctx();
+  if (!ctx) return fail(ICS_ERR_NOMEM, "context allocation failed");
+  ctx->device = device;
+  ctx->max_blocks = env_u32("ICSUM_MAX_BLOCKS", 0);
+  ctx->force_lps = int(env_u32("ICSUM_LPS", 0));
+  ctx->force_unroll = int(env_u32("ICSUM_UNROLL", 0));
+  *out = ctx;
+  return ICS_OK;
+}
+
+int ics_destroy(ics_ctx* ctx) {
+  if (!ctx) return ICS_OK;
+  if (bind(ctx) == ICS_OK) free_staging(ctx);
+  delete ctx;
+  return ICS_OK;
+}
+
+int ics_device_of(const ics_ctx* ctx, int* device) {
+  if (!ctx || !device) return fail(ICS_ERR_INVALID, "null argument");
+  *device = ctx->device;
+  return ICS_OK;
+}
+
+int ics_checksum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets, uint64_t stride,
+                       uint64_t seg_len, const uint32_t* d_init, uint16_t* d_out, uint64_t n,
+                       void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!d_bytes || !d_out) return fail(ICS_ERR_INVALID, "null device buffer");
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n};
+  const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, seg_len, n, 0));
+  ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, d_out, 0, g, ctx->max_blocks,
+                                 static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets, uint64_t stride,
+                  uint64_t seg_len, const uint32_t* d_init, const uint8_t* d_odd, uint32_t* d_sum,
+                  uint64_t n, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!d_bytes || !d_sum) return fail(ICS_ERR_INVALID, "null device buffer");
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n};
+  const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, seg_len, n, 0));
+  ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_sum, 1, g, ctx->max_blocks,
+                                 static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int ics_fold_batch(ics_ctx* ctx, const uint32_t* d_sum, uint16_t* d_out, uint64_t n, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!d_sum || !d_out) return fail(ICS_ERR_INVALID, "null device buffer");
+  ICS_HIP(icsum::launch_fold(d_sum, d_out, n, static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,
+                       uint64_t dgram_len, uint64_t n, int mode, uint16_t* d_ip_ck,
+                       uint16_t* d_tcp_ck, uint8_t* d_status, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (mode < ICS_MODE_COMPUTE || mode > ICS_MODE_PATCH) return fail(ICS_ERR_INVALID, "bad mode %d", mode);
+  if (n == 0) return ICS_OK;
+  if (!d_dgrams) return fail(ICS_ERR_INVALID, "null datagram buffer");
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n};
+  const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, dgram_len, n, 0));
+  ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks,
+                                 static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,
+                         uint64_t dgram_len, uint64_t n, uint8_t* d_status, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!d_dgrams || !d_status) return fail(ICS_ERR_INVALID, "null device buffer");
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n};
+  ICS_HIP(icsum::launch_router_ttl(sp, d_status, static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int ics_checksum_batch_host(ics_ctx* ctx, const void* h_bytes, const uint64_t* h_offsets,
+                            uint64_t stride, uint64_t seg_len, const uint32_t* h_init,
+                            uint16_t* h_out, uint64_t n) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!h_bytes || !h_out) return fail(ICS_ERR_INVALID, "null host buffer");
+  return host_pipeline(ctx, 0, const_cast<void*>(h_bytes), h_offsets, stride, seg_len, h_init, n, 0,
+                       h_out, nullptr, nullptr);
+}
+
+int ics_ipv4_tcp_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offsets, uint64_t stride,
+                            uint64_t dgram_len, uint64_t n, int mode, uint16_t* h_ip_ck,
+                            uint16_t* h_tcp_ck, uint8_t* h_status) {
+  if (int rc = bind(ctx)) return rc;
+  if (mode < ICS_MODE_COMPUTE || mode > ICS_MODE_PATCH) return fail(ICS_ERR_INVALID, "bad mode %d", mode);
+  if (n == 0) return ICS_OK;
+  if (!h_dgrams) return fail(ICS_ERR_INVALID, "null host buffer");
+  return host_pipeline(ctx, 1, h_dgrams, h_offsets, stride, dgram_len, nullptr, n, mode, h_ip_ck,
+                       h_tcp_ck, h_status);
+}
+
+int ics_malloc(ics_ctx* ctx, void** d_ptr, size_t bytes) {
+  if (int rc = bind(ctx)) return rc;
+  if (!d_ptr) return fail(ICS_ERR_INVALID, "null output pointer");
+  ICS_HIP(hipMalloc(d_ptr, bytes ? bytes : 1));
+  return ICS_OK;
+}
+
+int ics_free(ics_ctx* ctx, void* d_ptr) {
+  if (int rc = bind(ctx)) return rc;
+  if (d_ptr) ICS_HIP(hipFree(d_ptr));
+  return ICS_OK;
+}
+
+int ics_memcpy_htod(ics_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (!bytes) return ICS_OK;
+  ICS_HIP(hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int ics_memcpy_dtoh(ics_ctx* ctx, void* h_dst, const void* d_src, size_t bytes, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (!bytes) return ICS_OK;
+  ICS_HIP(hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int ics_stream_synchronize(ics_ctx* ctx, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  ICS_HIP(hipStreamSynchronize(static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+// ---- synthetic workloads (icsum_workload.h) -----------------------------
+
+int icsw_fill_bytes(ics_ctx* ctx, void* d_bytes, uint64_t nbytes, uint64_t seed, uint64_t pos0,
+                    void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (nbytes && !d_bytes) return fail(ICS_ERR_INVALID, "null device buffer");
+  ICS_HIP(icsum::launch_fill_bytes(static_cast<uint8_t*>(d_bytes), nbytes, seed, pos0,
+                                   static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int icsw_pseudo_inits(ics_ctx* ctx, uint32_t* d_init, const uint64_t* d_offsets, uint64_t seg_len,
+                      uint64_t n, uint64_t seed, uint64_t index0, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n && !d_init) return fail(ICS_ERR_INVALID, "null device buffer");
+  ICS_HIP(icsum::launch_pseudo_inits(d_init, d_offsets, seg_len, n, seed, index0,
+                                     static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int icsw_ipv4_tcp_headers(ics_ctx* ctx, void* d_dgrams, uint64_t stride, uint64_t dgram_len,
+                          uint64_t n, uint64_t seed, uint64_t index0, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n && !d_dgrams) return fail(ICS_ERR_INVALID, "null device buffer");
+  if (dgram_len < 20) return fail(ICS_ERR_INVALID, "datagram length %llu < 20", (unsigned long long)dgram_len);
+  ICS_HIP(icsum::launch_ipv4_tcp_headers(static_cast<uint8_t*>(d_dgrams), stride, dgram_len, n, seed,
+                                         index0, static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+static uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+uint64_t icsw_mixed_len(uint64_t seed, uint64_t i) {
+  const uint64_t m = mix64((seed ^ 0x3C3C3C3C3C3C3C3Cull) + (i + 1) * 0x9E3779B97F4A7C15ull);
+  const unsigned e = 6u + unsigned(m % 10u);
+  return (1ull << e) + ((m >> 8) & ((1ull << e) - 1));
+}
+
+int icsw_mixed_offsets(uint64_t* h_offsets, uint64_t n, uint64_t seed) {
+  if (!h_offsets) return fail(ICS_ERR_INVALID, "null offsets");
+  h_offsets[0] = 0;
+  for (uint64_t i = 0; i < n; ++i) h_offsets[i + 1] = h_offsets[i] + icsw_mixed_len(seed, i);
+  return ICS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,44 @@
+// icsum_launch.h — internal launcher interface between the C-ABI layer
+// (icsum_api.cpp) and the HIP kernels (icsum_kernels.hip).  Not installed.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <stdint.h>
+
+namespace icsum {
+
+// Lane-group geometry of one launch: LPS lanes share a segment, each lane
+// keeps UNROLL 16-byte loads in flight per step.
+struct Geometry {
+  int lps;
+  int unroll;
+};
+
+// Pick a geometry from the (average) segment length in bytes.
+Geometry pick_geometry(uint64_t avg_len);
+
+struct SegSpec {
+  const uint8_t* bytes;
+  const uint64_t* offsets;  // n+1 or nullptr
+  uint64_t stride;
+  uint64_t seg_len;
+  uint64_t n;
+};
+
+// out_kind 0: u16 value(), 1: u32 raw sum
+hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
+                           int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st);
+hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
+hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
+                           uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
+hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
+
+// synthetic workloads (icsum_workload.h)
+hipError_t launch_fill_bytes(uint8_t* d, uint64_t nbytes, uint64_t seed, uint64_t pos0,
+                             hipStream_t st);
+hipError_t launch_pseudo_inits(uint32_t* init, const uint64_t* offsets, uint64_t seg_len,
+                               uint64_t n, uint64_t seed, uint64_t index0, hipStream_t st);
+hipError_t launch_ipv4_tcp_headers(uint8_t* d, uint64_t stride, uint64_t dgram_len, uint64_t n,
+                                   uint64_t seed, uint64_t index0, hipStream_t st);
+
+}  // namespace icsum

@@ -1,0 +1,161 @@
+"""Python host mirror of the checksum engine (plumbing over libicsum.so).
+
+The reference's interface for this path is the C++ header surface of
+util/tools/checksum.h, util/ipv4_header, util/tcp_segment and util/tcp_over_ip
+(SURVEY.md §8b); its C++ mirror lives in csrc/host/.  This module exposes the
+same batch entry points to Python for tests and bench.py.  Device memory and
+streams come from PyTorch (plumbing only); every byte of arithmetic runs in
+the HIP kernels behind the C-ABI.  There is no fallback: a missing library or
+GPU raises.
+"""
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check
+
+MODE_COMPUTE, MODE_VERIFY, MODE_PATCH = _lib.ICS_MODE_COMPUTE, _lib.ICS_MODE_VERIFY, _lib.ICS_MODE_PATCH
+ST_ACCEPT = _lib.ICS_ST_ACCEPT
+
+
+def _ptr(t):
+    if t is None:
+        return None
+    if isinstance(t, np.ndarray):
+        return t.ctypes.data
+    return t.data_ptr()
+
+
+def _stream(stream, device):
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return ctypes.c_void_p(s.cuda_stream)
+
+
+class Engine:
+    """One engine context bound to one GPU (ics_create / ics_destroy)."""
+
+    def __init__(self, device=0):
+        self.lib = _lib.load()
+        self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
+        ctx = ctypes.c_void_p()
+        check(self.lib.ics_create(self.device.index or 0, ctypes.byref(ctx)))
+        self.ctx = ctx
+
+    def close(self):
+        if self.ctx:
+            self.lib.ics_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- a1-a4 -----------------------------------------------------------
+    def checksum_batch(self, data, n=None, offsets=None, stride=0, seg_len=0, init=None, out=None,
+                       stream=None):
+        """u16 InternetChecksum{init_i}.add(segment_i).value() for every segment."""
+        if n is None:
+            n = offsets.numel() - 1 if offsets is not None else data.numel() // max(stride, 1)
+        if out is None:
+            out = torch.empty(n, dtype=torch.int16, device=self.device)
+        check(self.lib.ics_checksum_batch(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len,
+                                          _ptr(init), _ptr(out), n, _stream(stream, self.device)))
+        return out
+
+    def sum_batch(self, data, n=None, offsets=None, stride=0, seg_len=0, init=None, odd=None,
+                  out=None, stream=None):
+        """Unfolded uint32 sum_ after add(segment_i) with parity odd_i (add() chains)."""
+        if n is None:
+            n = offsets.numel() - 1 if offsets is not None else data.numel() // max(stride, 1)
+        if out is None:
+            out = torch.empty(n, dtype=torch.int32, device=self.device)
+        check(self.lib.ics_sum_batch(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len, _ptr(init),
+                                     _ptr(odd), _ptr(out), n, _stream(stream, self.device)))
+        return out
+
+    def fold_batch(self, sums, out=None, stream=None):
+        n = sums.numel()
+        if out is None:
+            out = torch.empty(n, dtype=torch.int16, device=self.device)
+        check(self.lib.ics_fold_batch(self.ctx, _ptr(sums), _ptr(out), n, _stream(stream, self.device)))
+        return out
+
+    # ---- fused IPv4 + TCP --------------------------------------------------
+    def ipv4_tcp_batch(self, dgrams, mode, n=None, offsets=None, stride=0, dgram_len=0,
+                       ip_ck=None, tcp_ck=None, status=None, stream=None):
+        if n is None:
+            n = offsets.numel() - 1 if offsets is not None else dgrams.numel() // max(stride, 1)
+        mk = lambda dt: torch.empty(n, dtype=dt, device=self.device)  # noqa: E731
+        ip_ck = mk(torch.int16) if ip_ck is None else ip_ck
+        tcp_ck = mk(torch.int16) if tcp_ck is None else tcp_ck
+        status = mk(torch.uint8) if status is None else status
+        check(self.lib.ics_ipv4_tcp_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+                                          mode, _ptr(ip_ck), _ptr(tcp_ck), _ptr(status),
+                                          _stream(stream, self.device)))
+        return ip_ck, tcp_ck, status
+
+    def router_ttl_batch(self, dgrams, n=None, offsets=None, stride=0, dgram_len=0, status=None,
+                         stream=None):
+        if n is None:
+            n = offsets.numel() - 1 if offsets is not None else dgrams.numel() // max(stride, 1)
+        status = torch.empty(n, dtype=torch.uint8, device=self.device) if status is None else status
+        check(self.lib.ics_router_ttl_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+                                            _ptr(status), _stream(stream, self.device)))
+        return status
+
+    # ---- host-memory (PCIe-inclusive) variants -----------------------------
+    def checksum_batch_host(self, data, n, offsets=None, stride=0, seg_len=0, init=None):
+        out = np.empty(n, dtype=np.uint16)
+        check(self.lib.ics_checksum_batch_host(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len,
+                                               _ptr(init), _ptr(out), n))
+        return out
+
+    def ipv4_tcp_batch_host(self, dgrams, n, mode, offsets=None, stride=0, dgram_len=0):
+        ip = np.empty(n, dtype=np.uint16)
+        tcp = np.empty(n, dtype=np.uint16)
+        st = np.empty(n, dtype=np.uint8)
+        check(self.lib.ics_ipv4_tcp_batch_host(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len,
+                                               n, mode, _ptr(ip), _ptr(tcp), _ptr(st)))
+        return ip, tcp, st
+
+    # ---- synthetic workloads (include/icsum_workload.h) -------------------
+    def fill_bytes(self, t, seed, pos0=0, stream=None):
+        check(self.lib.icsw_fill_bytes(self.ctx, _ptr(t), t.numel() * t.element_size(), seed, pos0,
+                                       _stream(stream, self.device)))
+        return t
+
+    def pseudo_inits(self, n, seed, offsets=None, seg_len=0, index0=0, out=None, stream=None):
+        out = torch.empty(n, dtype=torch.int32, device=self.device) if out is None else out
+        check(self.lib.icsw_pseudo_inits(self.ctx, _ptr(out), _ptr(offsets), seg_len, n, seed, index0,
+                                         _stream(stream, self.device)))
+        return out
+
+    def ipv4_tcp_headers(self, dgrams, n, stride, dgram_len, seed, index0=0, stream=None):
+        check(self.lib.icsw_ipv4_tcp_headers(self.ctx, _ptr(dgrams), stride, dgram_len, n, seed, index0,
+                                             _stream(stream, self.device)))
+        return dgrams
+
+
+def device_count():
+    c = ctypes.c_int()
+    check(_lib.load().ics_device_count(ctypes.byref(c)))
+    return c.value
+
+
+def mixed_offsets(n, seed):
+    """Packed uint64 offsets (n+1) of the mixed-length workload (host)."""
+    off = np.empty(n + 1, dtype=np.uint64)
+    check(_lib.load().icsw_mixed_offsets(off.ctypes.data, n, seed))
+    return off
+
+
+def as_u16(t):
+    return t.cpu().numpy().view(np.uint16)
+
+
+def as_u32(t):
+    return t.cpu().numpy().view(np.uint32)

@@ -1,0 +1,70 @@
+"""CPU: the C-ABI library loads, exports every symbol include/*.h declares, and
+fails loudly (no fallback) when there is no GPU."""
+import ctypes
+import os
+import re
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+
+
+def declared_symbols():
+    syms = set()
+    for h in ("icsum.h", "icsum_workload.h"):
+        text = open(os.path.join(ROOT, "include", h)).read()
+        text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+        syms |= set(re.findall(r"\b(ics[w]?_[a-z0-9_]+)\s*\(", text))
+    return syms
+
+
+def test_library_exports_every_declared_symbol():
+    from tcpip_network_protocol_stack_amd import _lib
+
+    lib = _lib.load()
+    syms = declared_symbols()
+    assert len(syms) >= 24
+    missing = [s for s in syms if not hasattr(lib, s)]
+    assert not missing, missing
+    # and the ctypes binding covers exactly that surface
+    assert syms == set(_lib.SIGNATURES), syms ^ set(_lib.SIGNATURES)
+    out = subprocess.check_output(["nm", "-D", "--defined-only", _lib.LIB_PATH], text=True)
+    exported = {l.split()[-1] for l in out.splitlines() if " T " in l}
+    assert syms <= exported
+
+
+def test_version_and_abi():
+    from tcpip_network_protocol_stack_amd import _lib
+
+    lib = _lib.load()
+    assert lib.ics_abi_version() == 1
+    assert b"gfx950" in lib.ics_version()
+
+
+def test_no_gpu_fails_loudly():
+    import torch
+
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from tcpip_network_protocol_stack_amd import _lib
+
+    lib = _lib.load()
+    n = ctypes.c_int(-1)
+    assert lib.ics_device_count(ctypes.byref(n)) == 0 and n.value == 0
+    ctx = ctypes.c_void_p()
+    rc = lib.ics_create(0, ctypes.byref(ctx))
+    assert rc == -4 and not ctx.value
+    assert b"no GPU" in lib.ics_last_error()
+    with pytest.raises(_lib.IcsumError):
+        from tcpip_network_protocol_stack_amd.engine import Engine
+
+        Engine(0)
+
+
+def test_null_context_is_an_error_not_a_crash():
+    from tcpip_network_protocol_stack_amd import _lib
+
+    lib = _lib.load()
+    assert lib.ics_checksum_batch(None, None, None, 0, 0, None, None, 0, None) == -1
+    assert b"null context" in lib.ics_last_error()

@@ -1,0 +1,340 @@
+"""GPU parity: the HIP path through the C-ABI (libicsum.so) against the golden
+vectors of the real reference and against the oracle on seeded inputs.
+
+Bar: bit-exact (integer / byte work).  Every call goes through libicsum.so;
+torch only allocates device memory."""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import golden
+from helpers import kat_cases, pack_contiguous, wires
+
+pytestmark = pytest.mark.gpu
+
+GEOMETRIES = [(4, 2), (8, 4), (16, 4), (32, 3), (32, 4), (64, 4), (64, 8)]
+
+
+_SIGNED = {np.dtype(np.uint16): np.int16, np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
+
+
+def _t(a, dev="cuda:0"):
+    """numpy -> device tensor; unsigned words travel as same-width signed views."""
+    import torch
+
+    a = np.ascontiguousarray(a)
+    if a.dtype in _SIGNED:
+        a = a.view(_SIGNED[a.dtype])
+    return torch.from_numpy(a).to(dev)
+
+
+def _u16(t):
+    return t.cpu().numpy().view(np.uint16)
+
+
+def _u32(t):
+    return t.cpu().numpy().view(np.uint32)
+
+
+def _sha(a):
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+@pytest.fixture(scope="module", params=GEOMETRIES, ids=lambda g: f"lps{g[0]}x{g[1]}")
+def geo_engine(request):
+    """An engine per lane-group geometry (forced through ICSUM_LPS/ICSUM_UNROLL)."""
+    import torch
+
+    from tcpip_network_protocol_stack_amd.engine import Engine
+
+    os.environ["ICSUM_LPS"], os.environ["ICSUM_UNROLL"] = map(str, request.param)
+    try:
+        eng = Engine(0)
+    finally:
+        del os.environ["ICSUM_LPS"], os.environ["ICSUM_UNROLL"]
+    yield eng
+    torch.cuda.synchronize()
+    eng.close()
+
+
+# ---------------------------------------------------------------- a1-a4 --
+def test_kat_all_geometries(geo_engine):
+    cases = kat_cases({"rfc1071", "len", "init", "whole"})
+    segs = [b"".join(p) for _, p, _, _ in cases]
+    want = [c[2] for c in cases]
+    for lead in (0, 1, 6, 15):
+        buf, off = pack_contiguous(segs, lead)
+        init = np.array([c[0] for c in cases], dtype=np.uint32)
+        out = geo_engine.checksum_batch(_t(buf), offsets=_t(off), init=_t(init))
+        assert _u16(out).tolist() == want, f"lead={lead}"
+
+
+def test_kat_fill_and_wrap(engine):
+    # long all-0x00 / all-0xFF segments incl. the uint32 wrap past 131074 bytes
+    cases = kat_cases({"fill"})
+    segs = [b"".join(p) for _, p, _, _ in cases]
+    for lead in (0, 3):
+        buf, off = pack_contiguous(segs, lead)
+        init = np.array([c[0] for c in cases], dtype=np.uint32)
+        out = engine.checksum_batch(_t(buf), offsets=_t(off), init=_t(init))
+        assert _u16(out).tolist() == [c[2] for c in cases]
+
+
+def test_split_pieces_chain(engine):
+    # add(vector<string>) with parity carried across pieces (checksum.h:44-59):
+    # chain ics_sum_batch piece by piece, then ics_fold_batch
+    import torch
+
+    cases = kat_cases({"split"})
+    maxp = max(len(p) for _, p, _, _ in cases)
+    sums = np.array([c[0] for c in cases], dtype=np.uint32)
+    odd = np.zeros(len(cases), dtype=np.uint8)
+    for k in range(maxp):
+        segs = [p[k] if k < len(p) else b"" for _, p, _, _ in cases]
+        buf, off = pack_contiguous(segs, 1)
+        s = engine.sum_batch(_t(buf), offsets=_t(off), init=_t(sums), odd=_t(odd))
+        sums = _u32(s).copy()
+        odd ^= np.array([len(x) & 1 for x in segs], dtype=np.uint8)
+    vals = engine.fold_batch(_t(sums))
+    assert _u16(vals).tolist() == [c[2] for c in cases]
+    torch.cuda.synchronize()
+
+
+def test_random_differential(geo_engine, orc):
+    rng = np.random.default_rng(20250225)
+    n = 3000
+    lens = rng.integers(0, 5000, n)
+    lens[::97] = rng.integers(5000, 70000, lens[::97].size)  # some long ones
+    lens[::113] = 0
+    segs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    buf, off = pack_contiguous(segs, 7)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    out = geo_engine.checksum_batch(_t(buf), offsets=_t(off), init=_t(init))
+    want = orc.checksum_batch(buf, n, offsets=off, init=init)
+    assert (_u16(out) == want).all()
+    odd = rng.integers(0, 2, n).astype(np.uint8)
+    sums = geo_engine.sum_batch(_t(buf), offsets=_t(off), init=_t(init), odd=_t(odd))
+    assert (_u32(sums) == orc.sum_batch(buf, n, offsets=off, init=init, odd=odd)).all()
+
+
+@pytest.mark.parametrize("stride,seg_len", [(1500, 1500), (1501, 1497), (64, 64), (9000, 9000),
+                                            (16, 0), (24, 1), (9216, 9000), (7, 7)])
+def test_fixed_stride(engine, orc, stride, seg_len):
+    rng = np.random.default_rng(stride * 31 + seg_len)
+    n = 2048 + 5
+    buf = rng.integers(0, 256, n * stride + seg_len + 16, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    out = engine.checksum_batch(_t(buf), n=n, stride=stride, seg_len=seg_len, init=_t(init))
+    assert (_u16(out) == orc.checksum_batch(buf, n, stride=stride, seg_len=seg_len, init=init)).all()
+    out0 = engine.checksum_batch(_t(buf), n=n, stride=stride, seg_len=seg_len)  # init NULL = 0
+    assert (_u16(out0) == orc.checksum_batch(buf, n, stride=stride, seg_len=seg_len)).all()
+
+
+def test_empty_batch_and_single(engine, orc):
+    import torch
+
+    out = torch.full((4,), 7, dtype=torch.int16, device="cuda:0")
+    engine.checksum_batch(_t(np.zeros(16, np.uint8)), n=0, stride=16, seg_len=16, out=out)
+    assert _u16(out).tolist() == [7] * 4
+    one = engine.checksum_batch(_t(np.frombuffer(bytes.fromhex("0001f203f4f5f6f7") + bytes(8), np.uint8)),
+                                n=1, stride=8, seg_len=8)
+    assert _u16(one).tolist() == [0x220D]
+
+
+# ----------------------------------------------------- fused IPv4 + TCP ---
+def _pack_wires(ws, lead=5):
+    return pack_contiguous([bytes.fromhex(w) for w in ws], lead)
+
+
+@pytest.mark.parametrize("lead", [0, 1, 2, 3])
+def test_ipv4_tcp_verify_fixture(geo_engine, lead):
+    cases = wires("tcp_wrap.json")
+    buf, off = _pack_wires([c["wire"] for c in cases], lead)
+    ip, tcp, st = geo_engine.ipv4_tcp_batch(_t(buf), 1, offsets=_t(off))
+    ip, tcp, st = _u16(ip), _u16(tcp), st.cpu().numpy()
+    for i, c in enumerate(cases):
+        assert bool(st[i] & 1) == c["ip_parse_ok"], (i, c["tag"])
+        if "tcp_parse_ok" in c:
+            assert (st[i] & 6 == 6) == c["tcp_parse_ok"], (i, c["tag"])
+            assert tcp[i] == c["tcp_value"] and ip[i] == c["ip_computed"], (i, c["tag"])
+            assert bool(st[i] & 8) == (c["proto"] == 6)
+        if c["tag"] == "wrap":
+            assert st[i] == 0x0F
+
+
+def test_ipv4_tcp_compute_and_patch_fixture(geo_engine):
+    cases = wires("tcp_wrap.json", {"wrap"})
+    good = [bytearray.fromhex(c["wire"]) for c in cases]
+    junk = []
+    for w in good:
+        j = bytearray(w)
+        j[10:12] = b"\x5a\xa5"
+        j[36:38] = b"\xc3\x3c"
+        junk.append(bytes(j))
+    buf, off = pack_contiguous(junk, 3)
+    d = _t(buf)
+    ip, tcp, st = geo_engine.ipv4_tcp_batch(d, 0, offsets=_t(off))
+    assert _u16(ip).tolist() == [c["ip_cksum"] for c in cases]
+    assert _u16(tcp).tolist() == [w[36] << 8 | w[37] for w in good]
+    assert (st.cpu().numpy() == 0x0F).all()
+    geo_engine.ipv4_tcp_batch(d, 2, offsets=_t(off))
+    want, _ = pack_contiguous([bytes(w) for w in good], 3)
+    assert (d.cpu().numpy() == want).all()  # bytes outside the fields untouched too
+
+
+def test_ipv4_header_cases(engine, orc):
+    cases = wires("ipv4_cases.json")
+    buf, off = _pack_wires([c["bytes"] for c in cases], 1)
+    ip, tcp, st = engine.ipv4_tcp_batch(_t(buf), 1, offsets=_t(off))
+    ip, st = _u16(ip), st.cpu().numpy()
+    for i, c in enumerate(cases):
+        assert bool(st[i] & 1) == c["parse_ok"], c["tag"]
+        if "computed" in c:
+            assert ip[i] == c["computed"], c["tag"]
+    # and the full outputs equal the oracle in every mode
+    for mode in (0, 1, 2):
+        d = _t(buf)
+        g = engine.ipv4_tcp_batch(d, mode, offsets=_t(off))
+        hb = buf.copy()
+        w = orc.ipv4_tcp_batch(hb, len(cases), mode, offsets=off)
+        assert (_u16(g[0]) == w[0]).all() and (_u16(g[1]) == w[1]).all()
+        assert (g[2].cpu().numpy() == w[2]).all()
+        assert (d.cpu().numpy() == hb).all()
+
+
+def test_router_fixture(engine):
+    cases = wires("router_cases.json")
+    buf, off = _pack_wires([c["wire"] for c in cases], 2)
+    d = _t(buf)
+    st = engine.router_ttl_batch(d, offsets=_t(off)).cpu().numpy()
+    assert st.tolist() == [int(c["forwarded"]) for c in cases]
+    want, _ = _pack_wires([c["out"] for c in cases], 2)
+    assert (d.cpu().numpy() == want).all()
+
+
+# -------------------------------------------------- workload generators ---
+def test_workload_generators_match_spec(engine, orc):
+    import torch
+
+    for pos0, nb in [(0, 4096), (3, 1001), (8, 17), (12345, 70000)]:
+        t = torch.empty(nb, dtype=torch.uint8, device="cuda:0")
+        engine.fill_bytes(t, 0x10710004, pos0)
+        assert (t.cpu().numpy() == orc.fill_bytes(0x10710004, pos0, nb)).all()
+    init = engine.pseudo_inits(1000, 0x10710000, seg_len=1500, index0=77)
+    assert (_u32(init) == orc.pseudo_inits(0x10710000, 1000, length=1500, index0=77)).all()
+    d = torch.zeros(50 * 1500, dtype=torch.uint8, device="cuda:0")
+    engine.ipv4_tcp_headers(d, 50, 1500, 1500, 0x10710002)
+    h = np.zeros(50 * 1500, dtype=np.uint8)
+    for i in range(50):
+        orc.ipv4_tcp_headers(0x10710002, i, 1500, h[i * 1500:])
+    assert (d.cpu().numpy() == h).all()
+
+
+# --------------------------------- BASELINE configs at FULL size vs reference
+def _gen_bytes(engine, nbytes, seed):
+    import torch
+
+    t = torch.empty(nbytes, dtype=torch.uint8, device="cuda:0")
+    return engine.fill_bytes(t, seed)
+
+
+@pytest.mark.parametrize("k", ["0", "3", "5"])
+def test_config_fixed_stride_full_size(engine, k):
+    import torch
+
+    g = golden("configs.json")[k]
+    n, stride, seed = g["n"], g["stride"], g["seed"]
+    data = _gen_bytes(engine, n * stride, seed)
+    init = engine.pseudo_inits(n, seed, seg_len=g["seg_len"])
+    out = _u16(engine.checksum_batch(data, n=n, stride=stride, seg_len=g["seg_len"], init=init))
+    del data
+    torch.cuda.empty_cache()
+    assert out[:64].tolist() == g["out_head"]
+    assert _sha(out) == g["out_sha256"]
+
+
+def test_config4_mixed_full_size(engine):
+    import torch
+
+    from tcpip_network_protocol_stack_amd.engine import mixed_offsets
+
+    g = golden("configs.json")["4"]
+    n, seed = g["n"], g["seed"]
+    off = mixed_offsets(n, seed)
+    assert int(off[-1]) == 10292782014
+    data = _gen_bytes(engine, int(off[-1]), seed)
+    doff = _t(off.view(np.int64))
+    init = engine.pseudo_inits(n, seed, offsets=doff)
+    out = _u16(engine.checksum_batch(data, offsets=doff, init=init))
+    del data
+    torch.cuda.empty_cache()
+    assert out[:64].tolist() == g["out_head"]
+    assert _sha(out) == g["out_sha256"]
+
+
+def test_config2_ipv4_full_size(engine):
+    g = golden("configs.json")["2"]
+    n, L, seed = g["n"], g["stride"], g["seed"]
+    d = _gen_bytes(engine, n * L, seed)
+    engine.ipv4_tcp_headers(d, n, L, L, seed)
+    ip, tcp, st = engine.ipv4_tcp_batch(d, 0, n=n, stride=L, dgram_len=L)
+    assert _sha(_u16(ip)) == g["ipck_sha256"] and _sha(_u16(tcp)) == g["tcpck_sha256"]
+    engine.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)
+    assert _sha(d.cpu().numpy()) == g["patched_sha256"]
+    _, _, st = engine.ipv4_tcp_batch(d, 1, n=n, stride=L, dgram_len=L)
+    assert (st.cpu().numpy() == 0x0F).all()
+
+
+def test_corruption_detection_full_size(engine, orc):
+    # inject one random bit flip per datagram of config 2; every flip outside
+    # the IPv4 reserved flag bit (which the reference does not represent,
+    # ipv4_header.cpp:78) must be rejected, exactly as the oracle says
+    import torch
+
+    g = golden("configs.json")["2"]
+    n, L, seed = g["n"], g["stride"], g["seed"]
+    d = _gen_bytes(engine, n * L, seed)
+    engine.ipv4_tcp_headers(d, n, L, L, seed)
+    engine.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)
+    rng = np.random.default_rng(7)
+    bit = rng.integers(0, L * 8, n)
+    pos = torch.from_numpy(np.arange(n) * L + bit // 8).to("cuda:0")
+    mask = torch.from_numpy((1 << (bit % 8)).astype(np.uint8)).to("cuda:0")
+    d[pos] = d[pos] ^ mask
+    _, _, st = engine.ipv4_tcp_batch(d, 1, n=n, stride=L, dgram_len=L)
+    st = st.cpu().numpy()
+    reserved = bit == 6 * 8 + 7
+    assert (st[~reserved] != 0x0F).all()
+    assert (st[reserved] == 0x0F).all()
+    host = d.cpu().numpy()
+    sample = rng.choice(n, 512, replace=False)
+    for i in sample:
+        _, _, s, _ = orc.ipv4_tcp(host[i * L:(i + 1) * L].tobytes(), 1)
+        assert s == st[i]
+
+
+# ------------------------------------------------ host-memory variants ---
+def test_host_path_checksum(engine, orc):
+    rng = np.random.default_rng(5)
+    n, L = 200_000, 1500  # > one 64 MiB staging slot, exercises the 2-slot pipeline
+    buf = rng.integers(0, 256, n * L, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = engine.checksum_batch_host(buf, n, stride=L, seg_len=L, init=init)
+    assert (got == orc.checksum_batch(buf, n, stride=L, seg_len=L, init=init, threads=8)).all()
+    lens = rng.integers(0, 9000, 20_000)
+    segs = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in lens]
+    b2, off = pack_contiguous(segs, 1)
+    got = engine.checksum_batch_host(b2, len(segs), offsets=off)
+    assert (got == orc.checksum_batch(b2, len(segs), offsets=off)).all()
+
+
+def test_host_path_ipv4_patch(engine, orc):
+    cases = wires("tcp_wrap.json", {"wrap"})
+    good = [bytes.fromhex(c["wire"]) for c in cases]
+    junk = [w[:10] + b"\0\0" + w[12:36] + b"\0\0" + w[38:] for w in good]
+    buf, off = pack_contiguous(junk, 0)
+    ip, tcp, st = engine.ipv4_tcp_batch_host(buf, len(junk), 2, offsets=off)
+    want, _ = pack_contiguous(good, 0)
+    assert (buf == want).all() and (st == 0x0F).all()
