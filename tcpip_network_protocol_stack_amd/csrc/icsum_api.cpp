@@ -56,7 +56,7 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 struct ics_ctx {
   int device = 0;
   uint32_t max_blocks = 0;  // 0 = one lane group per segment (no grid-stride cap)
-  int force_lps = 0, force_unroll = 0;
+  int force_lps = 0, force_unroll = 0, force_nt = -1;
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
   static constexpr size_t kSlotBytes = size_t(64) << 20;
@@ -85,14 +85,16 @@ int bind(ics_ctx* ctx) {
 
 icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
   icsum::Geometry g = icsum::pick_geometry(avg_len);
-  if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll};
+  if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll, g.nt};
+  if (ctx->force_nt >= 0) g.nt = ctx->force_nt != 0;
+  if (!icsum::geometry_supported(g)) g = icsum::pick_geometry(avg_len);
   return g;
 }
 
 // average segment length for the geometry choice without reading d_offsets
 uint64_t avg_len_hint(const uint64_t* offsets, uint64_t seg_len, uint64_t n, uint64_t total_hint) {
   if (!offsets) return seg_len;
-  return total_hint && n ? total_hint / n : 4096;
+  return total_hint && n ? total_hint / n : 65536;  // unknown mix: the long-segment geometry
 }
 
 int ensure_staging(ics_ctx* ctx) {
@@ -265,6 +267,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->max_blocks = env_u32("ICSUM_MAX_BLOCKS", 0);
   ctx->force_lps = int(env_u32("ICSUM_LPS", 0));
   ctx->force_unroll = int(env_u32("ICSUM_UNROLL", 0));
+  ctx->force_nt = std::getenv("ICSUM_NT") ? int(env_u32("ICSUM_NT", 1)) : -1;
   *out = ctx;
   return ICS_OK;
 }

@@ -60,54 +60,95 @@ __device__ __forceinline__ uint16_t fold_value(uint32_t s) {
   return uint16_t(~r);
 }
 
-// This lane's share of the running sum over bytes [s, e) of `base`, with byte
-// roles relative to s, XOR `flip` (1 = the first byte is a low byte, i.e. the
-// reference's parity_ was already odd).  A group of LPS lanes covers the
-// 16-byte-aligned chunks that overlap [s, e); bytes outside [s, e) inside
-// those chunks are read and masked off (they share a 16-byte block, hence a
-// page, with bytes of the segment).
-template <int LPS, int UNROLL>
-__device__ __forceinline__ uint32_t range_partial(const uint8_t* __restrict__ base, uint64_t s,
-                                                  uint64_t e, uint32_t lane, uint32_t flip) {
-  uint32_t ev = 0, od = 0;
-  if (e > s) {
-    const uint64_t a0 = s & ~uint64_t(15);
-    const uint64_t span = e - a0;  // bytes from the first chunk start to the end
-    const uint32_t nch = uint32_t((span + 15) >> 4);
-    const uint32_t lo0 = uint32_t(s - a0);
-    const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
-    for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
-      u32x4 v[UNROLL];
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        const uint32_t cc = c + uint32_t(u * LPS);
-        v[u] = cc < nch ? __builtin_nontemporal_load(p + cc) : u32x4{0u, 0u, 0u, 0u};
-      }
-#pragma unroll
-      for (int u = 0; u < UNROLL; ++u) {
-        const uint32_t cc = c + uint32_t(u * LPS);
-        const uint64_t at = uint64_t(cc) << 4;
-        const uint32_t lo = cc == 0 ? lo0 : 0u;
-        const uint32_t hi = at >= span ? 0u : (span - at >= 16 ? 16u : uint32_t(span - at));
-        acc_chunk(v[u] & byte_range_mask(lo, hi), ev, od);
-      }
-    }
-  }
-  // absolute even addresses are high bytes iff the segment starts even
-  if (((uint32_t(s) & 1u) ^ flip) != 0u) {
-    const uint32_t t = ev;
-    ev = od;
-    od = t;
-  }
-  return ev * 256u + od;
+template <bool NT>
+__device__ __forceinline__ u32x4 load16(const u32x4* __restrict__ p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
 }
 
-// Sum over the LPS lanes of an aligned lane group (all 64 lanes must execute).
+// Even/odd byte sums of this lane's share of bytes [s, e) of `base`, roles by
+// ABSOLUTE address (even address -> `ev`).  The range is cut into the 16-byte
+// aligned chunks that overlap it: chunk 0 and chunk nch-1 are the only ones
+// that can be partial.  A group of LPS lanes streams the interior chunks
+// 1..nch-2 unmasked — lane l takes l+1, l+1+LPS, ... with UNROLL loads issued
+// back to back per step and no branches (slots past the end re-load the last
+// interior chunk and are zeroed) — then one masked slot handles the two
+// boundary chunks (lane 0: chunk 0, lane 1: chunk nch-1; LPS == 1 does both).
+// Bytes outside [s, e) inside a boundary chunk are read and discarded: they
+// share a 16-byte block, hence a page, with bytes of the segment.
+template <int LPS, int UNROLL, bool NT>
+__device__ __forceinline__ void range_sums(const uint8_t* __restrict__ base, uint64_t s, uint64_t e,
+                                           uint32_t lane, uint32_t& ev, uint32_t& od) {
+  const uint64_t a0 = s & ~uint64_t(15);
+  const uint64_t span = e > a0 ? e - a0 : 0;  // bytes from the first chunk start to the end
+  const uint32_t nch = uint32_t((span + 15) >> 4);
+  const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  // boundary chunks 0 and nch-1 are loaded FIRST so that their latency
+  // overlaps the interior stream: lane 0 -> chunk 0, lane 1 -> chunk nch-1
+  // (when distinct), other lanes re-load chunk 0 and mask it to nothing.
+  const uint32_t lo0 = uint32_t(s - a0);
+  const uint32_t tail = nch ? uint32_t(span - (uint64_t(nch - 1) << 4)) : 0u;  // valid bytes of the last chunk
+  const uint32_t lastc = nch ? nch - 1 : 0u;
+  u32x4 bh = {0u, 0u, 0u, 0u}, bt = {0u, 0u, 0u, 0u};
+  uint32_t blo = 0, bhi = 0;
+  if (LPS == 1) {
+    if (nch) {
+      bh = load16<NT>(p);
+      bt = load16<NT>(p + lastc);
+    }
+  } else if (nch) {
+    const bool is_tail = lane == 1 && nch >= 2;
+    bh = load16<NT>(p + (is_tail ? lastc : 0u));
+    blo = is_tail ? 0u : lo0;
+    bhi = (is_tail || nch == 1) ? tail : 16u;
+    if (lane >= 2 || (lane == 1 && nch < 2)) bhi = 0u;  // empty mask
+  }
+  // interior chunks [1, nch-1), unmasked
+  const uint32_t last_in = nch >= 2 ? nch - 2 : 0;  // last interior chunk index (if nch >= 3)
+  for (uint32_t c = lane + 1; c + 1 < nch; c += uint32_t(LPS * UNROLL)) {
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      v[u] = load16<NT>(p + (cc <= last_in ? cc : last_in));
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      const uint32_t keep = cc <= last_in ? ~0u : 0u;
+      acc_chunk(v[u] & keep, ev, od);
+    }
+  }
+  if (LPS == 1) {
+    if (nch) {
+      acc_chunk(bh & byte_range_mask(lo0, nch == 1 ? tail : 16u), ev, od);
+      if (nch >= 2) acc_chunk(bt & byte_range_mask(0u, tail), ev, od);
+    }
+  } else {
+    acc_chunk(bh & byte_range_mask(blo, bhi), ev, od);
+  }
+}
+
+// Sum over each aligned group of LPS lanes with DPP (no LDS round trips):
+// quad_perm xor1/xor2, row_half_mirror, row_mirror, then row_bcast15 /
+// row_bcast31 for 32/64-lane groups.  The complete sum lands in the group's
+// last lane (LPS-1); for LPS <= 16 every lane of the group holds it.  All 64
+// lanes must execute this.
 template <int LPS>
 __device__ __forceinline__ uint32_t group_sum(uint32_t x) {
-#pragma unroll
-  for (int o = LPS / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, 64);
+  if (LPS >= 2) x += __builtin_amdgcn_update_dpp(0u, x, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+  if (LPS >= 4) x += __builtin_amdgcn_update_dpp(0u, x, 0x4E, 0xF, 0xF, false);   // quad_perm [2,3,0,1]
+  if (LPS >= 8) x += __builtin_amdgcn_update_dpp(0u, x, 0x141, 0xF, 0xF, false);  // row_half_mirror
+  if (LPS >= 16) x += __builtin_amdgcn_update_dpp(0u, x, 0x140, 0xF, 0xF, false); // row_mirror
+  if (LPS >= 32) x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false); // row_bcast:15
+  if (LPS >= 64) x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false); // row_bcast:31
   return x;
+}
+
+// S contribution of a range from its absolute even/odd sums: the byte at the
+// range start is a high byte unless (start address parity XOR carried parity).
+__device__ __forceinline__ uint32_t combine_roles(uint32_t ev, uint32_t od, uint32_t swap) {
+  return swap ? od * 256u + ev : ev * 256u + od;
 }
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }

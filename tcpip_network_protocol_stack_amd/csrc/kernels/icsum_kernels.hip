@@ -38,7 +38,7 @@ __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets,
 }
 
 // ------------------------------------------------------------ a1-a4 -------
-template <int LPS, int UNROLL, int OUT>
+template <int LPS, int UNROLL, bool NT, int OUT>
 __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t seg_len,
@@ -48,19 +48,19 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
-  // the loop bound is uniform per block, so every lane reaches the shuffles
+  // the loop bound is uniform per block, so every lane reaches the DPP sums
   for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups; g0 < n; g0 += step) {
     const uint64_t seg = g0 + threadIdx.x / LPS;
     const bool valid = seg < n;
     uint64_t s = 0, e = 0;
-    uint32_t flip = 0;
-    if (valid) {
-      seg_bounds(offsets, stride, seg_len, seg, s, e);
-      if (odd) flip = odd[seg] & 1u;
-    }
-    const uint32_t part = range_partial<LPS, UNROLL>(bytes, s, e, lane, flip);
-    const uint32_t tot = group_sum<LPS>(part);
-    if (valid && lane == 0) {
+    if (valid) seg_bounds(offsets, stride, seg_len, seg, s, e);
+    uint32_t ev = 0, od = 0;
+    range_sums<LPS, UNROLL, NT>(bytes, s, e, lane, ev, od);
+    // a high byte at the start unless the start is odd XOR parity_ was odd
+    uint32_t swap = uint32_t(s) & 1u;
+    if (odd && valid) swap ^= odd[seg] & 1u;
+    const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, swap));
+    if (valid && lane == LPS - 1) {
       const uint32_t sum = (init ? init[seg] : 0u) + tot;
       if (OUT == 0)
         static_cast<uint16_t*>(out)[seg] = fold_value(sum);
@@ -70,9 +70,13 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
   }
 }
 
+// HSA dispatch packets carry the grid size in work-items as a uint32, so
+// element-wise kernels use a capped grid and stride over the rest.
+#define ICS_GRID_STRIDE(i, n) \
+  for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < (n); i += uint64_t(gridDim.x) * blockDim.x)
+
 __global__ void k_fold(const uint32_t* __restrict__ sum, uint16_t* __restrict__ out, uint64_t n) {
-  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = fold_value(sum[i]);
+  ICS_GRID_STRIDE(i, n) out[i] = fold_value(sum[i]);
 }
 
 // ---------------------------------------------- IPv4 header fields ------
@@ -125,7 +129,7 @@ __device__ __forceinline__ uint32_t ipv4_pseudo(const Hdr& h) {
 }
 
 // --------------------------------------------- fused IPv4 + TCP ----------
-template <int LPS, int UNROLL>
+template <int LPS, int UNROLL, bool NT>
 __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
@@ -150,9 +154,10 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
       if (off > e - s) off = e - s;
       t0 = s + off;
     }
-    const uint32_t part = range_partial<LPS, UNROLL>(dg, hdr ? t0 : 0, hdr ? e : 0, lane, 0u);
-    const uint32_t tot = group_sum<LPS>(part);
-    if (valid && lane == 0) {
+    uint32_t ev = 0, od = 0;
+    if (hdr) range_sums<LPS, UNROLL, NT>(dg, t0, e, lane, ev, od);
+    const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(t0) & 1u));
+    if (valid && lane == LPS - 1) {
       uint16_t ipc = 0, tcv = 0;
       uint8_t st = 0;
       if (hdr) {
@@ -197,8 +202,7 @@ __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
                                                        const uint64_t* __restrict__ offsets,
                                                        uint64_t stride, uint64_t dlen, uint64_t n,
                                                        uint8_t* __restrict__ status) {
-  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  ICS_GRID_STRIDE(i, n) {
   uint64_t s, e;
   seg_bounds(offsets, stride, dlen, i, s, e);
   uint8_t st = 0;
@@ -218,6 +222,7 @@ __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
     }
   }
   status[i] = st;
+  }
 }
 
 // ------------------------------------------------- workload spec ---------
@@ -234,17 +239,17 @@ __device__ __forceinline__ uint64_t spec_word(uint64_t seed, uint64_t c) {
 
 // Fast path: pos0 % 8 == 0 and d 16-byte aligned -> 16 bytes per thread.
 __global__ void k_fill16(u32x4* __restrict__ d, uint64_t nvec, uint64_t seed, uint64_t w0) {
-  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= nvec) return;
+  ICS_GRID_STRIDE(i, nvec) {
   const uint64_t a = spec_word(seed, w0 + 2 * i), b = spec_word(seed, w0 + 2 * i + 1);
   d[i] = u32x4{uint32_t(a), uint32_t(a >> 32), uint32_t(b), uint32_t(b >> 32)};
+  }
 }
 
 __global__ void k_fill1(uint8_t* __restrict__ d, uint64_t n, uint64_t seed, uint64_t pos0) {
-  const uint64_t j = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (j >= n) return;
-  const uint64_t p = pos0 + j;
-  d[j] = uint8_t(spec_word(seed, p >> 3) >> (8 * (p & 7)));
+  ICS_GRID_STRIDE(j, n) {
+    const uint64_t p = pos0 + j;
+    d[j] = uint8_t(spec_word(seed, p >> 3) >> (8 * (p & 7)));
+  }
 }
 
 __device__ __forceinline__ void spec_addrs(uint64_t seed, uint64_t i, uint32_t& src, uint32_t& dst) {
@@ -255,18 +260,17 @@ __device__ __forceinline__ void spec_addrs(uint64_t seed, uint64_t i, uint32_t& 
 
 __global__ void k_pseudo_inits(uint32_t* __restrict__ init, const uint64_t* __restrict__ offsets,
                                uint64_t seg_len, uint64_t n, uint64_t seed, uint64_t index0) {
-  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  ICS_GRID_STRIDE(i, n) {
   const uint64_t L = offsets ? offsets[i + 1] - offsets[i] : seg_len;
   uint32_t s, d;
   spec_addrs(seed, index0 + i, s, d);
   init[i] = (s >> 16) + (s & 0xffffu) + (d >> 16) + (d & 0xffffu) + 6u + uint32_t(L & 0xffffu);
+  }
 }
 
 __global__ void k_ipv4_tcp_headers(uint8_t* __restrict__ dg, uint64_t stride, uint64_t dlen,
                                    uint64_t n, uint64_t seed, uint64_t index0) {
-  const uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (i >= n) return;
+  ICS_GRID_STRIDE(i, n) {
   uint8_t* d = dg + i * stride;
   const uint64_t id = index0 + i;
   uint32_t s, t;
@@ -291,33 +295,42 @@ __global__ void k_ipv4_tcp_headers(uint8_t* __restrict__ dg, uint64_t stride, ui
     d[38] = 0;
     d[39] = 0;
   }
+  }
+}
+
+// element-wise grid: at most 64K blocks (16M work-items), grid-stride beyond
+inline uint32_t ew_blocks(uint64_t n) {
+  const uint64_t b = (n + kBlock - 1) / kBlock;
+  return uint32_t(b == 0 ? 1 : (b < 65536 ? b : 65536));
 }
 
 inline uint32_t blocks_for(uint64_t groups, uint32_t groups_per_block, uint32_t max_blocks) {
   uint64_t b = (groups + groups_per_block - 1) / groups_per_block;
   if (b == 0) b = 1;
-  const uint64_t cap = max_blocks ? max_blocks : 0x7fffffffull;
+  // cap keeps blocks * 256 work-items far below the uint32 AQL grid limit;
+  // the kernels grid-stride over the remaining segments
+  const uint64_t cap = max_blocks ? max_blocks : (uint64_t(1) << 22);
   return uint32_t(b < cap ? b : cap);
 }
 
-template <int LPS, int UNROLL>
+template <int LPS, int UNROLL, bool NT>
 hipError_t launch_checksum_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                              int out_kind, uint32_t max_blocks, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
   if (out_kind == 0)
-    hipLaunchKernelGGL((k_checksum<LPS, UNROLL, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
+    hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
                        sp.offsets, sp.stride, sp.seg_len, init, odd, out, sp.n);
   else
-    hipLaunchKernelGGL((k_checksum<LPS, UNROLL, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
+    hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
                        sp.offsets, sp.stride, sp.seg_len, init, odd, out, sp.n);
   return hipGetLastError();
 }
 
-template <int LPS, int UNROLL>
+template <int LPS, int UNROLL, bool NT>
 hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                          uint8_t* status, uint32_t max_blocks, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
-  hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL>), dim3(blocks), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL, NT>), dim3(blocks), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, mode,
                      ip_ck, tcp_ck, status);
   return hipGetLastError();
@@ -325,23 +338,34 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
 
 }  // namespace
 
-// geometry table: (LPS, UNROLL) pairs that are instantiated
+// Geometry choice from the (average) segment length, measured on MI355X
+// (tools/sweep_geometry.py, profiles/r1_sweep_geometry.jsonl): give a segment
+// about as many load slots (LPS * UNROLL) as it has interior 16-byte chunks,
+// so a 64-byte segment is 4 lanes x 1 load and a 1500-byte one 16 lanes x 6
+// loads, and let segments beyond ~4 KiB loop with 64 x 8 (8 KiB per wave
+// step).  Non-temporal loads everywhere (stream-once data).
 Geometry pick_geometry(uint64_t avg_len) {
-  const uint64_t chunks = avg_len / 16 + 2;
-  if (chunks <= 8) return {4, 2};
-  if (chunks <= 32) return {8, 4};
-  if (chunks <= 64) return {16, 4};
-  if (chunks <= 96) return {32, 3};
-  if (chunks <= 128) return {32, 4};
-  return {64, 4};
+  const uint64_t m = (avg_len + 15) / 16;  // ~ interior chunks + 1
+  if (m <= 5) return {4, 1, true};
+  if (m <= 9) return {4, 2, true};
+  if (m <= 17) return {8, 2, true};
+  if (m <= 65) return {16, 4, true};
+  if (m <= 97) return {16, 6, true};
+  if (m <= 257) return {32, 4, true};
+  return {64, 8, true};
 }
 
-#define ICS_GEOMETRIES(X) X(4, 2) X(8, 4) X(16, 4) X(32, 3) X(32, 4) X(64, 4) X(64, 8)
+// every instantiated (LPS, UNROLL, NT) triple
+#define ICS_GEOMETRIES(X)                                                                    \
+  X(1, 4, true) X(1, 8, true) X(2, 4, true) X(4, 1, true) X(4, 2, true) X(8, 2, true)        \
+  X(8, 4, true) X(16, 4, true) X(16, 6, true) X(16, 8, true) X(32, 3, true) X(32, 4, true)   \
+  X(64, 2, true) X(64, 3, true) X(64, 4, true) X(64, 8, true) X(16, 6, false) X(64, 2, false)
 
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st) {
-#define ICS_CASE(L, U) \
-  if (g.lps == L && g.unroll == U) return launch_checksum_t<L, U>(sp, init, odd, out, out_kind, max_blocks, st);
+#define ICS_CASE(L, U, T)                                      \
+  if (g.lps == L && g.unroll == U && g.nt == T)                \
+    return launch_checksum_t<L, U, T>(sp, init, odd, out, out_kind, max_blocks, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
@@ -349,22 +373,29 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
 
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st) {
-#define ICS_CASE(L, U) \
-  if (g.lps == L && g.unroll == U) return launch_ipv4_t<L, U>(sp, mode, ip_ck, tcp_ck, status, max_blocks, st);
+#define ICS_CASE(L, U, T)                                      \
+  if (g.lps == L && g.unroll == U && g.nt == T)                \
+    return launch_ipv4_t<L, U, T>(sp, mode, ip_ck, tcp_ck, status, max_blocks, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
 }
 
+bool geometry_supported(Geometry g) {
+#define ICS_CASE(L, U, T) \
+  if (g.lps == L && g.unroll == U && g.nt == T) return true;
+  ICS_GEOMETRIES(ICS_CASE)
+#undef ICS_CASE
+  return false;
+}
+
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st) {
-  const uint32_t blocks = uint32_t((n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_fold, dim3(blocks ? blocks : 1), dim3(kBlock), 0, st, sum, out, n);
+  hipLaunchKernelGGL(k_fold, dim3(ew_blocks(n)), dim3(kBlock), 0, st, sum, out, n);
   return hipGetLastError();
 }
 
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st) {
-  const uint32_t blocks = uint32_t((sp.n + kBlock - 1) / kBlock);
-  hipLaunchKernelGGL(k_router_ttl, dim3(blocks ? blocks : 1), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL(k_router_ttl, dim3(ew_blocks(sp.n)), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, status);
   return hipGetLastError();
 }
@@ -375,16 +406,14 @@ hipError_t launch_fill_bytes(uint8_t* d, uint64_t nbytes, uint64_t seed, uint64_
   if ((pos0 & 7) == 0 && (reinterpret_cast<uintptr_t>(d) & 15) == 0) {
     const uint64_t nvec = nbytes / 16;
     if (nvec) {
-      const uint64_t blocks = (nvec + kBlock - 1) / kBlock;
-      hipLaunchKernelGGL(k_fill16, dim3(uint32_t(blocks)), dim3(kBlock), 0, st,
+      hipLaunchKernelGGL(k_fill16, dim3(ew_blocks(nvec)), dim3(kBlock), 0, st,
                          reinterpret_cast<u32x4*>(d), nvec, seed, pos0 >> 3);
     }
     const uint64_t done = nvec * 16, rest = nbytes - done;
     if (rest)
       hipLaunchKernelGGL(k_fill1, dim3(1), dim3(kBlock), 0, st, d + done, rest, seed, pos0 + done);
   } else {
-    const uint64_t blocks = (nbytes + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(k_fill1, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, d, nbytes, seed, pos0);
+    hipLaunchKernelGGL(k_fill1, dim3(ew_blocks(nbytes)), dim3(kBlock), 0, st, d, nbytes, seed, pos0);
   }
   return hipGetLastError();
 }
@@ -392,7 +421,7 @@ hipError_t launch_fill_bytes(uint8_t* d, uint64_t nbytes, uint64_t seed, uint64_
 hipError_t launch_pseudo_inits(uint32_t* init, const uint64_t* offsets, uint64_t seg_len,
                                uint64_t n, uint64_t seed, uint64_t index0, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_pseudo_inits, dim3(uint32_t((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL(k_pseudo_inits, dim3(ew_blocks(n)), dim3(kBlock), 0, st,
                      init, offsets, seg_len, n, seed, index0);
   return hipGetLastError();
 }
@@ -400,7 +429,7 @@ hipError_t launch_pseudo_inits(uint32_t* init, const uint64_t* offsets, uint64_t
 hipError_t launch_ipv4_tcp_headers(uint8_t* d, uint64_t stride, uint64_t dgram_len, uint64_t n,
                                    uint64_t seed, uint64_t index0, hipStream_t st) {
   if (n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_ipv4_tcp_headers, dim3(uint32_t((n + kBlock - 1) / kBlock)), dim3(kBlock), 0,
+  hipLaunchKernelGGL(k_ipv4_tcp_headers, dim3(ew_blocks(n)), dim3(kBlock), 0,
                      st, d, stride, dgram_len, n, seed, index0);
   return hipGetLastError();
 }

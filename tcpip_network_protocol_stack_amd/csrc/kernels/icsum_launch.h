@@ -12,10 +12,12 @@ namespace icsum {
 struct Geometry {
   int lps;
   int unroll;
+  bool nt;  // non-temporal loads
 };
 
 // Pick a geometry from the (average) segment length in bytes.
 Geometry pick_geometry(uint64_t avg_len);
+bool geometry_supported(Geometry g);
 
 struct SegSpec {
   const uint8_t* bytes;

@@ -14,7 +14,9 @@ from helpers import kat_cases, pack_contiguous, wires
 
 pytestmark = pytest.mark.gpu
 
-GEOMETRIES = [(4, 2), (8, 4), (16, 4), (32, 3), (32, 4), (64, 4), (64, 8)]
+# every instantiated (LPS, UNROLL) — keep in sync with ICS_GEOMETRIES in icsum_kernels.hip
+GEOMETRIES = [(1, 4), (1, 8), (2, 4), (4, 1), (4, 2), (8, 2), (8, 4), (16, 4), (16, 6), (16, 8),
+              (32, 3), (32, 4), (64, 2), (64, 3), (64, 4), (64, 8)]
 
 
 _SIGNED = {np.dtype(np.uint16): np.int16, np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
