@@ -55,8 +55,9 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 // on first use and guarded by `mu`.
 struct ics_ctx {
   int device = 0;
+  void* d_zero = nullptr;  // 16 zero bytes (icsum::SegSpec::zero16)
   uint32_t max_blocks = 0;  // 0 = one lane group per segment (no grid-stride cap)
-  int force_lps = 0, force_unroll = 0, force_nt = -1;
+  int force_lps = 0, force_unroll = 0, force_nt = -1, force_mode = -1;
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
   static constexpr size_t kSlotBytes = size_t(64) << 20;
@@ -85,8 +86,9 @@ int bind(ics_ctx* ctx) {
 
 icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
   icsum::Geometry g = icsum::pick_geometry(avg_len);
-  if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll, g.nt};
+  if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll, g.nt, g.mode};
   if (ctx->force_nt >= 0) g.nt = ctx->force_nt != 0;
+  if (ctx->force_mode >= 0) g.mode = ctx->force_mode;
   if (!icsum::geometry_supported(g)) g = icsum::pick_geometry(avg_len);
   return g;
 }
@@ -202,7 +204,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       ICS_HIP(hipMemcpyAsync(ctx->d_off[slot], ctx->h_off[slot], (m + 1) * 8, hipMemcpyHostToDevice, st));
       d_off = ctx->d_off[slot];
     }
-    const icsum::SegSpec sp{ctx->d_in[slot], d_off, stride, seg_len, m};
+    const icsum::SegSpec sp{ctx->d_in[slot], d_off, stride, seg_len, m, ctx->d_zero};
     const uint64_t avg = h_offsets ? nb / m : seg_len;
     const icsum::Geometry g = geometry_for(ctx, avg);
     if (kind == 0) {
@@ -264,17 +266,25 @@ int ics_create(int device, ics_ctx** out) {
   ics_ctx* ctx = new (std::nothrow) ics_ctx();
   if (!ctx) return fail(ICS_ERR_NOMEM, "context allocation failed");
   ctx->device = device;
+  if (hipMalloc(&ctx->d_zero, 16) != hipSuccess || hipMemset(ctx->d_zero, 0, 16) != hipSuccess) {
+    delete ctx;
+    return fail(ICS_ERR_NOMEM, "device allocation failed");
+  }
   ctx->max_blocks = env_u32("ICSUM_MAX_BLOCKS", 0);
   ctx->force_lps = int(env_u32("ICSUM_LPS", 0));
   ctx->force_unroll = int(env_u32("ICSUM_UNROLL", 0));
   ctx->force_nt = std::getenv("ICSUM_NT") ? int(env_u32("ICSUM_NT", 1)) : -1;
+  ctx->force_mode = std::getenv("ICSUM_MODE") ? int(env_u32("ICSUM_MODE", 0)) : -1;
   *out = ctx;
   return ICS_OK;
 }
 
 int ics_destroy(ics_ctx* ctx) {
   if (!ctx) return ICS_OK;
-  if (bind(ctx) == ICS_OK) free_staging(ctx);
+  if (bind(ctx) == ICS_OK) {
+    free_staging(ctx);
+    if (ctx->d_zero) (void)hipFree(ctx->d_zero);
+  }
   delete ctx;
   return ICS_OK;
 }
@@ -291,7 +301,7 @@ int ics_checksum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offs
   if (int rc = bind(ctx)) return rc;
   if (n == 0) return ICS_OK;
   if (!d_bytes || !d_out) return fail(ICS_ERR_INVALID, "null device buffer");
-  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n};
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n, ctx->d_zero};
   const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, seg_len, n, 0));
   ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, d_out, 0, g, ctx->max_blocks,
                                  static_cast<hipStream_t>(stream)));
@@ -304,7 +314,7 @@ int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets, 
   if (int rc = bind(ctx)) return rc;
   if (n == 0) return ICS_OK;
   if (!d_bytes || !d_sum) return fail(ICS_ERR_INVALID, "null device buffer");
-  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n};
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n, ctx->d_zero};
   const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, seg_len, n, 0));
   ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_sum, 1, g, ctx->max_blocks,
                                  static_cast<hipStream_t>(stream)));
@@ -326,7 +336,7 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   if (mode < ICS_MODE_COMPUTE || mode > ICS_MODE_PATCH) return fail(ICS_ERR_INVALID, "bad mode %d", mode);
   if (n == 0) return ICS_OK;
   if (!d_dgrams) return fail(ICS_ERR_INVALID, "null datagram buffer");
-  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n};
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
   const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, dgram_len, n, 0));
   ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks,
                                  static_cast<hipStream_t>(stream)));
@@ -338,7 +348,7 @@ int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets
   if (int rc = bind(ctx)) return rc;
   if (n == 0) return ICS_OK;
   if (!d_dgrams || !d_status) return fail(ICS_ERR_INVALID, "null device buffer");
-  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n};
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
   ICS_HIP(icsum::launch_router_ttl(sp, d_status, static_cast<hipStream_t>(stream)));
   return ICS_OK;
 }

@@ -129,6 +129,94 @@ __device__ __forceinline__ void range_sums(const uint8_t* __restrict__ base, uin
   }
 }
 
+// Same sums with the chunk grid anchored on the 128-byte cache line that
+// holds s: slot u of a group covers chunks [u*LPS, (u+1)*LPS) from that line,
+// i.e. whole lines, so with LPS >= 8 no line is touched by two load
+// instructions of the wave (non-temporal streams would otherwise re-fetch the
+// shared lines).  Every slot is a plain unmasked load; the lanes that happen
+// to hold the head chunk (index cs) or the tail chunk keep a copy, masked
+// once at the end.  Chunks before cs in the head line are loaded (same line)
+// and discarded.
+template <int LPS, int UNROLL, bool NT>
+__device__ __forceinline__ void range_sums_line(const uint8_t* __restrict__ base, uint64_t s,
+                                                uint64_t e, uint32_t lane, uint32_t& ev,
+                                                uint32_t& od) {
+  const uint64_t a0 = s & ~uint64_t(127);
+  const uint64_t span = e > s ? e - a0 : 0;
+  const uint32_t nch = uint32_t((span + 15) >> 4);
+  const uint32_t cs = uint32_t(s - a0) >> 4;   // head chunk (0..7)
+  const uint32_t lastc = nch ? nch - 1 : 0u;   // tail chunk
+  const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  u32x4 hd = {0u, 0u, 0u, 0u}, td = {0u, 0u, 0u, 0u};
+  for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      v[u] = load16<NT>(p + (cc < lastc ? cc : lastc));
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      const uint32_t keep = (cc > cs && cc < lastc) ? ~0u : 0u;
+      acc_chunk(v[u] & keep, ev, od);
+      if (cc == cs) hd = v[u];
+      if (cc == lastc && lastc != cs) td = v[u];
+    }
+  }
+  if (nch) {
+    const uint32_t tail = uint32_t(span - (uint64_t(lastc) << 4));  // valid bytes of the tail chunk
+    const uint32_t lo0 = uint32_t(s) & 15u;
+    acc_chunk(hd & byte_range_mask(lo0, lastc == cs ? tail : 16u), ev, od);
+    acc_chunk(td & byte_range_mask(0u, tail), ev, od);
+  }
+}
+
+// Fully masked variant on the 16-byte grid: slot u of lane l is chunk
+// l + u*LPS of [s & ~15, e), every slot masked to [s, e).  One load per
+// useful chunk with no separate boundary instruction: the cheapest shape for
+// segments of a few chunks (64 B = 4 lanes x 1 load, one 1 KiB wave
+// instruction per 16 segments), at ~20 more VALU per slot.
+template <int LPS, int UNROLL, bool NT>
+__device__ __forceinline__ void range_sums_masked(const uint8_t* __restrict__ base, uint64_t s,
+                                                  uint64_t e, uint32_t lane, uint32_t& ev,
+                                                  uint32_t& od) {
+  const uint64_t a0 = s & ~uint64_t(15);
+  const uint64_t span = e > s ? e - a0 : 0;
+  const uint32_t nch = uint32_t((span + 15) >> 4);
+  const uint32_t lo0 = uint32_t(s - a0);
+  const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      v[u] = load16<NT>(p + (cc < nch ? cc : nch - 1));
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      const uint64_t at = uint64_t(cc) << 4;
+      const uint32_t lo = cc == 0 ? lo0 : 0u;
+      const uint32_t hi = at >= span ? 0u : (span - at >= 16 ? 16u : uint32_t(span - at));
+      acc_chunk(v[u] & byte_range_mask(lo, hi), ev, od);
+    }
+  }
+}
+
+// Chunk-grid modes (Geometry::mode): 0 = 16-byte grid, interior unmasked +
+// boundary instruction; 1 = 128-byte-line grid; 2 = 16-byte grid, all masked.
+template <int LPS, int UNROLL, bool NT, int MODE>
+__device__ __forceinline__ void seg_sums(const uint8_t* __restrict__ base, uint64_t s, uint64_t e,
+                                         uint32_t lane, uint32_t& ev, uint32_t& od) {
+  if (MODE == 1)
+    range_sums_line<LPS, UNROLL, NT>(base, s, e, lane, ev, od);
+  else if (MODE == 2)
+    range_sums_masked<LPS, UNROLL, NT>(base, s, e, lane, ev, od);
+  else
+    range_sums<LPS, UNROLL, NT>(base, s, e, lane, ev, od);
+}
+
 // Sum over each aligned group of LPS lanes with DPP (no LDS round trips):
 // quad_perm xor1/xor2, row_half_mirror, row_mirror, then row_bcast15 /
 // row_bcast31 for 32/64-lane groups.  The complete sum lands in the group's

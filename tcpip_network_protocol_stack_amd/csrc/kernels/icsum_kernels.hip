@@ -38,12 +38,16 @@ __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets,
 }
 
 // ------------------------------------------------------------ a1-a4 -------
-template <int LPS, int UNROLL, bool NT, int OUT>
+// `init` / `odd` are never null here: an absent array is replaced by a
+// 16-byte zero buffer read with index step 0 (init_step / odd_step).
+template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
 __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t seg_len,
                                                      const uint32_t* __restrict__ init,
+                                                     uint32_t init_step,
                                                      const uint8_t* __restrict__ odd,
+                                                     uint32_t odd_step,
                                                      void* __restrict__ out, uint64_t n) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
@@ -54,14 +58,20 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
     const bool valid = seg < n;
     uint64_t s = 0, e = 0;
     if (valid) seg_bounds(offsets, stride, seg_len, seg, s, e);
+    // per-segment metadata is requested together with the byte stream, so a
+    // wave waits on memory once (the leader lane folds it in at the end)
+    // (unconditional loads from a clamped index: a load under a divergent
+    // branch would make the compiler wait for it at the join)
+    const bool leader = valid && lane == LPS - 1;
+    const uint64_t cseg = valid ? seg : n - 1;
+    const uint32_t i0 = init[cseg * init_step];
+    // a high byte at the start unless the start is odd XOR parity_ was already odd
+    const uint32_t swap = (uint32_t(s) ^ uint32_t(odd[cseg * odd_step])) & 1u;
     uint32_t ev = 0, od = 0;
-    range_sums<LPS, UNROLL, NT>(bytes, s, e, lane, ev, od);
-    // a high byte at the start unless the start is odd XOR parity_ was odd
-    uint32_t swap = uint32_t(s) & 1u;
-    if (odd && valid) swap ^= odd[seg] & 1u;
+    seg_sums<LPS, UNROLL, NT, MODE>(bytes, s, e, lane, ev, od);
     const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, swap));
-    if (valid && lane == LPS - 1) {
-      const uint32_t sum = (init ? init[seg] : 0u) + tot;
+    if (leader) {
+      const uint32_t sum = i0 + tot;
       if (OUT == 0)
         static_cast<uint16_t*>(out)[seg] = fold_value(sum);
       else
@@ -103,6 +113,19 @@ __device__ __forceinline__ Hdr load_hdr(const uint8_t* p) {
   return h;
 }
 
+// TCP header bytes 12..19 of a segment starting at t (>= 18 bytes present):
+// tf0 = bytes 12..15, tf1 = bytes 16..19 (bytes 18, 19 only meaningful when
+// present).  Every dword loaded holds at least one byte of the segment.
+__device__ __forceinline__ void load_tcp_fields(const uint8_t* t, uint32_t& tf0, uint32_t& tf1) {
+  const uintptr_t a = reinterpret_cast<uintptr_t>(t + 12);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
+  const uint32_t sh = uint32_t(a & 3u);
+  const uint32_t d0 = q[0], d1 = q[1];
+  const uint32_t d2 = sh == 3 ? q[2] : d1;  // byte 17 spills into the third dword only at sh = 3
+  tf0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+  tf1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+}
+
 // IPv4Header::compute_checksum (ipv4_header.cpp:113-123): the 20 serialized
 // bytes equal the wire bytes with cksum = 0 and the reserved flag bit (0x8000
 // of the flags word, wire byte 6 bit 7) dropped (serialize, :78); options are
@@ -129,7 +152,7 @@ __device__ __forceinline__ uint32_t ipv4_pseudo(const Hdr& h) {
 }
 
 // --------------------------------------------- fused IPv4 + TCP ----------
-template <int LPS, int UNROLL, bool NT>
+template <int LPS, int UNROLL, bool NT, int MODE>
 __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
@@ -145,17 +168,33 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
     uint64_t s = 0, e = 0;
     if (valid) seg_bounds(offsets, stride, dlen, seg, s, e);
     const bool hdr = valid && e - s >= 20;
+    // Speculate the usual header length (hlen = 5): the IPv4 header dwords,
+    // the TCP fields the verdict needs (data offset, checksum) and the TCP
+    // byte stream are all requested before any of them returns; a datagram
+    // with options (rare) redoes its stream below.
+    uint64_t t0 = hdr ? s + 20 : e;  // TCP part: [t0, e)
     Hdr h = {};
-    uint64_t t0 = e;  // TCP part: [t0, e)
+    uint32_t tf0 = 0, tf1 = 0;  // TCP bytes 12..15 and 16..19 (little-endian)
+    if (hdr) h = load_hdr(dg + s);
+    if (hdr && e - t0 >= 18) load_tcp_fields(dg + t0, tf0, tf1);
+    uint32_t ev = 0, od = 0;
+    seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
+    bool redo = false;
     if (hdr) {
-      h = load_hdr(dg + s);
       uint64_t off = 4u * (h.byte(0) & 0x0fu);  // options skipped (ipv4_header.cpp:50)
       if (off < 20) off = 20;
       if (off > e - s) off = e - s;
+      redo = s + off != t0;
       t0 = s + off;
+      if (redo) {
+        tf0 = tf1 = 0;
+        if (e - t0 >= 18) load_tcp_fields(dg + t0, tf0, tf1);
+      }
     }
-    uint32_t ev = 0, od = 0;
-    if (hdr) range_sums<LPS, UNROLL, NT>(dg, t0, e, lane, ev, od);
+    if (__any(redo)) {  // wave-uniform; groups without options re-sum the same bytes
+      ev = od = 0;
+      seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
+    }
     const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(t0) & 1u));
     if (valid && lane == LPS - 1) {
       uint16_t ipc = 0, tcv = 0;
@@ -167,7 +206,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
         const uint32_t pseudo = ipv4_pseudo(h);
         const uint64_t rem = e - t0;
         if (h.byte(9) == 6) st |= 0x08;  // proto TCP
-        if (rem >= 20 && (dg[t0 + 12] >> 4) >= 5) st |= 0x04;  // tcp_segment.cpp:25-65
+        if (rem >= 20 && ((tf0 & 0xffu) >> 4) >= 5) st |= 0x04;  // tcp_segment.cpp:25-65
         if (mode == 1) {
           tcv = fold_value(pseudo + tot);  // tcp_segment.cpp:11-18
           if (hdr_ok && ipc == h.be16(10)) st |= 0x01;  // ipv4_header.cpp:53-58
@@ -175,8 +214,8 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
         } else {
           // tcp_segment.cpp:143: the checksum field counts as 0
           uint32_t sum = pseudo + tot;
-          if (rem > 16) sum -= uint32_t(dg[t0 + 16]) << 8;
-          if (rem > 17) sum -= uint32_t(dg[t0 + 17]);
+          if (rem > 16) sum -= (rem >= 18 ? tf1 & 0xffu : uint32_t(dg[t0 + 16])) << 8;
+          if (rem > 17) sum -= (tf1 >> 8) & 0xffu;
           tcv = fold_value(sum);
           if (hdr_ok) st |= 0x01;
           if (rem >= 18) st |= 0x02;
@@ -313,24 +352,27 @@ inline uint32_t blocks_for(uint64_t groups, uint32_t groups_per_block, uint32_t 
   return uint32_t(b < cap ? b : cap);
 }
 
-template <int LPS, int UNROLL, bool NT>
+template <int LPS, int UNROLL, bool NT, int MODE>
 hipError_t launch_checksum_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                              int out_kind, uint32_t max_blocks, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
+  const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
+  const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
+  const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
   if (out_kind == 0)
-    hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.stride, sp.seg_len, init, odd, out, sp.n);
+    hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
+                       sp.offsets, sp.stride, sp.seg_len, ip, is, op, os, out, sp.n);
   else
-    hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.stride, sp.seg_len, init, odd, out, sp.n);
+    hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
+                       sp.offsets, sp.stride, sp.seg_len, ip, is, op, os, out, sp.n);
   return hipGetLastError();
 }
 
-template <int LPS, int UNROLL, bool NT>
+template <int LPS, int UNROLL, bool NT, int MODE>
 hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                          uint8_t* status, uint32_t max_blocks, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
-  hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL, NT>), dim3(blocks), dim3(kBlock), 0, st,
+  hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, mode,
                      ip_ck, tcp_ck, status);
   return hipGetLastError();
@@ -339,33 +381,40 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
 }  // namespace
 
 // Geometry choice from the (average) segment length, measured on MI355X
-// (tools/sweep_geometry.py, profiles/r1_sweep_geometry.jsonl): give a segment
-// about as many load slots (LPS * UNROLL) as it has interior 16-byte chunks,
-// so a 64-byte segment is 4 lanes x 1 load and a 1500-byte one 16 lanes x 6
-// loads, and let segments beyond ~4 KiB loop with 64 x 8 (8 KiB per wave
-// step).  Non-temporal loads everywhere (stream-once data).
+// (tools/sweep_geometry.py; profiles/r1_sweep_geometry.jsonl and
+// profiles/r1_sweep_line_grid.jsonl).  Small segments: about one load slot
+// (LPS * UNROLL) per interior 16-byte chunk on a 16-byte grid, so a 64-byte
+// segment is 4 lanes x 1 load.  From ~270 bytes up: the 128-byte-line grid
+// (range_sums_line) with slots >= chunks + 8 so one step covers a segment
+// (1500 B -> 16 lanes x 8 loads), and 64 x 8 (8 KiB per wave step) looping
+// for long segments.  Non-temporal loads everywhere (stream-once data).
 Geometry pick_geometry(uint64_t avg_len) {
-  const uint64_t m = (avg_len + 15) / 16;  // ~ interior chunks + 1
-  if (m <= 5) return {4, 1, true};
-  if (m <= 9) return {4, 2, true};
-  if (m <= 17) return {8, 2, true};
-  if (m <= 65) return {16, 4, true};
-  if (m <= 97) return {16, 6, true};
-  if (m <= 257) return {32, 4, true};
-  return {64, 8, true};
+  const uint64_t m = (avg_len + 15) / 16;  // 16-byte chunks of the payload
+  if (m <= 5) return {4, 1, true, 0};
+  if (m <= 9) return {4, 2, true, 0};
+  if (m <= 17) return {8, 2, true, 0};
+  if (m <= 56) return {16, 4, true, 1};
+  if (m <= 120) return {16, 8, true, 1};
+  if (m <= 256) return {32, 4, true, 1};
+  return {64, 8, true, 1};
 }
 
 // every instantiated (LPS, UNROLL, NT) triple
-#define ICS_GEOMETRIES(X)                                                                    \
-  X(1, 4, true) X(1, 8, true) X(2, 4, true) X(4, 1, true) X(4, 2, true) X(8, 2, true)        \
-  X(8, 4, true) X(16, 4, true) X(16, 6, true) X(16, 8, true) X(32, 3, true) X(32, 4, true)   \
-  X(64, 2, true) X(64, 3, true) X(64, 4, true) X(64, 8, true) X(16, 6, false) X(64, 2, false)
+#define ICS_GEOMETRIES(X)                                                                 \
+  X(1, 4, true, 0) X(1, 8, true, 0) X(2, 4, true, 0) X(4, 1, true, 0) X(4, 2, true, 0)    \
+  X(8, 2, true, 0) X(8, 4, true, 0) X(16, 4, true, 0) X(16, 6, true, 0) X(16, 8, true, 0) \
+  X(32, 3, true, 0) X(32, 4, true, 0) X(64, 2, true, 0) X(64, 3, true, 0)                 \
+  X(64, 4, true, 0) X(64, 8, true, 0) X(16, 6, false, 0) X(64, 2, false, 0)               \
+  X(8, 4, true, 1) X(16, 4, true, 1) X(16, 6, true, 1) X(16, 8, true, 1) X(32, 3, true, 1) \
+  X(32, 4, true, 1) X(64, 4, true, 1) X(64, 8, true, 1) X(16, 6, false, 1)                 \
+  X(1, 4, true, 2) X(1, 8, true, 2) X(2, 4, true, 2) X(4, 1, true, 2) X(4, 2, true, 2)     \
+  X(8, 1, true, 2) X(8, 2, true, 2) X(16, 2, true, 2)
 
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st) {
-#define ICS_CASE(L, U, T)                                      \
-  if (g.lps == L && g.unroll == U && g.nt == T)                \
-    return launch_checksum_t<L, U, T>(sp, init, odd, out, out_kind, max_blocks, st);
+#define ICS_CASE(L, U, T, A)                                      \
+  if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
+    return launch_checksum_t<L, U, T, A>(sp, init, odd, out, out_kind, max_blocks, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
@@ -373,17 +422,17 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
 
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st) {
-#define ICS_CASE(L, U, T)                                      \
-  if (g.lps == L && g.unroll == U && g.nt == T)                \
-    return launch_ipv4_t<L, U, T>(sp, mode, ip_ck, tcp_ck, status, max_blocks, st);
+#define ICS_CASE(L, U, T, A)                                      \
+  if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
+    return launch_ipv4_t<L, U, T, A>(sp, mode, ip_ck, tcp_ck, status, max_blocks, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
 }
 
 bool geometry_supported(Geometry g) {
-#define ICS_CASE(L, U, T) \
-  if (g.lps == L && g.unroll == U && g.nt == T) return true;
+#define ICS_CASE(L, U, T, A) \
+  if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A) return true;
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return false;

@@ -12,7 +12,8 @@ namespace icsum {
 struct Geometry {
   int lps;
   int unroll;
-  bool nt;  // non-temporal loads
+  bool nt;   // non-temporal loads
+  int mode;  // chunk grid: 0 16-byte + boundary slot, 1 128-byte line, 2 16-byte all masked
 };
 
 // Pick a geometry from the (average) segment length in bytes.
@@ -25,6 +26,7 @@ struct SegSpec {
   uint64_t stride;
   uint64_t seg_len;
   uint64_t n;
+  const void* zero16;  // 16 zero bytes in device memory (stand-in for absent arrays)
 };
 
 // out_kind 0: u16 value(), 1: u32 raw sum

@@ -14,9 +14,14 @@ from helpers import kat_cases, pack_contiguous, wires
 
 pytestmark = pytest.mark.gpu
 
-# every instantiated (LPS, UNROLL) — keep in sync with ICS_GEOMETRIES in icsum_kernels.hip
-GEOMETRIES = [(1, 4), (1, 8), (2, 4), (4, 1), (4, 2), (8, 2), (8, 4), (16, 4), (16, 6), (16, 8),
-              (32, 3), (32, 4), (64, 2), (64, 3), (64, 4), (64, 8)]
+# every instantiated (LPS, UNROLL, MODE) with NT loads — keep in sync with
+# ICS_GEOMETRIES in icsum_kernels.hip (MODE 0: 16-byte grid + boundary slot,
+# 1: 128-byte-line grid, 2: 16-byte grid fully masked)
+GEOMETRIES = [(1, 4, 0), (1, 8, 0), (2, 4, 0), (4, 1, 0), (4, 2, 0), (8, 2, 0), (8, 4, 0), (16, 4, 0),
+              (16, 6, 0), (16, 8, 0), (32, 3, 0), (32, 4, 0), (64, 2, 0), (64, 3, 0), (64, 4, 0),
+              (64, 8, 0), (8, 4, 1), (16, 4, 1), (16, 6, 1), (16, 8, 1), (32, 3, 1), (32, 4, 1),
+              (64, 4, 1), (64, 8, 1), (1, 4, 2), (1, 8, 2), (2, 4, 2), (4, 1, 2), (4, 2, 2), (8, 1, 2),
+              (8, 2, 2), (16, 2, 2)]
 
 
 _SIGNED = {np.dtype(np.uint16): np.int16, np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
@@ -44,18 +49,20 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-@pytest.fixture(scope="module", params=GEOMETRIES, ids=lambda g: f"lps{g[0]}x{g[1]}")
+@pytest.fixture(scope="module", params=GEOMETRIES, ids=lambda g: f"lps{g[0]}x{g[1]}m{g[2]}")
 def geo_engine(request):
-    """An engine per lane-group geometry (forced through ICSUM_LPS/ICSUM_UNROLL)."""
+    """An engine per lane-group geometry (forced through ICSUM_LPS/UNROLL/LINE)."""
     import torch
 
     from tcpip_network_protocol_stack_amd.engine import Engine
 
-    os.environ["ICSUM_LPS"], os.environ["ICSUM_UNROLL"] = map(str, request.param)
+    keys = ("ICSUM_LPS", "ICSUM_UNROLL", "ICSUM_MODE")
+    os.environ.update(dict(zip(keys, map(str, request.param))))
     try:
         eng = Engine(0)
     finally:
-        del os.environ["ICSUM_LPS"], os.environ["ICSUM_UNROLL"]
+        for k in keys:
+            del os.environ[k]
     yield eng
     torch.cuda.synchronize()
     eng.close()

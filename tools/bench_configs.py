@@ -1,0 +1,156 @@
+#!/usr/bin/env python3
+"""Every BASELINE.json GPU configuration on one MI355X, plus the host-inclusive
+(PCIe) rate — the numbers DESIGN.md §Measurements quotes.  bench.py stays the
+driver's single headline line (north star); this is the wider table.
+
+    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,jumbo,jumbo_all,host] [--iters 20]
+
+Batches that fit the 256 MiB Infinity Cache (ipv4 98 MB, tcp64 67 MB) are
+rotated over >= 4 distinct copies (>= 393 / 268 MB) so every launch reads HBM.
+Times are HIP events on the launch stream around `iters` back-to-back launches
+(median of 5 rounds).  GiB = 2^30 B of algorithmic bytes (segment bytes, each
+read once); metadata (inits, offsets, outputs) is reported separately.
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tcpip_network_protocol_stack_amd.engine import Engine, mixed_offsets  # noqa: E402
+
+PEAK = 8000.0
+
+
+def timed(fn, iters, rounds=5, settle_ms=150.0):
+    st = torch.cuda.current_stream()
+    fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()  # settle power management (see bench.py --settle-ms)
+    while (time.perf_counter() - t0) * 1e3 < settle_ms:
+        for i in range(8):
+            fn(i)
+        torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for i in range(iters):
+            fn(i)
+        b.record(st)
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / 1e3 / iters)
+    return statistics.median(ts)
+
+
+def emit(name, nbytes, t, meta_bytes=0, **kw):
+    gbs = nbytes / t / 1e9
+    print(json.dumps({"config": name, "bytes": nbytes, "us": round(t * 1e6, 2),
+                      "GiB_s": round(nbytes / t / 2**30, 1), "GB_s": round(gbs, 1),
+                      "frac_hbm_peak": round(gbs / PEAK, 4), "metadata_bytes": meta_bytes, **kw}), flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--only", default="ns,ipv4,tcp64,mixed,jumbo,jumbo_all,host")
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    only = set(args.only.split(","))
+    eng = Engine(0)
+    dev = torch.device("cuda", 0)
+
+    if "ns" in only:  # north star: 1 M x 1500 B, pseudo-header inits
+        n, L, seed = 1 << 20, 1500, 0x10710000
+        d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed)
+        init = eng.pseudo_inits(n, seed, seg_len=L)
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        t = timed(lambda i=0: eng.checksum_batch(d, n=n, stride=L, seg_len=L, init=init, out=out), args.iters)
+        emit("ns_1Mx1500", n * L, t, n * 6, entry="ics_checksum_batch")
+        del d
+
+    if "ipv4" in only:  # config 2: 64 Ki x 1500 B IPv4 datagrams, fused header+pseudo+TCP
+        n, L, seed, R = 1 << 16, 1500, 0x10710002, 6
+        bufs = []
+        for r in range(R):
+            d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+            eng.ipv4_tcp_headers(d, n, L, L, seed, index0=r * n)
+            bufs.append(d)
+        ip = torch.empty(n, dtype=torch.int16, device=dev)
+        tcp = torch.empty(n, dtype=torch.int16, device=dev)
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        for mode, nm in ((0, "compute"), (2, "patch"), (1, "verify")):
+            t = timed(lambda i=0: eng.ipv4_tcp_batch(bufs[i % R], mode, n=n, stride=L, dgram_len=L,
+                                                     ip_ck=ip, tcp_ck=tcp, status=st), args.iters * 3)
+            emit(f"ipv4_64Kix1500_{nm}", n * L, t, n * 5, entry="ics_ipv4_tcp_batch", rotation=R)
+        assert (st.cpu().numpy() == 0x0F).all()
+        del bufs
+
+    if "tcp64" in only:  # config 3: 1 M x 64 B TCP segments with pseudo inits
+        n, L, seed, R = 1 << 20, 64, 0x10710003, 6
+        ds = [eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+              for r in range(R)]
+        inits = [eng.pseudo_inits(n, seed, seg_len=L, index0=r * n) for r in range(R)]
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        t = timed(lambda i=0: eng.checksum_batch(ds[i % R], n=n, stride=L, seg_len=L, init=inits[i % R], out=out),
+                  args.iters * 3)
+        emit("tcp_1Mx64", n * L, t, n * 6, entry="ics_checksum_batch", rotation=R)
+        del ds
+
+    if "mixed" in only:  # config 4: 1 M mixed 64 B - 64 KiB, packed offsets (odd starts)
+        n, seed = 1 << 20, 0x10710004
+        off = mixed_offsets(n, seed)
+        d = eng.fill_bytes(torch.empty(int(off[-1]), dtype=torch.uint8, device=dev), seed)
+        doff = torch.from_numpy(off.view(np.int64)).to(dev)
+        init = eng.pseudo_inits(n, seed, offsets=doff)
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        t = timed(lambda i=0: eng.checksum_batch(d, offsets=doff, init=init, out=out), args.iters // 2 or 1)
+        emit("mixed_1M_64B_64KiB", int(off[-1]), t, n * 14, entry="ics_checksum_batch(offsets)")
+        del d
+
+    if "jumbo" in only:  # config 5 per-GPU shard (weak scaling unit): 1 M x 9000 B
+        n, L, seed = 1 << 20, 9000, 0x10710005
+        d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed)
+        init = eng.pseudo_inits(n, seed, seg_len=L)
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        t = timed(lambda i=0: eng.checksum_batch(d, n=n, stride=L, seg_len=L, init=init, out=out), args.iters // 2)
+        emit("jumbo_1Mx9000_shard", n * L, t, n * 6, entry="ics_checksum_batch")
+        del d
+
+    if "jumbo_all" in only:  # config 5 whole batch on ONE GPU (strong-scaling N=1 point): 8 M x 9000 B
+        n, L, seed = 8 << 20, 9000, 0x10710005
+        d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed)
+        init = eng.pseudo_inits(n, seed, seg_len=L)
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        t = timed(lambda i=0: eng.checksum_batch(d, n=n, stride=L, seg_len=L, init=init, out=out), 3, rounds=3)
+        emit("jumbo_8Mx9000_1gpu", n * L, t, n * 6, entry="ics_checksum_batch")
+        del d
+        torch.cuda.empty_cache()
+
+    if "host" in only:  # PCIe-inclusive: host bytes in, host u16 out (ics_checksum_batch_host)
+        from oracle import oracle as orc  # workload bytes only (spec generator)
+
+        n, L, seed = 1 << 18, 1500, 0x10710000
+        for pinned in (True, False):
+            h = torch.empty(n * L, dtype=torch.uint8, pin_memory=pinned)
+            h.numpy()[:] = orc.fill_bytes(seed, 0, n * L)
+            hi = np.array([orc.pseudo_init(seed, i, L) for i in range(n)], dtype=np.uint32)
+            eng.checksum_batch_host(h.numpy(), n, stride=L, seg_len=L, init=hi)
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                eng.checksum_batch_host(h.numpy(), n, stride=L, seg_len=L, init=hi)
+                ts.append(time.perf_counter() - t0)
+            emit(f"host_inclusive_256Kix1500_{'pinned' if pinned else 'pageable'}", n * L, statistics.median(ts),
+                 n * 6, entry="ics_checksum_batch_host", note="H2D + kernel + D2H, 2-slot pipeline")
+    eng.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -24,9 +24,9 @@ WL = {"ns": (1 << 20, 1500), "tcp64": (1 << 20, 64), "jumbo": (1 << 20, 9000), "
       "s128": (1 << 20, 128), "s256": (1 << 20, 256), "s576": (1 << 20, 576), "s3000": (1 << 19, 3000)}
 
 
-def make_engine(lps, unroll, nt, cap):
+def make_engine(lps, unroll, nt, line, cap):
     env = {"ICSUM_LPS": str(lps), "ICSUM_UNROLL": str(unroll), "ICSUM_NT": str(int(nt)),
-           "ICSUM_MAX_BLOCKS": str(cap)}
+           "ICSUM_MODE": str(int(line)), "ICSUM_MAX_BLOCKS": str(cap)}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -47,8 +47,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
-    variants = [tuple(int(x) for x in v.split("x")) for v in args.variants.split(",") if v] or [
-        (64, 2, 1), (32, 3, 1), (32, 3, 0), (16, 6, 1), (8, 12, 1), (64, 4, 1), (64, 8, 1)]
+    # LPSxUNROLLxNT[xMODE]
+    variants = [tuple(int(x) for x in (v + "x0").split("x")[:4]) for v in args.variants.split(",") if v] or [
+        (16, 6, 1, 0), (16, 6, 1, 1), (32, 3, 1, 0), (32, 3, 1, 1), (64, 8, 1, 0), (64, 8, 1, 1)]
     caps = [int(c) for c in args.caps.split(",")]
     base = Engine(0)
     for wl in args.workloads.split(","):
@@ -66,8 +67,8 @@ def main():
         ref = base.checksum_batch(data, n=n, offsets=doff, stride=L or 0, seg_len=L or 0, init=init)
         torch.cuda.synchronize()
         engines = {}
-        for (lps, u, nt), cap in itertools.product(variants, caps):
-            engines[(lps, u, nt, cap)] = make_engine(lps, u, nt, cap)
+        for (lps, u, nt, line), cap in itertools.product(variants, caps):
+            engines[(lps, u, nt, line, cap)] = make_engine(lps, u, nt, line, cap)
         times = {k: [] for k in engines}
         st = torch.cuda.current_stream()
         for r in range(args.rounds):
@@ -84,7 +85,7 @@ def main():
                     assert torch.equal(out, ref), f"variant {k} mismatch"
         for k, ts in times.items():
             med = statistics.median(ts)
-            print(json.dumps({"workload": wl, "lps": k[0], "unroll": k[1], "nt": k[2], "cap": k[3],
+            print(json.dumps({"workload": wl, "lps": k[0], "unroll": k[1], "nt": k[2], "mode": k[3], "cap": k[4],
                               "med_us": round(med * 1e6, 1), "med_GBs": round(total / med / 1e9, 1),
                               "best_GBs": round(total / min(ts) / 1e9, 1)}), flush=True)
         for e in engines.values():
