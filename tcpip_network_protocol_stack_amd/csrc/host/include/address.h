@@ -1,0 +1,29 @@
+// address.h — the part of the reference's Address (util/address/address.h)
+// that the TCP-over-IPv4 adapter needs: an IPv4 address + port value type.
+// Socket/DNS resolution is the runtime's business and out of this engine's
+// scope; only numeric IPv4 literals are accepted here.
+#ifndef ICSUM_HOST_ADDRESS_H
+#define ICSUM_HOST_ADDRESS_H
+
+#include <cstdint>
+#include <string>
+#include <utility>
+
+class Address
+{
+    uint32_t ip_ = 0;  // host order
+    uint16_t port_ = 0;
+
+  public:
+    explicit Address(const std::string& ip, std::uint16_t port = 0);
+    bool operator==(const Address& o) const { return ip_ == o.ip_ && port_ == o.port_; }
+    bool operator!=(const Address& o) const { return !operator==(o); }
+    std::pair<std::string, uint16_t> ip_port() const { return {ip(), port_}; }
+    std::string ip() const;
+    uint16_t port() const { return port_; }
+    uint32_t ipv4_numeric() const { return ip_; }
+    static Address from_ipv4_numeric(uint32_t ip_address);
+    std::string to_string() const { return ip() + ":" + std::to_string(port_); }
+};
+
+#endif

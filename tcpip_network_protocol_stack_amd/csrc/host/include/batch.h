@@ -1,0 +1,62 @@
+// batch.h — batch entry points of the drop-in types, backed by the MI355X
+// engine (libicsum.so, include/icsum.h).  These are the calls a busy stack
+// makes instead of one compute_checksum()/parse() per object:
+//
+//   checksum()            InternetChecksum{init_i}.add(seg_i).value()     checksum.h:17-41
+//   compute_checksums()   TCPSegment::compute_checksum(pseudo) per pair    tcp_segment.cpp:109-118
+//                         IPv4Header::compute_checksum() per header        ipv4_header.cpp:113-123
+//   verify_raw()          IPv4Header::parse + TCPSegment::parse checks     ipv4_header.cpp:9-59, tcp_segment.cpp:11-65
+//   wrap()                TCPOverIPv4Adapter::wrap_tcp_in_ip per message   tcp_over_ip.cpp:69-88
+//   unwrap()/unwrap_raw() TCPOverIPv4Adapter::unwrap_tcp_in_ip per datagram tcp_over_ip.cpp:10-67
+//
+// Results are bit-identical to the per-object calls.  All checksum arithmetic
+// runs on the GPU; a BatchEngine cannot be constructed without one (there is
+// no silent CPU fallback).  One engine per thread, or guard it externally.
+#ifndef ICSUM_HOST_BATCH_H
+#define ICSUM_HOST_BATCH_H
+
+#include <cstdint>
+#include <optional>
+#include <span>
+#include <string>
+#include <string_view>
+#include <vector>
+
+#include "ipv4_datagram.h"
+#include "ipv4_header.h"
+#include "tcp_over_ip.h"
+#include "tcp_segment.h"
+
+struct ics_ctx;
+
+namespace icsum {
+
+class BatchEngine
+{
+  public:
+    explicit BatchEngine(int device = 0);  // throws std::runtime_error without a usable GPU
+    ~BatchEngine();
+    BatchEngine(const BatchEngine&) = delete;
+    BatchEngine& operator=(const BatchEngine&) = delete;
+
+    std::vector<uint16_t> checksum(std::span<const std::string_view> segs, std::span<const uint32_t> init = {});
+    void compute_checksums(std::span<TCPSegment> segs, std::span<const IPv4Header> hdrs);
+    void compute_checksums(std::span<IPv4Header> hdrs);
+    // ICS_ST_* status bits per raw wire datagram (ICS_ST_ACCEPT = all parse checks pass)
+    std::vector<uint8_t> verify_raw(std::span<const std::string_view> wires);
+    std::vector<InternetDatagram> wrap(TCPOverIPv4Adapter& adapter, std::span<const TCPMessage> msgs);
+    std::vector<std::optional<TCPMessage>> unwrap(TCPOverIPv4Adapter& adapter,
+                                                  std::span<const InternetDatagram> dgrams);
+    std::vector<std::optional<TCPMessage>> unwrap_raw(TCPOverIPv4Adapter& adapter,
+                                                      std::span<const std::string_view> wires);
+
+    int device() const { return device_; }
+
+  private:
+    ics_ctx* ctx_ = nullptr;
+    int device_ = 0;
+};
+
+}  // namespace icsum
+
+#endif

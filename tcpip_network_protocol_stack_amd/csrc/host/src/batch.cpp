@@ -1,0 +1,237 @@
+// batch.cpp — icsum::BatchEngine (see batch.h): packs objects into one
+// contiguous wire buffer + offsets, runs one engine call, scatters results.
+#include "batch.h"
+
+#include <stdexcept>
+
+#include "icsum.h"
+#include "tcp_segment_internal.h"
+
+namespace icsum {
+namespace {
+
+void check(int rc, const char* what)
+{
+    if (rc != ICS_OK) throw std::runtime_error(std::string(what) + ": " + ics_last_error());
+}
+
+// contiguous wire bytes of many pieces-lists with n+1 offsets
+struct Packed
+{
+    std::string bytes;
+    std::vector<uint64_t> off{0};
+
+    void begin() {}
+    void add(std::string_view s) { bytes.append(s); }
+    void end() { off.push_back(bytes.size()); }
+    uint64_t n() const { return off.size() - 1; }
+};
+
+// the 40 header bytes wrap_tcp_in_ip serializes (checksum fields 0) + payload
+void append_wire(Packed& p, const IPv4Header& h, const TCPSegment& seg)
+{
+    p.add(serialize(h).front());
+    for (const auto& piece : serialize(seg)) p.add(piece);
+    p.end();
+}
+
+}  // namespace
+
+BatchEngine::BatchEngine(int device) : device_(device)
+{
+    check(ics_create(device, &ctx_), "ics_create");
+}
+
+BatchEngine::~BatchEngine() { ics_destroy(ctx_); }
+
+std::vector<uint16_t> BatchEngine::checksum(std::span<const std::string_view> segs, std::span<const uint32_t> init)
+{
+    if (!init.empty() && init.size() != segs.size()) throw std::invalid_argument("init size != segment count");
+    Packed p;
+    for (auto s : segs) {
+        p.add(s);
+        p.end();
+    }
+    std::vector<uint16_t> out(segs.size());
+    if (!segs.empty())
+        check(ics_checksum_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, init.empty() ? nullptr : init.data(),
+                                      out.data(), p.n()),
+              "ics_checksum_batch_host");
+    return out;
+}
+
+void BatchEngine::compute_checksums(std::span<TCPSegment> segs, std::span<const IPv4Header> hdrs)
+{
+    if (hdrs.size() != segs.size()) throw std::invalid_argument("header count != segment count");
+    Packed p;
+    std::vector<uint32_t> init(segs.size());
+    for (size_t i = 0; i < segs.size(); ++i) {
+        segs[i].udinfo.cksum = 0;  // tcp_segment.cpp:111 — summed as zero
+        for (const auto& piece : serialize(segs[i])) p.add(piece);
+        p.end();
+        init[i] = hdrs[i].pseudo_checksum();
+    }
+    std::vector<uint16_t> out(segs.size());
+    if (!segs.empty())
+        check(ics_checksum_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, init.data(), out.data(), p.n()),
+              "ics_checksum_batch_host");
+    for (size_t i = 0; i < segs.size(); ++i) segs[i].udinfo.cksum = out[i];
+}
+
+void BatchEngine::compute_checksums(std::span<IPv4Header> hdrs)
+{
+    Packed p;
+    for (auto& h : hdrs) {
+        h.cksum = 0;
+        p.add(serialize(h).front());  // throws "wrong IP version" like the reference
+        p.end();
+    }
+    std::vector<uint16_t> ip(hdrs.size());
+    if (!hdrs.empty())
+        check(ics_ipv4_tcp_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, p.n(), ICS_MODE_COMPUTE, ip.data(),
+                                      nullptr, nullptr),
+              "ics_ipv4_tcp_batch_host");
+    for (size_t i = 0; i < hdrs.size(); ++i) hdrs[i].cksum = ip[i];
+}
+
+std::vector<uint8_t> BatchEngine::verify_raw(std::span<const std::string_view> wires)
+{
+    Packed p;
+    for (auto w : wires) {
+        p.add(w);
+        p.end();
+    }
+    std::vector<uint8_t> st(wires.size());
+    if (!wires.empty())
+        check(ics_ipv4_tcp_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, p.n(), ICS_MODE_VERIFY, nullptr,
+                                      nullptr, st.data()),
+              "ics_ipv4_tcp_batch_host");
+    return st;
+}
+
+std::vector<InternetDatagram> BatchEngine::wrap(TCPOverIPv4Adapter& adapter, std::span<const TCPMessage> msgs)
+{
+    // tcp_over_ip.cpp:69-88 for every message; both checksums in one device pass
+    std::vector<InternetDatagram> out(msgs.size());
+    std::vector<TCPSegment> segs(msgs.size());
+    Packed p;
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        TCPSegment& seg = segs[i];
+        seg.message = msgs[i];
+        seg.udinfo = {adapter.config().source.port(), adapter.config().destination.port(), 0};
+        IPv4Header& h = out[i].header;
+        h.src = adapter.config().source.ipv4_numeric();
+        h.dst = adapter.config().destination.ipv4_numeric();
+        h.len = static_cast<uint16_t>(h.hlen * 4 + 20 + seg.message.sender.payload.size());
+        h.cksum = 0;
+        append_wire(p, h, seg);
+    }
+    std::vector<uint16_t> ip(msgs.size()), tcp(msgs.size());
+    if (!msgs.empty())
+        check(ics_ipv4_tcp_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, p.n(), ICS_MODE_COMPUTE, ip.data(),
+                                      tcp.data(), nullptr),
+              "ics_ipv4_tcp_batch_host");
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        out[i].header.cksum = ip[i];
+        segs[i].udinfo.cksum = tcp[i];
+        out[i].payload = serialize(segs[i]);
+    }
+    return out;
+}
+
+namespace {
+// tcp_over_ip.cpp:39-64 — the port / listening filters after a successful parse
+std::optional<TCPMessage> finish_unwrap(TCPOverIPv4Adapter& a, const IPv4Header& h, TCPSegment& seg)
+{
+    if (seg.udinfo.dst_port != a.config().source.port()) return {};
+    if (a.listening()) {
+        if (!seg.message.sender.SYN || seg.message.sender.RST) return {};
+        a.config_mut().source = Address{Address::from_ipv4_numeric(h.dst).ip(), a.config().source.port()};
+        a.config_mut().destination = Address{Address::from_ipv4_numeric(h.src).ip(), seg.udinfo.src_port};
+        a.set_listening(false);
+    }
+    if (seg.udinfo.src_port != a.config().destination.port()) return {};
+    return seg.message;
+}
+
+bool address_ok(const TCPOverIPv4Adapter& a, const IPv4Header& h)
+{
+    if (!a.listening() && h.dst != a.config().source.ipv4_numeric()) return false;
+    if (!a.listening() && h.src != a.config().destination.ipv4_numeric()) return false;
+    return h.proto == IPv4Header::PROTO_TCP;
+}
+}  // namespace
+
+std::vector<std::optional<TCPMessage>> BatchEngine::unwrap(TCPOverIPv4Adapter& adapter,
+                                                           std::span<const InternetDatagram> dgrams)
+{
+    // TCPSegment::parse's checksum (value() of pseudo + all payload bytes) on
+    // the GPU for the whole batch, then field parsing + filters in order
+    Packed p;
+    std::vector<uint32_t> init(dgrams.size());
+    for (size_t i = 0; i < dgrams.size(); ++i) {
+        for (const auto& piece : dgrams[i].payload) p.add(piece);
+        p.end();
+        init[i] = dgrams[i].header.pseudo_checksum();
+    }
+    std::vector<uint16_t> v(dgrams.size());
+    if (!dgrams.empty())
+        check(ics_checksum_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, init.data(), v.data(), p.n()),
+              "ics_checksum_batch_host");
+    std::vector<std::optional<TCPMessage>> out(dgrams.size());
+    for (size_t i = 0; i < dgrams.size(); ++i) {
+        const IPv4Header& h = dgrams[i].header;
+        if (!address_ok(adapter, h) || v[i] != 0) continue;
+        TCPSegment seg;
+        Parser parser{dgrams[i].payload};
+        detail::parse_tcp_fields(parser, seg);
+        if (parser.has_error()) continue;
+        out[i] = finish_unwrap(adapter, h, seg);
+    }
+    return out;
+}
+
+std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_raw(TCPOverIPv4Adapter& adapter,
+                                                               std::span<const std::string_view> wires)
+{
+    // receive path from raw wire datagrams (a TUN / socket read batch):
+    // IPv4 parse + TCP checksum verified on the GPU, fields parsed on the host
+    const std::vector<uint8_t> st = verify_raw(wires);
+    std::vector<std::optional<TCPMessage>> out(wires.size());
+    for (size_t i = 0; i < wires.size(); ++i) {
+        if ((st[i] & (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) !=
+            (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK))
+            continue;
+        IPv4Datagram dg;
+        Parser ipp{std::vector<std::string>{std::string{wires[i]}}};
+        // fields only: the GPU already compared the header checksum
+        uint8_t first = 0;
+        ipp.integer(first);
+        dg.header.ver = first >> 4;
+        dg.header.hlen = first & 0x0f;
+        ipp.integer(dg.header.tos);
+        ipp.integer(dg.header.len);
+        ipp.integer(dg.header.id);
+        uint16_t fo = 0;
+        ipp.integer(fo);
+        dg.header.df = (fo & 0x4000) != 0;
+        dg.header.mf = (fo & 0x2000) != 0;
+        dg.header.offset = fo & 0x1fff;
+        ipp.integer(dg.header.ttl);
+        ipp.integer(dg.header.proto);
+        ipp.integer(dg.header.cksum);
+        ipp.integer(dg.header.src);
+        ipp.integer(dg.header.dst);
+        ipp.remove_prefix(static_cast<uint64_t>(dg.header.hlen) * 4 - IPv4Header::LENGTH);
+        ipp.all_remaining(dg.payload);
+        if (!address_ok(adapter, dg.header)) continue;
+        TCPSegment seg;
+        Parser tp{dg.payload};
+        detail::parse_tcp_fields(tp, seg);
+        if (tp.has_error()) continue;
+        out[i] = finish_unwrap(adapter, dg.header, seg);
+    }
+    return out;
+}
+
+}  // namespace icsum

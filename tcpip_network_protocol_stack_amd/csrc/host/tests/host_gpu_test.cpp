@@ -1,0 +1,144 @@
+// host_gpu_test.cpp — icsum::BatchEngine (GPU) against the per-object calls of
+// the same drop-in types (CPU) on seeded random traffic.  Exit 0 = identical.
+#include <cstdio>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "batch.h"
+#include "checksum.h"
+#include "icsum.h"
+
+namespace {
+int failures = 0;
+#define EXPECT(c)                                                     \
+    do {                                                              \
+        if (!(c)) {                                                   \
+            std::fprintf(stderr, "FAIL %s:%d %s\n", __FILE__, __LINE__, #c); \
+            ++failures;                                               \
+        }                                                             \
+    } while (0)
+
+std::string joined(const std::vector<std::string>& v)
+{
+    std::string r;
+    for (auto& s : v) r += s;
+    return r;
+}
+}  // namespace
+
+int main()
+{
+    icsum::BatchEngine eng(0);
+    std::mt19937_64 rng(0x1071);
+    auto bytes = [&](size_t n) {
+        std::string s(n, '\0');
+        for (auto& c : s) c = static_cast<char>(rng());
+        return s;
+    };
+
+    // checksum(): vs InternetChecksum per segment, odd lengths and empty ones
+    std::vector<std::string> segs;
+    std::vector<uint32_t> init;
+    for (int i = 0; i < 5000; ++i) {
+        segs.push_back(bytes(rng() % 3000));
+        init.push_back(static_cast<uint32_t>(rng()));
+    }
+    std::vector<std::string_view> views(segs.begin(), segs.end());
+    const auto v = eng.checksum(views, init);
+    for (size_t i = 0; i < segs.size(); ++i) {
+        InternetChecksum c{init[i]};
+        c.add(std::string_view{segs[i]});
+        EXPECT(v[i] == c.value());
+    }
+
+    // wrap(): vs wrap_tcp_in_ip per message
+    TCPOverIPv4Adapter A, B;
+    A.config_mut().source = Address{"10.1.2.3", 4321};
+    A.config_mut().destination = Address{"10.9.8.7", 80};
+    B.config_mut().source = Address{"10.9.8.7", 80};
+    B.config_mut().destination = Address{"10.1.2.3", 4321};
+    std::vector<TCPMessage> msgs;
+    for (int i = 0; i < 2000; ++i) {
+        TCPMessage m;
+        m.sender.seqno = Wrap32{static_cast<uint32_t>(rng())};
+        m.sender.SYN = rng() % 5 == 0;
+        m.sender.FIN = rng() % 7 == 0;
+        m.sender.payload = bytes(rng() % 1001);
+        if (rng() % 3) m.receiver.ackno = Wrap32{static_cast<uint32_t>(rng())};
+        m.receiver.window_size = static_cast<uint16_t>(rng());
+        msgs.push_back(m);
+    }
+    const auto dgs = eng.wrap(A, msgs);
+    std::vector<std::string> wires;
+    for (size_t i = 0; i < msgs.size(); ++i) {
+        const auto want = joined(serialize(A.wrap_tcp_in_ip(msgs[i])));
+        wires.push_back(joined(serialize(dgs[i])));
+        EXPECT(wires.back() == want);
+    }
+
+    // compute_checksums(): TCP and IPv4 header batches
+    {
+        std::vector<TCPSegment> ts;
+        std::vector<IPv4Header> hs;
+        for (size_t i = 0; i < 300; ++i) {
+            TCPSegment s;
+            s.message = msgs[i];
+            s.udinfo = {static_cast<uint16_t>(rng()), static_cast<uint16_t>(rng()), static_cast<uint16_t>(rng())};
+            IPv4Header h;
+            h.src = static_cast<uint32_t>(rng());
+            h.dst = static_cast<uint32_t>(rng());
+            h.len = static_cast<uint16_t>(40 + s.message.sender.payload.size());
+            h.ttl = static_cast<uint8_t>(rng());
+            h.id = static_cast<uint16_t>(rng());
+            ts.push_back(s);
+            hs.push_back(h);
+        }
+        auto ts_cpu = ts;
+        auto hs_cpu = hs;
+        eng.compute_checksums(ts, hs);
+        eng.compute_checksums(std::span<IPv4Header>(hs));
+        for (size_t i = 0; i < ts.size(); ++i) {
+            ts_cpu[i].compute_checksum(hs_cpu[i].pseudo_checksum());
+            hs_cpu[i].compute_checksum();
+            EXPECT(ts[i].udinfo.cksum == ts_cpu[i].udinfo.cksum);
+            EXPECT(hs[i].cksum == hs_cpu[i].cksum);
+        }
+    }
+
+    // verify_raw() / unwrap_raw() / unwrap(): clean and one-bit-corrupted wires
+    std::vector<std::string> rx;
+    for (size_t i = 0; i < wires.size(); ++i) {
+        std::string w = wires[i];
+        if (i % 2) w[rng() % w.size()] ^= static_cast<char>(1u << (rng() % 8));
+        rx.push_back(w);
+    }
+    std::vector<std::string_view> rxv(rx.begin(), rx.end());
+    const auto st = eng.verify_raw(rxv);
+    TCPOverIPv4Adapter Bcpu = B, Bgpu = B, Bgpu2 = B;
+    const auto got = eng.unwrap_raw(Bgpu, rxv);
+    std::vector<InternetDatagram> parsed(rx.size());
+    std::vector<bool> ip_ok(rx.size());
+    for (size_t i = 0; i < rx.size(); ++i) ip_ok[i] = parse(parsed[i], std::vector<std::string>{rx[i]});
+    const auto got2 = eng.unwrap(Bgpu2, parsed);
+    size_t accepted = 0;
+    for (size_t i = 0; i < rx.size(); ++i) {
+        TCPSegment seg;
+        const bool tcp_ok = parse(seg, parsed[i].payload, parsed[i].header.pseudo_checksum());
+        EXPECT(((st[i] & ICS_ST_IPV4_OK) != 0) == ip_ok[i]);
+        EXPECT(((st[i] & (ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) == (ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) ==
+               tcp_ok);
+        const auto want = ip_ok[i] ? Bcpu.unwrap_tcp_in_ip(parsed[i]) : std::optional<TCPMessage>{};
+        EXPECT(got[i].has_value() == want.has_value());
+        if (ip_ok[i]) EXPECT(got2[i].has_value() == want.has_value());
+        if (want) {
+            ++accepted;
+            EXPECT(got[i]->sender.payload == want->sender.payload);
+            EXPECT(got[i]->sender.SYN == want->sender.SYN && got[i]->sender.FIN == want->sender.FIN);
+        }
+    }
+    EXPECT(accepted >= wires.size() / 2);
+    std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
+                segs.size(), msgs.size(), rx.size(), accepted);
+    return failures ? 1 : 0;
+}

@@ -1,0 +1,118 @@
+// host_selftest.cpp — CPU checks of the drop-in types, driven line by line by
+// tests/test_host_cpp.py with the golden fixtures of the real reference.
+//   kat INIT HEX...                -> value (add(vector<string>) == add(vector<string_view>))
+//   ipv4 HEX                       -> "ok computed pseudo" from IPv4Header::parse
+//   tcpv HEX                       -> "ip_ok tcp_ok tcp_value ip_computed proto" (datagram parse path)
+//   wrap SRC SPORT DST DPORT SEQ SYN FIN RST HASACK ACK WIN PAYLOADHEX -> wire hex
+//   unwrap SRC SPORT DST DPORT HEX -> "1" if the adapter (source=SRC:SPORT) accepts, else "0"
+#include <cstdio>
+#include <iostream>
+#include <sstream>
+#include <string>
+#include <vector>
+
+#include "checksum.h"
+#include "ipv4_datagram.h"
+#include "parser.h"
+#include "tcp_over_ip.h"
+#include "tcp_segment.h"
+
+namespace {
+std::string unhex(const std::string& h)
+{
+    std::string s(h.size() / 2, '\0');
+    for (size_t i = 0; i < s.size(); ++i) s[i] = static_cast<char>(std::stoi(h.substr(2 * i, 2), nullptr, 16));
+    return s;
+}
+std::string tohex(const std::string& s)
+{
+    static const char* d = "0123456789abcdef";
+    std::string r;
+    for (unsigned char c : s) {
+        r.push_back(d[c >> 4]);
+        r.push_back(d[c & 15]);
+    }
+    return r;
+}
+std::string joined(const std::vector<std::string>& v)
+{
+    std::string r;
+    for (auto& s : v) r += s;
+    return r;
+}
+std::string ipstr(uint32_t a) { return Address::from_ipv4_numeric(a).ip(); }
+}  // namespace
+
+int main()
+{
+    std::string line;
+    while (std::getline(std::cin, line)) {
+        std::istringstream in(line);
+        std::string cmd;
+        in >> cmd;
+        if (cmd == "kat") {
+            uint64_t init = 0;
+            in >> init;
+            std::vector<std::string> pieces;
+            std::string h;
+            while (in >> h) pieces.push_back(h == "-" ? std::string{} : unhex(h));
+            InternetChecksum a{static_cast<uint32_t>(init)}, b{static_cast<uint32_t>(init)};
+            a.add(pieces);
+            std::vector<std::string_view> views(pieces.begin(), pieces.end());
+            b.add(views);
+            if (a.value() != b.value()) return 2;
+            std::cout << a.value() << "\n";
+        } else if (cmd == "ipv4") {
+            std::string h;
+            in >> h;
+            IPv4Header hd;
+            const bool ok = parse(hd, std::vector<std::string>{unhex(h)});
+            std::cout << ok << " " << hd.cksum << " " << (hd.ver == 4 ? hd.pseudo_checksum() : 0u) << "\n";
+        } else if (cmd == "tcpv") {
+            std::string h;
+            in >> h;
+            IPv4Datagram dg;
+            const bool ip_ok = parse(dg, std::vector<std::string>{unhex(h)});
+            TCPSegment seg;
+            const uint32_t pseudo = dg.header.pseudo_checksum();
+            const bool tcp_ok = parse(seg, dg.payload, pseudo);
+            InternetChecksum c{pseudo};
+            c.add(dg.payload);
+            std::cout << ip_ok << " " << tcp_ok << " " << c.value() << " " << dg.header.cksum << " "
+                      << +dg.header.proto << "\n";
+        } else if (cmd == "wrap") {
+            uint32_t src, dst, seq, ack;
+            unsigned sport, dport, syn, fin, rst, has_ack, win;
+            std::string ph;
+            in >> src >> sport >> dst >> dport >> seq >> syn >> fin >> rst >> has_ack >> ack >> win >> ph;
+            TCPOverIPv4Adapter A;
+            A.config_mut().source = Address{ipstr(src), static_cast<uint16_t>(sport)};
+            A.config_mut().destination = Address{ipstr(dst), static_cast<uint16_t>(dport)};
+            TCPMessage m;
+            m.sender.seqno = Wrap32{seq};
+            m.sender.SYN = syn;
+            m.sender.FIN = fin;
+            m.sender.RST = rst;
+            m.sender.payload = ph == "-" ? std::string{} : unhex(ph);
+            if (has_ack) m.receiver.ackno = Wrap32{ack};
+            m.receiver.window_size = static_cast<uint16_t>(win);
+            std::cout << tohex(joined(serialize(A.wrap_tcp_in_ip(m)))) << "\n";
+        } else if (cmd == "unwrap") {
+            uint32_t src, dst;
+            unsigned sport, dport;
+            std::string h;
+            in >> src >> sport >> dst >> dport >> h;
+            TCPOverIPv4Adapter B;
+            B.config_mut().source = Address{ipstr(src), static_cast<uint16_t>(sport)};
+            B.config_mut().destination = Address{ipstr(dst), static_cast<uint16_t>(dport)};
+            IPv4Datagram dg;
+            bool ok = parse(dg, std::vector<std::string>{unhex(h)});
+            ok = ok && B.unwrap_tcp_in_ip(dg).has_value();
+            std::cout << ok << "\n";
+        } else if (!cmd.empty()) {
+            std::cerr << "unknown command " << cmd << "\n";
+            return 1;
+        }
+    }
+    return 0;
+}
