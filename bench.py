@@ -34,10 +34,13 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level par
 KERNEL_PREFIX = "k_checksum"
 
 WORKLOADS = {
-    # name: (segments per rank, segment bytes, seed) — DESIGN.md §Workload spec
-    "ns_1Mx1500": (1 << 20, 1500, 0x10710000),
-    "tcp_1Mx64": (1 << 20, 64, 0x10710003),
-    "jumbo_1Mx9000": (1 << 20, 9000, 0x10710005),
+    # name: (segments, segment bytes, seed, scaling) — DESIGN.md §Workload spec.
+    # "weak": `segments` per rank (the global batch grows with N);
+    # "strong": `segments` in total, sharded across the N ranks.
+    "ns_1Mx1500": (1 << 20, 1500, 0x10710000, "weak"),
+    "tcp_1Mx64": (1 << 20, 64, 0x10710003, "weak"),
+    "jumbo_1Mx9000": (1 << 20, 9000, 0x10710005, "weak"),
+    "jumbo_8Mx9000": (8 << 20, 9000, 0x10710005, "strong"),  # BASELINE config 5
 }
 
 
@@ -130,7 +133,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    n, seg, seed = WORKLOADS[args.workload]
+    n_cfg, seg, seed, scaling = WORKLOADS[args.workload]
 
     # the PMC child pass runs before this process touches the GPU
     traffic, traffic_src = (None, "skipped")
@@ -142,17 +145,29 @@ def main():
 
     from tcpip_network_protocol_stack_amd.engine import Engine
 
+    # one process per GPU; ICSUM_DIST_BACKEND=gloo rehearses N ranks on fewer
+    # GPUs (ranks then share a card: local % device_count)
+    backend = os.environ.get("ICSUM_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
+    from tcpip_network_protocol_stack_amd import shard
+
     eng = Engine(local)
-    # rank r owns global segments [r*n, (r+1)*n) of one spec stream
-    data = torch.empty(n * seg, dtype=torch.uint8, device=dev)
-    eng.fill_bytes(data, seed, pos0=rank * n * seg)
-    init = eng.pseudo_inits(n, seed, seg_len=seg, index0=rank * n)
+    # rank r owns a contiguous range of global segments of ONE spec stream
+    n_total = n_cfg * world if scaling == "weak" else n_cfg
+    sh = shard.fixed_stride_shard(n_total, seg, seg, rank, world)
+    n = sh.n
+    data = torch.empty(sh.nbytes, dtype=torch.uint8, device=dev)
+    eng.fill_bytes(data, seed, pos0=sh.byte0)
+    init = eng.pseudo_inits(n, seed, seg_len=seg, index0=sh.index0)
     out = torch.empty(n, dtype=torch.int16, device=dev)
     stream = torch.cuda.current_stream(dev)
 
@@ -192,14 +207,12 @@ def main():
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # average launch duration
+    elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None,
+                                   dev if backend == "nccl" else torch.device("cpu"))
+    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # average launch duration (this rank)
 
     bytes_step = n * seg  # algorithmic bytes per rank per step (each byte read once)
-    value = world * bytes_step * args.steps / elapsed / 2**30
+    value = n_total * seg * args.steps / elapsed / 2**30  # all ranks' bytes / max-over-ranks time
     achieved = bytes_step / kern_s / 1e9  # GB/s, decimal like the 8 TB/s peak
 
     head = out[:4096].cpu().numpy().view(np.uint16).copy()
@@ -217,11 +230,12 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (seeded splitmix64 spec, DESIGN.md §Workload spec)",
-            "config": {"workload": args.workload, "segments_per_gpu": n, "segment_bytes": seg,
+            "config": {"workload": args.workload, "segments_total": n_total, "segments_per_gpu": n,
+                       "segment_bytes": seg,
                        "bytes_per_step_per_gpu": bytes_step, "inits": "IPv4 pseudo-header sums",
                        "entry": "ics_checksum_batch", "parallelism": f"shard{world}"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
