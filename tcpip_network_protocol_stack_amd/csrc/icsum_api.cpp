@@ -59,7 +59,7 @@ struct ics_ctx {
   int device = 0;
   void* d_zero = nullptr;  // 16 zero bytes (icsum::SegSpec::zero16)
   uint32_t max_blocks = 0;  // 0 = one lane group per segment (no grid-stride cap)
-  int force_lps = 0, force_unroll = 0, force_nt = -1, force_mode = -1;
+  int force_lps = 0, force_unroll = 0, force_nt = -1, force_mode = -1, force_segs = 0;
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
   static constexpr size_t kSlotBytes = size_t(64) << 20;
@@ -88,10 +88,20 @@ int bind(ics_ctx* ctx) {
 
 icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
   icsum::Geometry g = icsum::pick_geometry(avg_len);
-  if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll, g.nt, g.mode};
+  if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll, g.nt, g.mode, 1};
   if (ctx->force_nt >= 0) g.nt = ctx->force_nt != 0;
   if (ctx->force_mode >= 0) g.mode = ctx->force_mode;
+  if (ctx->force_segs > 0) g.segs = ctx->force_segs;
   if (!icsum::geometry_supported(g)) g = icsum::pick_geometry(avg_len);
+  return g;
+}
+
+// the fused IPv4 kernel has no small-segment (multi-segment) variant: use the
+// one-segment kernel of the same lane shape
+icsum::Geometry ipv4_geometry(icsum::Geometry g) {
+  g.segs = 1;
+  if (!icsum::geometry_supported(g)) g.mode = 0;
+  if (!icsum::geometry_supported(g)) g = {64, 8, true, 1, 1};
   return g;
 }
 
@@ -260,7 +270,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       uint16_t* a = reinterpret_cast<uint16_t*>(ctx->d_out[slot]);
       uint16_t* b = a + m;
       uint8_t* s = ctx->d_out[slot] + m * 4;
-      ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, a, b, s, g, ctx->max_blocks, st));
+      ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, a, b, s, ipv4_geometry(g), ctx->max_blocks, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 5, hipMemcpyDeviceToHost, st));
       if (mode == ICS_MODE_PATCH)
         ICS_HIP(hipMemcpyAsync(direct ? static_cast<uint8_t*>(h_bytes) + c.b0 : ctx->h_in[slot], ctx->d_in[slot],
@@ -316,6 +326,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->force_unroll = int(env_u32("ICSUM_UNROLL", 0));
   ctx->force_nt = std::getenv("ICSUM_NT") ? int(env_u32("ICSUM_NT", 1)) : -1;
   ctx->force_mode = std::getenv("ICSUM_MODE") ? int(env_u32("ICSUM_MODE", 0)) : -1;
+  ctx->force_segs = int(env_u32("ICSUM_SEGS", 0));
   *out = ctx;
   return ICS_OK;
 }
@@ -378,7 +389,7 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   if (n == 0) return ICS_OK;
   if (!d_dgrams) return fail(ICS_ERR_INVALID, "null datagram buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
-  const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, dgram_len, n, 0));
+  const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, avg_len_hint(d_offsets, dgram_len, n, 0)));
   ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks,
                                  static_cast<hipStream_t>(stream)));
   return ICS_OK;

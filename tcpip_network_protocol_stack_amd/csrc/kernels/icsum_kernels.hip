@@ -80,6 +80,88 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
   }
 }
 
+// Small segments (a few 16-byte chunks): a lane group owns SEGS segments per
+// pass and issues the first LPS*UNROLL chunk loads of ALL of them before any
+// is consumed, so a wave keeps SEGS times the bytes in flight of the
+// one-segment kernel (small segments are latency-bound, not VALU-bound).
+// Instruction k of a wave covers 64/LPS consecutive segments, i.e. one
+// contiguous 1 KiB run for 64-byte segments.  Every slot is masked to its
+// segment (range_sums_masked semantics); a segment longer than LPS*UNROLL
+// chunks finishes in a loop.  Absent per-segment arrays: zero16 + step 0.
+template <int LPS, int UNROLL, int SEGS, int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __restrict__ bytes,
+                                                           const uint64_t* __restrict__ offsets,
+                                                           uint64_t stride, uint64_t seg_len,
+                                                           const uint32_t* __restrict__ init,
+                                                           uint32_t init_step,
+                                                           const uint8_t* __restrict__ odd,
+                                                           uint32_t odd_step,
+                                                           const u32x4* __restrict__ zero16,
+                                                           void* __restrict__ out, uint64_t n) {
+  constexpr uint32_t kGroups = kBlock / LPS;
+  constexpr uint32_t kSlots = LPS * UNROLL;
+  const uint32_t lane = threadIdx.x & (LPS - 1);
+  const uint32_t group = threadIdx.x / LPS;
+  const uint64_t step = uint64_t(gridDim.x) * kGroups * SEGS;
+  for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups * SEGS; g0 < n; g0 += step) {
+    uint64_t s[SEGS], span[SEGS];
+    uint32_t nch[SEGS], i0[SEGS], swap[SEGS];
+    u32x4 v[SEGS][UNROLL];
+#pragma unroll
+    for (int k = 0; k < SEGS; ++k) {
+      const uint64_t seg = g0 + uint64_t(k) * kGroups + group;
+      const bool valid = seg < n;
+      uint64_t e = 0;
+      s[k] = 0;
+      if (valid) seg_bounds(offsets, stride, seg_len, seg, s[k], e);
+      const uint64_t a0 = s[k] & ~uint64_t(15);
+      span[k] = e > s[k] ? e - a0 : 0;
+      nch[k] = uint32_t((span[k] + 15) >> 4);
+      const uint64_t cseg = valid ? seg : n - 1;
+      i0[k] = init[cseg * init_step];
+      swap[k] = (uint32_t(s[k]) ^ uint32_t(odd[cseg * odd_step])) & 1u;
+      const u32x4* p = reinterpret_cast<const u32x4*>(bytes + a0);
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const uint32_t cc = lane + uint32_t(u * LPS);
+        // unconditional load from a valid address (empty segment -> zero16)
+        const u32x4* q = nch[k] ? p + (cc < nch[k] ? cc : nch[k] - 1) : zero16;
+        v[k][u] = __builtin_nontemporal_load(q);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < SEGS; ++k) {
+      uint32_t ev = 0, od = 0;
+      const uint32_t lo0 = uint32_t(s[k]) & 15u;
+#pragma unroll
+      for (int u = 0; u < UNROLL; ++u) {
+        const uint32_t cc = lane + uint32_t(u * LPS);
+        const uint64_t at = uint64_t(cc) << 4;
+        const uint32_t lo = cc == 0 ? lo0 : 0u;
+        const uint32_t hi = at >= span[k] ? 0u : (span[k] - at >= 16 ? 16u : uint32_t(span[k] - at));
+        acc_chunk(v[k][u] & byte_range_mask(lo, hi), ev, od);
+      }
+      if (nch[k] > kSlots) {  // long segment: the rest, masked (rare in this kernel's range)
+        const u32x4* p = reinterpret_cast<const u32x4*>(bytes + (s[k] & ~uint64_t(15)));
+        for (uint32_t cc = lane + kSlots; cc < nch[k]; cc += LPS) {
+          const uint64_t at = uint64_t(cc) << 4;
+          const uint32_t hi = span[k] - at >= 16 ? 16u : uint32_t(span[k] - at);
+          acc_chunk(__builtin_nontemporal_load(p + cc) & byte_range_mask(0u, hi), ev, od);
+        }
+      }
+      const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, swap[k]));
+      const uint64_t seg = g0 + uint64_t(k) * kGroups + group;
+      if (seg < n && lane == LPS - 1) {
+        const uint32_t sum = i0[k] + tot;
+        if (OUT == 0)
+          static_cast<uint16_t*>(out)[seg] = fold_value(sum);
+        else
+          static_cast<uint32_t*>(out)[seg] = sum;
+      }
+    }
+  }
+}
+
 // HSA dispatch packets carry the grid size in work-items as a uint32, so
 // element-wise kernels use a capped grid and stride over the rest.
 #define ICS_GRID_STRIDE(i, n) \
@@ -368,6 +450,23 @@ hipError_t launch_checksum_t(const SegSpec& sp, const uint32_t* init, const uint
   return hipGetLastError();
 }
 
+template <int LPS, int UNROLL, int SEGS>
+hipError_t launch_checksum_small_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
+                                   int out_kind, uint32_t max_blocks, hipStream_t st) {
+  const uint32_t blocks = blocks_for((sp.n + SEGS - 1) / SEGS, kBlock / LPS, max_blocks);
+  const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
+  const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
+  const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
+  const u32x4* z = static_cast<const u32x4*>(sp.zero16);
+  if (out_kind == 0)
+    hipLaunchKernelGGL((k_checksum_small<LPS, UNROLL, SEGS, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
+                       sp.offsets, sp.stride, sp.seg_len, ip, is, op, os, z, out, sp.n);
+  else
+    hipLaunchKernelGGL((k_checksum_small<LPS, UNROLL, SEGS, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
+                       sp.offsets, sp.stride, sp.seg_len, ip, is, op, os, z, out, sp.n);
+  return hipGetLastError();
+}
+
 template <int LPS, int UNROLL, bool NT, int MODE>
 hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                          uint8_t* status, uint32_t max_blocks, hipStream_t st) {
@@ -381,22 +480,22 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
 }  // namespace
 
 // Geometry choice from the (average) segment length, measured on MI355X
-// (tools/sweep_geometry.py; profiles/r1_sweep_geometry.jsonl and
-// profiles/r1_sweep_line_grid.jsonl).  Small segments: about one load slot
-// (LPS * UNROLL) per interior 16-byte chunk on a 16-byte grid, so a 64-byte
-// segment is 4 lanes x 1 load.  From ~270 bytes up: the 128-byte-line grid
+// (tools/sweep_geometry.py; profiles/r1_sweep_geometry.jsonl,
+// r1_sweep_line_grid.jsonl, r1_sweep_small.jsonl).  Small segments
+// (<= ~270 B): k_checksum_small with about one load slot per 16-byte chunk
+// and 2 segments per lane group in flight (64 B = 4 lanes x 1 load x 2).  From ~270 bytes up: the 128-byte-line grid
 // (range_sums_line) with slots >= chunks + 8 so one step covers a segment
 // (1500 B -> 16 lanes x 8 loads), and 64 x 8 (8 KiB per wave step) looping
 // for long segments.  Non-temporal loads everywhere (stream-once data).
 Geometry pick_geometry(uint64_t avg_len) {
   const uint64_t m = (avg_len + 15) / 16;  // 16-byte chunks of the payload
-  if (m <= 5) return {4, 1, true, 0};
-  if (m <= 9) return {4, 2, true, 0};
-  if (m <= 17) return {8, 2, true, 0};
-  if (m <= 56) return {16, 4, true, 1};
-  if (m <= 120) return {16, 8, true, 1};
-  if (m <= 256) return {32, 4, true, 1};
-  return {64, 8, true, 1};
+  if (m <= 5) return {4, 1, true, 2, 2};   // small-segment kernel, 2 segments per group in flight
+  if (m <= 9) return {4, 2, true, 2, 2};
+  if (m <= 17) return {8, 2, true, 2, 2};
+  if (m <= 56) return {16, 4, true, 1, 1};
+  if (m <= 120) return {16, 8, true, 1, 1};
+  if (m <= 256) return {32, 4, true, 1, 1};
+  return {64, 8, true, 1, 1};
 }
 
 // every instantiated (LPS, UNROLL, NT) triple
@@ -410,8 +509,20 @@ Geometry pick_geometry(uint64_t avg_len) {
   X(1, 4, true, 2) X(1, 8, true, 2) X(2, 4, true, 2) X(4, 1, true, 2) X(4, 2, true, 2)     \
   X(8, 1, true, 2) X(8, 2, true, 2) X(16, 2, true, 2)
 
+// small-segment kernel instantiations (LPS, UNROLL, SEGS); Geometry::segs > 1
+#define ICS_SMALL_GEOMETRIES(X) \
+  X(4, 1, 2) X(4, 1, 4) X(4, 1, 8) X(4, 2, 2) X(4, 2, 4) X(8, 1, 4) X(8, 2, 2) X(8, 2, 4) X(16, 2, 2)
+
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st) {
+  if (g.segs > 1) {
+#define ICS_SMALL(L, U, K)                                                            \
+  if (g.lps == L && g.unroll == U && g.segs == K)                                     \
+    return launch_checksum_small_t<L, U, K>(sp, init, odd, out, out_kind, max_blocks, st);
+    ICS_SMALL_GEOMETRIES(ICS_SMALL)
+#undef ICS_SMALL
+    return hipErrorInvalidValue;
+  }
 #define ICS_CASE(L, U, T, A)                                      \
   if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
     return launch_checksum_t<L, U, T, A>(sp, init, odd, out, out_kind, max_blocks, st);
@@ -431,6 +542,13 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 }
 
 bool geometry_supported(Geometry g) {
+  if (g.segs > 1) {
+#define ICS_SMALL(L, U, K) \
+  if (g.lps == L && g.unroll == U && g.segs == K) return true;
+    ICS_SMALL_GEOMETRIES(ICS_SMALL)
+#undef ICS_SMALL
+    return false;
+  }
 #define ICS_CASE(L, U, T, A) \
   if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A) return true;
   ICS_GEOMETRIES(ICS_CASE)

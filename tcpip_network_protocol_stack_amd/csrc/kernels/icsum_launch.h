@@ -14,6 +14,7 @@ struct Geometry {
   int unroll;
   bool nt;   // non-temporal loads
   int mode;  // chunk grid: 0 16-byte + boundary slot, 1 128-byte line, 2 16-byte all masked
+  int segs = 1;  // > 1: small-segment kernel, SEGS segments per lane group in flight
 };
 
 // Pick a geometry from the (average) segment length in bytes.

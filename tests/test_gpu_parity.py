@@ -22,6 +22,9 @@ GEOMETRIES = [(1, 4, 0), (1, 8, 0), (2, 4, 0), (4, 1, 0), (4, 2, 0), (8, 2, 0), 
               (64, 8, 0), (8, 4, 1), (16, 4, 1), (16, 6, 1), (16, 8, 1), (32, 3, 1), (32, 4, 1),
               (64, 4, 1), (64, 8, 1), (1, 4, 2), (1, 8, 2), (2, 4, 2), (4, 1, 2), (4, 2, 2), (8, 1, 2),
               (8, 2, 2), (16, 2, 2)]
+# small-segment kernel (k_checksum_small): (LPS, UNROLL, MODE unused, SEGS) — ICS_SMALL_GEOMETRIES
+SMALL_GEOMETRIES = [(4, 1, 0, 2), (4, 1, 0, 4), (4, 1, 0, 8), (4, 2, 0, 2), (4, 2, 0, 4), (8, 1, 0, 4),
+                    (8, 2, 0, 2), (8, 2, 0, 4), (16, 2, 0, 2)]
 
 
 _SIGNED = {np.dtype(np.uint16): np.int16, np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
@@ -49,19 +52,20 @@ def _sha(a):
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 
 
-@pytest.fixture(scope="module", params=GEOMETRIES, ids=lambda g: f"lps{g[0]}x{g[1]}m{g[2]}")
+@pytest.fixture(scope="module", params=GEOMETRIES + SMALL_GEOMETRIES,
+                ids=lambda g: f"lps{g[0]}x{g[1]}m{g[2]}" + (f"s{g[3]}" if len(g) > 3 else ""))
 def geo_engine(request):
-    """An engine per lane-group geometry (forced through ICSUM_LPS/UNROLL/LINE)."""
+    """An engine per lane-group geometry (forced through ICSUM_LPS/UNROLL/MODE/SEGS)."""
     import torch
 
     from tcpip_network_protocol_stack_amd.engine import Engine
 
-    keys = ("ICSUM_LPS", "ICSUM_UNROLL", "ICSUM_MODE")
-    os.environ.update(dict(zip(keys, map(str, request.param))))
+    env = dict(zip(("ICSUM_LPS", "ICSUM_UNROLL", "ICSUM_MODE", "ICSUM_SEGS"), map(str, request.param)))
+    os.environ.update(env)
     try:
         eng = Engine(0)
     finally:
-        for k in keys:
+        for k in env:
             del os.environ[k]
     yield eng
     torch.cuda.synchronize()

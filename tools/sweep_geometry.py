@@ -24,9 +24,9 @@ WL = {"ns": (1 << 20, 1500), "tcp64": (1 << 20, 64), "jumbo": (1 << 20, 9000), "
       "s128": (1 << 20, 128), "s256": (1 << 20, 256), "s576": (1 << 20, 576), "s3000": (1 << 19, 3000)}
 
 
-def make_engine(lps, unroll, nt, line, cap):
+def make_engine(lps, unroll, nt, line, segs, cap):
     env = {"ICSUM_LPS": str(lps), "ICSUM_UNROLL": str(unroll), "ICSUM_NT": str(int(nt)),
-           "ICSUM_MODE": str(int(line)), "ICSUM_MAX_BLOCKS": str(cap)}
+           "ICSUM_MODE": str(int(line)), "ICSUM_SEGS": str(segs), "ICSUM_MAX_BLOCKS": str(cap)}
     old = {k: os.environ.get(k) for k in env}
     os.environ.update(env)
     try:
@@ -47,9 +47,13 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
-    # LPSxUNROLLxNT[xMODE]
-    variants = [tuple(int(x) for x in (v + "x0").split("x")[:4]) for v in args.variants.split(",") if v] or [
-        (16, 6, 1, 0), (16, 6, 1, 1), (32, 3, 1, 0), (32, 3, 1, 1), (64, 8, 1, 0), (64, 8, 1, 1)]
+    # LPSxUNROLLxNT[xMODE[xSEGS]]
+    def parse_variant(v):
+        parts = [int(x) for x in v.split("x")]
+        return tuple(parts + [1, 0, 1][len(parts) - 2:])[:5]  # defaults: NT 1, MODE 0, SEGS 1
+
+    variants = [parse_variant(v) for v in args.variants.split(",") if v] or [
+        (16, 6, 1, 0, 1), (16, 8, 1, 1, 1), (32, 4, 1, 1, 1), (64, 8, 1, 1, 1)]
     caps = [int(c) for c in args.caps.split(",")]
     base = Engine(0)
     for wl in args.workloads.split(","):
@@ -67,8 +71,8 @@ def main():
         ref = base.checksum_batch(data, n=n, offsets=doff, stride=L or 0, seg_len=L or 0, init=init)
         torch.cuda.synchronize()
         engines = {}
-        for (lps, u, nt, line), cap in itertools.product(variants, caps):
-            engines[(lps, u, nt, line, cap)] = make_engine(lps, u, nt, line, cap)
+        for (lps, u, nt, line, segs), cap in itertools.product(variants, caps):
+            engines[(lps, u, nt, line, segs, cap)] = make_engine(lps, u, nt, line, segs, cap)
         times = {k: [] for k in engines}
         st = torch.cuda.current_stream()
         for r in range(args.rounds):
@@ -85,7 +89,7 @@ def main():
                     assert torch.equal(out, ref), f"variant {k} mismatch"
         for k, ts in times.items():
             med = statistics.median(ts)
-            print(json.dumps({"workload": wl, "lps": k[0], "unroll": k[1], "nt": k[2], "mode": k[3], "cap": k[4],
+            print(json.dumps({"workload": wl, "lps": k[0], "unroll": k[1], "nt": k[2], "mode": k[3], "segs": k[4], "cap": k[5],
                               "med_us": round(med * 1e6, 1), "med_GBs": round(total / med / 1e9, 1),
                               "best_GBs": round(total / min(ts) / 1e9, 1)}), flush=True)
         for e in engines.values():
