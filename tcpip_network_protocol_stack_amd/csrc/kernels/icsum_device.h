@@ -172,6 +172,52 @@ __device__ __forceinline__ void range_sums_line(const uint8_t* __restrict__ base
   }
 }
 
+// Line-anchored grid with the two boundary chunks loaded FIRST, with the
+// default (cache-allocating) policy, by lanes 0 (head) and 1 (tail) of the
+// group; the slot loop then streams only the interior chunks non-temporally
+// and unmasked (a keep mask per slot, no per-slot copies).  The boundary lines
+// are the ones a neighbouring segment also touches: kept in L2 they are read
+// from HBM once.
+template <int LPS, int UNROLL, bool NT>
+__device__ __forceinline__ void range_sums_line_primed(const uint8_t* __restrict__ base, uint64_t s,
+                                                       uint64_t e, uint32_t lane, uint32_t& ev,
+                                                       uint32_t& od) {
+  const uint64_t a0 = s & ~uint64_t(127);
+  const uint64_t span = e > s ? e - a0 : 0;
+  const uint32_t nch = uint32_t((span + 15) >> 4);
+  const uint32_t cs = uint32_t(s - a0) >> 4;  // head chunk (0..7)
+  const uint32_t lastc = nch ? nch - 1 : 0u;  // tail chunk
+  const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  const uint32_t tail = nch ? uint32_t(span - (uint64_t(lastc) << 4)) : 0u;
+  u32x4 bnd = {0u, 0u, 0u, 0u};
+  uint32_t blo = 0, bhi = 0;
+  if (nch) {
+    const bool is_tail = (LPS == 1 ? false : lane == 1) && lastc != cs;
+    bnd = load16<false>(p + (is_tail ? lastc : cs));
+    blo = is_tail ? 0u : (uint32_t(s) & 15u);
+    bhi = (is_tail || lastc == cs) ? tail : 16u;
+    if (LPS > 1 && (lane >= 2 || (lane == 1 && lastc == cs))) bhi = 0u;
+  }
+  u32x4 bt = {0u, 0u, 0u, 0u};
+  if (LPS == 1 && nch && lastc != cs) bt = load16<false>(p + lastc);
+  for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      v[u] = load16<NT>(p + (cc < lastc ? cc : lastc));
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      const uint32_t keep = (cc > cs && cc < lastc) ? ~0u : 0u;
+      acc_chunk(v[u] & keep, ev, od);
+    }
+  }
+  acc_chunk(bnd & byte_range_mask(blo, bhi), ev, od);
+  if (LPS == 1) acc_chunk(bt & byte_range_mask(0u, tail), ev, od);
+}
+
 // Fully masked variant on the 16-byte grid: slot u of lane l is chunk
 // l + u*LPS of [s & ~15, e), every slot masked to [s, e).  One load per
 // useful chunk with no separate boundary instruction: the cheapest shape for
@@ -205,12 +251,15 @@ __device__ __forceinline__ void range_sums_masked(const uint8_t* __restrict__ ba
 }
 
 // Chunk-grid modes (Geometry::mode): 0 = 16-byte grid, interior unmasked +
-// boundary instruction; 1 = 128-byte-line grid; 2 = 16-byte grid, all masked.
+// boundary instruction; 1 = 128-byte-line grid; 2 = 16-byte grid, all masked;
+// 3 = 128-byte-line grid with default-policy boundary loads issued first.
 template <int LPS, int UNROLL, bool NT, int MODE>
 __device__ __forceinline__ void seg_sums(const uint8_t* __restrict__ base, uint64_t s, uint64_t e,
                                          uint32_t lane, uint32_t& ev, uint32_t& od) {
   if (MODE == 1)
     range_sums_line<LPS, UNROLL, NT>(base, s, e, lane, ev, od);
+  else if (MODE == 3)
+    range_sums_line_primed<LPS, UNROLL, NT>(base, s, e, lane, ev, od);
   else if (MODE == 2)
     range_sums_masked<LPS, UNROLL, NT>(base, s, e, lane, ev, od);
   else

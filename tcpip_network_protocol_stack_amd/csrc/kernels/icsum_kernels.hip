@@ -483,19 +483,21 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
 // (tools/sweep_geometry.py; profiles/r1_sweep_geometry.jsonl,
 // r1_sweep_line_grid.jsonl, r1_sweep_small.jsonl).  Small segments
 // (<= ~270 B): k_checksum_small with about one load slot per 16-byte chunk
-// and 2 segments per lane group in flight (64 B = 4 lanes x 1 load x 2).  From ~270 bytes up: the 128-byte-line grid
-// (range_sums_line) with slots >= chunks + 8 so one step covers a segment
-// (1500 B -> 16 lanes x 8 loads), and 64 x 8 (8 KiB per wave step) looping
-// for long segments.  Non-temporal loads everywhere (stream-once data).
+// and 2 segments per lane group in flight (64 B = 4 lanes x 1 load x 2).
+// From ~270 bytes up: the 128-byte-line grid with default-policy boundary
+// loads first (mode 3, range_sums_line_primed; profiles/r1_sweep_primed.jsonl)
+// with slots >= chunks + 8 so one step covers a segment (1500 B -> 16 lanes x
+// 8 loads), and 64 x 8 (8 KiB per wave step) looping for long segments.
+// Interior chunks stream non-temporally (read once).
 Geometry pick_geometry(uint64_t avg_len) {
   const uint64_t m = (avg_len + 15) / 16;  // 16-byte chunks of the payload
   if (m <= 5) return {4, 1, true, 2, 2};   // small-segment kernel, 2 segments per group in flight
   if (m <= 9) return {4, 2, true, 2, 2};
   if (m <= 17) return {8, 2, true, 2, 2};
-  if (m <= 56) return {16, 4, true, 1, 1};
-  if (m <= 120) return {16, 8, true, 1, 1};
-  if (m <= 256) return {32, 4, true, 1, 1};
-  return {64, 8, true, 1, 1};
+  if (m <= 56) return {16, 4, true, 3, 1};
+  if (m <= 120) return {16, 8, true, 3, 1};
+  if (m <= 256) return {32, 4, true, 3, 1};
+  return {64, 8, true, 3, 1};
 }
 
 // every instantiated (LPS, UNROLL, NT) triple
@@ -507,7 +509,8 @@ Geometry pick_geometry(uint64_t avg_len) {
   X(8, 4, true, 1) X(16, 4, true, 1) X(16, 6, true, 1) X(16, 8, true, 1) X(32, 3, true, 1) \
   X(32, 4, true, 1) X(64, 4, true, 1) X(64, 8, true, 1) X(16, 6, false, 1)                 \
   X(1, 4, true, 2) X(1, 8, true, 2) X(2, 4, true, 2) X(4, 1, true, 2) X(4, 2, true, 2)     \
-  X(8, 1, true, 2) X(8, 2, true, 2) X(16, 2, true, 2)
+  X(8, 1, true, 2) X(8, 2, true, 2) X(16, 2, true, 2) X(16, 8, false, 1) X(64, 8, false, 1)    \
+  X(16, 8, true, 3) X(32, 4, true, 3) X(64, 8, true, 3) X(16, 4, true, 3)
 
 // small-segment kernel instantiations (LPS, UNROLL, SEGS); Geometry::segs > 1
 #define ICS_SMALL_GEOMETRIES(X) \
