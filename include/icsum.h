@@ -150,6 +150,10 @@ int ics_ipv4_tcp_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offs
 /* ---- device memory helpers for FFI callers without an allocator -------- */
 int ics_malloc(ics_ctx* ctx, void** d_ptr, size_t bytes);
 int ics_free(ics_ctx* ctx, void* d_ptr);
+/* Page-locked host memory: batches in it are DMA'd by the *_host calls with
+ * no staging copy (the receive/transmit rings of a batched TUN/socket path). */
+int ics_host_alloc(ics_ctx* ctx, void** h_ptr, size_t bytes);
+int ics_host_free(ics_ctx* ctx, void* h_ptr);
 int ics_memcpy_htod(ics_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, void* stream);
 int ics_memcpy_dtoh(ics_ctx* ctx, void* h_dst, const void* d_src, size_t bytes, void* stream);
 int ics_stream_synchronize(ics_ctx* ctx, void* stream);

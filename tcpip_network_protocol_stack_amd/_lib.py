@@ -38,6 +38,8 @@ SIGNATURES = {
     "ics_ipv4_tcp_batch_host": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p]),
     "ics_malloc": (_int, [_p, ctypes.POINTER(_p), ctypes.c_size_t]),
     "ics_free": (_int, [_p, _p]),
+    "ics_host_alloc": (_int, [_p, ctypes.POINTER(_p), ctypes.c_size_t]),
+    "ics_host_free": (_int, [_p, _p]),
     "ics_memcpy_htod": (_int, [_p, _p, _p, ctypes.c_size_t, _p]),
     "ics_memcpy_dtoh": (_int, [_p, _p, _p, ctypes.c_size_t, _p]),
     "ics_stream_synchronize": (_int, [_p, _p]),

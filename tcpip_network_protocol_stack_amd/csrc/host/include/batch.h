@@ -50,6 +50,17 @@ class BatchEngine
     std::vector<std::optional<TCPMessage>> unwrap_raw(TCPOverIPv4Adapter& adapter,
                                                       std::span<const std::string_view> wires);
 
+    // the same operations on an already packed batch (bytes + n+1 offsets),
+    // e.g. a DatagramBatch arena in page-locked memory: no packing copy
+    std::vector<uint8_t> verify_packed(const uint8_t* bytes, const uint64_t* offsets, size_t n);
+    void patch_packed(uint8_t* bytes, const uint64_t* offsets, size_t n);  // compute + store both checksums
+    std::vector<std::optional<TCPMessage>> unwrap_packed(TCPOverIPv4Adapter& adapter, const uint8_t* bytes,
+                                                         const uint64_t* offsets, size_t n);
+
+    // page-locked host memory from the engine's device runtime
+    void* host_alloc(size_t bytes);
+    void host_free(void* p);
+
     int device() const { return device_; }
 
   private:

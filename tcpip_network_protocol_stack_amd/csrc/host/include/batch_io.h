@@ -1,0 +1,72 @@
+// batch_io.h — batched datagram I/O for the engine.
+//
+// The reference reads one datagram per syscall into {20 B, 16 KiB} buffers
+// (util/tuntap/tuntap_adapter.cpp:5-21 -> FileDescriptor::read,
+// util/file_descriptor/file_descriptor.cpp:127-178, kReadBufferSize 16384 at
+// file_descriptor.h:47) and checksums each one on the CPU.  A DatagramBatch
+// is one arena of back-to-back wire datagrams + n+1 offsets, filled straight
+// from a file descriptor (recvmmsg on datagram sockets, read() per datagram on
+// TUN or other packet fds) and written back with sendmmsg / write(); with an
+// engine it lives in page-locked memory, so verify / unwrap / patch DMA the
+// arena with no staging copy.
+#ifndef ICSUM_HOST_BATCH_IO_H
+#define ICSUM_HOST_BATCH_IO_H
+
+#include <cstddef>
+#include <cstdint>
+#include <optional>
+#include <string_view>
+#include <vector>
+
+#include "batch.h"
+
+namespace icsum {
+
+class DatagramBatch
+{
+  public:
+    static constexpr size_t kMaxDatagram = 16384 + 20;  // the reference's readv shape
+
+    // page-locked arena from `engine` (GPU path)
+    DatagramBatch(BatchEngine& engine, size_t capacity_bytes = size_t(64) << 20, size_t max_datagrams = 1 << 16);
+    // ordinary memory (I/O only, no engine)
+    explicit DatagramBatch(size_t capacity_bytes = size_t(64) << 20, size_t max_datagrams = 1 << 16);
+    ~DatagramBatch();
+    DatagramBatch(const DatagramBatch&) = delete;
+    DatagramBatch& operator=(const DatagramBatch&) = delete;
+
+    void clear() { off_.assign(1, 0); }
+    size_t size() const { return off_.size() - 1; }
+    size_t bytes() const { return off_.back(); }
+    std::string_view operator[](size_t i) const
+    {
+        return {reinterpret_cast<const char*>(arena_) + off_[i], static_cast<size_t>(off_[i + 1] - off_[i])};
+    }
+    const uint8_t* data() const { return arena_; }
+    uint8_t* data() { return arena_; }
+    const uint64_t* offsets() const { return off_.data(); }
+
+    bool push(std::string_view wire);  // false when the arena is full
+
+    // up to `max` datagrams from `fd` (non-blocking fds stop at EAGAIN;
+    // blocking ones return after the first batch); returns the count read
+    size_t read_from(int fd, size_t max);
+    // every datagram to `fd`; returns the count written
+    size_t write_to(int fd) const;
+
+    // engine calls on the arena (require the engine constructor)
+    std::vector<uint8_t> verify();
+    std::vector<std::optional<TCPMessage>> unwrap(TCPOverIPv4Adapter& adapter);
+    void patch();
+
+  private:
+    BatchEngine* engine_ = nullptr;
+    uint8_t* arena_ = nullptr;
+    size_t cap_ = 0, max_n_ = 0;
+    std::vector<uint64_t> off_{0};
+    bool room(size_t n) const { return size() < max_n_ && bytes() + n <= cap_; }
+};
+
+}  // namespace icsum
+
+#endif

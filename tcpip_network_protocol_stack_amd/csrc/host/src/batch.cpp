@@ -194,16 +194,55 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap(TCPOverIPv4Adapter& a
 std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_raw(TCPOverIPv4Adapter& adapter,
                                                                std::span<const std::string_view> wires)
 {
+    Packed p;
+    for (auto w : wires) {
+        p.add(w);
+        p.end();
+    }
+    return unwrap_packed(adapter, reinterpret_cast<const uint8_t*>(p.bytes.data()), p.off.data(), p.n());
+}
+
+std::vector<uint8_t> BatchEngine::verify_packed(const uint8_t* bytes, const uint64_t* offsets, size_t n)
+{
+    std::vector<uint8_t> st(n);
+    if (n)
+        check(ics_ipv4_tcp_batch_host(ctx_, const_cast<uint8_t*>(bytes), offsets, 0, 0, n, ICS_MODE_VERIFY, nullptr,
+                                      nullptr, st.data()),
+              "ics_ipv4_tcp_batch_host");
+    return st;
+}
+
+void BatchEngine::patch_packed(uint8_t* bytes, const uint64_t* offsets, size_t n)
+{
+    if (n)
+        check(ics_ipv4_tcp_batch_host(ctx_, bytes, offsets, 0, 0, n, ICS_MODE_PATCH, nullptr, nullptr, nullptr),
+              "ics_ipv4_tcp_batch_host");
+}
+
+void* BatchEngine::host_alloc(size_t bytes)
+{
+    void* p = nullptr;
+    check(ics_host_alloc(ctx_, &p, bytes), "ics_host_alloc");
+    return p;
+}
+
+void BatchEngine::host_free(void* p) { ics_host_free(ctx_, p); }
+
+std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_packed(TCPOverIPv4Adapter& adapter, const uint8_t* bytes,
+                                                                  const uint64_t* offsets, size_t n)
+{
     // receive path from raw wire datagrams (a TUN / socket read batch):
     // IPv4 parse + TCP checksum verified on the GPU, fields parsed on the host
-    const std::vector<uint8_t> st = verify_raw(wires);
-    std::vector<std::optional<TCPMessage>> out(wires.size());
-    for (size_t i = 0; i < wires.size(); ++i) {
+    const std::vector<uint8_t> st = verify_packed(bytes, offsets, n);
+    std::vector<std::optional<TCPMessage>> out(n);
+    for (size_t i = 0; i < n; ++i) {
+        const std::string_view wire{reinterpret_cast<const char*>(bytes) + offsets[i],
+                                    static_cast<size_t>(offsets[i + 1] - offsets[i])};
         if ((st[i] & (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) !=
             (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK))
             continue;
         IPv4Datagram dg;
-        Parser ipp{std::vector<std::string>{std::string{wires[i]}}};
+        Parser ipp{std::vector<std::string>{std::string{wire}}};
         // fields only: the GPU already compared the header checksum
         uint8_t first = 0;
         ipp.integer(first);

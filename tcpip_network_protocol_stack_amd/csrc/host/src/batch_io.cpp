@@ -1,0 +1,158 @@
+// batch_io.cpp — icsum::DatagramBatch (see batch_io.h)
+#include "batch_io.h"
+
+#include <errno.h>
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include <cstdlib>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+
+namespace icsum {
+namespace {
+
+bool is_datagram_socket(int fd)
+{
+    int type = 0;
+    socklen_t len = sizeof type;
+    return getsockopt(fd, SOL_SOCKET, SO_TYPE, &type, &len) == 0 && (type == SOCK_DGRAM || type == SOCK_SEQPACKET);
+}
+
+[[noreturn]] void sys_fail(const char* what)
+{
+    throw std::runtime_error(std::string(what) + ": " + std::strerror(errno));
+}
+
+}  // namespace
+
+DatagramBatch::DatagramBatch(BatchEngine& engine, size_t capacity_bytes, size_t max_datagrams)
+    : engine_(&engine), cap_(capacity_bytes), max_n_(max_datagrams)
+{
+    arena_ = static_cast<uint8_t*>(engine.host_alloc(cap_));
+    off_.reserve(max_n_ + 1);
+}
+
+DatagramBatch::DatagramBatch(size_t capacity_bytes, size_t max_datagrams) : cap_(capacity_bytes), max_n_(max_datagrams)
+{
+    arena_ = static_cast<uint8_t*>(std::malloc(cap_ ? cap_ : 1));
+    if (!arena_) throw std::bad_alloc();
+    off_.reserve(max_n_ + 1);
+}
+
+DatagramBatch::~DatagramBatch()
+{
+    if (engine_)
+        engine_->host_free(arena_);
+    else
+        std::free(arena_);
+}
+
+bool DatagramBatch::push(std::string_view wire)
+{
+    if (!room(wire.size())) return false;
+    std::memcpy(arena_ + bytes(), wire.data(), wire.size());
+    off_.push_back(bytes() + wire.size());
+    return true;
+}
+
+size_t DatagramBatch::read_from(int fd, size_t max)
+{
+    size_t got = 0;
+    if (is_datagram_socket(fd)) {
+        // recvmmsg into kMaxDatagram slots carved from the arena's free tail,
+        // then compact the datagrams back to back (offsets stay contiguous)
+        while (got < max) {
+            const size_t free_bytes = cap_ - bytes();
+            const size_t k = std::min({max - got, max_n_ - size(), free_bytes / kMaxDatagram, size_t(1024)});
+            if (k == 0) break;
+            std::vector<mmsghdr> msgs(k);
+            std::vector<iovec> iov(k);
+            uint8_t* base = arena_ + bytes();
+            for (size_t j = 0; j < k; ++j) {
+                iov[j] = {base + j * kMaxDatagram, kMaxDatagram};
+                msgs[j].msg_hdr = {};
+                msgs[j].msg_hdr.msg_iov = &iov[j];
+                msgs[j].msg_hdr.msg_iovlen = 1;
+            }
+            const int r = recvmmsg(fd, msgs.data(), static_cast<unsigned>(k), got ? MSG_DONTWAIT : 0, nullptr);
+            if (r < 0) {
+                if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
+                sys_fail("recvmmsg");
+            }
+            for (int j = 0; j < r; ++j) {
+                const size_t len = msgs[j].msg_len;
+                if (j) std::memmove(arena_ + bytes(), base + size_t(j) * kMaxDatagram, len);
+                off_.push_back(bytes() + len);
+            }
+            got += size_t(r);
+            if (size_t(r) < k) break;
+        }
+        return got;
+    }
+    // packet fds (TUN): one datagram per read(), written in place
+    while (got < max && room(kMaxDatagram)) {
+        const ssize_t r = ::read(fd, arena_ + bytes(), kMaxDatagram);
+        if (r < 0) {
+            if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
+            sys_fail("read");
+        }
+        if (r == 0) break;
+        off_.push_back(bytes() + size_t(r));
+        ++got;
+    }
+    return got;
+}
+
+size_t DatagramBatch::write_to(int fd) const
+{
+    const size_t n = size();
+    if (is_datagram_socket(fd)) {
+        size_t done = 0;
+        while (done < n) {
+            const size_t k = std::min<size_t>(n - done, 1024);
+            std::vector<mmsghdr> msgs(k);
+            std::vector<iovec> iov(k);
+            for (size_t j = 0; j < k; ++j) {
+                const size_t i = done + j;
+                iov[j] = {arena_ + off_[i], static_cast<size_t>(off_[i + 1] - off_[i])};
+                msgs[j].msg_hdr = {};
+                msgs[j].msg_hdr.msg_iov = &iov[j];
+                msgs[j].msg_hdr.msg_iovlen = 1;
+            }
+            const int r = sendmmsg(fd, msgs.data(), static_cast<unsigned>(k), 0);
+            if (r < 0) {
+                if (errno == EINTR) continue;
+                sys_fail("sendmmsg");
+            }
+            done += size_t(r);
+        }
+        return done;
+    }
+    for (size_t i = 0; i < n; ++i) {
+        const size_t len = static_cast<size_t>(off_[i + 1] - off_[i]);
+        if (::write(fd, arena_ + off_[i], len) != static_cast<ssize_t>(len)) sys_fail("write");
+    }
+    return n;
+}
+
+std::vector<uint8_t> DatagramBatch::verify()
+{
+    if (!engine_) throw std::logic_error("DatagramBatch::verify needs an engine");
+    return engine_->verify_packed(arena_, off_.data(), size());
+}
+
+std::vector<std::optional<TCPMessage>> DatagramBatch::unwrap(TCPOverIPv4Adapter& adapter)
+{
+    if (!engine_) throw std::logic_error("DatagramBatch::unwrap needs an engine");
+    return engine_->unwrap_packed(adapter, arena_, off_.data(), size());
+}
+
+void DatagramBatch::patch()
+{
+    if (!engine_) throw std::logic_error("DatagramBatch::patch needs an engine");
+    engine_->patch_packed(arena_, off_.data(), size());
+}
+
+}  // namespace icsum

@@ -5,7 +5,11 @@
 #include <string>
 #include <vector>
 
+#include <sys/socket.h>
+#include <unistd.h>
+
 #include "batch.h"
+#include "batch_io.h"
 #include "checksum.h"
 #include "icsum.h"
 
@@ -138,6 +142,39 @@ int main()
         }
     }
     EXPECT(accepted >= wires.size() / 2);
+
+    // batched datagram I/O: the same received wires through
+    // a SOCK_DGRAM socketpair into a page-locked arena, unwrapped in place
+    {
+        int sv[2];
+        EXPECT(socketpair(AF_UNIX, SOCK_DGRAM, 0, sv) == 0);
+        icsum::DatagramBatch txb(size_t(1) << 20), rxb(eng, size_t(64) << 20);
+        for (size_t i = 0; i < rx.size();) {
+            txb.clear();
+            size_t j = i;
+            for (; j < rx.size() && j - i < 32 && txb.push(rx[j]); ++j) {
+            }
+            EXPECT(txb.write_to(sv[0]) == j - i);
+            EXPECT(rxb.read_from(sv[1], j - i) == j - i);
+            i = j;
+        }
+        close(sv[0]);
+        close(sv[1]);
+        EXPECT(rxb.size() == rx.size());
+        TCPOverIPv4Adapter Bio = B;
+        const auto got3 = rxb.unwrap(Bio);
+        for (size_t i = 0; i < rx.size(); ++i) EXPECT(got3[i].has_value() == got[i].has_value());
+        // transmit side: wires with both checksum fields zeroed, patched in the arena
+        icsum::DatagramBatch out(eng, size_t(16) << 20);
+        for (const auto& w : wires) {
+            std::string z = w;
+            z[10] = z[11] = 0;
+            z[36] = z[37] = 0;
+            EXPECT(out.push(z));
+        }
+        out.patch();
+        for (size_t i = 0; i < wires.size(); ++i) EXPECT(out[i] == wires[i]);
+    }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);
     return failures ? 1 : 0;

@@ -11,6 +11,10 @@
 #include <string>
 #include <vector>
 
+#include <sys/socket.h>
+#include <unistd.h>
+
+#include "batch_io.h"
 #include "checksum.h"
 #include "ipv4_datagram.h"
 #include "parser.h"
@@ -109,6 +113,31 @@ int main()
             bool ok = parse(dg, std::vector<std::string>{unhex(h)});
             ok = ok && B.unwrap_tcp_in_ip(dg).has_value();
             std::cout << ok << "\n";
+        } else if (cmd == "io") {
+            // DatagramBatch round trip through a SOCK_DGRAM socketpair:
+            // push -> sendmmsg -> recvmmsg (compacted arena) -> same bytes
+            std::vector<std::string> ws;
+            std::string h;
+            while (in >> h) ws.push_back(unhex(h));
+            int sv[2];
+            if (socketpair(AF_UNIX, SOCK_DGRAM, 0, sv) != 0) return 3;
+            icsum::DatagramBatch tx(size_t(1) << 20), rx(size_t(1) << 22);
+            size_t sent = 0, got = 0;
+            bool same = true;
+            for (size_t i = 0; i < ws.size();) {  // in rounds that fit the socket buffer
+                tx.clear();
+                size_t j = i;
+                for (; j < ws.size() && j - i < 32 && tx.push(ws[j]); ++j) {
+                }
+                sent += tx.write_to(sv[0]);
+                const size_t before = rx.size();
+                got += rx.read_from(sv[1], j - i);
+                for (size_t k = before; k < rx.size(); ++k) same = same && rx[k] == ws[k];
+                i = j;
+            }
+            close(sv[0]);
+            close(sv[1]);
+            std::cout << sent << " " << got << " " << same << " " << rx.bytes() << "\n";
         } else if (!cmd.empty()) {
             std::cerr << "unknown command " << cmd << "\n";
             return 1;

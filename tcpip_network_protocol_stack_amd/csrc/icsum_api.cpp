@@ -439,6 +439,19 @@ int ics_free(ics_ctx* ctx, void* d_ptr) {
   return ICS_OK;
 }
 
+int ics_host_alloc(ics_ctx* ctx, void** h_ptr, size_t bytes) {
+  if (int rc = bind(ctx)) return rc;
+  if (!h_ptr) return fail(ICS_ERR_INVALID, "null output pointer");
+  ICS_HIP(hipHostMalloc(h_ptr, bytes ? bytes : 1, 0));
+  return ICS_OK;
+}
+
+int ics_host_free(ics_ctx* ctx, void* h_ptr) {
+  if (int rc = bind(ctx)) return rc;
+  if (h_ptr) ICS_HIP(hipHostFree(h_ptr));
+  return ICS_OK;
+}
+
 int ics_memcpy_htod(ics_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, void* stream) {
   if (int rc = bind(ctx)) return rc;
   if (!bytes) return ICS_OK;

@@ -195,6 +195,16 @@ __device__ __forceinline__ Hdr load_hdr(const uint8_t* p) {
   return h;
 }
 
+// big-endian 16-bit field store: one short store when 2-byte aligned
+__device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {
+  if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0) {
+    *reinterpret_cast<uint16_t*>(p) = uint16_t(((v & 0xffu) << 8) | ((v >> 8) & 0xffu));
+  } else {
+    p[0] = uint8_t(v >> 8);
+    p[1] = uint8_t(v);
+  }
+}
+
 // TCP header bytes 12..19 of a segment starting at t (>= 18 bytes present):
 // tf0 = bytes 12..15, tf1 = bytes 16..19 (bytes 18, 19 only meaningful when
 // present).  Every dword loaded holds at least one byte of the segment.
@@ -302,12 +312,8 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
           if (hdr_ok) st |= 0x01;
           if (rem >= 18) st |= 0x02;
           if (mode == 2) {
-            dg[s + 10] = uint8_t(ipc >> 8);
-            dg[s + 11] = uint8_t(ipc);
-            if (rem >= 18) {
-              dg[t0 + 16] = uint8_t(tcv >> 8);
-              dg[t0 + 17] = uint8_t(tcv);
-            }
+            store_be16(dg + s + 10, ipc);
+            if (rem >= 18) store_be16(dg + t0 + 16, tcv);
           }
         }
       }
@@ -337,8 +343,7 @@ __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
       const uint16_t c = fold_value(ipv4_header_sum(h));
       dg[s + 6] = uint8_t(h.byte(6) & 0x7fu);  // re-serialized flags word
       dg[s + 8] = uint8_t(ttl - 1);
-      dg[s + 10] = uint8_t(c >> 8);
-      dg[s + 11] = uint8_t(c);
+      store_be16(dg + s + 10, c);
       st = 1;
     }
   }

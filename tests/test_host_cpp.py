@@ -72,3 +72,13 @@ def test_reference_stack_runs_on_dropin_types(selftest):
     out = subprocess.run([exe], capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stdout[-2000:]
     assert out.stdout.startswith("OK: CPU path, 1048576 + 300000 bytes")
+
+
+def test_datagram_batch_socket_round_trip(selftest):
+    # batched datagram I/O (sendmmsg / recvmmsg into one
+    # compacted arena with n+1 offsets) preserves every datagram byte for byte
+    cases = wires("tcp_wrap.json")
+    line = "io " + " ".join(c["wire"] for c in cases)
+    sent, got, same, nbytes = (int(x) for x in selftest([line])[0].split())
+    assert sent == got == len(cases) and same == 1
+    assert nbytes == sum(len(c["wire"]) // 2 for c in cases)

@@ -92,6 +92,15 @@ def main():
         assert (st.cpu().numpy() == 0x0F).all()
         del bufs
 
+    if "ns64k" in only:  # reference point for config 2: plain checksum over the same 64 Ki x 1500 B, rotated
+        n, L, seed, R = 1 << 16, 1500, 0x10710002, 6
+        ds = [eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+              for r in range(R)]
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        t = timed(lambda i=0: eng.checksum_batch(ds[i % R], n=n, stride=L, seg_len=L, out=out), args.iters * 3)
+        emit("plain_64Kix1500", n * L, t, n * 2, entry="ics_checksum_batch", rotation=R)
+        del ds
+
     if "tcp64" in only:  # config 3: 1 M x 64 B TCP segments with pseudo inits
         n, L, seed, R = 1 << 20, 64, 0x10710003, 6
         ds = [eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
