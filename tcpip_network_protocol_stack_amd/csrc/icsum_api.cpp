@@ -60,6 +60,10 @@ struct ics_ctx {
   void* d_zero = nullptr;  // 16 zero bytes (icsum::SegSpec::zero16)
   uint32_t max_blocks = 0;  // 0 = one lane group per segment (no grid-stride cap)
   int force_lps = 0, force_unroll = 0, force_nt = -1, force_mode = -1, force_segs = 0;
+  // length binning of offsets batches: -1 auto (n >= bin_min), 0 off, 1 always
+  int bin = -1;
+  uint64_t bin_min = 0;
+  uint32_t bin_blocks = 0;  // grid of each bin's launch (its size is only known on the device)
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
   static constexpr size_t kSlotBytes = size_t(64) << 20;
@@ -109,6 +113,40 @@ icsum::Geometry ipv4_geometry(icsum::Geometry g) {
 uint64_t avg_len_hint(const uint64_t* offsets, uint64_t seg_len, uint64_t n, uint64_t total_hint) {
   if (!offsets) return seg_len;
   return total_hint && n ? total_hint / n : 65536;  // unknown mix: the long-segment geometry
+}
+
+bool forced_geometry(const ics_ctx* ctx) {
+  return ctx->force_lps || ctx->force_unroll || ctx->force_nt >= 0 || ctx->force_mode >= 0 ||
+         ctx->force_segs;
+}
+
+// a1-a4 on device buffers.  An offsets batch of unknown length mix is split
+// into length bins on the device (two passes over the offsets), and every bin
+// runs with the geometry that suits its lengths; the bin lists live in
+// stream-ordered scratch, so concurrent calls on different streams are safe.
+int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
+                    void* d_out, int out_kind, hipStream_t st) {
+  const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
+                      (ctx->bin == 1 || (ctx->bin < 0 && sp.n >= ctx->bin_min && !forced_geometry(ctx)));
+  if (!binned) {
+    const icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len, sp.n, 0));
+    ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
+    return ICS_OK;
+  }
+  void* ws = nullptr;
+  const size_t meta_bytes = icsum::kBinMetaWords * sizeof(uint32_t);
+  ICS_HIP(hipMallocAsync(&ws, meta_bytes + sp.n * 16, st));
+  uint32_t* meta = static_cast<uint32_t*>(ws);
+  void* list = static_cast<uint8_t*>(ws) + meta_bytes;
+  hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, st);
+  const uint32_t cap = ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks;
+  for (int b = 0; b < icsum::kBins && e == hipSuccess; ++b)
+    e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, b), d_init, d_odd, d_out, out_kind,
+                               icsum::bin_geometry(b), cap, st);
+  const hipError_t f = hipFreeAsync(ws, st);
+  ICS_HIP(e);
+  ICS_HIP(f);
+  return ICS_OK;
 }
 
 int ensure_staging(ics_ctx* ctx) {
@@ -327,6 +365,9 @@ int ics_create(int device, ics_ctx** out) {
   ctx->force_nt = std::getenv("ICSUM_NT") ? int(env_u32("ICSUM_NT", 1)) : -1;
   ctx->force_mode = std::getenv("ICSUM_MODE") ? int(env_u32("ICSUM_MODE", 0)) : -1;
   ctx->force_segs = int(env_u32("ICSUM_SEGS", 0));
+  ctx->bin = std::getenv("ICSUM_BIN") ? int(env_u32("ICSUM_BIN", 1)) : -1;
+  ctx->bin_min = env_u32("ICSUM_BIN_MIN", 1u << 16);
+  ctx->bin_blocks = env_u32("ICSUM_BIN_BLOCKS", 2048);
   *out = ctx;
   return ICS_OK;
 }
@@ -354,10 +395,7 @@ int ics_checksum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offs
   if (n == 0) return ICS_OK;
   if (!d_bytes || !d_out) return fail(ICS_ERR_INVALID, "null device buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n, ctx->d_zero};
-  const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, seg_len, n, 0));
-  ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, d_out, 0, g, ctx->max_blocks,
-                                 static_cast<hipStream_t>(stream)));
-  return ICS_OK;
+  return checksum_device(ctx, sp, d_init, nullptr, d_out, 0, static_cast<hipStream_t>(stream));
 }
 
 int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets, uint64_t stride,
@@ -367,10 +405,7 @@ int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets, 
   if (n == 0) return ICS_OK;
   if (!d_bytes || !d_sum) return fail(ICS_ERR_INVALID, "null device buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n, ctx->d_zero};
-  const icsum::Geometry g = geometry_for(ctx, avg_len_hint(d_offsets, seg_len, n, 0));
-  ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_sum, 1, g, ctx->max_blocks,
-                                 static_cast<hipStream_t>(stream)));
-  return ICS_OK;
+  return checksum_device(ctx, sp, d_init, d_odd, d_sum, 1, static_cast<hipStream_t>(stream));
 }
 
 int ics_fold_batch(ics_ctx* ctx, const uint32_t* d_sum, uint16_t* d_out, uint64_t n, void* stream) {

@@ -37,13 +37,47 @@ __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets,
   }
 }
 
+// Where a launch finds its segments: fixed stride, packed offsets, or a
+// length bin written by k_bin_segments (entries {start lo, start hi, length,
+// segment index}; the bin's size is read from *count on the device, so the
+// launch needs no host round trip).
+struct SegSrc {
+  const uint64_t* offsets;
+  uint64_t stride, seg_len;
+  const u32x4* list;
+  const uint32_t* count;
+  const uint32_t* base;
+};
+
+constexpr uint32_t kLongEntry = 0xFFFFFFFFu;  // entry length: >= 4 GiB, re-read the offsets
+
+__device__ __forceinline__ uint64_t src_count(const SegSrc& src, uint64_t n) {
+  return src.list ? uint64_t(*src.count) : n;
+}
+
+// segment number, start and end of work item gi (< src_count)
+__device__ __forceinline__ void src_locate(const SegSrc& src, uint64_t gi, uint64_t& seg, uint64_t& s,
+                                           uint64_t& e) {
+  if (src.list) {
+    const u32x4 ent = src.list[*src.base + gi];
+    seg = ent.w;
+    if (ent.z != kLongEntry) {
+      s = uint64_t(ent.x) | (uint64_t(ent.y) << 32);
+      e = s + ent.z;
+    } else {
+      seg_bounds(src.offsets, 0, 0, seg, s, e);
+    }
+  } else {
+    seg = gi;
+    seg_bounds(src.offsets, src.stride, src.seg_len, gi, s, e);
+  }
+}
+
 // ------------------------------------------------------------ a1-a4 -------
 // `init` / `odd` are never null here: an absent array is replaced by a
 // 16-byte zero buffer read with index step 0 (init_step / odd_step).
 template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
-__global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes,
-                                                     const uint64_t* __restrict__ offsets,
-                                                     uint64_t stride, uint64_t seg_len,
+__global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes, SegSrc src,
                                                      const uint32_t* __restrict__ init,
                                                      uint32_t init_step,
                                                      const uint8_t* __restrict__ odd,
@@ -52,18 +86,19 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
+  const uint64_t items = src_count(src, n);
   // the loop bound is uniform per block, so every lane reaches the DPP sums
-  for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups; g0 < n; g0 += step) {
-    const uint64_t seg = g0 + threadIdx.x / LPS;
-    const bool valid = seg < n;
-    uint64_t s = 0, e = 0;
-    if (valid) seg_bounds(offsets, stride, seg_len, seg, s, e);
+  for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups; g0 < items; g0 += step) {
+    const uint64_t gi = g0 + threadIdx.x / LPS;
+    const bool valid = gi < items;
+    uint64_t seg = 0, s = 0, e = 0;
+    if (valid) src_locate(src, gi, seg, s, e);
     // per-segment metadata is requested together with the byte stream, so a
     // wave waits on memory once (the leader lane folds it in at the end)
     // (unconditional loads from a clamped index: a load under a divergent
     // branch would make the compiler wait for it at the join)
     const bool leader = valid && lane == LPS - 1;
-    const uint64_t cseg = valid ? seg : n - 1;
+    const uint64_t cseg = seg;  // 0 for idle lanes (n >= 1)
     const uint32_t i0 = init[cseg * init_step];
     // a high byte at the start unless the start is odd XOR parity_ was already odd
     const uint32_t swap = (uint32_t(s) ^ uint32_t(odd[cseg * odd_step])) & 1u;
@@ -89,9 +124,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
 // segment (range_sums_masked semantics); a segment longer than LPS*UNROLL
 // chunks finishes in a loop.  Absent per-segment arrays: zero16 + step 0.
 template <int LPS, int UNROLL, int SEGS, int OUT>
-__global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __restrict__ bytes,
-                                                           const uint64_t* __restrict__ offsets,
-                                                           uint64_t stride, uint64_t seg_len,
+__global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __restrict__ bytes, SegSrc src,
                                                            const uint32_t* __restrict__ init,
                                                            uint32_t init_step,
                                                            const uint8_t* __restrict__ odd,
@@ -103,21 +136,24 @@ __global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __rest
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint32_t group = threadIdx.x / LPS;
   const uint64_t step = uint64_t(gridDim.x) * kGroups * SEGS;
-  for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups * SEGS; g0 < n; g0 += step) {
-    uint64_t s[SEGS], span[SEGS];
+  const uint64_t items = src_count(src, n);
+  for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups * SEGS; g0 < items; g0 += step) {
+    uint64_t s[SEGS], span[SEGS], segk[SEGS];
+    bool validk[SEGS];
     uint32_t nch[SEGS], i0[SEGS], swap[SEGS];
     u32x4 v[SEGS][UNROLL];
 #pragma unroll
     for (int k = 0; k < SEGS; ++k) {
-      const uint64_t seg = g0 + uint64_t(k) * kGroups + group;
-      const bool valid = seg < n;
+      const uint64_t gi = g0 + uint64_t(k) * kGroups + group;
+      validk[k] = gi < items;
       uint64_t e = 0;
       s[k] = 0;
-      if (valid) seg_bounds(offsets, stride, seg_len, seg, s[k], e);
+      segk[k] = 0;
+      if (validk[k]) src_locate(src, gi, segk[k], s[k], e);
       const uint64_t a0 = s[k] & ~uint64_t(15);
       span[k] = e > s[k] ? e - a0 : 0;
       nch[k] = uint32_t((span[k] + 15) >> 4);
-      const uint64_t cseg = valid ? seg : n - 1;
+      const uint64_t cseg = segk[k];  // 0 for idle lanes (n >= 1)
       i0[k] = init[cseg * init_step];
       swap[k] = (uint32_t(s[k]) ^ uint32_t(odd[cseg * odd_step])) & 1u;
       const u32x4* p = reinterpret_cast<const u32x4*>(bytes + a0);
@@ -150,8 +186,8 @@ __global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __rest
         }
       }
       const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, swap[k]));
-      const uint64_t seg = g0 + uint64_t(k) * kGroups + group;
-      if (seg < n && lane == LPS - 1) {
+      const uint64_t seg = segk[k];
+      if (validk[k] && lane == LPS - 1) {
         const uint32_t sum = i0[k] + tot;
         if (OUT == 0)
           static_cast<uint16_t*>(out)[seg] = fold_value(sum);
@@ -424,6 +460,132 @@ __global__ void k_ipv4_tcp_headers(uint8_t* __restrict__ dg, uint64_t stride, ui
   }
 }
 
+
+// ------------------------------------------------------- length binning ---
+// Bin of a segment by its 16-byte chunk count; the boundaries are those of
+// pick_geometry, so bin b runs with the geometry pick_geometry gives a batch
+// of such segments.
+constexpr uint64_t kBinMaxChunks[kBins - 1] = {9, 56, 120, 256};
+constexpr int kBinPerThread = 8;  // segments per thread per tile
+constexpr int kBinTile = kBlock * kBinPerThread;
+constexpr int kBinField = 12;  // bits per bin in a packed count
+
+__device__ __forceinline__ int bin_of(uint64_t len) {
+  const uint64_t m = (len + 15) >> 4;
+  int b = 0;
+#pragma unroll
+  for (int k = 0; k < kBins - 1; ++k) b += m > kBinMaxChunks[k];
+  return b;
+}
+
+// Packed per-bin counts: kBins fields of 12 bits in a uint64 (a tile holds
+// 2048 segments, so no field overflows and adding packed words never carries
+// across fields).
+__device__ __forceinline__ uint32_t field(uint64_t p, int b) {
+  return uint32_t(p >> (kBinField * b)) & ((1u << kBinField) - 1);
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t u = __shfl_up(v, d, 64);
+    if (lane >= uint32_t(d)) v += u;
+  }
+  return v;
+}
+
+// exclusive block scan of packed counts; returns the block total in `total`
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total) {
+  __shared__ uint64_t wsum[kBlock / 64];
+  const uint64_t inc = wave_incl_scan(v);
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) wsum[w] = inc;
+  __syncthreads();
+  uint64_t before = 0;
+  total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kBlock / 64; ++k) {
+    before += k < w ? wsum[k] : 0;
+    total += wsum[k];
+  }
+  __syncthreads();  // wsum is reused by the next tile
+  return before + inc - v;
+}
+
+// pass 1: bin sizes (one atomic per bin per block)
+__global__ __launch_bounds__(kBlock) void k_bin_count(const uint64_t* __restrict__ off, uint64_t n,
+                                                      uint32_t* __restrict__ meta) {
+  uint32_t cnt[kBins] = {};
+  ICS_GRID_STRIDE(i, n) {
+    const int b = bin_of(off[i + 1] - off[i]);
+#pragma unroll
+    for (int k = 0; k < kBins; ++k) cnt[k] += b == k;
+  }
+  __shared__ uint32_t bsum[kBins];
+  if (threadIdx.x < kBins) bsum[threadIdx.x] = 0;
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < kBins; ++k) {
+    uint32_t c = cnt[k];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
+    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&bsum[k], c);
+  }
+  __syncthreads();
+  if (threadIdx.x < kBins && bsum[threadIdx.x]) atomicAdd(&meta[threadIdx.x], bsum[threadIdx.x]);
+}
+
+// pass 2: scatter entries; bin b occupies [base_b, base_b + size_b) of the
+// list.  Each tile reserves its slice of every bin with one atomic per bin.
+__global__ __launch_bounds__(kBlock) void k_bin_scatter(const uint64_t* __restrict__ off, uint64_t n,
+                                                        uint32_t* __restrict__ meta,
+                                                        u32x4* __restrict__ list) {
+  uint32_t base[kBins];
+  uint32_t acc = 0;
+#pragma unroll
+  for (int k = 0; k < kBins; ++k) {
+    base[k] = acc;
+    acc += meta[k];
+  }
+  if (blockIdx.x == 0 && threadIdx.x < kBins) meta[16 + threadIdx.x] = base[threadIdx.x];
+  __shared__ uint32_t resv[kBins];
+  for (uint64_t t0 = uint64_t(blockIdx.x) * kBinTile; t0 < n; t0 += uint64_t(gridDim.x) * kBinTile) {
+    uint64_t s[kBinPerThread], len[kBinPerThread];
+    int bin[kBinPerThread];
+    uint64_t mine = 0;
+#pragma unroll
+    for (int j = 0; j < kBinPerThread; ++j) {
+      const uint64_t i = t0 + uint64_t(j) * kBlock + threadIdx.x;
+      bin[j] = -1;
+      if (i < n) {
+        s[j] = off[i];
+        len[j] = off[i + 1] - s[j];
+        bin[j] = bin_of(len[j]);
+        mine += uint64_t(1) << (kBinField * bin[j]);
+      }
+    }
+    uint64_t total;
+    uint64_t excl = block_excl_scan(mine, total);
+    if (threadIdx.x < kBins) {
+      const uint32_t c = field(total, threadIdx.x);
+      resv[threadIdx.x] = c ? atomicAdd(&meta[8 + threadIdx.x], c) : 0;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int j = 0; j < kBinPerThread; ++j) {
+      if (bin[j] < 0) continue;
+      const int b = bin[j];
+      const uint32_t pos = base[b] + resv[b] + field(excl, b);
+      excl += uint64_t(1) << (kBinField * b);
+      const uint64_t i = t0 + uint64_t(j) * kBlock + threadIdx.x;
+      const uint32_t l = len[j] < kLongEntry ? uint32_t(len[j]) : kLongEntry;
+      list[pos] = u32x4{uint32_t(s[j]), uint32_t(s[j] >> 32), l, uint32_t(i)};
+    }
+    __syncthreads();  // resv is reused by the next tile
+  }
+}
+
 // element-wise grid: at most 64K blocks (16M work-items), grid-stride beyond
 inline uint32_t ew_blocks(uint64_t n) {
   const uint64_t b = (n + kBlock - 1) / kBlock;
@@ -439,6 +601,10 @@ inline uint32_t blocks_for(uint64_t groups, uint32_t groups_per_block, uint32_t 
   return uint32_t(b < cap ? b : cap);
 }
 
+inline SegSrc src_of(const SegSpec& sp) {
+  return SegSrc{sp.offsets, sp.stride, sp.seg_len, static_cast<const u32x4*>(sp.list), sp.count, sp.base};
+}
+
 template <int LPS, int UNROLL, bool NT, int MODE>
 hipError_t launch_checksum_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                              int out_kind, uint32_t max_blocks, hipStream_t st) {
@@ -448,10 +614,10 @@ hipError_t launch_checksum_t(const SegSpec& sp, const uint32_t* init, const uint
   const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
   if (out_kind == 0)
     hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.stride, sp.seg_len, ip, is, op, os, out, sp.n);
+                       src_of(sp), ip, is, op, os, out, sp.n);
   else
     hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.stride, sp.seg_len, ip, is, op, os, out, sp.n);
+                       src_of(sp), ip, is, op, os, out, sp.n);
   return hipGetLastError();
 }
 
@@ -465,10 +631,10 @@ hipError_t launch_checksum_small_t(const SegSpec& sp, const uint32_t* init, cons
   const u32x4* z = static_cast<const u32x4*>(sp.zero16);
   if (out_kind == 0)
     hipLaunchKernelGGL((k_checksum_small<LPS, UNROLL, SEGS, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.stride, sp.seg_len, ip, is, op, os, z, out, sp.n);
+                       src_of(sp), ip, is, op, os, z, out, sp.n);
   else
     hipLaunchKernelGGL((k_checksum_small<LPS, UNROLL, SEGS, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.stride, sp.seg_len, ip, is, op, os, z, out, sp.n);
+                       src_of(sp), ip, is, op, os, z, out, sp.n);
   return hipGetLastError();
 }
 
@@ -537,6 +703,33 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta,
+                               hipStream_t st) {
+  if (!offsets || n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  if (hipError_t e = hipMemsetAsync(meta, 0, kBinMetaWords * sizeof(uint32_t), st)) return e;
+  hipLaunchKernelGGL(k_bin_count, dim3(ew_blocks(n) < 2048 ? ew_blocks(n) : 2048), dim3(kBlock), 0, st,
+                     offsets, n, meta);
+  if (hipError_t e = hipGetLastError()) return e;
+  uint64_t tiles = (n + kBinTile - 1) / kBinTile;
+  hipLaunchKernelGGL(k_bin_scatter, dim3(uint32_t(tiles < 2048 ? tiles : 2048)), dim3(kBlock), 0, st,
+                     offsets, n, meta, static_cast<u32x4*>(list));
+  return hipGetLastError();
+}
+
+Geometry bin_geometry(int bin) {
+  // the upper edge of the bin (the last bin: a long segment)
+  const uint64_t len = bin < kBins - 1 ? kBinMaxChunks[bin] * 16 : uint64_t(1) << 16;
+  return pick_geometry(len);
+}
+
+SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, int bin) {
+  SegSpec sp = whole;
+  sp.list = list;
+  sp.count = meta + bin;
+  sp.base = meta + 16 + bin;
+  return sp;
 }
 
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,

@@ -28,7 +28,29 @@ struct SegSpec {
   uint64_t seg_len;
   uint64_t n;
   const void* zero16;  // 16 zero bytes in device memory (stand-in for absent arrays)
+  // length-binned launch: work items come from a bin list (16-byte entries,
+  // see launch_bin_segments) of *count entries starting at entry *base;
+  // n stays the batch size (an upper bound of *count)
+  const void* list = nullptr;
+  const uint32_t* count = nullptr;
+  const uint32_t* base = nullptr;
 };
+
+// Length binning of an offsets batch (mixed segment sizes): every segment
+// goes to the bin whose geometry suits its length, and each bin is run with
+// its own geometry, reading its work list on the device.
+//   list  n entries of 16 bytes ({start lo, start hi, length, segment};
+//         length 0xFFFFFFFF = re-read the offsets), bins stored back to back
+//   meta  kBinMetaWords uint32: [0, kBins) bin sizes, [8, 8 + kBins) cursors,
+//         [16, 16 + kBins) bin bases (written by the scatter pass)
+// Needs n < 2^32.  The launcher zeroes meta itself.
+constexpr int kBins = 5;
+constexpr int kBinMetaWords = 32;
+hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta,
+                               hipStream_t st);
+Geometry bin_geometry(int bin);
+// bin b's launch spec: list = bin's entries, count = its size
+SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, int bin);
 
 // out_kind 0: u16 value(), 1: u32 raw sum
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,

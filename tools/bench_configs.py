@@ -3,7 +3,7 @@
 (PCIe) rate — the numbers DESIGN.md §Measurements quotes.  bench.py stays the
 driver's single headline line (north star); this is the wider table.
 
-    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,jumbo,jumbo_all,host] [--iters 20]
+    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host] [--iters 20]
 
 Batches that fit the 256 MiB Infinity Cache (ipv4 98 MB, tcp64 67 MB) are
 rotated over >= 4 distinct copies (>= 393 / 268 MB) so every launch reads HBM.
@@ -59,11 +59,14 @@ def emit(name, nbytes, t, meta_bytes=0, **kw):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="ns,ipv4,tcp64,mixed,jumbo,jumbo_all,host")
+    ap.add_argument("--only", default="ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host")
     ap.add_argument("--iters", type=int, default=20)
     args = ap.parse_args()
     only = set(args.only.split(","))
     eng = Engine(0)
+    os.environ["ICSUM_BIN"] = "0"  # single-geometry dispatch for offsets batches, for comparison
+    eng_nobin = Engine(0)
+    del os.environ["ICSUM_BIN"]
     dev = torch.device("cuda", 0)
 
     if "ns" in only:  # north star: 1 M x 1500 B, pseudo-header inits
@@ -119,8 +122,26 @@ def main():
         doff = torch.from_numpy(off.view(np.int64)).to(dev)
         init = eng.pseudo_inits(n, seed, offsets=doff)
         out = torch.empty(n, dtype=torch.int16, device=dev)
-        t = timed(lambda i=0: eng.checksum_batch(d, offsets=doff, init=init, out=out), args.iters // 2 or 1)
-        emit("mixed_1M_64B_64KiB", int(off[-1]), t, n * 14, entry="ics_checksum_batch(offsets)")
+        for tag, e in (("", eng), ("_unbinned", eng_nobin)):
+            t = timed(lambda i=0: e.checksum_batch(d, offsets=doff, init=init, out=out), args.iters // 2 or 1)
+            emit("mixed_1M_64B_64KiB" + tag, int(off[-1]), t, n * 14, entry="ics_checksum_batch(offsets)",
+                 binned=not tag)
+        del d
+
+    if "bimodal" in only:  # ACK-sized and MSS-sized TCP segments interleaved, packed offsets
+        n, seed = 2 << 20, 0x10710006
+        rng = np.random.default_rng(seed)
+        lens = np.where(rng.random(n) < 0.5, 40, 1460) + rng.integers(0, 4, n)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        d = eng.fill_bytes(torch.empty(int(off[-1]) + 16, dtype=torch.uint8, device=dev), seed)
+        doff = torch.from_numpy(off.view(np.int64)).to(dev)
+        init = eng.pseudo_inits(n, seed, offsets=doff)
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        for tag, e in (("", eng), ("_unbinned", eng_nobin)):
+            t = timed(lambda i=0: e.checksum_batch(d, offsets=doff, init=init, out=out), args.iters)
+            emit("bimodal_2M_40B_1460B" + tag, int(off[-1]), t, n * 14, entry="ics_checksum_batch(offsets)",
+                 binned=not tag)
         del d
 
     if "jumbo" in only:  # config 5 per-GPU shard (weak scaling unit): 1 M x 9000 B
