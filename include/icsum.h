@@ -100,6 +100,18 @@ int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets,
                   uint64_t stride, uint64_t seg_len, const uint32_t* d_init,
                   const uint8_t* d_odd, uint32_t* d_sum, uint64_t n, void* stream);
 
+/* Dispatch of offsets batches (d_offsets != NULL) in ics_checksum_batch /
+ * ics_sum_batch.  BINNED splits the batch into length bins on the device and
+ * runs each bin with the lane geometry that suits it (a one-block plan kernel
+ * falls back to the whole-batch launch when the long segments dominate);
+ * SINGLE runs one launch with the long-segment geometry.  AUTO (default) =
+ * BINNED for batches of >= 65536 segments.  Results are identical; only the
+ * speed differs.  Per context; not a reference interface. */
+#define ICS_BINNING_AUTO (-1)
+#define ICS_BINNING_SINGLE 0
+#define ICS_BINNING_BINNED 1
+int ics_set_binning(ics_ctx* ctx, int mode);
+
 /* d_out[i] = InternetChecksum::value() of a raw sum (checksum.h:31-41). */
 int ics_fold_batch(ics_ctx* ctx, const uint32_t* d_sum, uint16_t* d_out, uint64_t n,
                    void* stream);

@@ -14,6 +14,7 @@ ICS_OK = 0
 ICS_MODE_COMPUTE, ICS_MODE_VERIFY, ICS_MODE_PATCH = 0, 1, 2
 ICS_ST_IPV4_OK, ICS_ST_TCP_CKSUM_OK, ICS_ST_TCP_HDR_OK, ICS_ST_PROTO_TCP = 0x01, 0x02, 0x04, 0x08
 ICS_ST_ACCEPT = 0x0F
+ICS_BINNING_AUTO, ICS_BINNING_SINGLE, ICS_BINNING_BINNED = -1, 0, 1
 
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -31,6 +32,7 @@ SIGNATURES = {
     "ics_last_error": (ctypes.c_char_p, []),
     "ics_checksum_batch": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _u64, _p]),
     "ics_sum_batch": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _p, _u64, _p]),
+    "ics_set_binning": (_int, [_p, _int]),
     "ics_fold_batch": (_int, [_p, _p, _p, _u64, _p]),
     "ics_ipv4_tcp_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p, _p]),
     "ics_router_ttl_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p]),

@@ -64,6 +64,7 @@ struct ics_ctx {
   int bin = -1;
   uint64_t bin_min = 0;
   uint32_t bin_blocks = 0;  // grid of each bin's launch (its size is only known on the device)
+  int bin_plan = -1;        // -1: decided on the device per batch, 0: whole, 1: split (tests)
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
   static constexpr size_t kSlotBytes = size_t(64) << 20;
@@ -134,15 +135,28 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     return ICS_OK;
   }
   void* ws = nullptr;
-  const size_t meta_bytes = icsum::kBinMetaWords * sizeof(uint32_t);
-  ICS_HIP(hipMallocAsync(&ws, meta_bytes + sp.n * 16, st));
+  const size_t meta_bytes = (icsum::kBinMetaBytesTotal + 255) & ~size_t(255);
+  ICS_HIP(hipMallocAsync(&ws, meta_bytes + sp.n * 16 * icsum::kBins, st));
   uint32_t* meta = static_cast<uint32_t*>(ws);
   void* list = static_cast<uint8_t*>(ws) + meta_bytes;
-  hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, st);
-  const uint32_t cap = ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks;
-  for (int b = 0; b < icsum::kBins && e == hipSuccess; ++b)
-    e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, b), d_init, d_odd, d_out, out_kind,
-                               icsum::bin_geometry(b), cap, st);
+  hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, ctx->bin_plan, st);
+  // bins 0..3: one launch, a capped grid striding over each bin; the last
+  // bin: one lane group per segment of the batch (it takes the whole batch
+  // under that plan)
+  if (e == hipSuccess)
+    e = icsum::launch_checksum_bins(icsum::bin_spec(sp, list, meta, 0), d_init, d_odd, d_out, out_kind,
+                                    ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks, st);
+  if (e == hipSuccess)
+    e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, icsum::kBins - 1), d_init, d_odd, d_out, out_kind,
+                               icsum::bin_geometry(icsum::kBins - 1), ctx->max_blocks, st);
+  if (e == hipSuccess && std::getenv("ICSUM_BIN_DEBUG")) {  // dev: dump the binning pass's meta words
+    uint32_t h[icsum::kBinMetaWords];
+    if (hipMemcpyAsync(h, meta, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess) {
+      std::fprintf(stderr, "icsum bin meta:");
+      for (int k = 0; k < icsum::kBinMetaWords; ++k) std::fprintf(stderr, " %u", h[k]);
+      std::fprintf(stderr, "\n");
+    }
+  }
   const hipError_t f = hipFreeAsync(ws, st);
   ICS_HIP(e);
   ICS_HIP(f);
@@ -368,6 +382,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin = std::getenv("ICSUM_BIN") ? int(env_u32("ICSUM_BIN", 1)) : -1;
   ctx->bin_min = env_u32("ICSUM_BIN_MIN", 1u << 16);
   ctx->bin_blocks = env_u32("ICSUM_BIN_BLOCKS", 2048);
+  ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
   *out = ctx;
   return ICS_OK;
 }
@@ -406,6 +421,13 @@ int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets, 
   if (!d_bytes || !d_sum) return fail(ICS_ERR_INVALID, "null device buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n, ctx->d_zero};
   return checksum_device(ctx, sp, d_init, d_odd, d_sum, 1, static_cast<hipStream_t>(stream));
+}
+
+int ics_set_binning(ics_ctx* ctx, int mode) {
+  if (!ctx) return fail(ICS_ERR_INVALID, "null context");
+  if (mode < ICS_BINNING_AUTO || mode > ICS_BINNING_BINNED) return fail(ICS_ERR_INVALID, "bad binning mode %d", mode);
+  ctx->bin = mode;
+  return ICS_OK;
 }
 
 int ics_fold_batch(ics_ctx* ctx, const uint32_t* d_sum, uint16_t* d_out, uint64_t n, void* stream) {

@@ -37,62 +37,221 @@ __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets,
   }
 }
 
+// ------------------------------------------------------- length binning ---
+// Bin of a segment by its 16-byte chunk count; the boundaries are those of
+// pick_geometry, so bin b runs with the geometry pick_geometry gives a batch
+// of such segments.
+constexpr uint64_t kBinMaxChunks[kBins - 1] = {9, 56, 120, 256};
+constexpr int kBinPerThread = 8;  // segments per thread per tile
+constexpr int kBinTile = kBlock * kBinPerThread;
+constexpr int kBinField = 12;  // bits per bin in a packed count
+
+__device__ __forceinline__ int bin_of(uint64_t len) {
+  const uint64_t m = (len + 15) >> 4;
+  int b = 0;
+#pragma unroll
+  for (int k = 0; k < kBins - 1; ++k) b += m > kBinMaxChunks[k];
+  return b;
+}
+
+// Packed per-bin counts: kBins fields of 12 bits in a uint64 (a tile holds
+// 2048 segments, so no field overflows and adding packed words never carries
+// across fields).
+__device__ __forceinline__ uint32_t field(uint64_t p, int b) {
+  return uint32_t(p >> (kBinField * b)) & ((1u << kBinField) - 1);
+}
+
+__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
+  const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint64_t u = __shfl_up(v, d, 64);
+    if (lane >= uint32_t(d)) v += u;
+  }
+  return v;
+}
+
+// exclusive block scan of packed counts; returns the block total in `total`
+__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total) {
+  __shared__ uint64_t wsum[kBlock / 64];
+  const uint64_t inc = wave_incl_scan(v);
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 63) wsum[w] = inc;
+  __syncthreads();
+  uint64_t before = 0;
+  total = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kBlock / 64; ++k) {
+    before += k < w ? wsum[k] : 0;
+    total += wsum[k];
+  }
+  __syncthreads();  // wsum is reused by the next tile
+  return before + inc - v;
+}
+
+// Dispatch plan of a binned batch, decided on the device (k_bin_plan, one
+// block after the stats pass) from
+// the bin sizes the binning pass recorded, with no host round trip: split into
+// bins, or run the whole batch with the long-segment geometry (the last bin's
+// launch takes every segment, in byte-balanced contiguous runs; the other
+// launches exit at once).  Cost model in ns, measured on MI355X
+// (tools/bin_probe.py):
+//   whole: max(bytes / 7100 GB/s, n * 0.45 ns)   one (64 x 8) group per segment
+//   split: sum over bins of max(bytes_b / rate_b, n_b * 0.1 ns) + 10 us, with
+//          rate 5000 GB/s for bins 0-3 and 6400 GB/s for the last (its
+//          segments are no longer contiguous in memory)
+__global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta, const uint32_t* __restrict__ cnt_part,
+                                                     const uint64_t* __restrict__ by_part, uint32_t parts, uint64_t n,
+                                                     int force) {
+  // totals per bin from the stats pass's per-block partials (parts <= kBlock:
+  // one partial per thread, all loads in flight together)
+  __shared__ uint32_t wc[kBlock / 64][kBins];
+  __shared__ uint64_t wb[kBlock / 64][kBins];
+  const uint32_t w = threadIdx.x >> 6;
+  const bool mine = threadIdx.x < parts;
+  uint32_t cs[kBins];
+  uint64_t vs[kBins];
+#pragma unroll
+  for (int k = 0; k < kBins; ++k) {
+    cs[k] = mine ? cnt_part[k * parts + threadIdx.x] : 0;
+    vs[k] = mine ? by_part[k * parts + threadIdx.x] : 0;
+  }
+#pragma unroll
+  for (int k = 0; k < kBins; ++k) {
+    uint32_t c = cs[k];
+    uint64_t v = vs[k];
+#pragma unroll
+    for (int d = 32; d >= 1; d >>= 1) {
+      c += __shfl_xor(c, d, 64);
+      v += __shfl_xor(v, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      wc[w][k] = c;
+      wb[w][k] = v;
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t total = 0, t = 10000;
+#pragma unroll
+    for (int k = 0; k < kBins; ++k) {
+      uint32_t c = 0;
+      uint64_t v = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < kBlock / 64; ++q) {
+        c += wc[q][k];
+        v += wb[q][k];
+      }
+      meta[kBinMetaCount + k] = c;
+      total += v;
+      const uint64_t tb = v / (k == kBins - 1 ? 6400 : 5000), tn = c / 10;
+      t += tb > tn ? tb : tn;
+    }
+    const uint64_t tb = total / 7100, tn = n * 45 / 100;
+    const bool split = force >= 0 ? force > 0 : t < (tb > tn ? tb : tn);
+    meta[kBinMetaPlan] = split ? 1u : 0u;
+  }
+}
+
 // Where a launch finds its segments: fixed stride, packed offsets, or a
 // length bin written by k_bin_segments (entries {start lo, start hi, length,
-// segment index}; the bin's size is read from *count on the device, so the
-// launch needs no host round trip).
+// segment index}; capacity n, so any index < n is a safe read).
 struct SegSrc {
   const uint64_t* offsets;
   uint64_t stride, seg_len;
-  const u32x4* list;
-  const uint32_t* count;
-  const uint32_t* base;
+  const u32x4* list;     // bin launch: this bin's entries
+  const uint32_t* meta;  // bin launch: the binning pass's sizes and plan
+  int bin;
 };
+
+// A launch's work, resolved once at kernel start: the bin's list (split plan)
+// or, for the last bin's launch under the whole-batch plan, every segment by
+// index.  Items are walked by a grid stride; the last bin's launch has one
+// lane group per segment of the batch (no stride), bins 0..3 a capped grid.
+struct Work {
+  uint64_t items;
+  const u32x4* list;  // null: segment i = item i
+};
+
+__device__ __forceinline__ Work resolve(const SegSrc& src, uint64_t n) {
+  if (!src.list) return Work{n, nullptr};
+  // selects, not branches, keep every path explicit
+  const uint32_t split = src.meta[kBinMetaPlan];
+  const bool last = src.bin == kBins - 1;
+  Work w;
+  w.items = split ? uint64_t(src.meta[kBinMetaCount + src.bin]) : (last ? n : 0);
+  w.list = split ? src.list : nullptr;
+  return w;
+}
 
 constexpr uint32_t kLongEntry = 0xFFFFFFFFu;  // entry length: >= 4 GiB, re-read the offsets
 
-__device__ __forceinline__ uint64_t src_count(const SegSrc& src, uint64_t n) {
-  return src.list ? uint64_t(*src.count) : n;
+// Raw metadata of one work item (loads from clamped indices, so they are
+// unconditional and never wait at a join).
+struct ItemMeta {
+  u32x4 ent;     // list entry
+  uint64_t a, b;  // offsets[i], offsets[i + 1]
+};
+
+__device__ __forceinline__ ItemMeta src_fetch(const SegSrc& src, const Work& w, uint64_t gi, uint64_t n) {
+  ItemMeta m{};
+  const uint64_t c = gi < n ? gi : n - 1;  // list capacity n, offsets n + 1
+  if (w.list) {
+    m.ent = w.list[c];
+  } else if (src.offsets) {
+    m.a = src.offsets[c];
+    m.b = src.offsets[c + 1];
+  }
+  return m;
 }
 
-// segment number, start and end of work item gi (< src_count)
-__device__ __forceinline__ void src_locate(const SegSrc& src, uint64_t gi, uint64_t& seg, uint64_t& s,
-                                           uint64_t& e) {
-  if (src.list) {
-    const u32x4 ent = src.list[*src.base + gi];
-    seg = ent.w;
-    if (ent.z != kLongEntry) {
-      s = uint64_t(ent.x) | (uint64_t(ent.y) << 32);
-      e = s + ent.z;
+// segment number, start and end of work item gi; an item past the end
+// (gi >= items) gets seg = s = e = 0
+__device__ __forceinline__ void src_decode(const SegSrc& src, const Work& w, uint64_t gi, const ItemMeta& m,
+                                           uint64_t& seg, uint64_t& s, uint64_t& e) {
+  seg = s = e = 0;
+  if (gi >= w.items) return;
+  if (w.list) {
+    seg = m.ent.w;
+    if (m.ent.z != kLongEntry) {
+      s = uint64_t(m.ent.x) | (uint64_t(m.ent.y) << 32);
+      e = s + m.ent.z;
     } else {
       seg_bounds(src.offsets, 0, 0, seg, s, e);
     }
   } else {
     seg = gi;
-    seg_bounds(src.offsets, src.stride, src.seg_len, gi, s, e);
+    if (src.offsets) {
+      s = m.a;
+      e = m.b;
+    } else {
+      s = gi * src.stride;
+      e = s + src.seg_len;
+    }
   }
+}
+
+__device__ __forceinline__ void src_locate(const SegSrc& src, const Work& w, uint64_t gi, uint64_t n,
+                                           uint64_t& seg, uint64_t& s, uint64_t& e) {
+  src_decode(src, w, gi, src_fetch(src, w, gi, n), seg, s, e);
 }
 
 // ------------------------------------------------------------ a1-a4 -------
 // `init` / `odd` are never null here: an absent array is replaced by a
 // 16-byte zero buffer read with index step 0 (init_step / odd_step).
+// (block blk of nblk: a kernel of its own, or one bin's share of k_checksum_bins)
 template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
-__global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes, SegSrc src,
-                                                     const uint32_t* __restrict__ init,
-                                                     uint32_t init_step,
-                                                     const uint8_t* __restrict__ odd,
-                                                     uint32_t odd_step,
-                                                     void* __restrict__ out, uint64_t n) {
+__device__ __forceinline__ void checksum_body(const uint8_t* __restrict__ bytes, const SegSrc& src,
+                                              const uint32_t* __restrict__ init, uint32_t init_step,
+                                              const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                              void* __restrict__ out, uint64_t n, uint32_t blk, uint32_t nblk) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
-  const uint64_t step = uint64_t(gridDim.x) * kGroups;
-  const uint64_t items = src_count(src, n);
-  // the loop bound is uniform per block, so every lane reaches the DPP sums
-  for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups; g0 < items; g0 += step) {
-    const uint64_t gi = g0 + threadIdx.x / LPS;
-    const bool valid = gi < items;
-    uint64_t seg = 0, s = 0, e = 0;
-    if (valid) src_locate(src, gi, seg, s, e);
+  const Work w = resolve(src, n);
+  auto item = [&](uint64_t gi, const ItemMeta& m) {
+    uint64_t seg, s, e;
+    src_decode(src, w, gi, m, seg, s, e);
+    const bool valid = gi < w.items;
     // per-segment metadata is requested together with the byte stream, so a
     // wave waits on memory once (the leader lane folds it in at the end)
     // (unconditional loads from a clamped index: a load under a divergent
@@ -112,7 +271,23 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
       else
         static_cast<uint32_t*>(out)[seg] = sum;
     }
+  };
+  // the pass bound is uniform per block, so every lane reaches the DPP sums
+  for (uint64_t g0 = uint64_t(blk) * kGroups; g0 < w.items; g0 += uint64_t(nblk) * kGroups) {
+    const uint64_t gi = g0 + threadIdx.x / LPS;
+    item(gi, src_fetch(src, w, gi, n));
   }
+}
+
+template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes, SegSrc src,
+                                                     const uint32_t* __restrict__ init,
+                                                     uint32_t init_step,
+                                                     const uint8_t* __restrict__ odd,
+                                                     uint32_t odd_step,
+                                                     void* __restrict__ out, uint64_t n) {
+  checksum_body<LPS, UNROLL, NT, MODE, OUT>(bytes, src, init, init_step, odd, odd_step, out, n, blockIdx.x,
+                                            gridDim.x);
 }
 
 // Small segments (a few 16-byte chunks): a lane group owns SEGS segments per
@@ -124,20 +299,17 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
 // segment (range_sums_masked semantics); a segment longer than LPS*UNROLL
 // chunks finishes in a loop.  Absent per-segment arrays: zero16 + step 0.
 template <int LPS, int UNROLL, int SEGS, int OUT>
-__global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __restrict__ bytes, SegSrc src,
-                                                           const uint32_t* __restrict__ init,
-                                                           uint32_t init_step,
-                                                           const uint8_t* __restrict__ odd,
-                                                           uint32_t odd_step,
-                                                           const u32x4* __restrict__ zero16,
-                                                           void* __restrict__ out, uint64_t n) {
+__device__ __forceinline__ void checksum_small_body(const uint8_t* __restrict__ bytes, const SegSrc& src,
+                                                    const uint32_t* __restrict__ init, uint32_t init_step,
+                                                    const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                                    const u32x4* __restrict__ zero16, void* __restrict__ out,
+                                                    uint64_t n, uint32_t blk, uint32_t nblk) {
   constexpr uint32_t kGroups = kBlock / LPS;
   constexpr uint32_t kSlots = LPS * UNROLL;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint32_t group = threadIdx.x / LPS;
-  const uint64_t step = uint64_t(gridDim.x) * kGroups * SEGS;
-  const uint64_t items = src_count(src, n);
-  for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups * SEGS; g0 < items; g0 += step) {
+  const Work w = resolve(src, n);  // never a whole-batch run (the last bin is not small)
+  for (uint64_t g0 = uint64_t(blk) * kGroups * SEGS; g0 < w.items; g0 += uint64_t(nblk) * kGroups * SEGS) {
     uint64_t s[SEGS], span[SEGS], segk[SEGS];
     bool validk[SEGS];
     uint32_t nch[SEGS], i0[SEGS], swap[SEGS];
@@ -145,11 +317,9 @@ __global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __rest
 #pragma unroll
     for (int k = 0; k < SEGS; ++k) {
       const uint64_t gi = g0 + uint64_t(k) * kGroups + group;
-      validk[k] = gi < items;
-      uint64_t e = 0;
-      s[k] = 0;
-      segk[k] = 0;
-      if (validk[k]) src_locate(src, gi, segk[k], s[k], e);
+      validk[k] = gi < w.items;
+      uint64_t e;
+      src_locate(src, w, gi, n, segk[k], s[k], e);
       const uint64_t a0 = s[k] & ~uint64_t(15);
       span[k] = e > s[k] ? e - a0 : 0;
       nch[k] = uint32_t((span[k] + 15) >> 4);
@@ -195,6 +365,48 @@ __global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __rest
           static_cast<uint32_t*>(out)[seg] = sum;
       }
     }
+  }
+}
+
+template <int LPS, int UNROLL, int SEGS, int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __restrict__ bytes, SegSrc src,
+                                                           const uint32_t* __restrict__ init,
+                                                           uint32_t init_step,
+                                                           const uint8_t* __restrict__ odd,
+                                                           uint32_t odd_step,
+                                                           const u32x4* __restrict__ zero16,
+                                                           void* __restrict__ out, uint64_t n) {
+  checksum_small_body<LPS, UNROLL, SEGS, OUT>(bytes, src, init, init_step, odd, odd_step, zero16, out, n,
+                                              blockIdx.x, gridDim.x);
+}
+
+// Bins 0..kBins-2 of a binned batch in ONE launch: nblk blocks per bin, each
+// bin with its own geometry (kBinGeometry; blocks of bin b = [b*nblk,
+// (b+1)*nblk)).  One launch instead of four: no drain between bins, and one
+// launch to skip under the whole-batch plan.
+template <int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum_bins(const uint8_t* __restrict__ bytes, SegSrc src,
+                                                          const uint32_t* __restrict__ init, uint32_t init_step,
+                                                          const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                                          const u32x4* __restrict__ zero16,
+                                                          void* __restrict__ out, uint64_t n, uint32_t nblk) {
+  const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x - b * nblk;
+  SegSrc bs = src;
+  bs.list = src.list + uint64_t(b) * n;
+  bs.bin = int(b);
+  switch (b) {
+    case 0:
+      checksum_small_body<4, 2, 2, OUT>(bytes, bs, init, init_step, odd, odd_step, zero16, out, n, blk, nblk);
+      break;
+    case 1:
+      checksum_body<16, 4, true, 3, OUT>(bytes, bs, init, init_step, odd, odd_step, out, n, blk, nblk);
+      break;
+    case 2:
+      checksum_body<16, 8, true, 3, OUT>(bytes, bs, init, init_step, odd, odd_step, out, n, blk, nblk);
+      break;
+    default:
+      checksum_body<32, 4, true, 3, OUT>(bytes, bs, init, init_step, odd, odd_step, out, n, blk, nblk);
+      break;
   }
 }
 
@@ -461,94 +673,74 @@ __global__ void k_ipv4_tcp_headers(uint8_t* __restrict__ dg, uint64_t stride, ui
 }
 
 
-// ------------------------------------------------------- length binning ---
-// Bin of a segment by its 16-byte chunk count; the boundaries are those of
-// pick_geometry, so bin b runs with the geometry pick_geometry gives a batch
-// of such segments.
-constexpr uint64_t kBinMaxChunks[kBins - 1] = {9, 56, 120, 256};
-constexpr int kBinPerThread = 8;  // segments per thread per tile
-constexpr int kBinTile = kBlock * kBinPerThread;
-constexpr int kBinField = 12;  // bits per bin in a packed count
-
-__device__ __forceinline__ int bin_of(uint64_t len) {
-  const uint64_t m = (len + 15) >> 4;
-  int b = 0;
-#pragma unroll
-  for (int k = 0; k < kBins - 1; ++k) b += m > kBinMaxChunks[k];
-  return b;
-}
-
-// Packed per-bin counts: kBins fields of 12 bits in a uint64 (a tile holds
-// 2048 segments, so no field overflows and adding packed words never carries
-// across fields).
-__device__ __forceinline__ uint32_t field(uint64_t p, int b) {
-  return uint32_t(p >> (kBinField * b)) & ((1u << kBinField) - 1);
-}
-
-__device__ __forceinline__ uint64_t wave_incl_scan(uint64_t v) {
-  const uint32_t lane = threadIdx.x & 63;
-#pragma unroll
-  for (int d = 1; d < 64; d <<= 1) {
-    const uint64_t u = __shfl_up(v, d, 64);
-    if (lane >= uint32_t(d)) v += u;
-  }
-  return v;
-}
-
-// exclusive block scan of packed counts; returns the block total in `total`
-__device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total) {
-  __shared__ uint64_t wsum[kBlock / 64];
-  const uint64_t inc = wave_incl_scan(v);
-  const uint32_t w = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 63) wsum[w] = inc;
-  __syncthreads();
-  uint64_t before = 0;
-  total = 0;
-#pragma unroll
-  for (uint32_t k = 0; k < kBlock / 64; ++k) {
-    before += k < w ? wsum[k] : 0;
-    total += wsum[k];
-  }
-  __syncthreads();  // wsum is reused by the next tile
-  return before + inc - v;
-}
-
-// pass 1: bin sizes (one atomic per bin per block)
-__global__ __launch_bounds__(kBlock) void k_bin_count(const uint64_t* __restrict__ off, uint64_t n,
-                                                      uint32_t* __restrict__ meta) {
+// Pass 1: segments and bytes per bin, one partial per block (no same-address
+// atomics: they serialise at a few ns each; no last-block reduction: its
+// device-wide fence writes back L2 in every block); k_bin_plan adds them up.
+__global__ __launch_bounds__(kBlock) void k_bin_stats(const uint64_t* __restrict__ off, uint64_t n,
+                                                      uint32_t* __restrict__ cnt_part,
+                                                      uint64_t* __restrict__ by_part) {
   uint32_t cnt[kBins] = {};
-  ICS_GRID_STRIDE(i, n) {
-    const int b = bin_of(off[i + 1] - off[i]);
+  uint64_t by[kBins] = {};
+  // tiles of kBinTile segments; a thread's kBinPerThread offset pairs are all
+  // requested before any is used
+  for (uint64_t t0 = uint64_t(blockIdx.x) * kBinTile; t0 < n; t0 += uint64_t(gridDim.x) * kBinTile) {
+    uint64_t a[kBinPerThread], z[kBinPerThread];
 #pragma unroll
-    for (int k = 0; k < kBins; ++k) cnt[k] += b == k;
+    for (int j = 0; j < kBinPerThread; ++j) {
+      const uint64_t i = t0 + uint64_t(j) * kBlock + threadIdx.x;
+      const uint64_t c = i < n ? i : n - 1;
+      a[j] = off[c];
+      z[j] = off[c + 1];
+    }
+#pragma unroll
+    for (int j = 0; j < kBinPerThread; ++j) {
+      const bool in = t0 + uint64_t(j) * kBlock + threadIdx.x < n;
+      const uint64_t len = z[j] - a[j];
+      const int b = bin_of(len);
+#pragma unroll
+      for (int k = 0; k < kBins; ++k) {
+        cnt[k] += in && b == k;
+        by[k] += in && b == k ? len : 0;
+      }
+    }
   }
-  __shared__ uint32_t bsum[kBins];
-  if (threadIdx.x < kBins) bsum[threadIdx.x] = 0;
-  __syncthreads();
+  __shared__ uint32_t wc[kBlock / 64][kBins];
+  __shared__ uint64_t wb[kBlock / 64][kBins];
+  const uint32_t w = threadIdx.x >> 6;
 #pragma unroll
   for (int k = 0; k < kBins; ++k) {
     uint32_t c = cnt[k];
+    uint64_t v = by[k];
 #pragma unroll
-    for (int d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, d, 64);
-    if ((threadIdx.x & 63) == 0 && c) atomicAdd(&bsum[k], c);
+    for (int d = 32; d >= 1; d >>= 1) {
+      c += __shfl_xor(c, d, 64);
+      v += __shfl_xor(v, d, 64);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      wc[w][k] = c;
+      wb[w][k] = v;
+    }
   }
   __syncthreads();
-  if (threadIdx.x < kBins && bsum[threadIdx.x]) atomicAdd(&meta[threadIdx.x], bsum[threadIdx.x]);
+  if (threadIdx.x < kBins) {
+    uint32_t c = 0;
+    uint64_t v = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kBlock / 64; ++q) {
+      c += wc[q][threadIdx.x];
+      v += wb[q][threadIdx.x];
+    }
+    cnt_part[threadIdx.x * gridDim.x + blockIdx.x] = c;
+    by_part[threadIdx.x * gridDim.x + blockIdx.x] = v;
+  }
 }
 
-// pass 2: scatter entries; bin b occupies [base_b, base_b + size_b) of the
-// list.  Each tile reserves its slice of every bin with one atomic per bin.
+// Pass 3 (split plan only): every tile reserves its slice of each bin with
+// one atomic per bin (bin b's list holds its entries at list + b * n).
 __global__ __launch_bounds__(kBlock) void k_bin_scatter(const uint64_t* __restrict__ off, uint64_t n,
                                                         uint32_t* __restrict__ meta,
                                                         u32x4* __restrict__ list) {
-  uint32_t base[kBins];
-  uint32_t acc = 0;
-#pragma unroll
-  for (int k = 0; k < kBins; ++k) {
-    base[k] = acc;
-    acc += meta[k];
-  }
-  if (blockIdx.x == 0 && threadIdx.x < kBins) meta[16 + threadIdx.x] = base[threadIdx.x];
+  if (meta[kBinMetaPlan] == 0) return;  // whole-batch plan: no lists
   __shared__ uint32_t resv[kBins];
   for (uint64_t t0 = uint64_t(blockIdx.x) * kBinTile; t0 < n; t0 += uint64_t(gridDim.x) * kBinTile) {
     uint64_t s[kBinPerThread], len[kBinPerThread];
@@ -569,14 +761,14 @@ __global__ __launch_bounds__(kBlock) void k_bin_scatter(const uint64_t* __restri
     uint64_t excl = block_excl_scan(mine, total);
     if (threadIdx.x < kBins) {
       const uint32_t c = field(total, threadIdx.x);
-      resv[threadIdx.x] = c ? atomicAdd(&meta[8 + threadIdx.x], c) : 0;
+      resv[threadIdx.x] = c ? atomicAdd(&meta[kBinMetaCursor + threadIdx.x], c) : 0;
     }
     __syncthreads();
 #pragma unroll
     for (int j = 0; j < kBinPerThread; ++j) {
       if (bin[j] < 0) continue;
       const int b = bin[j];
-      const uint32_t pos = base[b] + resv[b] + field(excl, b);
+      const uint64_t pos = uint64_t(b) * n + resv[b] + field(excl, b);
       excl += uint64_t(1) << (kBinField * b);
       const uint64_t i = t0 + uint64_t(j) * kBlock + threadIdx.x;
       const uint32_t l = len[j] < kLongEntry ? uint32_t(len[j]) : kLongEntry;
@@ -602,7 +794,7 @@ inline uint32_t blocks_for(uint64_t groups, uint32_t groups_per_block, uint32_t 
 }
 
 inline SegSrc src_of(const SegSpec& sp) {
-  return SegSrc{sp.offsets, sp.stride, sp.seg_len, static_cast<const u32x4*>(sp.list), sp.count, sp.base};
+  return SegSrc{sp.offsets, sp.stride, sp.seg_len, static_cast<const u32x4*>(sp.list), sp.meta, sp.bin};
 }
 
 template <int LPS, int UNROLL, bool NT, int MODE>
@@ -705,16 +897,47 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta,
+hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
                                hipStream_t st) {
   if (!offsets || n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   if (hipError_t e = hipMemsetAsync(meta, 0, kBinMetaWords * sizeof(uint32_t), st)) return e;
-  hipLaunchKernelGGL(k_bin_count, dim3(ew_blocks(n) < 2048 ? ew_blocks(n) : 2048), dim3(kBlock), 0, st,
-                     offsets, n, meta);
+  uint32_t* cnt_part = meta + kBinMetaWords;
+  uint64_t* by_part = reinterpret_cast<uint64_t*>(cnt_part + kBins * kBinStatBlocks);
+  const uint64_t tiles = (n + kBinTile - 1) / kBinTile;
+  const uint32_t parts = uint32_t(tiles < kBinStatBlocks ? tiles : kBinStatBlocks);
+  hipLaunchKernelGGL(k_bin_stats, dim3(parts), dim3(kBlock), 0, st, offsets, n, cnt_part, by_part);
   if (hipError_t e = hipGetLastError()) return e;
-  uint64_t tiles = (n + kBinTile - 1) / kBinTile;
+  hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(kBlock), 0, st, meta, cnt_part, by_part, parts, n, force_plan);
+  if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL(k_bin_scatter, dim3(uint32_t(tiles < 2048 ? tiles : 2048)), dim3(kBlock), 0, st,
                      offsets, n, meta, static_cast<u32x4*>(list));
+  return hipGetLastError();
+}
+
+// geometries k_checksum_bins hard-codes for bins 0..kBins-2
+constexpr Geometry kBinGeometry[kBins - 1] = {{4, 2, true, 2, 2}, {16, 4, true, 3, 1}, {16, 8, true, 3, 1},
+                                              {32, 4, true, 3, 1}};
+
+hipError_t launch_checksum_bins(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
+                                int out_kind, uint32_t blocks_per_bin, hipStream_t st) {
+  for (int b = 0; b < kBins - 1; ++b) {  // the table must agree with bin_geometry
+    const Geometry g = bin_geometry(b), h = kBinGeometry[b];
+    if (g.lps != h.lps || g.unroll != h.unroll || g.nt != h.nt || g.mode != h.mode || g.segs != h.segs)
+      return hipErrorInvalidValue;
+  }
+  if (!sp.list || blocks_per_bin == 0) return hipErrorInvalidValue;
+  if (blocks_per_bin > (1u << 20)) blocks_per_bin = 1u << 20;  // grid work-items stay < 2^32
+  const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
+  const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
+  const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
+  const u32x4* z = static_cast<const u32x4*>(sp.zero16);
+  const dim3 grid(blocks_per_bin * (kBins - 1));
+  if (out_kind == 0)
+    hipLaunchKernelGGL(k_checksum_bins<0>, grid, dim3(kBlock), 0, st, sp.bytes, src_of(sp), ip, is, op, os, z,
+                       out, sp.n, blocks_per_bin);
+  else
+    hipLaunchKernelGGL(k_checksum_bins<1>, grid, dim3(kBlock), 0, st, sp.bytes, src_of(sp), ip, is, op, os, z,
+                       out, sp.n, blocks_per_bin);
   return hipGetLastError();
 }
 
@@ -726,9 +949,9 @@ Geometry bin_geometry(int bin) {
 
 SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, int bin) {
   SegSpec sp = whole;
-  sp.list = list;
-  sp.count = meta + bin;
-  sp.base = meta + 16 + bin;
+  sp.list = static_cast<const u32x4*>(list) + uint64_t(bin) * whole.n;
+  sp.meta = meta;
+  sp.bin = bin;
   return sp;
 }
 

@@ -28,28 +28,44 @@ struct SegSpec {
   uint64_t seg_len;
   uint64_t n;
   const void* zero16;  // 16 zero bytes in device memory (stand-in for absent arrays)
-  // length-binned launch: work items come from a bin list (16-byte entries,
-  // see launch_bin_segments) of *count entries starting at entry *base;
-  // n stays the batch size (an upper bound of *count)
+  // length-binned launch (bin_spec): bin `bin`'s list (16-byte entries, see
+  // launch_bin_segments) and the binning pass's meta words; n stays the batch
+  // size (the list's capacity)
   const void* list = nullptr;
-  const uint32_t* count = nullptr;
-  const uint32_t* base = nullptr;
+  const uint32_t* meta = nullptr;
+  int bin = -1;
 };
 
 // Length binning of an offsets batch (mixed segment sizes): every segment
 // goes to the bin whose geometry suits its length, and each bin is run with
 // its own geometry, reading its work list on the device.
-//   list  n entries of 16 bytes ({start lo, start hi, length, segment};
-//         length 0xFFFFFFFF = re-read the offsets), bins stored back to back
-//   meta  kBinMetaWords uint32: [0, kBins) bin sizes, [8, 8 + kBins) cursors,
-//         [16, 16 + kBins) bin bases (written by the scatter pass)
-// Needs n < 2^32.  The launcher zeroes meta itself.
+//   list  kBins * n entries of 16 bytes ({start lo, start hi, length,
+//         segment}; length 0xFFFFFFFF = re-read the offsets): bin b's
+//         entries at list + b * n, in no particular order
+//   meta  kBinMetaBytesTotal bytes: bin sizes at kBinMetaCount, the plan at
+//         kBinMetaPlan, scatter cursors, then the stats pass's partials
+// Passes: bin statistics, a one-block plan kernel and, under the split plan
+// only, the scatter into the lists; needs n < 2^32.  The launcher zeroes meta itself.  The plan
+// (k_bin_plan) decides on the device whether the batch runs split into bins
+// or whole with the long-segment geometry (then the last bin's launch, one
+// lane group per segment of the batch, takes every segment).
 constexpr int kBins = 5;
+constexpr int kBinMetaCount = 0;
+constexpr int kBinMetaCursor = 20;  // scatter pass: entries placed per bin
+constexpr int kBinMetaPlan = 28;    // 1: split into bins, 0: whole batch
 constexpr int kBinMetaWords = 32;
-hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta,
+constexpr uint32_t kBinStatBlocks = 256;  // stats pass partials follow meta (<= 256: one per plan thread)
+// bytes of meta + the stats pass's partials (the lists follow, 16-byte aligned)
+constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks * 12;
+// force_plan: -1 the device plan decides, 0 whole batch, 1 split (tests)
+hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
                                hipStream_t st);
 Geometry bin_geometry(int bin);
-// bin b's launch spec: list = bin's entries, count = its size
+// bins 0..kBins-2 in one launch (sp = bin_spec(whole, list, meta, 0)),
+// blocks_per_bin blocks striding over each bin
+hipError_t launch_checksum_bins(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
+                                int out_kind, uint32_t blocks_per_bin, hipStream_t st);
+// bin b's launch spec
 SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, int bin);
 
 // out_kind 0: u16 value(), 1: u32 raw sum

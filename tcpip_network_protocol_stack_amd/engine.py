@@ -43,6 +43,11 @@ class Engine:
         check(self.lib.ics_create(self.device.index or 0, ctypes.byref(ctx)))
         self.ctx = ctx
 
+    def set_binning(self, mode):
+        """Dispatch of offsets batches: _lib.ICS_BINNING_AUTO / SINGLE / BINNED
+        (ics_set_binning)."""
+        check(self.lib.ics_set_binning(self.ctx, int(mode)))
+
     def close(self):
         if self.ctx:
             self.lib.ics_destroy(self.ctx)

@@ -64,9 +64,8 @@ def main():
     args = ap.parse_args()
     only = set(args.only.split(","))
     eng = Engine(0)
-    os.environ["ICSUM_BIN"] = "0"  # single-geometry dispatch for offsets batches, for comparison
     eng_nobin = Engine(0)
-    del os.environ["ICSUM_BIN"]
+    eng_nobin.set_binning(0)  # ICS_BINNING_SINGLE: single-geometry dispatch of offsets batches, for comparison
     dev = torch.device("cuda", 0)
 
     if "ns" in only:  # north star: 1 M x 1500 B, pseudo-header inits
