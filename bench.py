@@ -204,9 +204,12 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize(dev)
+    # this rank's time stops when its own K steps have drained; the closing
+    # barrier keeps the ranks bracketed, and the MAX below makes the slowest
+    # rank's time the job's (a barrier's own latency is not a step's work)
+    elapsed = time.perf_counter() - t0
     if world > 1:
         dist.barrier()
-    elapsed = time.perf_counter() - t0
     elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None,
                                    dev if backend == "nccl" else torch.device("cpu"))
     kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # average launch duration (this rank)
