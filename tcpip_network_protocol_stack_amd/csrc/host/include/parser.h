@@ -1,13 +1,23 @@
-// parser.h — drop-in Parser / Serializer (reference: util/tools/parser.h:17-289).
+// parser.h — the stack's byte codec: Parser, Serializer, parse<T>(),
+// serialize<T>() (reference util/tools/parser.h:17-289).
 //
-// Same API and error behaviour: Parser reads big-endian integers out of a
-// list of string pieces and sets an error flag (never throws) on underflow;
-// Serializer appends big-endian integers to a pending buffer and whole string
-// pieces (taken by value, not copied twice) to its output list.  parse<T>() and
-// serialize<T>() are the generic entry points the stack calls.
+// Contract kept from the reference (the stack's code and its error handling
+// depend on it):
+//   * input and output are lists of std::string pieces; a value may straddle
+//     two pieces;
+//   * integers are big-endian; a read past the end sets the error flag and
+//     leaves the destination untouched — Parser never throws on short input;
+//   * all_remaining() hands the unread bytes over piece by piece (the first one
+//     trimmed), buffer() views them without copying — TCPSegment::parse
+//     checksums exactly those views;
+//   * Serializer gathers integers in a pending piece and appends whole
+//     strings as their own pieces, so a payload is moved, never re-copied.
 //
-// Implementation differs from the reference: the parser keeps the pieces in a
-// vector with a (piece, offset) cursor instead of a deque of owned strings.
+// Representation (ours): the Parser owns the pieces in a vector and keeps a
+// flat read cursor (piece index + offset into it).  Reads that fit in the
+// current piece take one memcpy + byte swap instead of a byte loop.  The
+// reference's nested BufferList and Parser::input() accessor are not part of
+// this surface: nothing on the stack's path uses them.
 #ifndef ICSUM_HOST_PARSER_H
 #define ICSUM_HOST_PARSER_H
 
@@ -16,205 +26,213 @@
 #include <cstdint>
 #include <cstring>
 #include <span>
-#include <stdexcept>
 #include <string>
 #include <string_view>
 #include <utility>
 #include <vector>
 
+namespace icsum::detail {
+template <std::unsigned_integral T>
+constexpr T from_big_endian(T v)
+{
+    if constexpr (sizeof(T) == 1) return v;
+    else if constexpr (sizeof(T) == 2) return static_cast<T>(__builtin_bswap16(v));
+    else if constexpr (sizeof(T) == 4) return static_cast<T>(__builtin_bswap32(v));
+    else return static_cast<T>(__builtin_bswap64(v));
+}
+}  // namespace icsum::detail
+
 class Parser
 {
-    class BufferList
+    std::vector<std::string> chunks_;
+    size_t cur_ = 0;         // index of the chunk the cursor is in
+    size_t pos_ = 0;         // cursor offset inside chunks_[cur_]
+    uint64_t remaining_ = 0; // unread bytes across all chunks
+    bool error_ = false;
+
+    // advance past exhausted chunks so chunks_[cur_] (if any) has unread bytes
+    void normalise()
     {
-        std::vector<std::string> pieces_{};
-        size_t piece_ = 0;   // first piece with unread bytes
-        uint64_t skip_ = 0;  // bytes already consumed from pieces_[piece_]
-        uint64_t size_ = 0;  // unread bytes in total
-
-        void settle()
-        {
-            while (piece_ < pieces_.size() && skip_ == pieces_[piece_].size()) {
-                ++piece_;
-                skip_ = 0;
-            }
+        while (cur_ < chunks_.size() && pos_ >= chunks_[cur_].size()) {
+            ++cur_;
+            pos_ = 0;
         }
+    }
 
-      public:
-        explicit BufferList(const std::vector<std::string>& buffers)
-        {
-            for (const auto& b : buffers) append(b);
-        }
-
-        uint64_t size() const { return size_; }
-        uint64_t serialized_length() const { return size_; }
-        bool empty() const { return size_ == 0; }
-
-        std::string_view peek() const
-        {
-            if (piece_ >= pieces_.size()) throw std::runtime_error("peek on empty BufferList");
-            return std::string_view{pieces_[piece_]}.substr(skip_);
-        }
-
-        void remove_prefix(uint64_t len)
-        {
-            while (len > 0 && piece_ < pieces_.size()) {
-                const uint64_t avail = pieces_[piece_].size() - skip_;
-                const uint64_t take = std::min(len, avail);
-                skip_ += take;
-                size_ -= take;
-                len -= take;
-                settle();
-            }
-        }
-
-        void dump_all(std::vector<std::string>& out)
-        {
-            out.clear();
-            for (size_t i = piece_; i < pieces_.size(); ++i) {
-                std::string s = std::move(pieces_[i]);
-                if (i == piece_ && skip_) s.erase(0, skip_);
-                if (!s.empty()) out.emplace_back(std::move(s));
-            }
-            pieces_.clear();
-            piece_ = 0;
-            skip_ = 0;
-            size_ = 0;
-        }
-
-        void dump_all(std::string& out)
-        {
-            std::vector<std::string> parts;
-            dump_all(parts);
-            if (parts.size() == 1) {
-                out = std::move(parts.front());
-                return;
-            }
-            out.clear();
-            for (const auto& s : parts) out.append(s);
-        }
-
-        std::vector<std::string_view> buffer() const
-        {
-            std::vector<std::string_view> r;
-            if (empty()) return r;
-            r.reserve(pieces_.size() - piece_);
-            for (size_t i = piece_; i < pieces_.size(); ++i)
-                r.push_back(std::string_view{pieces_[i]}.substr(i == piece_ ? skip_ : 0));
-            return r;
-        }
-
-        void append(std::string str)
-        {
-            size_ += str.size();
-            if (!str.empty()) pieces_.push_back(std::move(str));
-            settle();
-        }
-    };
-
-    BufferList input_;
-    bool error_{};
-
-    void check_size(size_t size)
+    // copy n unread bytes (n <= remaining_) into dst and consume them
+    void take(char* dst, size_t n)
     {
-        if (size > input_.size()) error_ = true;
+        while (n) {
+            const std::string& c = chunks_[cur_];
+            const size_t k = std::min(n, c.size() - pos_);
+            std::memcpy(dst, c.data() + pos_, k);
+            dst += k;
+            n -= k;
+            pos_ += k;
+            remaining_ -= k;
+            normalise();
+        }
+    }
+
+    bool need(uint64_t n)
+    {
+        if (n > remaining_) error_ = true;
+        return !error_;
     }
 
   public:
-    explicit Parser(const std::vector<std::string>& input) : input_(input) {}
+    explicit Parser(const std::vector<std::string>& input)
+    {
+        chunks_.reserve(input.size());
+        for (const std::string& s : input) {
+            if (s.empty()) continue;
+            remaining_ += s.size();
+            chunks_.push_back(s);
+        }
+    }
 
-    const BufferList& input() const { return input_; }
     bool has_error() const { return error_; }
     void set_error() { error_ = true; }
-    void remove_prefix(size_t n) { input_.remove_prefix(n); }
 
-    // big-endian unsigned integer; sets the error flag if too few bytes remain
+    // skip up to n bytes (clamped at the end of the input, never an error)
+    void remove_prefix(size_t n)
+    {
+        uint64_t left = std::min<uint64_t>(n, remaining_);
+        remaining_ -= left;
+        while (left) {
+            const size_t k = std::min<uint64_t>(left, chunks_[cur_].size() - pos_);
+            pos_ += k;
+            left -= k;
+            normalise();
+        }
+        normalise();
+    }
+
     template <std::unsigned_integral T>
     void integer(T& out)
     {
-        check_size(sizeof(T));
-        if (has_error()) return;
-        T v = 0;
-        for (size_t i = 0; i < sizeof(T); ++i) {
-            if constexpr (sizeof(T) > 1) v <<= 8;
-            v |= static_cast<uint8_t>(input_.peek().front());
-            input_.remove_prefix(1);
+        if (!need(sizeof(T))) return;
+        T raw;
+        const std::string& c = chunks_[cur_];
+        if (c.size() - pos_ >= sizeof(T)) {  // common case: one memcpy
+            std::memcpy(&raw, c.data() + pos_, sizeof(T));
+            pos_ += sizeof(T);
+            remaining_ -= sizeof(T);
+            normalise();
+        } else {
+            take(reinterpret_cast<char*>(&raw), sizeof(T));
         }
-        out = v;
+        out = icsum::detail::from_big_endian(raw);
     }
 
     void string(std::span<char> out)
     {
-        check_size(out.size());
-        if (has_error()) return;
-        size_t done = 0;
-        while (done < out.size()) {
-            const auto view = input_.peek().substr(0, out.size() - done);
-            std::memcpy(out.data() + done, view.data(), view.size());
-            done += view.size();
-            input_.remove_prefix(view.size());
-        }
+        if (!need(out.size())) return;
+        take(out.data(), out.size());
     }
 
-    void all_remaining(std::vector<std::string>& out) { input_.dump_all(out); }
-    void all_remaining(std::string& out) { input_.dump_all(out); }
-    std::vector<std::string_view> buffer() const { return input_.buffer(); }
+    void all_remaining(std::vector<std::string>& out)
+    {
+        out.clear();
+        for (; cur_ < chunks_.size(); ++cur_, pos_ = 0) {
+            std::string& c = chunks_[cur_];
+            if (pos_) c.erase(0, pos_);
+            if (!c.empty()) out.push_back(std::move(c));
+        }
+        chunks_.clear();
+        cur_ = pos_ = 0;
+        remaining_ = 0;
+    }
+
+    void all_remaining(std::string& out)
+    {
+        std::vector<std::string> parts;
+        all_remaining(parts);
+        if (parts.size() == 1) {
+            out = std::move(parts[0]);
+            return;
+        }
+        out.clear();
+        out.reserve(remaining_bytes(parts));
+        for (const std::string& p : parts) out += p;
+    }
+
+    std::vector<std::string_view> buffer() const
+    {
+        std::vector<std::string_view> views;
+        if (remaining_ == 0) return views;
+        views.reserve(chunks_.size() - cur_);
+        views.emplace_back(chunks_[cur_].data() + pos_, chunks_[cur_].size() - pos_);
+        for (size_t i = cur_ + 1; i < chunks_.size(); ++i) views.emplace_back(chunks_[i]);
+        return views;
+    }
+
+  private:
+    static size_t remaining_bytes(const std::vector<std::string>& parts)
+    {
+        size_t n = 0;
+        for (const std::string& p : parts) n += p.size();
+        return n;
+    }
 };
 
 class Serializer
 {
-    std::vector<std::string> output_{};
-    std::string buffer_{};
+    std::vector<std::string> pieces_{};
+    std::string pending_{};  // integers written since the last whole piece
 
   public:
     Serializer() = default;
-    explicit Serializer(std::string&& buffer) : buffer_(std::move(buffer)) {}
+    explicit Serializer(std::string&& buffer) : pending_(std::move(buffer)) {}
 
     template <std::unsigned_integral T>
     void integer(const T val)
     {
-        for (size_t i = sizeof(T); i-- > 0;) buffer_.push_back(static_cast<char>(static_cast<uint8_t>(val >> (8 * i))));
+        const T be = icsum::detail::from_big_endian(val);  // the swap is its own inverse
+        pending_.append(reinterpret_cast<const char*>(&be), sizeof(T));
     }
 
     void buffer(std::string buf)
     {
         flush();
-        if (!buf.empty()) output_.push_back(std::move(buf));
+        if (!buf.empty()) pieces_.push_back(std::move(buf));
     }
 
     void buffer(const std::vector<std::string>& bufs)
     {
-        for (const auto& b : bufs) buffer(b);
+        for (const std::string& b : bufs) buffer(b);
     }
 
     void flush()
     {
-        if (!buffer_.empty()) {
-            output_.emplace_back(std::move(buffer_));
-            buffer_.clear();
-        }
+        if (pending_.empty()) return;
+        pieces_.push_back(std::move(pending_));
+        pending_.clear();
     }
 
     const std::vector<std::string>& output()
     {
         flush();
-        return output_;
+        return pieces_;
     }
 };
 
+// obj.serialize(Serializer&) -> its pieces
 template <typename T>
 std::vector<std::string> serialize(const T& obj)
 {
-    Serializer s;
-    obj.serialize(s);
-    return s.output();
+    Serializer out;
+    obj.serialize(out);
+    return out.output();
 }
 
+// obj.parse(Parser&, extra...) over `buffers`; true iff no error was flagged
 template <typename T, typename... Targs>
 bool parse(T& obj, const std::vector<std::string>& buffers, Targs&&... Fargs)
 {
-    Parser p{buffers};
-    obj.parse(p, std::forward<Targs>(Fargs)...);
-    return !p.has_error();
+    Parser in{buffers};
+    obj.parse(in, std::forward<Targs>(Fargs)...);
+    return !in.has_error();
 }
 
 #endif

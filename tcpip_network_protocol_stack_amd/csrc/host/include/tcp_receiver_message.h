@@ -1,17 +1,4 @@
-// tcp_receiver_message.h — reference: util/tools/tcp_receiver_message.h:22-27
-#ifndef ICSUM_HOST_TCP_RECEIVER_MESSAGE_H
-#define ICSUM_HOST_TCP_RECEIVER_MESSAGE_H
-
-#include <cstdint>
-#include <optional>
-
-#include "wrapping_integers.h"
-
-struct TCPReceiverMessage
-{
-    std::optional<Wrap32> ackno{};
-    uint16_t window_size{};
-    bool RST{};
-};
-
-#endif
+// tcp_receiver_message.h: include-name forwarder.  The stack #includes "tcp_receiver_message.h" (reference
+// util/tools/tcp_receiver_message.h); the declarations live in icsum_wire.h.
+#pragma once
+#include "icsum_wire.h"

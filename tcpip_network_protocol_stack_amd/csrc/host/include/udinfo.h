@@ -1,14 +1,4 @@
-// udinfo.h — reference: util/tools/udinfo.h:7-12 (holds the TCP checksum field)
-#ifndef ICSUM_HOST_UDINFO_H
-#define ICSUM_HOST_UDINFO_H
-
-#include <cstdint>
-
-struct UserDatagramInfo
-{
-    uint16_t src_port;
-    uint16_t dst_port;
-    uint16_t cksum;
-};
-
-#endif
+// udinfo.h: include-name forwarder.  The stack #includes "udinfo.h" (reference
+// util/tools/udinfo.h); the declarations live in icsum_wire.h.
+#pragma once
+#include "icsum_wire.h"

@@ -5,7 +5,7 @@
 #include <stdexcept>
 
 #include "icsum.h"
-#include "tcp_segment_internal.h"
+#include "wire_internal.h"
 
 namespace icsum {
 namespace {
@@ -117,12 +117,8 @@ std::vector<InternetDatagram> BatchEngine::wrap(TCPOverIPv4Adapter& adapter, std
     Packed p;
     for (size_t i = 0; i < msgs.size(); ++i) {
         TCPSegment& seg = segs[i];
-        seg.message = msgs[i];
-        seg.udinfo = {adapter.config().source.port(), adapter.config().destination.port(), 0};
         IPv4Header& h = out[i].header;
-        h.src = adapter.config().source.ipv4_numeric();
-        h.dst = adapter.config().destination.ipv4_numeric();
-        h.len = static_cast<uint16_t>(h.hlen * 4 + 20 + seg.message.sender.payload.size());
+        detail::stamp_outgoing(adapter.config(), msgs[i], h, seg);
         h.cksum = 0;
         append_wire(p, h, seg);
     }
@@ -139,28 +135,6 @@ std::vector<InternetDatagram> BatchEngine::wrap(TCPOverIPv4Adapter& adapter, std
     return out;
 }
 
-namespace {
-// tcp_over_ip.cpp:39-64 — the port / listening filters after a successful parse
-std::optional<TCPMessage> finish_unwrap(TCPOverIPv4Adapter& a, const IPv4Header& h, TCPSegment& seg)
-{
-    if (seg.udinfo.dst_port != a.config().source.port()) return {};
-    if (a.listening()) {
-        if (!seg.message.sender.SYN || seg.message.sender.RST) return {};
-        a.config_mut().source = Address{Address::from_ipv4_numeric(h.dst).ip(), a.config().source.port()};
-        a.config_mut().destination = Address{Address::from_ipv4_numeric(h.src).ip(), seg.udinfo.src_port};
-        a.set_listening(false);
-    }
-    if (seg.udinfo.src_port != a.config().destination.port()) return {};
-    return seg.message;
-}
-
-bool address_ok(const TCPOverIPv4Adapter& a, const IPv4Header& h)
-{
-    if (!a.listening() && h.dst != a.config().source.ipv4_numeric()) return false;
-    if (!a.listening() && h.src != a.config().destination.ipv4_numeric()) return false;
-    return h.proto == IPv4Header::PROTO_TCP;
-}
-}  // namespace
 
 std::vector<std::optional<TCPMessage>> BatchEngine::unwrap(TCPOverIPv4Adapter& adapter,
                                                            std::span<const InternetDatagram> dgrams)
@@ -181,12 +155,12 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap(TCPOverIPv4Adapter& a
     std::vector<std::optional<TCPMessage>> out(dgrams.size());
     for (size_t i = 0; i < dgrams.size(); ++i) {
         const IPv4Header& h = dgrams[i].header;
-        if (!address_ok(adapter, h) || v[i] != 0) continue;
+        if (!detail::ip_gate(adapter, h) || v[i] != 0) continue;
         TCPSegment seg;
         Parser parser{dgrams[i].payload};
         detail::parse_tcp_fields(parser, seg);
         if (parser.has_error()) continue;
-        out[i] = finish_unwrap(adapter, h, seg);
+        out[i] = detail::tcp_gate(adapter, h, seg);
     }
     return out;
 }
@@ -263,12 +237,12 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_packed(TCPOverIPv4Ada
         ipp.integer(dg.header.dst);
         ipp.remove_prefix(static_cast<uint64_t>(dg.header.hlen) * 4 - IPv4Header::LENGTH);
         ipp.all_remaining(dg.payload);
-        if (!address_ok(adapter, dg.header)) continue;
+        if (!detail::ip_gate(adapter, dg.header)) continue;
         TCPSegment seg;
         Parser tp{dg.payload};
         detail::parse_tcp_fields(tp, seg);
         if (tp.has_error()) continue;
-        out[i] = finish_unwrap(adapter, dg.header, seg);
+        out[i] = detail::tcp_gate(adapter, dg.header, seg);
     }
     return out;
 }

@@ -6,7 +6,7 @@
 #include "tcp_segment.h"
 
 #include "checksum.h"
-#include "tcp_segment_internal.h"
+#include "wire_internal.h"
 
 namespace {
 constexpr uint8_t kMinDataOffset = 5;  // 32-bit words
