@@ -64,6 +64,7 @@ struct ics_ctx {
   int bin = -1;
   uint64_t bin_min = 0;
   uint32_t bin_blocks = 0;  // grid of each bin's launch (its size is only known on the device)
+  uint32_t last_bin_blocks = 0;  // grid cap of the last bin's launch (0: one lane group per segment)
   int bin_plan = -1;        // -1: decided on the device per batch, 0: whole, 1: split (tests)
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
@@ -148,7 +149,8 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
                                     ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks, st);
   if (e == hipSuccess)
     e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, icsum::kBins - 1), d_init, d_odd, d_out, out_kind,
-                               icsum::bin_geometry(icsum::kBins - 1), ctx->max_blocks, st);
+                               icsum::bin_geometry(icsum::kBins - 1),
+                               ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks, st);
   if (e == hipSuccess && std::getenv("ICSUM_BIN_DEBUG")) {  // dev: dump the binning pass's meta words
     uint32_t h[icsum::kBinMetaWords];
     if (hipMemcpyAsync(h, meta, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess) {
@@ -382,7 +384,9 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin = std::getenv("ICSUM_BIN") ? int(env_u32("ICSUM_BIN", 1)) : -1;
   ctx->bin_min = env_u32("ICSUM_BIN_MIN", 1u << 16);
   ctx->bin_blocks = env_u32("ICSUM_BIN_BLOCKS", 2048);
+  ctx->last_bin_blocks = env_u32("ICSUM_LAST_BIN_BLOCKS", 0);
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
+  if (std::getenv("ICSUM_XCD_REMAP")) icsum::set_xcd_remap(env_u32("ICSUM_XCD_REMAP", 0));
   *out = ctx;
   return ICS_OK;
 }

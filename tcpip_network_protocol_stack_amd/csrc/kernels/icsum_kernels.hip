@@ -279,14 +279,47 @@ __device__ __forceinline__ void checksum_body(const uint8_t* __restrict__ bytes,
   }
 }
 
+// XCD-aware block order.  Blocks b and b + 8 are observed to share an XCD
+// (MI355X_MICROARCH.md §Workgroup dispatch: blocks are dealt round-robin over
+// the 8 XCDs), so the hardware order gives every XCD every 8th block — each
+// XCD's L2 and address translation see 8 disjoint pieces per run of blocks.
+// Remapped, XCD label x = b % 8 takes runs of c consecutive logical blocks
+// (c = min(run, grid / 8), powers of two): each XCD streams contiguous memory, neighbouring
+// segments (whose shared boundary lines mode 3 keeps in L2) sit on one XCD,
+// and the 8 runs still form one front of 8c blocks.  Blocks past the last
+// whole 8c window keep their order (a bijection for any grid).  Measured,
+// interleaved in one process on 5 boxes (profiles/r1_ab_xcd.jsonl):
+//   NS 1 M x 1500 B     213.3 -> 208.5 us   (FETCH 1.5855 -> 1.5771 GB)
+//   1 M x 9000 B       1307.0 -> 1255.5 us
+//   8 M x 9000 B      10524.9 -> 10087.9 us
+// (c = grid / 8, i.e. eight contiguous eighths, lost 1.8 % on the 75 GB batch).
+// c is a power of two (run_log2 caps it), so the mapping is shifts and masks:
+// short-lived blocks (small segments) pay a few scalar instructions, not an
+// emulated integer division per block.
+__device__ __forceinline__ uint32_t block_order(uint32_t run_log2) {
+  const uint32_t nblk = gridDim.x, b = blockIdx.x;
+  if (run_log2 == 0 || nblk < 16) return b;
+  const uint32_t fl = 31u - uint32_t(__builtin_clz(nblk >> 3));  // floor(log2(nblk / 8))
+  const uint32_t lc = fl < run_log2 ? fl : run_log2;              // c = 2^lc
+  const uint32_t full = (nblk >> (lc + 3)) << (lc + 3);           // whole 8c windows
+  if (b >= full) return b;
+  const uint32_t k = b >> 3, x = b & 7u;
+  return ((k >> lc) << (lc + 3)) + (x << lc) + (k & ((1u << lc) - 1u));
+}
+
 template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
 __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes, SegSrc src,
                                                      const uint32_t* __restrict__ init,
                                                      uint32_t init_step,
                                                      const uint8_t* __restrict__ odd,
                                                      uint32_t odd_step,
-                                                     void* __restrict__ out, uint64_t n) {
-  checksum_body<LPS, UNROLL, NT, MODE, OUT>(bytes, src, init, init_step, odd, odd_step, out, n, blockIdx.x,
+                                                     void* __restrict__ out, uint64_t n, uint32_t remap) {
+  // a bin launch whose bin is empty (the last bin under the split plan) is
+  // dispatch-bound — ~0.05 ns per wave whatever the block shape (measured,
+  // tools/probe/dispatch_probe.hip) — so its waves leave before anything else
+  if (src.list && resolve(src, n).items == 0) return;
+  const uint32_t blk = block_order(remap);
+  checksum_body<LPS, UNROLL, NT, MODE, OUT>(bytes, src, init, init_step, odd, odd_step, out, n, blk,
                                             gridDim.x);
 }
 
@@ -498,11 +531,11 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
                                                      int mode, uint16_t* __restrict__ ip_ck,
                                                      uint16_t* __restrict__ tcp_ck,
-                                                     uint8_t* __restrict__ status) {
+                                                     uint8_t* __restrict__ status, uint32_t remap) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
-  for (uint64_t g0 = uint64_t(blockIdx.x) * kGroups; g0 < n; g0 += step) {
+  for (uint64_t g0 = uint64_t(block_order(remap)) * kGroups; g0 < n; g0 += step) {
     const uint64_t seg = g0 + threadIdx.x / LPS;
     const bool valid = seg < n;
     uint64_t s = 0, e = 0;
@@ -793,6 +826,8 @@ inline uint32_t blocks_for(uint64_t groups, uint32_t groups_per_block, uint32_t 
   return uint32_t(b < cap ? b : cap);
 }
 
+uint32_t g_xcd_remap = 10;  // log2 of the XCD run length of block_order (1024 blocks); 0: hardware order
+
 inline SegSrc src_of(const SegSpec& sp) {
   return SegSrc{sp.offsets, sp.stride, sp.seg_len, static_cast<const u32x4*>(sp.list), sp.meta, sp.bin};
 }
@@ -806,10 +841,10 @@ hipError_t launch_checksum_t(const SegSpec& sp, const uint32_t* init, const uint
   const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
   if (out_kind == 0)
     hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, out, sp.n);
+                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap);
   else
     hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, out, sp.n);
+                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap);
   return hipGetLastError();
 }
 
@@ -836,7 +871,7 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
   hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, mode,
-                     ip_ck, tcp_ck, status);
+                     ip_ck, tcp_ck, status, g_xcd_remap);
   return hipGetLastError();
 }
 
@@ -940,6 +975,8 @@ hipError_t launch_checksum_bins(const SegSpec& sp, const uint32_t* init, const u
                        out, sp.n, blocks_per_bin);
   return hipGetLastError();
 }
+
+void set_xcd_remap(uint32_t run_log2) { g_xcd_remap = run_log2 < 31 ? run_log2 : 31; }
 
 Geometry bin_geometry(int bin) {
   // the upper edge of the bin (the last bin: a long segment)

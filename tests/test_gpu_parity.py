@@ -513,3 +513,38 @@ def test_router_random(engine, orc):
     assert st.tolist() == want
     assert (d.cpu().numpy() == hb).all()
     assert 0 < sum(want) < len(segs)
+
+
+@pytest.mark.parametrize("run", [0, 1, 3, 10])
+def test_xcd_block_order_is_a_permutation(run, orc):
+    """block_order (k_checksum / k_ipv4_tcp) only permutes blocks: every run
+    length (2^run blocks; 0 = hardware order), on grids that are not a multiple of the 8-block window, gives the
+    oracle's result for every segment (a dropped or doubled block would leave
+    outputs unwritten / wrong).  The order is process-wide, so the default is
+    restored afterwards."""
+    import torch
+
+    gen = _engine_with({"ICSUM_XCD_REMAP": str(run)})
+    eng = next(gen)
+    try:
+        rng = np.random.default_rng(run + 7)
+        for n, L in ((16 * 8 * 3 + 5, 1500), (16 * 8 * 1024 + 16 * 3 + 1, 576), (4 * 8 * 7 + 3, 9000)):
+            data = rng.integers(0, 256, n * L, dtype=np.uint8)
+            init = rng.integers(0, 1 << 20, n, dtype=np.uint32)
+            got = _u16(eng.checksum_batch(_t(data), n=n, stride=L, seg_len=L, init=_t(init)))
+            want = orc.checksum_batch(data, n, stride=L, seg_len=L, init=init)
+            assert (got == want).all(), (run, n, L, np.flatnonzero(got != want)[:8])
+        # the fused datagram kernel uses the same order
+        n, L = 16 * 8 * 3 + 9, 1500
+        dg = torch.empty(n * L, dtype=torch.uint8, device="cuda:0")
+        eng.fill_bytes(dg, 0x10710002)
+        eng.ipv4_tcp_headers(dg, n, L, L, 0x10710002)
+        ip, tcp, st = eng.ipv4_tcp_batch(dg, 0, n=n, stride=L, dgram_len=L)
+        host = dg.cpu().numpy().copy()
+        want_ip, want_tcp, want_st = orc.ipv4_tcp_batch(host, n, 0, stride=L, dgram_len=L)
+        assert (_u16(ip) == want_ip).all() and (_u16(tcp) == want_tcp).all()
+        assert (st.cpu().numpy() == want_st).all()
+    finally:
+        torch.cuda.synchronize()
+        eng.close()
+        next(_engine_with({"ICSUM_XCD_REMAP": "10"})).close()  # restore the default order
