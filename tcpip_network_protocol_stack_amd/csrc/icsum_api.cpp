@@ -65,6 +65,7 @@ struct ics_ctx {
   uint64_t bin_min = 0;
   uint32_t bin_blocks = 0;  // grid of each bin's launch (its size is only known on the device)
   uint32_t last_bin_blocks = 0;  // grid cap of the last bin's launch (0: one lane group per segment)
+  int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
   int bin_plan = -1;        // -1: decided on the device per batch, 0: whole, 1: split (tests)
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
@@ -131,6 +132,14 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
                       (ctx->bin == 1 || (ctx->bin < 0 && sp.n >= ctx->bin_min && !forced_geometry(ctx)));
   if (!binned) {
+    // dense fixed-stride batch of short segments (config 3): the flat kernel
+    if (!d_odd && ctx->dense_segs > 0 && !forced_geometry(ctx) && icsum::dense_supported(sp)) {
+      const hipError_t e = icsum::launch_checksum_dense(sp, d_init, d_out, out_kind, ctx->dense_segs, st);
+      if (e != hipErrorInvalidValue) {
+        ICS_HIP(e);
+        return ICS_OK;
+      }
+    }
     const icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len, sp.n, 0));
     ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
     return ICS_OK;
@@ -385,6 +394,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin_min = env_u32("ICSUM_BIN_MIN", 1u << 16);
   ctx->bin_blocks = env_u32("ICSUM_BIN_BLOCKS", 2048);
   ctx->last_bin_blocks = env_u32("ICSUM_LAST_BIN_BLOCKS", 0);
+  if (std::getenv("ICSUM_DENSE_SEGS")) ctx->dense_segs = int(env_u32("ICSUM_DENSE_SEGS", 4));
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
   if (std::getenv("ICSUM_XCD_REMAP")) icsum::set_xcd_remap(env_u32("ICSUM_XCD_REMAP", 0));
   *out = ctx;

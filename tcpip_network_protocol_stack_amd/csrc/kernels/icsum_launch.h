@@ -71,6 +71,13 @@ SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, i
 // out_kind 0: u16 value(), 1: u32 raw sum
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st);
+// Dense fixed-stride batches (stride == seg_len in {32, 64, 128}, 16-byte
+// aligned bytes, no parity array): k_checksum_dense, SEGS segments per lane
+// group in flight (segs in {1, 2, 4, 8}; not every (seg_len, segs) pair exists)
+bool dense_supported(const SegSpec& sp);
+hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* out, int out_kind, int segs,
+                                 hipStream_t st);
+
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
 void set_xcd_remap(uint32_t run_log2);  // log2 XCD run length (default 10 = 1024 blocks), 0: hardware order
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);

@@ -548,3 +548,37 @@ def test_xcd_block_order_is_a_permutation(run, orc):
         torch.cuda.synchronize()
         eng.close()
         next(_engine_with({"ICSUM_XCD_REMAP": "10"})).close()  # restore the default order
+
+
+@pytest.mark.parametrize("segs", [1, 2, 4, 8])
+def test_dense_fixed_stride_kernel(segs, orc):
+    """k_checksum_dense (stride == seg_len in {32, 64, 128}, aligned, no
+    parity array) at every SEGS: u16 values and raw u32 sums, with and without
+    inits, on batch sizes that leave partial waves and blocks; unsupported
+    (seg_len, segs) pairs fall back to the general kernels and must agree too."""
+    gen = _engine_with({"ICSUM_DENSE_SEGS": str(segs)})
+    eng = next(gen)
+    try:
+        rng = np.random.default_rng(100 + segs)
+        for L in (32, 64, 128):
+            for n in (1, 15, 16 * segs + 3, 4096 * 3 + 7):
+                data = rng.integers(0, 256, n * L, dtype=np.uint8)
+                init = rng.integers(0, 1 << 32, n, dtype=np.uint64).astype(np.uint32)
+                d = _t(data)
+                for ini in (None, init):
+                    got = _u16(eng.checksum_batch(d, n=n, stride=L, seg_len=L, init=None if ini is None else _t(ini)))
+                    want = orc.checksum_batch(data, n, stride=L, seg_len=L, init=ini)
+                    assert (got == want).all(), (segs, L, n, ini is None)
+                got = _u32(eng.sum_batch(d, n=n, stride=L, seg_len=L, init=_t(init)))
+                assert (got == orc.sum_batch(data, n, stride=L, seg_len=L, init=init)).all(), (segs, L, n)
+        # an all-0xFF batch: sums near the fold boundary, value() of 0xFFFF inits
+        n, L = 5000, 64
+        data = np.full(n * L, 0xFF, dtype=np.uint8)
+        init = np.full(n, 0xFFFF, dtype=np.uint32)
+        got = _u16(eng.checksum_batch(_t(data), n=n, stride=L, seg_len=L, init=_t(init)))
+        assert (got == orc.checksum_batch(data, n, stride=L, seg_len=L, init=init)).all()
+    finally:
+        import torch
+
+        torch.cuda.synchronize()
+        eng.close()
