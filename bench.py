@@ -106,26 +106,47 @@ def cpu_baseline(n_total, seg, seed, budget_s, gpu_out_head):
     ref = orc.ref_lib()
     kind = "reference" if ref is not None else "port"
 
-    def run():
-        if ref is not None:
-            ref.ref_checksum_batch(data.ctypes.data, None, seg, seg, init.ctypes.data, out.ctypes.data,
-                                   sample, threads)
-        else:
-            out[:] = orc.checksum_batch(data, sample, stride=seg, seg_len=seg, init=init, threads=threads)
+    def timed(nthreads, budget, count):
+        """passes of `count` segments on `nthreads` threads until `budget` s"""
+        def one():
+            if ref is not None:
+                ref.ref_checksum_batch(data.ctypes.data, None, seg, seg, init.ctypes.data, out.ctypes.data,
+                                       count, nthreads)
+            else:
+                out[:count] = orc.checksum_batch(data[: count * seg], count, stride=seg, seg_len=seg,
+                                                 init=init[:count], threads=nthreads)
+        one()  # warm
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            one()
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= budget:
+                return passes, el
 
-    run()  # warm
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        run()
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= budget_s:
-            break
+    passes, el = timed(threads, 0.75 * budget_s, sample)
     gib = passes * sample * seg / el / 2**30
     match = bool((out[: len(gpu_out_head)] == gpu_out_head).all())
+    # one core on a smaller slice, same bytes (SURVEY.md §8d: all cores plus a 1-core number)
+    one_n = max(1, sample // threads)
+    p1, el1 = timed(1, 0.25 * budget_s, one_n)
+    gib1 = p1 * one_n * seg / el1 / 2**30
     return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
+            "value_1core": round(gib1, 3), "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
             "sample": f"first {sample} segments x {seg} B of the same batch, {passes} passes "
-                      f"in {el:.1f} s; outputs bit-identical to the GPU: {match}"}
+                      f"in {el:.1f} s on {threads} threads ({one_n} segments, {p1} passes in {el1:.1f} s "
+                      f"on 1); outputs bit-identical to the GPU: {match}"}
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return None
 
 
 def main():

@@ -5,14 +5,24 @@
 // two peers move a bidirectional byte stream through wire datagrams with
 // checksums computed and verified by the drop-in path (per object on the
 // CPU, or per tick in one batch through icsum::BatchEngine with --gpu).
+//
+// BASELINE config 1 (the reference's own CPU case: 1 MiB through its stack,
+// checksums via util/tcp_over_ip) is this program.  oracle/ref/Makefile builds
+// the same source with -DICSUM_REFERENCE_UTIL against the reference's OWN util
+// sources (oracle/_ref/stack_loop_ref), so the wall time printed here compares
+// the reference path with the drop-in path on identical traffic.
+#include <chrono>
 #include <cstdio>
 #include <cstring>
 #include <memory>
+#include <optional>
 #include <random>
 #include <string>
 #include <vector>
 
+#ifndef ICSUM_REFERENCE_UTIL
 #include "batch.h"
+#endif
 #include "ipv4_datagram.h"
 #include "tcp_over_ip.h"
 #include "tcp_receiver.h"
@@ -37,9 +47,16 @@ std::string joined(const std::vector<std::string>& v)
 
 int main(int argc, char** argv)
 {
+#ifdef ICSUM_REFERENCE_UTIL
+    constexpr bool gpu = false;
+    (void)argc;
+    (void)argv;
+#else
     const bool gpu = argc > 1 && std::strcmp(argv[1], "--gpu") == 0;
     std::unique_ptr<icsum::BatchEngine> eng;
     if (gpu) eng = std::make_unique<icsum::BatchEngine>(0);
+#endif
+    const auto t0 = std::chrono::steady_clock::now();
     Peer a(137), b(4242);
     a.adapter.config_mut().source = Address{"169.254.144.9", 5555};
     a.adapter.config_mut().destination = Address{"169.254.145.9", 80};
@@ -75,19 +92,24 @@ int main(int argc, char** argv)
             if (msgs.empty() && (p.receiver.send().ackno.has_value()))
                 msgs.push_back(TCPMessage{p.sender.make_empty_message(), p.receiver.send()});
             std::vector<std::string> out;
+#ifndef ICSUM_REFERENCE_UTIL
             if (gpu) {
                 for (auto& d : eng->wrap(p.adapter, msgs)) out.push_back(joined(serialize(d)));
-            } else {
-                for (auto& m : msgs) out.push_back(joined(serialize(p.adapter.wrap_tcp_in_ip(m))));
+                return out;
             }
+#endif
+            for (auto& m : msgs) out.push_back(joined(serialize(p.adapter.wrap_tcp_in_ip(m))));
             return out;
         };
         auto deliver = [&](Peer& p, const std::vector<std::string>& ws) {
             std::vector<std::optional<TCPMessage>> msgs;
+#ifndef ICSUM_REFERENCE_UTIL
             if (gpu) {
                 std::vector<std::string_view> v(ws.begin(), ws.end());
                 msgs = eng->unwrap_raw(p.adapter, v);
-            } else {
+            }
+#endif
+            if (!gpu) {
                 for (auto& w : ws) {
                     IPv4Datagram dg;
                     msgs.push_back(parse(dg, std::vector<std::string>{w}) ? p.adapter.unwrap_tcp_in_ip(dg)
@@ -123,8 +145,14 @@ int main(int argc, char** argv)
         drain(a, got_down);
         if (b.receiver.reader().is_finished() && a.receiver.reader().is_finished()) break;
     }
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     const bool ok = got_up == up && got_down == down;
-    std::printf("%s: %s path, %zu + %zu bytes delivered bit-exact over %zu datagrams (%zu rejected)\n",
-                ok ? "OK" : "FAILED", gpu ? "GPU batch" : "CPU", got_up.size(), got_down.size(), wires, dropped);
+#ifdef ICSUM_REFERENCE_UTIL
+    const char* path = "reference util";
+#else
+    const char* path = gpu ? "GPU batch" : "CPU";
+#endif
+    std::printf("%s: %s path, %zu + %zu bytes delivered bit-exact over %zu datagrams (%zu rejected) in %.1f ms\n",
+                ok ? "OK" : "FAILED", path, got_up.size(), got_down.size(), wires, dropped, ms);
     return ok ? 0 : 1;
 }

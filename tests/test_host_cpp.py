@@ -74,6 +74,32 @@ def test_reference_stack_runs_on_dropin_types(selftest):
     assert out.stdout.startswith("OK: CPU path, 1048576 + 300000 bytes")
 
 
+def _loop_line(stdout):
+    line = [x for x in stdout.splitlines() if x.startswith(("OK", "FAILED"))][-1]
+    words = line.split()
+    return line, int(words[words.index("over") + 1]), int(words[words.index("over") + 3].strip("(")), \
+        float(words[-2])
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(ROOT, "oracle", "_ref", "stack_loop_ref")),
+                    reason="needs the reference built in place (oracle/_ref)")
+def test_config1_loopback_same_traffic_as_reference_util(selftest):
+    """BASELINE config 1: the same 1 MiB + 300 KB loopback program on the
+    reference's own util (oracle/_ref/stack_loop_ref) and on the drop-in types:
+    both deliver bit-exact, over the SAME number of datagrams with the SAME
+    number rejected by the checksum (one corrupted datagram in 50).  Wall times
+    are printed for DESIGN.md (not asserted: a shared CPU is noisy)."""
+    ref = subprocess.run([os.path.join(ROOT, "oracle", "_ref", "stack_loop_ref")], capture_output=True,
+                         text=True, timeout=300)
+    ours = subprocess.run([os.path.join(BIN, "dropin_stack")], capture_output=True, text=True, timeout=300)
+    assert ref.returncode == 0 and ours.returncode == 0
+    rl, rw, rd, rms = _loop_line(ref.stdout)
+    ol, ow, od, oms = _loop_line(ours.stdout)
+    assert rl.startswith("OK: reference util path, 1048576 + 300000 bytes")
+    assert (rw, rd) == (ow, od), (rl, ol)
+    print(f"\nconfig 1: reference util {rms:.1f} ms, drop-in CPU {oms:.1f} ms")
+
+
 def test_datagram_batch_socket_round_trip(selftest):
     # SURVEY §8f rank 4: batched datagram I/O (sendmmsg / recvmmsg into one
     # compacted arena with n+1 offsets) preserves every datagram byte for byte
