@@ -67,6 +67,7 @@ struct ics_ctx {
   uint32_t last_bin_blocks = 0;  // grid cap of the last bin's launch (0: one lane group per segment)
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
   int bin_plan = -1;        // -1: decided on the device per batch, 0: whole, 1: split (tests)
+  bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
   static constexpr size_t kSlotBytes = size_t(64) << 20;
@@ -333,7 +334,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       uint16_t* a = reinterpret_cast<uint16_t*>(ctx->d_out[slot]);
       uint16_t* b = a + m;
       uint8_t* s = ctx->d_out[slot] + m * 4;
-      ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, a, b, s, ipv4_geometry(g), ctx->max_blocks, st));
+      ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, a, b, s, ipv4_geometry(g), ctx->max_blocks, ctx->patch_wt, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 5, hipMemcpyDeviceToHost, st));
       if (mode == ICS_MODE_PATCH)
         ICS_HIP(hipMemcpyAsync(direct ? static_cast<uint8_t*>(h_bytes) + c.b0 : ctx->h_in[slot], ctx->d_in[slot],
@@ -396,6 +397,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->last_bin_blocks = env_u32("ICSUM_LAST_BIN_BLOCKS", 0);
   if (std::getenv("ICSUM_DENSE_SEGS")) ctx->dense_segs = int(env_u32("ICSUM_DENSE_SEGS", 4));
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
+  ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
   if (std::getenv("ICSUM_XCD_REMAP")) icsum::set_xcd_remap(env_u32("ICSUM_XCD_REMAP", 0));
   *out = ctx;
   return ICS_OK;
@@ -461,7 +463,7 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   if (!d_dgrams) return fail(ICS_ERR_INVALID, "null datagram buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
   const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, avg_len_hint(d_offsets, dgram_len, n, 0)));
-  ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks,
+  ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt,
                                  static_cast<hipStream_t>(stream)));
   return ICS_OK;
 }

@@ -520,13 +520,33 @@ __device__ __forceinline__ Hdr load_hdr(const uint8_t* p) {
   return h;
 }
 
-// big-endian 16-bit field store: one short store when 2-byte aligned
+// big-endian 16-bit field store: one short store when 2-byte aligned.
+// WT: write-through (sc1; a relaxed agent-scope atomic store is a plain
+// global_store_short/byte with sc1 on gfx950).  A patched field is the only
+// written part of its 128-byte line; a default-policy store leaves that line
+// dirty in the XCD's L2 until the end-of-kernel release writes every such
+// line back (MI355X_MICROARCH.md, boundary row: + dirty bytes / 6 TB/s),
+// after the stream.  Written through, the bytes leave during the stream.
+template <bool WT>
+__device__ __forceinline__ void store_byte(uint8_t* p, uint32_t v) {
+  if (WT)
+    __hip_atomic_store(p, uint8_t(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  else
+    *p = uint8_t(v);
+}
+
+template <bool WT = false>
 __device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {
   if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0) {
-    *reinterpret_cast<uint16_t*>(p) = uint16_t(((v & 0xffu) << 8) | ((v >> 8) & 0xffu));
+    uint16_t* q = reinterpret_cast<uint16_t*>(p);
+    const uint16_t w = uint16_t(((v & 0xffu) << 8) | ((v >> 8) & 0xffu));
+    if (WT)
+      __hip_atomic_store(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else
+      *q = w;
   } else {
-    p[0] = uint8_t(v >> 8);
-    p[1] = uint8_t(v);
+    store_byte<WT>(p, v >> 8);
+    store_byte<WT>(p + 1, v);
   }
 }
 
@@ -575,7 +595,8 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
                                                      int mode, uint16_t* __restrict__ ip_ck,
                                                      uint16_t* __restrict__ tcp_ck,
-                                                     uint8_t* __restrict__ status, uint32_t remap) {
+                                                     uint8_t* __restrict__ status, uint32_t remap,
+                                                     int patch_wt) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
@@ -636,7 +657,10 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
           tcv = fold_value(sum);
           if (hdr_ok) st |= 0x01;
           if (rem >= 18) st |= 0x02;
-          if (mode == 2) {
+          if (mode == 2 && patch_wt) {
+            store_be16<true>(dg + s + 10, ipc);
+            if (rem >= 18) store_be16<true>(dg + t0 + 16, tcv);
+          } else if (mode == 2) {
             store_be16(dg + s + 10, ipc);
             if (rem >= 18) store_be16(dg + t0 + 16, tcv);
           }
@@ -927,11 +951,11 @@ hipError_t launch_dense_t(const SegSpec& sp, const uint32_t* init, void* out, in
 
 template <int LPS, int UNROLL, bool NT, int MODE>
 hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
-                         uint8_t* status, uint32_t max_blocks, hipStream_t st) {
+                         uint8_t* status, uint32_t max_blocks, bool patch_wt, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
   hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, mode,
-                     ip_ck, tcp_ck, status, g_xcd_remap);
+                     ip_ck, tcp_ck, status, g_xcd_remap, int(patch_wt));
   return hipGetLastError();
 }
 
@@ -1072,10 +1096,10 @@ SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, i
 }
 
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
-                           uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st) {
+                           uint8_t* status, Geometry g, uint32_t max_blocks, bool patch_wt, hipStream_t st) {
 #define ICS_CASE(L, U, T, A)                                      \
   if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
-    return launch_ipv4_t<L, U, T, A>(sp, mode, ip_ck, tcp_ck, status, max_blocks, st);
+    return launch_ipv4_t<L, U, T, A>(sp, mode, ip_ck, tcp_ck, status, max_blocks, patch_wt, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;

@@ -81,8 +81,9 @@ hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
 void set_xcd_remap(uint32_t run_log2);  // log2 XCD run length (default 10 = 1024 blocks), 0: hardware order
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
+// patch_wt: PATCH-mode field stores write-through (sc1) instead of write-back
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
-                           uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
+                           uint8_t* status, Geometry g, uint32_t max_blocks, bool patch_wt, hipStream_t st);
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
 
 // synthetic workloads (icsum_workload.h)
