@@ -57,7 +57,7 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 // on first use and guarded by `mu`.
 struct ics_ctx {
   int device = 0;
-  void* d_zero = nullptr;  // 16 zero bytes (icsum::SegSpec::zero16)
+  void* d_zero = nullptr;  // 64 zero bytes (icsum::SegSpec::zero16; the IPv4 kernel's header pad)
   uint32_t max_blocks = 0;  // 0 = one lane group per segment (no grid-stride cap)
   int force_lps = 0, force_unroll = 0, force_nt = -1, force_mode = -1, force_segs = 0;
   // length binning of offsets batches: -1 auto (n >= bin_min), 0 off, 1 always
@@ -381,7 +381,7 @@ int ics_create(int device, ics_ctx** out) {
   ics_ctx* ctx = new (std::nothrow) ics_ctx();
   if (!ctx) return fail(ICS_ERR_NOMEM, "context allocation failed");
   ctx->device = device;
-  if (hipMalloc(&ctx->d_zero, 16) != hipSuccess || hipMemset(ctx->d_zero, 0, 16) != hipSuccess) {
+  if (hipMalloc(&ctx->d_zero, 64) != hipSuccess || hipMemset(ctx->d_zero, 0, 64) != hipSuccess) {
     delete ctx;
     return fail(ICS_ERR_NOMEM, "device allocation failed");
   }

@@ -498,22 +498,34 @@ __global__ void k_fold(const uint32_t* __restrict__ sum, uint16_t* __restrict__ 
 
 // ---------------------------------------------- IPv4 header fields ------
 // The first 20 wire bytes of a datagram as 5 little-endian dwords relative to
-// its (possibly unaligned) start: 6 aligned dword loads + alignbyte.  The
-// sixth dword may extend <= 3 bytes past a 20-byte datagram inside the same
-// aligned dword, never into another page.
+// its (possibly unaligned) start: 6 aligned dword loads + alignbyte.
 struct Hdr {
   uint32_t w[5];
   __device__ __forceinline__ uint32_t byte(int k) const { return (w[k >> 2] >> (8 * (k & 3))) & 0xffu; }
   __device__ __forceinline__ uint32_t be16(int k) const { return (byte(k) << 8) | byte(k + 1); }
 };
 
-__device__ __forceinline__ Hdr load_hdr(const uint8_t* p) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(p);
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-  const uint32_t sh = uint32_t(a & 3u);
+// The aligned dword holding the byte before `end`: the last dword a load for
+// a range ending at `end` (exclusive) may touch.
+__device__ __forceinline__ const uint32_t* last_dword(const uint8_t* end) {
+  const uint8_t* b = end - 1;
+  return reinterpret_cast<const uint32_t*>(b - (reinterpret_cast<uintptr_t>(b) & 3u));
+}
+
+// Header of the datagram at p (>= 20 bytes; `last` = last_dword of its end).
+// Address arithmetic stays on the global pointer p (an integer-to-pointer
+// cast would turn these into flat loads, which count in both vmcnt and
+// lgkmcnt and are waited for before the byte stream is issued), and every
+// load is unconditional: the sixth dword, which reaches up to 3 bytes past
+// byte 19 when the start is aligned, is clamped to `last`, so nothing past
+// the datagram's final dword is read.
+__device__ __forceinline__ Hdr load_hdr(const uint8_t* p, const uint32_t* last) {
+  const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
   uint32_t d[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) d[k] = q[k];
+  for (int k = 0; k < 5; ++k) d[k] = q[k];
+  d[5] = *(q + 5 < last ? q + 5 : last);
   Hdr h;
 #pragma unroll
   for (int k = 0; k < 5; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
@@ -550,15 +562,18 @@ __device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {
   }
 }
 
-// TCP header bytes 12..19 of a segment starting at t (>= 18 bytes present):
-// tf0 = bytes 12..15, tf1 = bytes 16..19 (bytes 18, 19 only meaningful when
-// present).  Every dword loaded holds at least one byte of the segment.
-__device__ __forceinline__ void load_tcp_fields(const uint8_t* t, uint32_t& tf0, uint32_t& tf1) {
-  const uintptr_t a = reinterpret_cast<uintptr_t>(t + 12);
-  const uint32_t* q = reinterpret_cast<const uint32_t*>(a & ~uintptr_t(3));
-  const uint32_t sh = uint32_t(a & 3u);
+// TCP header bytes 12..19 of a segment starting at t (>= 18 bytes present;
+// `last` = last_dword of its end): tf0 = bytes 12..15, tf1 = bytes 16..19
+// (bytes 18, 19 only meaningful when present).  Unconditional global loads;
+// the third dword (needed only when byte 12 sits at offset 3 of its dword) is
+// clamped to `last`.
+__device__ __forceinline__ void load_tcp_fields(const uint8_t* t, const uint32_t* last, uint32_t& tf0,
+                                                uint32_t& tf1) {
+  const uint8_t* p = t + 12;
+  const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
   const uint32_t d0 = q[0], d1 = q[1];
-  const uint32_t d2 = sh == 3 ? q[2] : d1;  // byte 17 spills into the third dword only at sh = 3
+  const uint32_t d2 = *(q + 2 < last ? q + 2 : last);
   tf0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
   tf1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
 }
@@ -596,25 +611,32 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      int mode, uint16_t* __restrict__ ip_ck,
                                                      uint16_t* __restrict__ tcp_ck,
                                                      uint8_t* __restrict__ status, uint32_t remap,
-                                                     int patch_wt) {
+                                                     int patch_wt, const uint8_t* __restrict__ zpad) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
+  const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;  // zpad: 32 zero bytes
   for (uint64_t g0 = uint64_t(block_order(remap)) * kGroups; g0 < n; g0 += step) {
     const uint64_t seg = g0 + threadIdx.x / LPS;
     const bool valid = seg < n;
-    uint64_t s = 0, e = 0;
-    if (valid) seg_bounds(offsets, stride, dlen, seg, s, e);
-    const bool hdr = valid && e - s >= 20;
+    // offsets from a clamped index, unconditionally (a load under a divergent
+    // branch is waited for at the join, before the stream below is issued)
+    uint64_t s, e;
+    seg_bounds(offsets, stride, dlen, valid ? seg : n - 1, s, e);
+    if (!valid) e = s;
+    const bool hdr = e - s >= 20;
     // Speculate the usual header length (hlen = 5): the IPv4 header dwords,
     // the TCP fields the verdict needs (data offset, checksum) and the TCP
-    // byte stream are all requested before any of them returns; a datagram
-    // with options (rare) redoes its stream below.
+    // byte stream are all requested before any of them returns; every lane
+    // loads the header (same addresses per group, one request per wave
+    // instruction), from the 32-byte zero pad when the datagram is too short.
+    // A datagram with options (rare) redoes its stream below.
     uint64_t t0 = hdr ? s + 20 : e;  // TCP part: [t0, e)
-    Hdr h = {};
+    const uint32_t* last = hdr ? last_dword(dg + e) : zlast;
+    Hdr h = load_hdr(hdr ? dg + s : zpad, last);
     uint32_t tf0 = 0, tf1 = 0;  // TCP bytes 12..15 and 16..19 (little-endian)
-    if (hdr) h = load_hdr(dg + s);
-    if (hdr && e - t0 >= 18) load_tcp_fields(dg + t0, tf0, tf1);
+    const bool tcpf = hdr && e - t0 >= 18;
+    load_tcp_fields(tcpf ? dg + t0 : zpad, tcpf ? last : zlast, tf0, tf1);
     uint32_t ev = 0, od = 0;
     seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
     bool redo = false;
@@ -626,7 +648,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
       t0 = s + off;
       if (redo) {
         tf0 = tf1 = 0;
-        if (e - t0 >= 18) load_tcp_fields(dg + t0, tf0, tf1);
+        if (e - t0 >= 18) load_tcp_fields(dg + t0, last, tf0, tf1);
       }
     }
     if (__any(redo)) {  // wave-uniform; groups without options re-sum the same bytes
@@ -683,7 +705,7 @@ __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
   seg_bounds(offsets, stride, dlen, i, s, e);
   uint8_t st = 0;
   if (e - s >= 20) {
-    Hdr h = load_hdr(dg + s);
+    Hdr h = load_hdr(dg + s, last_dword(dg + e));
     const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu, ttl = h.byte(8);
     // NetworkInterface::recv_frame parse (network_interface.cpp:51) then
     // Router::route: ttl <= 1 dropped, else ttl-- and compute_checksum()
@@ -955,7 +977,7 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
   hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, mode,
-                     ip_ck, tcp_ck, status, g_xcd_remap, int(patch_wt));
+                     ip_ck, tcp_ck, status, g_xcd_remap, int(patch_wt), static_cast<const uint8_t*>(sp.zero16));
   return hipGetLastError();
 }
 

@@ -27,7 +27,7 @@ struct SegSpec {
   uint64_t stride;
   uint64_t seg_len;
   uint64_t n;
-  const void* zero16;  // 16 zero bytes in device memory (stand-in for absent arrays)
+  const void* zero16;  // 64 zero bytes in device memory (stand-in for absent arrays, header pad)
   // length-binned launch (bin_spec): bin `bin`'s list (16-byte entries, see
   // launch_bin_segments) and the binning pass's meta words; n stays the batch
   // size (the list's capacity)
