@@ -130,6 +130,9 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       wb[w][k] = v;
     }
   }
+  // the scatter pass's cursors start at 0 (zeroed here, in stream order before
+  // it, instead of by a separate memset launch: one dispatch less per batch)
+  if (threadIdx.x < kBins) meta[kBinMetaCursor + threadIdx.x] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t total = 0, t = 10000;
@@ -1060,7 +1063,6 @@ hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* 
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
                                hipStream_t st) {
   if (!offsets || n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
-  if (hipError_t e = hipMemsetAsync(meta, 0, kBinMetaWords * sizeof(uint32_t), st)) return e;
   uint32_t* cnt_part = meta + kBinMetaWords;
   uint64_t* by_part = reinterpret_cast<uint64_t*>(cnt_part + kBins * kBinStatBlocks);
   const uint64_t tiles = (n + kBinTile - 1) / kBinTile;

@@ -45,7 +45,7 @@ struct SegSpec {
 //   meta  kBinMetaBytesTotal bytes: bin sizes at kBinMetaCount, the plan at
 //         kBinMetaPlan, scatter cursors, then the stats pass's partials
 // Passes: bin statistics, a one-block plan kernel and, under the split plan
-// only, the scatter into the lists; needs n < 2^32.  The launcher zeroes meta itself.  The plan
+// only, the scatter into the lists; needs n < 2^32.  The plan kernel zeroes the scatter cursors.  The plan
 // (k_bin_plan) decides on the device whether the batch runs split into bins
 // or whole with the long-segment geometry (then the last bin's launch, one
 // lane group per segment of the batch, takes every segment).
