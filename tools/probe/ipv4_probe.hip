@@ -7,7 +7,8 @@
 //   v<F>     a copy of k_ipv4_tcp's COMPUTE path with parts switched off by
 //            the bits of F: 1 no IPv4 header loads, 2 no TCP field loads,
 //            4 no output stores, 8 16-byte grid (mode 0) instead of mode 3,
-//            16 hardware block order; and PATCH-store shapes P (1 two 2-byte
+//            16 hardware block order, 32 boundary chunks non-temporal too;
+//            and PATCH-store shapes P (1 two 2-byte
 //            field stores, 2 the same write-through (sc1), 3 non-temporal,
 //            4 the two aligned 16-byte chunks holding the fields, 5 those
 //            non-temporal, 6 the aligned 64-byte blocks; 7 the whole 128-byte
@@ -31,6 +32,44 @@
 
 namespace icsum {
 namespace {
+
+// range_sums_line_primed with the boundary chunks non-temporal too (F & 32):
+// no line of the datagram is kept in L2 by the checksum pass
+template <int LPS, int UNROLL>
+__device__ __forceinline__ void line_primed_all_nt(const uint8_t* __restrict__ base, uint64_t s, uint64_t e,
+                                                   uint32_t lane, uint32_t& ev, uint32_t& od) {
+  const uint64_t a0 = s & ~uint64_t(127);
+  const uint64_t span = e > s ? e - a0 : 0;
+  const uint32_t nch = uint32_t((span + 15) >> 4);
+  const uint32_t cs = uint32_t(s - a0) >> 4;
+  const uint32_t lastc = nch ? nch - 1 : 0u;
+  const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  const uint32_t tail = nch ? uint32_t(span - (uint64_t(lastc) << 4)) : 0u;
+  u32x4 bnd = {0u, 0u, 0u, 0u};
+  uint32_t blo = 0, bhi = 0;
+  if (nch) {
+    const bool is_tail = lane == 1 && lastc != cs;
+    bnd = load16<true>(p + (is_tail ? lastc : cs));
+    blo = is_tail ? 0u : (uint32_t(s) & 15u);
+    bhi = (is_tail || lastc == cs) ? tail : 16u;
+    if (lane >= 2 || (lane == 1 && lastc == cs)) bhi = 0u;
+  }
+  for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
+    u32x4 v[UNROLL];
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      v[u] = load16<true>(p + (cc < lastc ? cc : lastc));
+    }
+#pragma unroll
+    for (int u = 0; u < UNROLL; ++u) {
+      const uint32_t cc = c + uint32_t(u * LPS);
+      const uint32_t keep = (cc > cs && cc < lastc) ? ~0u : 0u;
+      acc_chunk(v[u] & keep, ev, od);
+    }
+  }
+  acc_chunk(bnd & byte_range_mask(blo, bhi), ev, od);
+}
 
 template <int P>
 __device__ __forceinline__ void patch_store(uint8_t* dg, uint64_t s, uint64_t t0, uint32_t ipc, uint32_t tcv) {
@@ -76,7 +115,10 @@ __global__ __launch_bounds__(kBlock) void k_v(uint8_t* __restrict__ dg, uint64_t
   if (!(F & 1) && hdr) h = load_hdr(dg + s, last_dword(dg + e));
   if (!(F & 2) && hdr && e - t0 >= 18) load_tcp_fields(dg + t0, last_dword(dg + e), tf0, tf1);
   uint32_t ev = 0, od = 0;
-  seg_sums<LPS, UNROLL, true, MODE>(dg, t0, e, lane, ev, od);
+  if (F & 32)
+    line_primed_all_nt<LPS, UNROLL>(dg, t0, e, lane, ev, od);
+  else
+    seg_sums<LPS, UNROLL, true, MODE>(dg, t0, e, lane, ev, od);
   const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(t0) & 1u));
   if ((P == 7 || P == 8) && valid && lane < 8) {  // whole head line, junk
     u32x4* c = reinterpret_cast<u32x4*>(dg + (s & ~uint64_t(127))) + lane;
@@ -227,6 +269,19 @@ int main() {
                   hipLaunchKernelGGL((k_v<0, 0>), dim3(blocks), dim3(256), 0, nullptr, B.d[c], kL, kL, kN, B.ip, B.tcp,
                                      B.st, 10u);
                   hipLaunchKernelGGL(k_scatter<true>, dim3(sblocks), dim3(256), 0, nullptr, B.d[c], kL, kN, B.ip, B.tcp);
+                }});
+  vs.push_back({"v32", [&](int c) {
+                  hipLaunchKernelGGL((k_v<32, 0>), dim3(blocks), dim3(256), 0, nullptr, B.d[c], kL, kL, kN, B.ip, B.tcp,
+                                     B.st, 10u);
+                }});
+  vs.push_back({"p1_v32", [&](int c) {
+                  hipLaunchKernelGGL((k_v<32, 1>), dim3(blocks), dim3(256), 0, nullptr, B.d[c], kL, kL, kN, B.ip, B.tcp,
+                                     B.st, 10u);
+                }});
+  vs.push_back({"split_v32", [&](int c) {
+                  hipLaunchKernelGGL((k_v<32, 0>), dim3(blocks), dim3(256), 0, nullptr, B.d[c], kL, kL, kN, B.ip, B.tcp,
+                                     B.st, 10u);
+                  hipLaunchKernelGGL(k_scatter<false>, dim3(sblocks), dim3(256), 0, nullptr, B.d[c], kL, kN, B.ip, B.tcp);
                 }});
   vs.push_back({"scatter", [&](int c) {
                   hipLaunchKernelGGL(k_scatter<false>, dim3(sblocks), dim3(256), 0, nullptr, B.d[c], kL, kN, B.ip, B.tcp);
