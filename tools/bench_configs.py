@@ -178,6 +178,19 @@ def main():
                 ts.append(time.perf_counter() - t0)
             emit(f"host_inclusive_256Kix1500_{'pinned' if pinned else 'pageable'}", n * L, statistics.median(ts),
                  n * 6, entry="ics_checksum_batch_host", note="H2D + kernel + D2H, 2-slot pipeline")
+            if pinned:  # the link's own ceiling: one plain H2D copy of the same pinned bytes, no kernel
+                d = torch.empty(n * L, dtype=torch.uint8, device=dev)
+                d.copy_(h, non_blocking=True)
+                torch.cuda.synchronize()
+                ts = []
+                for _ in range(5):
+                    t0 = time.perf_counter()
+                    d.copy_(h, non_blocking=True)
+                    torch.cuda.synchronize()
+                    ts.append(time.perf_counter() - t0)
+                emit("pcie_h2d_copy_256Kix1500_pinned", n * L, statistics.median(ts), 0, entry="torch copy_ (hipMemcpyAsync)",
+                     note="reference ceiling for the host-inclusive rows: H2D only")
+                del d
     eng.close()
 
 
