@@ -65,6 +65,7 @@ struct ics_ctx {
   uint64_t bin_min = 0;
   uint32_t bin_blocks = 0;  // grid of each bin's launch (its size is only known on the device)
   uint32_t last_bin_blocks = 0;  // grid cap of the last bin's launch (0: one lane group per segment)
+  uint32_t last_bin_lps = 0;     // lanes per segment of the last bin's launch (0: auto, see checksum_device)
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
   int bin_plan = -1;        // -1: decided on the device per batch, 0: whole, 1: split (tests)
   bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
@@ -157,10 +158,15 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   if (e == hipSuccess)
     e = icsum::launch_checksum_bins(icsum::bin_spec(sp, list, meta, 0), d_init, d_odd, d_out, out_kind,
                                     ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks, st);
+  // the last bin's launch dispatches one lane group per segment of the whole
+  // batch (whatever the plan); above 1 M segments 32-lane groups halve the
+  // waves an empty last bin costs to dispatch
+  icsum::Geometry g_last = icsum::bin_geometry(icsum::kBins - 1);
+  const uint32_t lps = ctx->last_bin_lps ? ctx->last_bin_lps : (sp.n > (uint64_t(1) << 20) ? 32u : 64u);
+  if (lps == 32) g_last = {32, 8, true, 3, 1};
   if (e == hipSuccess)
     e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, icsum::kBins - 1), d_init, d_odd, d_out, out_kind,
-                               icsum::bin_geometry(icsum::kBins - 1),
-                               ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks, st);
+                               g_last, ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks, st);
   if (e == hipSuccess && std::getenv("ICSUM_BIN_DEBUG")) {  // dev: dump the binning pass's meta words
     uint32_t h[icsum::kBinMetaWords];
     if (hipMemcpyAsync(h, meta, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess) {
@@ -395,6 +401,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin_min = env_u32("ICSUM_BIN_MIN", 1u << 16);
   ctx->bin_blocks = env_u32("ICSUM_BIN_BLOCKS", 2048);
   ctx->last_bin_blocks = env_u32("ICSUM_LAST_BIN_BLOCKS", 0);
+  ctx->last_bin_lps = env_u32("ICSUM_LAST_BIN_LPS", 0);
   if (std::getenv("ICSUM_DENSE_SEGS")) ctx->dense_segs = int(env_u32("ICSUM_DENSE_SEGS", 4));
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
-"""Dev tool: interleaved in-process A/B of the grid cap of the binned
-dispatch's last-bin launch (ICSUM_LAST_BIN_BLOCKS; 0 = one 64-lane group per
-segment of the batch).  Workloads: BASELINE config 4 (1 M mixed 64 B-64 KiB,
+"""Dev tool: interleaved in-process A/B of the binned dispatch's last-bin
+launch: its grid cap (ICSUM_LAST_BIN_BLOCKS; 0 = one lane group per segment of
+the batch) or its lanes per segment (--var ICSUM_LAST_BIN_LPS --caps 64,32).  Workloads: BASELINE config 4 (1 M mixed 64 B-64 KiB,
 whole-batch plan), the 2 M bimodal 40 B / 1460 B batch (split plan, empty last
 bin) and 2 M segments of 4-6 KiB (whole-batch plan with > 1 M segments).
 
@@ -22,12 +22,15 @@ import torch  # noqa: E402
 from tcpip_network_protocol_stack_amd.engine import Engine, mixed_offsets  # noqa: E402
 
 
+VAR = "ICSUM_LAST_BIN_BLOCKS"
+
+
 def engine(cap):
-    os.environ["ICSUM_LAST_BIN_BLOCKS"] = str(cap)
+    os.environ[VAR] = str(cap)
     try:
         return Engine(0)
     finally:
-        del os.environ["ICSUM_LAST_BIN_BLOCKS"]
+        del os.environ[VAR]
 
 
 def batch(kind, dev, eng):
@@ -49,7 +52,10 @@ def main():
     ap.add_argument("--caps", default="0,262144,131072")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--var", default="ICSUM_LAST_BIN_BLOCKS")
     args = ap.parse_args()
+    global VAR
+    VAR = args.var
     dev = torch.device("cuda", 0)
     caps = [int(c) for c in args.caps.split(",")]
     engs = {c: engine(c) for c in caps}
@@ -74,7 +80,7 @@ def main():
                 times[c].append(a.elapsed_time(b) * 1e3 / args.iters)
         for c, ts in times.items():
             med = statistics.median(ts)
-            print(json.dumps({"workload": kind, "segments": n, "bytes": nbytes, "last_bin_blocks": c,
+            print(json.dumps({"workload": kind, "segments": n, "bytes": nbytes, VAR: c,
                               "med_us": round(med, 2), "min_us": round(min(ts), 2),
                               "GB_s": round(nbytes / med / 1e3, 1)}), flush=True)
         del d, off
