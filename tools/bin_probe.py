@@ -2,7 +2,7 @@
 single-geometry dispatch (run under rocprofv3 --kernel-trace to split the
 time per bin kernel).  ICSUM_BIN / ICSUM_BIN_BLOCKS come from the environment.
 
-    python tools/bin_probe.py {mixed|long|bimodal} [iters]
+    python tools/bin_probe.py {mixed|long|bimodal|mss|ack} [iters]
 """
 import os
 import sys
@@ -22,6 +22,9 @@ def main():
     lens = np.diff(off)
     if kind == "long":  # only the segments of the last bin (> 4 KiB), packed
         lens = lens[lens > 4096]
+    elif kind in ("mss", "ack"):  # one bin's worth: 1 M x 1460-1463 B or 40-43 B
+        rng = np.random.default_rng(seed)
+        lens = (1460 if kind == "mss" else 40) + rng.integers(0, 4, n)
     elif kind == "bimodal":
         rng = np.random.default_rng(seed)
         lens = np.where(rng.random(2 * n) < 0.5, 40, 1460) + rng.integers(0, 4, 2 * n)
