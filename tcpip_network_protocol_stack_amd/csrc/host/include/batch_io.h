@@ -12,10 +12,16 @@
 #ifndef ICSUM_HOST_BATCH_IO_H
 #define ICSUM_HOST_BATCH_IO_H
 
+#include <condition_variable>
 #include <cstddef>
 #include <cstdint>
+#include <deque>
+#include <exception>
+#include <memory>
+#include <mutex>
 #include <optional>
 #include <string_view>
+#include <thread>
 #include <vector>
 
 #include "batch.h"
@@ -49,7 +55,9 @@ class DatagramBatch
     bool push(std::string_view wire);  // false when the arena is full
 
     // up to `max` datagrams from `fd` (non-blocking fds stop at EAGAIN;
-    // blocking ones return after the first batch); returns the count read
+    // blocking ones wait for the first datagram, then take what is queued);
+    // returns the count read (0 at end of stream; on a socket an empty
+    // message, which is what SOCK_SEQPACKET reads at end of stream, ends it)
     size_t read_from(int fd, size_t max);
     // every datagram to `fd`; returns the count written
     size_t write_to(int fd) const;
@@ -65,6 +73,43 @@ class DatagramBatch
     size_t cap_ = 0, max_n_ = 0;
     std::vector<uint64_t> off_{0};
     bool room(size_t n) const { return size() < max_n_ && bytes() + n <= cap_; }
+};
+
+// A ring of page-locked DatagramBatch arenas with a reader thread: while the
+// caller runs batch k through the engine (verify / unwrap / patch), the reader
+// fills arena k+1 from the fd, so socket reads overlap the PCIe + GPU pass.
+// The fd is the caller's and must be blocking; the reader stops at end of
+// stream (read_from returns 0: the peer closed, or the socket was shut down
+// for reading).  The destructor shuts a socket down for reading to wake the
+// reader, then joins it.  Only the reader thread touches the fd; only the
+// caller's thread touches the engine.
+class DatagramRing
+{
+  public:
+    DatagramRing(BatchEngine& engine, int fd, size_t slots = 3, size_t capacity_bytes = size_t(32) << 20,
+                 size_t max_datagrams = 1 << 14);
+    ~DatagramRing();
+    DatagramRing(const DatagramRing&) = delete;
+    DatagramRing& operator=(const DatagramRing&) = delete;
+
+    // the next filled batch (blocks until one is ready), or nullptr once the
+    // stream ended and every filled batch was taken; rethrows a reader error
+    DatagramBatch* next();
+    // hand a batch taken with next() back for refilling
+    void release(DatagramBatch* batch);
+
+  private:
+    void reader();
+
+    int fd_;
+    size_t max_n_;
+    std::vector<std::unique_ptr<DatagramBatch>> arenas_;
+    std::deque<DatagramBatch*> free_, ready_;
+    std::mutex mu_;
+    std::condition_variable cv_;
+    bool eof_ = false, stop_ = false;
+    std::exception_ptr error_;
+    std::thread thread_;
 };
 
 }  // namespace icsum

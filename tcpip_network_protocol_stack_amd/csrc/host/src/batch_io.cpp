@@ -9,6 +9,7 @@
 #include <cstring>
 #include <stdexcept>
 #include <string>
+#include <utility>
 
 namespace icsum {
 namespace {
@@ -76,18 +77,26 @@ size_t DatagramBatch::read_from(int fd, size_t max)
                 msgs[j].msg_hdr.msg_iov = &iov[j];
                 msgs[j].msg_hdr.msg_iovlen = 1;
             }
-            const int r = recvmmsg(fd, msgs.data(), static_cast<unsigned>(k), got ? MSG_DONTWAIT : 0, nullptr);
+            // the first call waits for one datagram only (a plain blocking
+            // recvmmsg would wait until all k arrived), later calls take what
+            // is already queued
+            const int r = recvmmsg(fd, msgs.data(), static_cast<unsigned>(k), got ? MSG_DONTWAIT : MSG_WAITFORONE,
+                                   nullptr);
             if (r < 0) {
                 if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
                 sys_fail("recvmmsg");
             }
-            for (int j = 0; j < r; ++j) {
+            // a zero-length message ends the stream: at end of stream a
+            // SOCK_SEQPACKET recvmmsg reports every remaining slot as an
+            // empty message (an IPv4 datagram is never empty)
+            int j = 0;
+            for (; j < r && msgs[j].msg_len > 0; ++j) {
                 const size_t len = msgs[j].msg_len;
                 if (j) std::memmove(arena_ + bytes(), base + size_t(j) * kMaxDatagram, len);
                 off_.push_back(bytes() + len);
             }
-            got += size_t(r);
-            if (size_t(r) < k) break;
+            got += size_t(j);
+            if (j < r || size_t(r) < k) break;
         }
         return got;
     }
@@ -153,6 +162,85 @@ void DatagramBatch::patch()
 {
     if (!engine_) throw std::logic_error("DatagramBatch::patch needs an engine");
     engine_->patch_packed(arena_, off_.data(), size());
+}
+
+DatagramRing::DatagramRing(BatchEngine& engine, int fd, size_t slots, size_t capacity_bytes, size_t max_datagrams)
+    : fd_(fd), max_n_(max_datagrams)
+{
+    if (slots < 2) throw std::invalid_argument("DatagramRing needs at least 2 slots");
+    for (size_t k = 0; k < slots; ++k) {
+        arenas_.push_back(std::make_unique<DatagramBatch>(engine, capacity_bytes, max_datagrams));
+        free_.push_back(arenas_.back().get());
+    }
+    thread_ = std::thread([this] { reader(); });
+}
+
+DatagramRing::~DatagramRing()
+{
+    bool ended;
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        stop_ = true;
+        ended = eof_;
+    }
+    cv_.notify_all();
+    if (!ended && is_datagram_socket(fd_)) (void)::shutdown(fd_, SHUT_RD);  // wake a blocked recvmmsg
+    thread_.join();
+}
+
+void DatagramRing::reader()
+{
+    for (;;) {
+        DatagramBatch* b = nullptr;
+        {
+            std::unique_lock<std::mutex> lock(mu_);
+            cv_.wait(lock, [this] { return stop_ || !free_.empty(); });
+            if (stop_) break;
+            b = free_.front();
+            free_.pop_front();
+        }
+        b->clear();
+        size_t got = 0;
+        try {
+            got = b->read_from(fd_, max_n_);
+        } catch (...) {
+            std::lock_guard<std::mutex> lock(mu_);
+            error_ = std::current_exception();
+        }
+        std::lock_guard<std::mutex> lock(mu_);
+        if (got == 0) {  // end of stream (or an error): hand the arena back and stop
+            free_.push_back(b);
+            eof_ = true;
+            break;
+        }
+        ready_.push_back(b);
+        cv_.notify_all();
+    }
+    std::lock_guard<std::mutex> lock(mu_);
+    eof_ = true;
+    cv_.notify_all();
+}
+
+DatagramBatch* DatagramRing::next()
+{
+    std::unique_lock<std::mutex> lock(mu_);
+    cv_.wait(lock, [this] { return !ready_.empty() || eof_; });
+    if (!ready_.empty()) {
+        DatagramBatch* b = ready_.front();
+        ready_.pop_front();
+        return b;
+    }
+    if (error_) std::rethrow_exception(error_);
+    return nullptr;
+}
+
+void DatagramRing::release(DatagramBatch* batch)
+{
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        free_.push_back(batch);
+    }
+    cv_.notify_all();
 }
 
 }  // namespace icsum

@@ -3,6 +3,7 @@
 #include <cstdio>
 #include <random>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <sys/socket.h>
@@ -174,6 +175,46 @@ int main()
         }
         out.patch();
         for (size_t i = 0; i < wires.size(); ++i) EXPECT(out[i] == wires[i]);
+    }
+    // DatagramRing: a writer thread streams the received wires (8 passes) over
+    // a SOCK_SEQPACKET socketpair and closes its end; the ring's reader fills
+    // arenas while this thread verifies them; every datagram arrives once, in
+    // order, with the status verify_raw() gave it
+    {
+        int sv[2];
+        EXPECT(socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) == 0);
+        constexpr size_t kPasses = 8;
+        std::thread writer([&] {
+            icsum::DatagramBatch txb(size_t(1) << 20);
+            for (size_t p = 0; p < kPasses; ++p) {
+                for (size_t i = 0; i < rx.size();) {
+                    txb.clear();
+                    size_t j = i;
+                    for (; j < rx.size() && j - i < 64 && txb.push(rx[j]); ++j) {
+                    }
+                    txb.write_to(sv[0]);
+                    i = j;
+                }
+            }
+            close(sv[0]);
+        });
+        size_t seen = 0, batches = 0;
+        {
+            icsum::DatagramRing ring(eng, sv[1], 3, size_t(4) << 20, 700);
+            while (icsum::DatagramBatch* b = ring.next()) {
+                const auto vs = b->verify();
+                for (size_t k = 0; k < vs.size(); ++k, ++seen) {
+                    EXPECT((*b)[k] == rx[seen % rx.size()]);
+                    EXPECT(vs[k] == st[seen % rx.size()]);
+                }
+                ++batches;
+                ring.release(b);
+            }
+        }
+        writer.join();
+        close(sv[1]);
+        EXPECT(seen == kPasses * rx.size());
+        EXPECT(batches > 1);
     }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);

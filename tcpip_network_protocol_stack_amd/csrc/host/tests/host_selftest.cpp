@@ -9,6 +9,7 @@
 #include <iostream>
 #include <sstream>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include <sys/socket.h>
@@ -138,6 +139,39 @@ int main()
             close(sv[0]);
             close(sv[1]);
             std::cout << sent << " " << got << " " << same << " " << rx.bytes() << "\n";
+        } else if (cmd == "ioseq") {
+            // SOCK_SEQPACKET stream: a writer thread sends every wire 4 times
+            // and closes its end; read_from(64) until it reports end of stream
+            std::vector<std::string> ws;
+            std::string h;
+            while (in >> h) ws.push_back(unhex(h));
+            int sv[2];
+            if (socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) != 0) return 3;
+            size_t sent = 0;
+            std::thread w([&] {
+                icsum::DatagramBatch tx(size_t(1) << 20);
+                for (int p = 0; p < 4; ++p)
+                    for (const auto& x : ws) {
+                        tx.clear();
+                        tx.push(x);
+                        sent += tx.write_to(sv[0]);
+                    }
+                close(sv[0]);
+            });
+            icsum::DatagramBatch rx(size_t(1) << 22, 64);
+            size_t got = 0, reads = 0;
+            bool same = true;
+            for (;;) {
+                rx.clear();
+                const size_t k = rx.read_from(sv[1], 64);
+                ++reads;
+                if (k == 0) break;
+                for (size_t i = 0; i < k; ++i) same = same && rx[i] == ws[(got + i) % ws.size()];
+                got += k;
+            }
+            w.join();
+            close(sv[1]);
+            std::cout << sent << " " << got << " " << same << " " << (reads > 1) << "\n";
         } else if (!cmd.empty()) {
             std::cerr << "unknown command " << cmd << "\n";
             return 1;

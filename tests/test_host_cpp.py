@@ -108,3 +108,13 @@ def test_datagram_batch_socket_round_trip(selftest):
     sent, got, same, nbytes = (int(x) for x in selftest([line])[0].split())
     assert sent == got == len(cases) and same == 1
     assert nbytes == sum(len(c["wire"]) // 2 for c in cases)
+
+
+def test_datagram_batch_seqpacket_end_of_stream(selftest):
+    # a SOCK_SEQPACKET stream closed by the writer: read_from returns every
+    # datagram once, in order, then 0 (the empty messages recvmmsg reports at
+    # end of stream are not datagrams) — what DatagramRing's reader relies on
+    cases = wires("tcp_wrap.json")
+    line = "ioseq " + " ".join(c["wire"] for c in cases)
+    sent, got, same, several = (int(x) for x in selftest([line])[0].split())
+    assert sent == got == 4 * len(cases) and same == 1 and several == 1
