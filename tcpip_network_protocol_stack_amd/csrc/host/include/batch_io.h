@@ -78,11 +78,12 @@ class DatagramBatch
 // A ring of page-locked DatagramBatch arenas with a reader thread: while the
 // caller runs batch k through the engine (verify / unwrap / patch), the reader
 // fills arena k+1 from the fd, so socket reads overlap the PCIe + GPU pass.
-// The fd is the caller's and must be blocking; the reader stops at end of
-// stream (read_from returns 0: the peer closed, or the socket was shut down
-// for reading).  The destructor shuts a socket down for reading to wake the
-// reader, then joins it.  Only the reader thread touches the fd; only the
-// caller's thread touches the engine.
+// The fd is the caller's and must be blocking (a socket, TUN or other packet
+// fd); the reader polls it, reads once it is readable, and stops at end of
+// stream (read_from returns 0: the peer closed).  The destructor stops and
+// joins the reader within one 50 ms poll interval, and leaves the fd as it
+// was.  Only the reader thread touches the fd; only the caller's thread
+// touches the engine.
 class DatagramRing
 {
   public:

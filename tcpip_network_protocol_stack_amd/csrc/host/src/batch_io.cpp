@@ -2,6 +2,7 @@
 #include "batch_io.h"
 
 #include <errno.h>
+#include <poll.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -177,15 +178,12 @@ DatagramRing::DatagramRing(BatchEngine& engine, int fd, size_t slots, size_t cap
 
 DatagramRing::~DatagramRing()
 {
-    bool ended;
     {
         std::lock_guard<std::mutex> lock(mu_);
         stop_ = true;
-        ended = eof_;
     }
     cv_.notify_all();
-    if (!ended && is_datagram_socket(fd_)) (void)::shutdown(fd_, SHUT_RD);  // wake a blocked recvmmsg
-    thread_.join();
+    thread_.join();  // the reader polls the fd and checks stop_ every 50 ms
 }
 
 void DatagramRing::reader()
@@ -202,7 +200,18 @@ void DatagramRing::reader()
         b->clear();
         size_t got = 0;
         try {
-            got = b->read_from(fd_, max_n_);
+            // wait until the fd is readable (or at end of stream), looking at
+            // stop_ in between, so the destructor never waits on a blocked read
+            bool go = false;
+            while (!go) {
+                pollfd p{fd_, POLLIN, 0};
+                const int r = ::poll(&p, 1, 50);
+                if (r < 0 && errno != EINTR) sys_fail("poll");
+                go = r > 0;
+                std::lock_guard<std::mutex> lock(mu_);
+                if (stop_ && !go) break;
+            }
+            if (go) got = b->read_from(fd_, max_n_);
         } catch (...) {
             std::lock_guard<std::mutex> lock(mu_);
             error_ = std::current_exception();

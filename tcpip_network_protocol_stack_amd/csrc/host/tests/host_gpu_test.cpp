@@ -1,5 +1,6 @@
 // host_gpu_test.cpp — icsum::BatchEngine (GPU) against the per-object calls of
 // the same drop-in types (CPU) on seeded random traffic.  Exit 0 = identical.
+#include <chrono>
 #include <cstdio>
 #include <random>
 #include <string>
@@ -215,6 +216,17 @@ int main()
         close(sv[1]);
         EXPECT(seen == kPasses * rx.size());
         EXPECT(batches > 1);
+        // destroyed while the stream is still open and idle: the reader stops
+        // within its poll interval and leaves the socket usable
+        EXPECT(socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) == 0);
+        const auto t0 = std::chrono::steady_clock::now();
+        { icsum::DatagramRing idle(eng, sv[1], 2, size_t(1) << 20, 64); }
+        EXPECT(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2));
+        EXPECT(send(sv[0], "x", 1, 0) == 1);
+        char c = 0;
+        EXPECT(recv(sv[1], &c, 1, 0) == 1 && c == 'x');
+        close(sv[0]);
+        close(sv[1]);
     }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);
