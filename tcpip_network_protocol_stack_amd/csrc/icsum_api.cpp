@@ -67,7 +67,7 @@ struct ics_ctx {
   uint32_t last_bin_blocks = 0;  // grid cap of the last bin's launch (0: one lane group per segment)
   uint32_t last_bin_lps = 0;     // lanes per segment of the last bin's launch (0: auto, see checksum_device)
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
-  int bin_plan = -1;        // -1: decided on the device per batch, 0: whole, 1: split (tests)
+  int bin_plan = -1;        // -1: decided on the device per batch; forced (tests): 0 whole, 1 split, 2 whole16
   bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
@@ -151,19 +151,19 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   ICS_HIP(hipMallocAsync(&ws, meta_bytes + sp.n * 16 * icsum::kBins, st));
   uint32_t* meta = static_cast<uint32_t*>(ws);
   void* list = static_cast<uint8_t*>(ws) + meta_bytes;
-  hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, ctx->bin_plan, st);
-  // bins 0..3: one launch, a capped grid striding over each bin; the last
-  // bin: one lane group per segment of the batch (it takes the whole batch
-  // under that plan)
-  if (e == hipSuccess)
-    e = icsum::launch_checksum_bins(icsum::bin_spec(sp, list, meta, 0), d_init, d_odd, d_out, out_kind,
-                                    ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks, st);
   // the last bin's launch dispatches one lane group per segment of the whole
   // batch (whatever the plan); above 1 M segments 32-lane groups halve the
   // waves an empty last bin costs to dispatch
   icsum::Geometry g_last = icsum::bin_geometry(icsum::kBins - 1);
   const uint32_t lps = ctx->last_bin_lps ? ctx->last_bin_lps : (sp.n > (uint64_t(1) << 20) ? 32u : 64u);
   if (lps == 32) g_last = {32, 8, true, 3, 1};
+  hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, ctx->bin_plan, lps, st);
+  // bins 0..3: one launch, a capped grid striding over each bin; the last
+  // bin: one lane group per segment of the batch (it takes the whole batch
+  // under the whole-batch plans)
+  if (e == hipSuccess)
+    e = icsum::launch_checksum_bins(icsum::bin_spec(sp, list, meta, 0), d_init, d_odd, d_out, out_kind,
+                                    ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks, st);
   if (e == hipSuccess)
     e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, icsum::kBins - 1), d_init, d_odd, d_out, out_kind,
                                g_last, ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks, st);
@@ -404,6 +404,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->last_bin_lps = env_u32("ICSUM_LAST_BIN_LPS", 0);
   if (std::getenv("ICSUM_DENSE_SEGS")) ctx->dense_segs = int(env_u32("ICSUM_DENSE_SEGS", 4));
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
+  if (ctx->bin_plan > 2) ctx->bin_plan = -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
   if (std::getenv("ICSUM_XCD_REMAP")) icsum::set_xcd_remap(env_u32("ICSUM_XCD_REMAP", 0));
   *out = ctx;

@@ -91,18 +91,31 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total)
 
 // Dispatch plan of a binned batch, decided on the device (k_bin_plan, one
 // block after the stats pass) from
-// the bin sizes the binning pass recorded, with no host round trip: split into
-// bins, or run the whole batch with the long-segment geometry (the last bin's
-// launch takes every segment, in byte-balanced contiguous runs; the other
-// launches exit at once).  Cost model in ns, measured on MI355X
-// (tools/bin_probe.py):
-//   whole: max(bytes / 7100 GB/s, n * 0.45 ns)   one (64 x 8) group per segment
-//   split: sum over bins of max(bytes_b / rate_b, n_b * 0.1 ns) + 10 us, with
-//          rate 5000 GB/s for bins 0-3 and 6400 GB/s for the last (its
-//          segments are no longer contiguous in memory)
+// the bin sizes the binning pass recorded, with no host round trip:
+//   kPlanWhole  the last bin's launch takes every segment with its own
+//               (64- or 32-lane) geometry; the other launches exit at once
+//   kPlanSplit  every bin runs from its list with its own geometry
+//   kPlanWhole16 the last bin's launch takes every segment with 16-lane
+//               groups in its first n/16 blocks (the rest exit at once)
+// Cost model in ns, measured on MI355X (tools/ab_bins.py, tools/ab_lastbin.py);
+// the last bin's launch dispatches n * last_lps / 64 waves under every plan,
+// ≈0.053 ns each when they find no work:
+//   whole:   max(bytes / 7100 GB/s, n * 0.45 ns)   (64 lanes per segment)
+//   split:   sum over bins of max(bytes_b / rate_b, n_b * 0.1 ns) + 26 us
+//            + the empty last-bin waves, with rate 5000 GB/s for bins 0-3 and
+//            6400 GB/s for the last (its segments no longer contiguous)
+//   whole16: sum over bins of max(bytes_b / r16_b, n_b * 0.16 ns) + the
+//            waves past n/4, r16 = 7000 GB/s up to 1920-byte segments, 6500 up
+//            to 4 KiB, 5000 above (16 lanes loop over long segments)
+// Measured under each forced plan (tools/ab_lastbin.py --var ICSUM_BIN_PLAN,
+// profiles/r1_ab_plans.jsonl), µs whole / split / whole16: config 4
+// 1429 / 1622 / 1682, 2 M bimodal 40+1460 B 525 / 473 / 364, 2 M x 4-6 KiB
+// 1515 / 1589 / 1593, 1 M x 1460 B 520 / 429 / 296, 1 M x 40 B 451 / 168 / 205.
+constexpr uint32_t kPlanWhole = 0, kPlanSplit = 1, kPlanWhole16 = 2;
+
 __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta, const uint32_t* __restrict__ cnt_part,
                                                      const uint64_t* __restrict__ by_part, uint32_t parts, uint64_t n,
-                                                     int force) {
+                                                     int force, uint32_t last_lps) {
   // totals per bin from the stats pass's per-block partials (parts <= kBlock:
   // one partial per thread, all loads in flight together)
   __shared__ uint32_t wc[kBlock / 64][kBins];
@@ -135,7 +148,8 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
   if (threadIdx.x < kBins) meta[kBinMetaCursor + threadIdx.x] = 0;
   __syncthreads();
   if (threadIdx.x == 0) {
-    uint64_t total = 0, t = 10000;
+    const uint64_t waves = n * last_lps / 64;  // the last bin's launch
+    uint64_t total = 0, t_split = 26000 + waves * 53 / 1000, t16 = (waves - n / 4) * 53 / 1000;
 #pragma unroll
     for (int k = 0; k < kBins; ++k) {
       uint32_t c = 0;
@@ -148,11 +162,20 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       meta[kBinMetaCount + k] = c;
       total += v;
       const uint64_t tb = v / (k == kBins - 1 ? 6400 : 5000), tn = c / 10;
-      t += tb > tn ? tb : tn;
+      t_split += tb > tn ? tb : tn;
+      const uint64_t sb = v / (k < kBins - 2 ? 7000 : (k == kBins - 2 ? 6500 : 5000)), sn = uint64_t(c) * 16 / 100;
+      t16 += sb > sn ? sb : sn;
     }
-    const uint64_t tb = total / 7100, tn = n * 45 / 100;
-    const bool split = force >= 0 ? force > 0 : t < (tb > tn ? tb : tn);
-    meta[kBinMetaPlan] = split ? 1u : 0u;
+    const uint64_t tb = total / 7100, tn = n * 45 / 100, t_whole = tb > tn ? tb : tn;
+    uint32_t plan = kPlanWhole;
+    if (force >= 0) {
+      plan = uint32_t(force);
+    } else {
+      uint64_t best = t_whole;
+      if (t_split < best) best = t_split, plan = kPlanSplit;
+      if (t16 < best) plan = kPlanWhole16;
+    }
+    meta[kBinMetaPlan] = plan;
   }
 }
 
@@ -179,10 +202,11 @@ struct Work {
 __device__ __forceinline__ Work resolve(const SegSrc& src, uint64_t n) {
   if (!src.list) return Work{n, nullptr};
   // selects, not branches, keep every path explicit
-  const uint32_t split = src.meta[kBinMetaPlan];
+  const uint32_t plan = src.meta[kBinMetaPlan];
+  const bool split = plan == kPlanSplit;
   const bool last = src.bin == kBins - 1;
   Work w;
-  w.items = split ? uint64_t(src.meta[kBinMetaCount + src.bin]) : (last ? n : 0);
+  w.items = split ? uint64_t(src.meta[kBinMetaCount + src.bin]) : (last && plan == kPlanWhole ? n : 0);
   w.list = split ? src.list : nullptr;
   return w;
 }
@@ -317,11 +341,25 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
                                                      const uint8_t* __restrict__ odd,
                                                      uint32_t odd_step,
                                                      void* __restrict__ out, uint64_t n, uint32_t remap) {
+  const uint32_t blk = block_order(remap);
+  if constexpr (MODE == 3 && NT && UNROLL == 8 && (LPS == 32 || LPS == 64)) {
+    // the last bin's launch under kPlanWhole16: every segment of the batch,
+    // 16-lane groups in the first n/16 (logical) blocks, the rest exit
+    if (src.list && src.bin == kBins - 1 && src.meta[kBinMetaPlan] == kPlanWhole16) {
+      constexpr uint32_t kG16 = kBlock / 16;
+      const uint64_t need = (n + kG16 - 1) / kG16;
+      const uint32_t nblk16 = uint32_t(need < gridDim.x ? need : gridDim.x);
+      if (blk >= nblk16) return;
+      SegSrc whole = src;
+      whole.list = nullptr;  // resolve(): every segment by index
+      checksum_body<16, 8, true, 3, OUT>(bytes, whole, init, init_step, odd, odd_step, out, n, blk, nblk16);
+      return;
+    }
+  }
   // a bin launch whose bin is empty (the last bin under the split plan) is
   // dispatch-bound — ~0.05 ns per wave whatever the block shape (measured,
   // tools/probe/dispatch_probe.hip) — so its waves leave before anything else
   if (src.list && resolve(src, n).items == 0) return;
-  const uint32_t blk = block_order(remap);
   checksum_body<LPS, UNROLL, NT, MODE, OUT>(bytes, src, init, init_step, odd, odd_step, out, n, blk,
                                             gridDim.x);
 }
@@ -866,7 +904,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_stats(const uint64_t* __restrict
 __global__ __launch_bounds__(kBlock) void k_bin_scatter(const uint64_t* __restrict__ off, uint64_t n,
                                                         uint32_t* __restrict__ meta,
                                                         u32x4* __restrict__ list) {
-  if (meta[kBinMetaPlan] == 0) return;  // whole-batch plan: no lists
+  if (meta[kBinMetaPlan] != kPlanSplit) return;  // whole-batch plans: no lists
   __shared__ uint32_t resv[kBins];
   for (uint64_t t0 = uint64_t(blockIdx.x) * kBinTile; t0 < n; t0 += uint64_t(gridDim.x) * kBinTile) {
     uint64_t s[kBinPerThread], len[kBinPerThread];
@@ -1061,7 +1099,7 @@ hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* 
 }
 
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
-                               hipStream_t st) {
+                               uint32_t last_lps, hipStream_t st) {
   if (!offsets || n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   uint32_t* cnt_part = meta + kBinMetaWords;
   uint64_t* by_part = reinterpret_cast<uint64_t*>(cnt_part + kBins * kBinStatBlocks);
@@ -1069,7 +1107,8 @@ hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, 
   const uint32_t parts = uint32_t(tiles < kBinStatBlocks ? tiles : kBinStatBlocks);
   hipLaunchKernelGGL(k_bin_stats, dim3(parts), dim3(kBlock), 0, st, offsets, n, cnt_part, by_part);
   if (hipError_t e = hipGetLastError()) return e;
-  hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(kBlock), 0, st, meta, cnt_part, by_part, parts, n, force_plan);
+  hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(kBlock), 0, st, meta, cnt_part, by_part, parts, n, force_plan,
+                     last_lps);
   if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL(k_bin_scatter, dim3(uint32_t(tiles < 2048 ? tiles : 2048)), dim3(kBlock), 0, st,
                      offsets, n, meta, static_cast<u32x4*>(list));

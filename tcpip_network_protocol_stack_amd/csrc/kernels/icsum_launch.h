@@ -52,14 +52,16 @@ struct SegSpec {
 constexpr int kBins = 5;
 constexpr int kBinMetaCount = 0;
 constexpr int kBinMetaCursor = 20;  // scatter pass: entries placed per bin
-constexpr int kBinMetaPlan = 28;    // 1: split into bins, 0: whole batch
+constexpr int kBinMetaPlan = 28;    // 0: whole batch, 1: split into bins, 2: whole batch in 16-lane groups
 constexpr int kBinMetaWords = 32;
 constexpr uint32_t kBinStatBlocks = 256;  // stats pass partials follow meta (<= 256: one per plan thread)
 // bytes of meta + the stats pass's partials (the lists follow, 16-byte aligned)
 constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks * 12;
-// force_plan: -1 the device plan decides, 0 whole batch, 1 split (tests)
+// force_plan: -1 the device plan decides, 0 whole batch, 1 split, 2 whole
+// batch in 16-lane groups (tests); last_lps: lanes per segment of the last
+// bin's launch (its wave count enters the plan's cost model)
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
-                               hipStream_t st);
+                               uint32_t last_lps, hipStream_t st);
 Geometry bin_geometry(int bin);
 // bins 0..kBins-2 in one launch (sp = bin_spec(whole, list, meta, 0)),
 // blocks_per_bin blocks striding over each bin

@@ -87,6 +87,9 @@ BIN_ENVS = [{"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "1"},
             # the 32-lane last-bin launch (auto above 1 M segments) under both plans
             {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "0", "ICSUM_LAST_BIN_LPS": "32"},
             {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "1", "ICSUM_LAST_BIN_LPS": "32"},
+            # the whole batch in 16-lane groups from the last bin's launch
+            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "2"},
+            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "2", "ICSUM_LAST_BIN_LPS": "32", "ICSUM_LAST_BIN_BLOCKS": "7"},
             {"ICSUM_BIN": "1"},
             {"ICSUM_BIN": "0"}]
 

@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Dev tool: interleaved in-process A/B of the binned dispatch's last-bin
 launch: its grid cap (ICSUM_LAST_BIN_BLOCKS; 0 = one lane group per segment of
-the batch) or its lanes per segment (--var ICSUM_LAST_BIN_LPS --caps 64,32).  Workloads: BASELINE config 4 (1 M mixed 64 B-64 KiB,
+the batch), its lanes per segment (--var ICSUM_LAST_BIN_LPS --caps 64,32) or
+the plan (--var ICSUM_BIN_PLAN --caps 0,1,2,-1; -1 = decided on the device).  Workloads: BASELINE config 4 (1 M mixed 64 B-64 KiB,
 whole-batch plan), the 2 M bimodal 40 B / 1460 B batch (split plan, empty last
 bin) and 2 M segments of 4-6 KiB (whole-batch plan with > 1 M segments).
 
@@ -36,6 +37,11 @@ def engine(cap):
 def batch(kind, dev, eng):
     if kind == "config4":
         off = mixed_offsets(1 << 20, 0x10710004).astype(np.int64)
+    elif kind in ("mss", "ack"):
+        rng = np.random.default_rng(0x1460)
+        lens = (1460 if kind == "mss" else 40) + rng.integers(0, 4, 1 << 20)
+        off = np.zeros(lens.size + 1, dtype=np.int64)
+        off[1:] = np.cumsum(lens)
     else:
         rng = np.random.default_rng(0x10710006)
         n = 2 << 20
@@ -53,6 +59,7 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--var", default="ICSUM_LAST_BIN_BLOCKS")
+    ap.add_argument("--workloads", default="config4,bimodal,long2m", help="config4,bimodal,long2m,mss,ack")
     args = ap.parse_args()
     global VAR
     VAR = args.var
@@ -60,7 +67,7 @@ def main():
     caps = [int(c) for c in args.caps.split(",")]
     engs = {c: engine(c) for c in caps}
     st = torch.cuda.current_stream()
-    for kind in ("config4", "bimodal", "long2m"):
+    for kind in args.workloads.split(","):
         d, off, n, nbytes = batch(kind, dev, engs[caps[0]])
         out = {c: torch.empty(n, dtype=torch.int16, device=dev) for c in caps}
         for c in caps:
