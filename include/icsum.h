@@ -101,9 +101,10 @@ int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets,
                   const uint8_t* d_odd, uint32_t* d_sum, uint64_t n, void* stream);
 
 /* Dispatch of offsets batches (d_offsets != NULL) in ics_checksum_batch /
- * ics_sum_batch.  BINNED splits the batch into length bins on the device and
- * runs each bin with the lane geometry that suits it (a one-block plan kernel
- * falls back to the whole-batch launch when the long segments dominate);
+ * ics_sum_batch.  BINNED measures the length mix on the device and a one-block
+ * plan kernel picks, per batch: split into length bins (each run with the lane
+ * geometry that suits it), or the whole batch in one launch with 64/32-lane
+ * groups (long segments dominate) or 16-lane groups (short and MTU-sized);
  * SINGLE runs one launch with the long-segment geometry.  AUTO (default) =
  * BINNED for batches of >= 65536 segments.  Results are identical; only the
  * speed differs.  Per context; not a reference interface. */
