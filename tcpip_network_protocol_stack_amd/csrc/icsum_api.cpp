@@ -71,19 +71,22 @@ struct ics_ctx {
   bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
-  static constexpr size_t kSlotBytes = size_t(64) << 20;
+  // slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each (ICSUM_HOST_SLOT_MB)
+  static constexpr int kMaxSlots = 4;
   static constexpr size_t kSlotSegs = size_t(1) << 20;
+  int nslots = 3;  // 3 x 32 MiB: pageable 49.2 -> 51.4 GB/s over 2 x 64 MiB, pinned equal (tools/ab_host.py)
+  size_t slot_bytes = size_t(32) << 20;
   bool staged = false;
-  hipStream_t st[2] = {nullptr, nullptr};
-  hipEvent_t ev[2] = {nullptr, nullptr};
-  uint8_t* h_in[2] = {nullptr, nullptr};
-  uint8_t* d_in[2] = {nullptr, nullptr};
-  uint64_t* h_off[2] = {nullptr, nullptr};
-  uint64_t* d_off[2] = {nullptr, nullptr};
-  uint32_t* h_init[2] = {nullptr, nullptr};
-  uint32_t* d_init[2] = {nullptr, nullptr};
-  uint8_t* h_out[2] = {nullptr, nullptr};   // u16 outputs or 5-byte ipv4 results
-  uint8_t* d_out[2] = {nullptr, nullptr};
+  hipStream_t st[kMaxSlots] = {};
+  hipEvent_t ev[kMaxSlots] = {};
+  uint8_t* h_in[kMaxSlots] = {};
+  uint8_t* d_in[kMaxSlots] = {};
+  uint64_t* h_off[kMaxSlots] = {};
+  uint64_t* d_off[kMaxSlots] = {};
+  uint32_t* h_init[kMaxSlots] = {};
+  uint32_t* d_init[kMaxSlots] = {};
+  uint8_t* h_out[kMaxSlots] = {};   // u16 outputs or 5-byte ipv4 results
+  uint8_t* d_out[kMaxSlots] = {};
 };
 
 namespace {
@@ -183,11 +186,11 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
 
 int ensure_staging(ics_ctx* ctx) {
   if (ctx->staged) return ICS_OK;
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < ctx->nslots; ++k) {
     ICS_HIP(hipStreamCreateWithFlags(&ctx->st[k], hipStreamNonBlocking));
     ICS_HIP(hipEventCreateWithFlags(&ctx->ev[k], hipEventDisableTiming));
-    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_in[k]), ics_ctx::kSlotBytes, 0));
-    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_in[k]), ics_ctx::kSlotBytes));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_in[k]), ctx->slot_bytes, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_in[k]), ctx->slot_bytes));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_off[k]), (ics_ctx::kSlotSegs + 1) * 8, 0));
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_off[k]), (ics_ctx::kSlotSegs + 1) * 8));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_init[k]), ics_ctx::kSlotSegs * 4, 0));
@@ -200,7 +203,7 @@ int ensure_staging(ics_ctx* ctx) {
 }
 
 void free_staging(ics_ctx* ctx) {
-  for (int k = 0; k < 2; ++k) {
+  for (int k = 0; k < ics_ctx::kMaxSlots; ++k) {
     if (ctx->st[k]) (void)hipStreamSynchronize(ctx->st[k]);
     if (ctx->h_in[k]) (void)hipHostFree(ctx->h_in[k]);
     if (ctx->d_in[k]) (void)hipFree(ctx->d_in[k]);
@@ -223,14 +226,14 @@ struct Chunk {
 
 // Next chunk starting at segment i0 that fits the slot (a single segment
 // larger than a slot is an error for the host path).
-int next_chunk(const uint64_t* offsets, uint64_t stride, uint64_t seg_len, uint64_t n, uint64_t i0,
-               Chunk* c) {
-  const uint64_t cap_b = ics_ctx::kSlotBytes, cap_n = ics_ctx::kSlotSegs;
+int next_chunk(const ics_ctx* ctx, const uint64_t* offsets, uint64_t stride, uint64_t seg_len, uint64_t n,
+               uint64_t i0, Chunk* c) {
+  const uint64_t cap_b = ctx->slot_bytes, cap_n = ics_ctx::kSlotSegs;
   if (!offsets) {
     const uint64_t per = std::max<uint64_t>(stride, seg_len);
     uint64_t k = per ? cap_b / per : cap_n;
     if (k == 0) return fail(ICS_ERR_INVALID, "segment of %llu bytes exceeds the %zu-byte staging slot",
-                            (unsigned long long)per, ics_ctx::kSlotBytes);
+                            (unsigned long long)per, ctx->slot_bytes);
     k = std::min<uint64_t>({k, cap_n, n - i0});
     *c = {i0, i0 + k, i0 * stride, (i0 + k - 1) * stride + seg_len};
     return ICS_OK;
@@ -276,8 +279,8 @@ void par_memcpy(void* dst, const void* src, size_t n) {
 }
 
 // kind 0: checksum batch (u16 out); kind 1: ipv4_tcp batch (ip u16, tcp u16, status u8).
-// Two slots alternate on two streams: while the GPU moves and sums chunk k,
-// the host prepares chunk k+1.  Pinned user buffers are DMA'd directly (no
+// The slots take turns, one stream each: while the GPU moves and sums chunk
+// k, the host prepares chunk k+1.  Pinned user buffers are DMA'd directly (no
 // host copy); pageable ones are staged through the pinned slots by par_memcpy.
 int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets,
                   uint64_t stride, uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode,
@@ -285,8 +288,8 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (int rc = ensure_staging(ctx)) return rc;
   const bool direct = host_pinned(h_bytes);
-  Chunk pending[2];
-  bool busy[2] = {false, false};
+  Chunk pending[ics_ctx::kMaxSlots];
+  bool busy[ics_ctx::kMaxSlots] = {};
   auto retire = [&](int k) -> int {
     if (!busy[k]) return ICS_OK;
     ICS_HIP(hipEventSynchronize(ctx->ev[k]));
@@ -308,7 +311,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   int slot = 0;
   while (i0 < n) {
     Chunk c;
-    if (int rc = next_chunk(h_offsets, stride, seg_len, n, i0, &c)) return rc;
+    if (int rc = next_chunk(ctx, h_offsets, stride, seg_len, n, i0, &c)) return rc;
     if (int rc = retire(slot)) return rc;
     const uint64_t m = c.i1 - c.i0, nb = c.b1 - c.b0;
     uint8_t* src = static_cast<uint8_t*>(h_bytes) + c.b0;
@@ -350,10 +353,10 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
     pending[slot] = c;
     busy[slot] = true;
     i0 = c.i1;
-    slot ^= 1;
+    slot = (slot + 1) % ctx->nslots;
   }
-  if (int rc = retire(slot)) return rc;
-  if (int rc = retire(slot ^ 1)) return rc;
+  for (int k = 0; k < ctx->nslots; ++k)  // oldest first
+    if (int rc = retire((slot + k) % ctx->nslots)) return rc;
   return ICS_OK;
 }
 
@@ -406,6 +409,8 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
   if (ctx->bin_plan > 2) ctx->bin_plan = -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
+  ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
+  ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
   if (std::getenv("ICSUM_XCD_REMAP")) icsum::set_xcd_remap(env_u32("ICSUM_XCD_REMAP", 0));
   *out = ctx;
   return ICS_OK;

@@ -430,7 +430,7 @@ def test_corruption_detection_full_size(engine, orc):
 # ------------------------------------------------ host-memory variants ---
 def test_host_path_checksum(engine, orc):
     rng = np.random.default_rng(5)
-    n, L = 200_000, 1500  # > one 64 MiB staging slot, exercises the 2-slot pipeline
+    n, L = 200_000, 1500  # > one 32 MiB staging slot: every slot of the pipeline, several times
     buf = rng.integers(0, 256, n * L, dtype=np.uint8)
     init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     got = engine.checksum_batch_host(buf, n, stride=L, seg_len=L, init=init)

@@ -177,7 +177,7 @@ def main():
                 eng.checksum_batch_host(h.numpy(), n, stride=L, seg_len=L, init=hi)
                 ts.append(time.perf_counter() - t0)
             emit(f"host_inclusive_256Kix1500_{'pinned' if pinned else 'pageable'}", n * L, statistics.median(ts),
-                 n * 6, entry="ics_checksum_batch_host", note="H2D + kernel + D2H, 2-slot pipeline")
+                 n * 6, entry="ics_checksum_batch_host", note="H2D + kernel + D2H, 3-slot pipeline")
             if pinned:  # the link's own ceiling: one plain H2D copy of the same pinned bytes, no kernel
                 d = torch.empty(n * L, dtype=torch.uint8, device=dev)
                 d.copy_(h, non_blocking=True)
