@@ -67,7 +67,7 @@ struct ics_ctx {
   uint32_t last_bin_blocks = 0;  // grid cap of the last bin's launch (0: one lane group per segment)
   uint32_t last_bin_lps = 0;     // lanes per segment of the last bin's launch (0: auto, see checksum_device)
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
-  int bin_plan = -1;        // -1: decided on the device per batch; forced (tests): 0 whole, 1 split, 2 whole16
+  int bin_plan = -1;        // -1: decided on the device per batch; forced (tests): 0 whole, 1 split, 2 whole16, 3 wholeS
   bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
   std::mutex mu;
   // host path: two slots, each with pinned in/out staging and device buffers
@@ -407,7 +407,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->last_bin_lps = env_u32("ICSUM_LAST_BIN_LPS", 0);
   if (std::getenv("ICSUM_DENSE_SEGS")) ctx->dense_segs = int(env_u32("ICSUM_DENSE_SEGS", 4));
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
-  if (ctx->bin_plan > 2) ctx->bin_plan = -1;
+  if (ctx->bin_plan > 3) ctx->bin_plan = -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;

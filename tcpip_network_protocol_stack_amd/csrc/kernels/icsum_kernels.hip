@@ -107,11 +107,15 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total)
 //   whole16: sum over bins of max(bytes_b / r16_b, n_b * 0.16 ns) + the
 //            waves past n/4, r16 = 7000 GB/s up to 1920-byte segments, 6500 up
 //            to 4 KiB, 5000 above (16 lanes loop over long segments)
+//   wholeS:  the small-segment body (4 lanes, 2 segments per group in flight)
+//            over every segment: bin 0 max(bytes / 5000, n_b * 0.02 ns), any
+//            longer segment max(bytes / 800, n_b * 0.5 ns) (4 lanes loop), +
+//            the waves past n/32 — for batches of ACK-sized segments
 // Measured under each forced plan (tools/ab_lastbin.py --var ICSUM_BIN_PLAN,
 // profiles/r1_ab_plans.jsonl), µs whole / split / whole16: config 4
 // 1429 / 1622 / 1682, 2 M bimodal 40+1460 B 525 / 473 / 364, 2 M x 4-6 KiB
 // 1515 / 1589 / 1593, 1 M x 1460 B 520 / 429 / 296, 1 M x 40 B 451 / 168 / 205.
-constexpr uint32_t kPlanWhole = 0, kPlanSplit = 1, kPlanWhole16 = 2;
+constexpr uint32_t kPlanWhole = 0, kPlanSplit = 1, kPlanWhole16 = 2, kPlanWholeSmall = 3;
 
 __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta, const uint32_t* __restrict__ cnt_part,
                                                      const uint64_t* __restrict__ by_part, uint32_t parts, uint64_t n,
@@ -149,7 +153,8 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint64_t waves = n * last_lps / 64;  // the last bin's launch
-    uint64_t total = 0, t_split = 26000 + waves * 53 / 1000, t16 = (waves - n / 4) * 53 / 1000;
+    uint64_t total = 0, t_split = 26000 + waves * 53 / 1000, t16 = (waves - n / 4) * 53 / 1000,
+             t_small = (waves - n / 32) * 53 / 1000;
 #pragma unroll
     for (int k = 0; k < kBins; ++k) {
       uint32_t c = 0;
@@ -165,6 +170,8 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       t_split += tb > tn ? tb : tn;
       const uint64_t sb = v / (k < kBins - 2 ? 7000 : (k == kBins - 2 ? 6500 : 5000)), sn = uint64_t(c) * 16 / 100;
       t16 += sb > sn ? sb : sn;
+      const uint64_t mb = v / (k == 0 ? 5000 : 800), mn = uint64_t(c) * (k == 0 ? 2 : 50) / 100;
+      t_small += mb > mn ? mb : mn;
     }
     const uint64_t tb = total / 7100, tn = n * 45 / 100, t_whole = tb > tn ? tb : tn;
     uint32_t plan = kPlanWhole;
@@ -173,7 +180,8 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
     } else {
       uint64_t best = t_whole;
       if (t_split < best) best = t_split, plan = kPlanSplit;
-      if (t16 < best) plan = kPlanWhole16;
+      if (t16 < best) best = t16, plan = kPlanWhole16;
+      if (t_small < best) plan = kPlanWholeSmall;
     }
     meta[kBinMetaPlan] = plan;
   }
@@ -334,13 +342,21 @@ __device__ __forceinline__ uint32_t block_order(uint32_t run_log2) {
   return ((k >> lc) << (lc + 3)) + (x << lc) + (k & ((1u << lc) - 1u));
 }
 
+template <int LPS, int UNROLL, int SEGS, int OUT>
+__device__ __forceinline__ void checksum_small_body(const uint8_t* __restrict__ bytes, const SegSrc& src,
+                                                    const uint32_t* __restrict__ init, uint32_t init_step,
+                                                    const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                                    const u32x4* __restrict__ zero16, void* __restrict__ out,
+                                                    uint64_t n, uint32_t blk, uint32_t nblk);  // below
+
 template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
 __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes, SegSrc src,
                                                      const uint32_t* __restrict__ init,
                                                      uint32_t init_step,
                                                      const uint8_t* __restrict__ odd,
                                                      uint32_t odd_step,
-                                                     void* __restrict__ out, uint64_t n, uint32_t remap) {
+                                                     void* __restrict__ out, uint64_t n, uint32_t remap,
+                                                     const u32x4* __restrict__ zero16) {
   const uint32_t blk = block_order(remap);
   if constexpr (MODE == 3 && NT && UNROLL == 8 && (LPS == 32 || LPS == 64)) {
     // the last bin's launch under kPlanWhole16: every segment of the batch,
@@ -353,6 +369,18 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
       SegSrc whole = src;
       whole.list = nullptr;  // resolve(): every segment by index
       checksum_body<16, 8, true, 3, OUT>(bytes, whole, init, init_step, odd, odd_step, out, n, blk, nblk16);
+      return;
+    }
+    // ... under kPlanWholeSmall: the small-segment body (4 lanes, 2 segments
+    // per group in flight) in the first n/128 (logical) blocks
+    if (src.list && src.bin == kBins - 1 && src.meta[kBinMetaPlan] == kPlanWholeSmall) {
+      constexpr uint32_t kPerBlock = (kBlock / 4) * 2;
+      const uint64_t need = (n + kPerBlock - 1) / kPerBlock;
+      const uint32_t nblks = uint32_t(need < gridDim.x ? need : gridDim.x);
+      if (blk >= nblks) return;
+      SegSrc whole = src;
+      whole.list = nullptr;
+      checksum_small_body<4, 2, 2, OUT>(bytes, whole, init, init_step, odd, odd_step, zero16, out, n, blk, nblks);
       return;
     }
   }
@@ -972,10 +1000,10 @@ hipError_t launch_checksum_t(const SegSpec& sp, const uint32_t* init, const uint
   const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
   if (out_kind == 0)
     hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap);
+                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap, static_cast<const u32x4*>(sp.zero16));
   else
     hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap);
+                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap, static_cast<const u32x4*>(sp.zero16));
   return hipGetLastError();
 }
 

@@ -52,13 +52,14 @@ struct SegSpec {
 constexpr int kBins = 5;
 constexpr int kBinMetaCount = 0;
 constexpr int kBinMetaCursor = 20;  // scatter pass: entries placed per bin
-constexpr int kBinMetaPlan = 28;    // 0: whole batch, 1: split into bins, 2: whole batch in 16-lane groups
+constexpr int kBinMetaPlan = 28;    // 0: whole batch, 1: split into bins, 2: whole batch in 16-lane groups,
+                                    // 3: whole batch through the small-segment body
 constexpr int kBinMetaWords = 32;
 constexpr uint32_t kBinStatBlocks = 256;  // stats pass partials follow meta (<= 256: one per plan thread)
 // bytes of meta + the stats pass's partials (the lists follow, 16-byte aligned)
 constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks * 12;
 // force_plan: -1 the device plan decides, 0 whole batch, 1 split, 2 whole
-// batch in 16-lane groups (tests); last_lps: lanes per segment of the last
+// batch in 16-lane groups, 3 whole batch through the small-segment body (tests); last_lps: lanes per segment of the last
 // bin's launch (its wave count enters the plan's cost model)
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
                                uint32_t last_lps, hipStream_t st);

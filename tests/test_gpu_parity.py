@@ -90,6 +90,9 @@ BIN_ENVS = [{"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "1"},
             # the whole batch in 16-lane groups from the last bin's launch
             {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "2"},
             {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "2", "ICSUM_LAST_BIN_LPS": "32", "ICSUM_LAST_BIN_BLOCKS": "7"},
+            # ... or through the small-segment body
+            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "3"},
+            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "3", "ICSUM_LAST_BIN_LPS": "32", "ICSUM_LAST_BIN_BLOCKS": "5"},
             {"ICSUM_BIN": "1"},
             {"ICSUM_BIN": "0"}]
 
