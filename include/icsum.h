@@ -104,7 +104,8 @@ int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets,
  * ics_sum_batch.  BINNED measures the length mix on the device and a one-block
  * plan kernel picks, per batch: split into length bins (each run with the lane
  * geometry that suits it), or the whole batch in one launch with 64/32-lane
- * groups (long segments dominate) or 16-lane groups (short and MTU-sized);
+ * groups (long segments dominate), 16-lane groups (short and MTU-sized) or
+ * the small-segment body (ACK-sized);
  * SINGLE runs one launch with the long-segment geometry.  AUTO (default) =
  * BINNED for batches of >= 65536 segments.  Results are identical; only the
  * speed differs.  Per context; not a reference interface. */
