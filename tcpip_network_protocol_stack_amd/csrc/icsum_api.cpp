@@ -69,9 +69,10 @@ struct ics_ctx {
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
   int bin_plan = -1;        // -1: decided on the device per batch; forced (tests): 0 whole, 1 split, 2 whole16, 3 wholeS
   bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
+  bool bin_debug = false;   // ICSUM_BIN_DEBUG: dump the binning pass's meta words after each binned call (dev)
   std::mutex mu;
-  // host path: two slots, each with pinned in/out staging and device buffers
-  // slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each (ICSUM_HOST_SLOT_MB)
+  // host path: nslots slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each
+  // (ICSUM_HOST_SLOT_MB), each with pinned in/out staging, device buffers and a stream
   static constexpr int kMaxSlots = 4;
   static constexpr size_t kSlotSegs = size_t(1) << 20;
   int nslots = 3;  // 3 x 32 MiB: pageable 49.2 -> 51.4 GB/s over 2 x 64 MiB, pinned equal (tools/ab_host.py)
@@ -170,7 +171,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   if (e == hipSuccess)
     e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, icsum::kBins - 1), d_init, d_odd, d_out, out_kind,
                                g_last, ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks, st);
-  if (e == hipSuccess && std::getenv("ICSUM_BIN_DEBUG")) {  // dev: dump the binning pass's meta words
+  if (e == hipSuccess && ctx->bin_debug) {  // dev: dump the binning pass's meta words
     uint32_t h[icsum::kBinMetaWords];
     if (hipMemcpyAsync(h, meta, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess) {
       std::fprintf(stderr, "icsum bin meta:");
@@ -409,6 +410,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
   if (ctx->bin_plan > 3) ctx->bin_plan = -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
+  ctx->bin_debug = std::getenv("ICSUM_BIN_DEBUG") != nullptr;
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
   if (std::getenv("ICSUM_XCD_REMAP")) icsum::set_xcd_remap(env_u32("ICSUM_XCD_REMAP", 0));
