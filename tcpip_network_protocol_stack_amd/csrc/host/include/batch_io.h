@@ -41,8 +41,16 @@ class DatagramBatch
     DatagramBatch(const DatagramBatch&) = delete;
     DatagramBatch& operator=(const DatagramBatch&) = delete;
 
-    void clear() { off_.assign(1, 0); }
+    void clear()
+    {
+        off_.assign(1, 0);
+        ended_ = false;
+    }
     size_t size() const { return off_.size() - 1; }
+    // no room for another datagram of the reference's maximum read size
+    bool full() const { return !room(kMaxDatagram); }
+    // the last read_from saw the end of the stream (0-byte read or message)
+    bool ended() const { return ended_; }
     size_t bytes() const { return off_.back(); }
     std::string_view operator[](size_t i) const
     {
@@ -72,12 +80,18 @@ class DatagramBatch
     uint8_t* arena_ = nullptr;
     size_t cap_ = 0, max_n_ = 0;
     std::vector<uint64_t> off_{0};
+    bool ended_ = false;
     bool room(size_t n) const { return size() < max_n_ && bytes() + n <= cap_; }
 };
 
 // A ring of page-locked DatagramBatch arenas with a reader thread: while the
 // caller runs batch k through the engine (verify / unwrap / patch), the reader
 // fills arena k+1 from the fd, so socket reads overlap the PCIe + GPU pass.
+// The reader keeps appending to its arena while the caller is busy and hands
+// it over when it is full or as soon as the caller waits in next(): batches
+// grow with the caller's pass time instead of one socket drain each, so the
+// ring does not run out of free arenas (and a UDP socket does not overflow)
+// behind a stream of small batches.
 // The fd is the caller's and must be blocking (a socket, TUN or other packet
 // fd); the reader polls it, reads once it is readable, and stops at end of
 // stream (read_from returns 0: the peer closed).  The destructor stops and
@@ -108,7 +122,7 @@ class DatagramRing
     std::deque<DatagramBatch*> free_, ready_;
     std::mutex mu_;
     std::condition_variable cv_;
-    bool eof_ = false, stop_ = false;
+    bool eof_ = false, stop_ = false, waiting_ = false;
     std::exception_ptr error_;
     std::thread thread_;
 };

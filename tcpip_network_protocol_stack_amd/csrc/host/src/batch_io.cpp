@@ -97,7 +97,11 @@ size_t DatagramBatch::read_from(int fd, size_t max)
                 off_.push_back(bytes() + len);
             }
             got += size_t(j);
-            if (j < r || size_t(r) < k) break;
+            if (j < r) {
+                ended_ = true;
+                break;
+            }
+            if (size_t(r) < k) break;
         }
         return got;
     }
@@ -108,7 +112,10 @@ size_t DatagramBatch::read_from(int fd, size_t max)
             if (errno == EAGAIN || errno == EWOULDBLOCK || errno == EINTR) break;
             sys_fail("read");
         }
-        if (r == 0) break;
+        if (r == 0) {
+            ended_ = true;
+            break;
+        }
         off_.push_back(bytes() + size_t(r));
         ++got;
     }
@@ -198,32 +205,40 @@ void DatagramRing::reader()
             free_.pop_front();
         }
         b->clear();
-        size_t got = 0;
+        bool end = false;
         try {
-            // wait until the fd is readable (or at end of stream), looking at
-            // stop_ in between, so the destructor never waits on a blocked read
-            bool go = false;
-            while (!go) {
+            // append until the arena is full, the stream ends, or the caller
+            // waits with a non-empty arena here; poll with a timeout, looking
+            // at stop_ in between, so the destructor never waits on a blocked
+            // read (1 ms while holding datagrams, so an idle caller gets them)
+            for (;;) {
+                {
+                    std::lock_guard<std::mutex> lock(mu_);
+                    if (stop_ || (b->size() && waiting_)) break;
+                }
                 pollfd p{fd_, POLLIN, 0};
-                const int r = ::poll(&p, 1, 50);
+                const int r = ::poll(&p, 1, b->size() ? 1 : 50);
                 if (r < 0 && errno != EINTR) sys_fail("poll");
-                go = r > 0;
-                std::lock_guard<std::mutex> lock(mu_);
-                if (stop_ && !go) break;
+                if (r <= 0) continue;
+                b->read_from(fd_, max_n_ - b->size());
+                if (b->ended()) {
+                    end = true;
+                    break;
+                }
+                if (b->full()) break;
             }
-            if (go) got = b->read_from(fd_, max_n_);
         } catch (...) {
             std::lock_guard<std::mutex> lock(mu_);
             error_ = std::current_exception();
+            end = true;
         }
         std::lock_guard<std::mutex> lock(mu_);
-        if (got == 0) {  // end of stream (or an error): hand the arena back and stop
+        if (b->size())
+            ready_.push_back(b);
+        else
             free_.push_back(b);
-            eof_ = true;
-            break;
-        }
-        ready_.push_back(b);
         cv_.notify_all();
+        if (end || stop_) break;
     }
     std::lock_guard<std::mutex> lock(mu_);
     eof_ = true;
@@ -233,7 +248,9 @@ void DatagramRing::reader()
 DatagramBatch* DatagramRing::next()
 {
     std::unique_lock<std::mutex> lock(mu_);
+    waiting_ = true;
     cv_.wait(lock, [this] { return !ready_.empty() || eof_; });
+    waiting_ = false;
     if (!ready_.empty()) {
         DatagramBatch* b = ready_.front();
         ready_.pop_front();

@@ -1,5 +1,6 @@
 // host_gpu_test.cpp — icsum::BatchEngine (GPU) against the per-object calls of
 // the same drop-in types (CPU) on seeded random traffic.  Exit 0 = identical.
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <random>
@@ -7,6 +8,8 @@
 #include <thread>
 #include <vector>
 
+#include <arpa/inet.h>
+#include <netinet/in.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -227,6 +230,64 @@ int main()
         EXPECT(recv(sv[1], &c, 1, 0) == 1 && c == 'x');
         close(sv[0]);
         close(sv[1]);
+    }
+    // DatagramRing over a UDP socket on 127.0.0.1 (the transport the
+    // reference's endtoend relay uses): no end of stream and drops allowed,
+    // so the writer repeats an empty datagram (the end marker) until the ring
+    // stops; what arrives is an in-order subsequence of what was sent, every
+    // datagram with the status verify_raw() gave it
+    {
+        int tx = socket(AF_INET, SOCK_DGRAM, 0), rxfd = socket(AF_INET, SOCK_DGRAM, 0);
+        sockaddr_in a{};
+        a.sin_family = AF_INET;
+        a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+        socklen_t alen = sizeof a;
+        const int buf = 4 << 20;
+        (void)setsockopt(rxfd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+        EXPECT(tx >= 0 && rxfd >= 0);
+        EXPECT(bind(rxfd, reinterpret_cast<sockaddr*>(&a), sizeof a) == 0);
+        EXPECT(getsockname(rxfd, reinterpret_cast<sockaddr*>(&a), &alen) == 0);
+        EXPECT(connect(tx, reinterpret_cast<sockaddr*>(&a), sizeof a) == 0);
+        constexpr size_t kPasses = 8;
+        std::atomic<bool> done{false};
+        std::thread writer([&] {
+            icsum::DatagramBatch txb(size_t(1) << 20);
+            for (size_t p = 0; p < kPasses; ++p) {
+                for (size_t i = 0; i < rx.size();) {
+                    txb.clear();
+                    size_t j = i;
+                    for (; j < rx.size() && j - i < 64 && txb.push(rx[j]); ++j) {
+                    }
+                    txb.write_to(tx);
+                    i = j;
+                }
+            }
+            while (!done.load()) {
+                (void)send(tx, "", 0, 0);
+                std::this_thread::sleep_for(std::chrono::milliseconds(1));
+            }
+        });
+        size_t seen = 0, pos = 0;
+        bool ordered = true;
+        {
+            icsum::DatagramRing ring(eng, rxfd, 3, size_t(4) << 20, 700);
+            while (icsum::DatagramBatch* b = ring.next()) {
+                const auto vs = b->verify();
+                for (size_t k = 0; k < vs.size(); ++k, ++seen) {
+                    while (pos < kPasses * rx.size() && (*b)[k] != rx[pos % rx.size()]) ++pos;
+                    ordered = ordered && pos < kPasses * rx.size();
+                    if (ordered) EXPECT(vs[k] == st[pos % rx.size()]);
+                    ++pos;
+                }
+                ring.release(b);
+            }
+        }
+        done = true;
+        writer.join();
+        close(tx);
+        close(rxfd);
+        EXPECT(ordered);
+        EXPECT(seen > 0 && seen <= kPasses * rx.size());
     }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);

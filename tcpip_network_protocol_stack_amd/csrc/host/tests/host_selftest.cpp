@@ -141,7 +141,7 @@ int main()
             std::cout << sent << " " << got << " " << same << " " << rx.bytes() << "\n";
         } else if (cmd == "ioseq") {
             // SOCK_SEQPACKET stream: a writer thread sends every wire 4 times
-            // and closes its end; read_from(64) until it reports end of stream
+            // and closes its end; read_from(64) until it returns 0
             std::vector<std::string> ws;
             std::string h;
             while (in >> h) ws.push_back(unhex(h));
@@ -160,18 +160,21 @@ int main()
             });
             icsum::DatagramBatch rx(size_t(1) << 22, 64);
             size_t got = 0, reads = 0;
-            bool same = true;
+            bool same = true, ended_early = false;
             for (;;) {
                 rx.clear();
                 const size_t k = rx.read_from(sv[1], 64);
                 ++reads;
                 if (k == 0) break;
+                ended_early = ended_early || (rx.ended() && got + k < 4 * ws.size());
                 for (size_t i = 0; i < k; ++i) same = same && rx[i] == ws[(got + i) % ws.size()];
                 got += k;
             }
             w.join();
             close(sv[1]);
-            std::cout << sent << " " << got << " " << same << " " << (reads > 1) << "\n";
+            // ended() is set by the read that meets the end, never before
+            std::cout << sent << " " << got << " " << same << " " << (reads > 1) << " "
+                      << (rx.ended() && !ended_early) << "\n";
         } else if (!cmd.empty()) {
             std::cerr << "unknown command " << cmd << "\n";
             return 1;

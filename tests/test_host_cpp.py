@@ -116,5 +116,5 @@ def test_datagram_batch_seqpacket_end_of_stream(selftest):
     # end of stream are not datagrams) — what DatagramRing's reader relies on
     cases = wires("tcp_wrap.json")
     line = "ioseq " + " ".join(c["wire"] for c in cases)
-    sent, got, same, several = (int(x) for x in selftest([line])[0].split())
-    assert sent == got == 4 * len(cases) and same == 1 and several == 1
+    sent, got, same, several, ended = (int(x) for x in selftest([line])[0].split())
+    assert sent == got == 4 * len(cases) and same == 1 and several == 1 and ended == 1
