@@ -14,7 +14,11 @@
 // `writers` > 1 splits the passes over that many writer threads on the same
 // socket, so the sender side (which does the kernel's per-datagram work on
 // loopback) stops being the ceiling and the receive path is measured.
-//   build/ring_bench [passes] [seqpacket|udp] [writers]
+// `readers` > 1 gives every reader its own socket, engine and ring on its own
+// thread (writer k sends to socket k % readers; one port per socket stands in
+// for SO_REUSEPORT's flow hashing, which would not let the bench end each
+// socket's stream), to see whether the host side scales with reading threads.
+//   build/ring_bench [passes] [seqpacket|udp] [writers] [readers]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
@@ -22,6 +26,9 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
+#include <memory>
+#include <mutex>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -58,11 +65,15 @@ std::vector<std::string> make_wires(icsum::BatchEngine& eng, size_t n)
     return wires;
 }
 
-std::atomic<bool> g_rx_done{false};
-std::atomic<int> g_writers_left{0};
+// one receiving socket and its writers' end-of-stream bookkeeping
+struct Lane {
+    int tx = -1, rx = -1;
+    std::atomic<int> writers_left{0};
+    std::atomic<bool> rx_done{false};
+};
 
-// the last writer to finish ends the stream (close, or UDP end markers)
-void writer(int fd, const std::vector<std::string>& wires, size_t passes, bool udp)
+// the last writer of a lane ends its stream (close, or UDP end markers)
+void writer(Lane& lane, const std::vector<std::string>& wires, size_t passes, bool udp)
 {
     icsum::DatagramBatch txb(size_t(4) << 20);
     for (size_t p = 0; p < passes; ++p)
@@ -71,16 +82,16 @@ void writer(int fd, const std::vector<std::string>& wires, size_t passes, bool u
             size_t j = i;
             for (; j < wires.size() && j - i < 1024 && txb.push(wires[j]); ++j) {
             }
-            txb.write_to(fd);
+            txb.write_to(lane.tx);
             i = j;
         }
-    if (g_writers_left.fetch_sub(1) != 1) return;
+    if (lane.writers_left.fetch_sub(1) != 1) return;
     if (udp)  // end marker: an empty datagram, repeated since UDP may drop it
-        while (!g_rx_done.load()) {
-            (void)send(fd, "", 0, 0);
+        while (!lane.rx_done.load()) {
+            (void)send(lane.tx, "", 0, 0);
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
         }
-    close(fd);
+    close(lane.tx);
 }
 
 // a connected pair of UDP sockets on 127.0.0.1: sv[0] sends, sv[1] receives
@@ -105,46 +116,80 @@ void big_buffers(int fd)
     (void)setsockopt(fd, SOL_SOCKET, SO_RCVBUF, &sz, sizeof sz);
 }
 
+// `readers` receiving sockets (one receive() call each, on its own thread
+// when readers > 1), writer k sending to socket k % readers
 template <class Receive>
 void run(const char* mode, const std::vector<std::string>& wires, size_t passes, bool udp, size_t writers,
-         Receive receive)
+         std::vector<std::unique_ptr<icsum::BatchEngine>>& engs, Receive receive)
 {
-    int sv[2];
-    if (udp ? !udp_pair(sv) : socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) != 0) {
-        std::perror(udp ? "udp socket" : "socketpair");
-        std::exit(1);
-    }
-    big_buffers(sv[0]);
-    big_buffers(sv[1]);
+    const size_t readers = engs.size();
+    std::vector<Lane> lanes(readers);
     int rcvbuf = 0;
-    socklen_t optlen = sizeof rcvbuf;
-    (void)getsockopt(sv[1], SOL_SOCKET, SO_RCVBUF, &rcvbuf, &optlen);
-    g_rx_done = false;
-    g_writers_left = static_cast<int>(writers);
-    // the receiver sets up its arenas (page-locked allocations take tens of
-    // ms) and then calls start(): the clock and the writers start there, so
-    // a UDP socket does not overflow while nobody can read it yet
+    for (auto& l : lanes) {
+        int sv[2];
+        if (udp ? !udp_pair(sv) : socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) != 0) {
+            std::perror(udp ? "udp socket" : "socketpair");
+            std::exit(1);
+        }
+        l.tx = sv[0];
+        l.rx = sv[1];
+        big_buffers(l.tx);
+        big_buffers(l.rx);
+        socklen_t optlen = sizeof rcvbuf;
+        (void)getsockopt(l.rx, SOL_SOCKET, SO_RCVBUF, &rcvbuf, &optlen);
+    }
+    for (size_t k = 0; k < writers; ++k) ++lanes[k % readers].writers_left;
+    // each receiver sets up its arenas (page-locked allocations take tens of
+    // ms) and then calls start(); the clock and the writers start once every
+    // receiver is ready, so no UDP socket overflows while nobody can read it
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t ready = 0;
+    bool go = false;
+    auto start = [&] {
+        std::unique_lock<std::mutex> lock(mu);
+        ++ready;
+        cv.notify_all();
+        cv.wait(lock, [&] { return go; });
+    };
+    std::vector<size_t> got(readers, 0), accepted(readers, 0);
+    std::vector<std::thread> rs;
+    for (size_t r = 0; r < readers; ++r)
+        rs.emplace_back([&, r] {
+            got[r] = receive(lanes[r].rx, *engs[r], accepted[r], start);
+            lanes[r].rx_done = true;
+        });
     std::chrono::steady_clock::time_point t0;
     std::vector<std::thread> ws;
-    auto start = [&] {
+    {
+        std::unique_lock<std::mutex> lock(mu);
+        cv.wait(lock, [&] { return ready == readers; });
         t0 = std::chrono::steady_clock::now();
         for (size_t k = 0; k < writers; ++k)
-            ws.emplace_back(writer, sv[0], std::cref(wires), passes / writers + (k < passes % writers), udp);
-    };
-    size_t accepted = 0;
-    const size_t got = receive(sv[1], accepted, start);
-    g_rx_done = true;
+            ws.emplace_back(writer, std::ref(lanes[k % readers]), std::cref(wires),
+                            passes / writers + (k < passes % writers), udp);
+        go = true;
+    }
+    cv.notify_all();
+    for (auto& t : rs) t.join();
+    const auto t1 = std::chrono::steady_clock::now();
     for (auto& w : ws) w.join();
-    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-    close(sv[1]);
-    const double bytes = double(got) * double(wires[0].size());
+    for (auto& l : lanes) close(l.rx);
+    const double s = std::chrono::duration<double>(t1 - t0).count();
+    size_t n = 0, acc = 0;
+    for (size_t r = 0; r < readers; ++r) {
+        n += got[r];
+        acc += accepted[r];
+    }
+    const double bytes = double(n) * double(wires[0].size());
     const size_t sent = wires.size() * passes;
-    std::printf("{\"transport\": \"%s\", \"writers\": %zu, \"mode\": \"%s\", \"sent\": %zu, \"datagrams\": %zu, "
-                "\"accepted\": %zu, \"rcvbuf\": %d, \"seconds\": %.4f, \"Mdgram_s\": %.3f, \"GB_s\": %.3f}\n",
-                udp ? "udp_loopback" : "seqpacket_socketpair", writers, mode, sent, got, accepted, rcvbuf, s, got / s / 1e6,
-                bytes / s / 1e9);
+    std::printf("{\"transport\": \"%s\", \"writers\": %zu, \"readers\": %zu, \"mode\": \"%s\", \"sent\": %zu, "
+                "\"datagrams\": %zu, \"accepted\": %zu, \"rcvbuf\": %d, \"seconds\": %.4f, \"Mdgram_s\": %.3f, "
+                "\"GB_s\": %.3f}\n",
+                udp ? "udp_loopback" : "seqpacket_socketpair", writers, readers, mode, sent, n, acc, rcvbuf, s,
+                n / s / 1e6, bytes / s / 1e9);
     // UDP may drop (reported above); nothing may arrive corrupted or twice
-    if ((udp ? got > sent : got != sent) || (accepted != 0 && accepted != got)) std::exit(2);
+    if ((udp ? n > sent : n != sent) || (acc != 0 && acc != n)) std::exit(2);
 }
 
 }  // namespace
@@ -153,37 +198,43 @@ int main(int argc, char** argv)
 {
     const size_t passes = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 4;
     const bool udp = argc > 2 && std::string(argv[2]) == "udp";
-    const size_t writers = std::max<size_t>(1, argc > 3 ? std::strtoul(argv[3], nullptr, 10) : 1);
-    icsum::BatchEngine eng(0);
-    const auto wires = make_wires(eng, size_t(1) << 16);
+    const size_t readers = std::max<size_t>(1, argc > 4 ? std::strtoul(argv[4], nullptr, 10) : 1);
+    // every socket needs a writer to end its stream
+    const size_t writers = std::max<size_t>(readers, argc > 3 ? std::strtoul(argv[3], nullptr, 10) : 1);
+    // one engine per receiving thread (a context is used by one thread)
+    std::vector<std::unique_ptr<icsum::BatchEngine>> engs;
+    for (size_t r = 0; r < readers; ++r) engs.push_back(std::make_unique<icsum::BatchEngine>(0));
+    const auto wires = make_wires(*engs[0], size_t(1) << 16);
     constexpr size_t kBatch = 1 << 14;  // datagrams per arena (24 MB of 1500-byte datagrams)
 
-    run("read_only", wires, passes, udp, writers, [&](int fd, size_t&, auto start) {
+    run("read_only", wires, passes, udp, writers, engs, [&](int fd, icsum::BatchEngine& eng, size_t&, auto start) {
         icsum::DatagramBatch rxb(eng, size_t(32) << 20, kBatch);
         start();
         size_t n = 0;
         while (true) {
             rxb.clear();
             const size_t k = rxb.read_from(fd, kBatch);
-            if (k == 0) break;
             n += k;
+            if (k == 0 || rxb.ended()) break;
         }
         return n;
     });
-    run("read_then_verify", wires, passes, udp, writers, [&](int fd, size_t& accepted, auto start) {
+    run("read_then_verify", wires, passes, udp, writers, engs, [&](int fd, icsum::BatchEngine& eng, size_t& accepted, auto start) {
         icsum::DatagramBatch rxb(eng, size_t(32) << 20, kBatch);
         start();
         size_t n = 0;
         while (true) {
             rxb.clear();
             const size_t k = rxb.read_from(fd, kBatch);
-            if (k == 0) break;
-            for (uint8_t st : rxb.verify()) accepted += st == ICS_ST_ACCEPT;
-            n += k;
+            if (k) {
+                for (uint8_t st : rxb.verify()) accepted += st == ICS_ST_ACCEPT;
+                n += k;
+            }
+            if (k == 0 || rxb.ended()) break;
         }
         return n;
     });
-    run("ring_3x_verify", wires, passes, udp, writers, [&](int fd, size_t& accepted, auto start) {
+    run("ring_3x_verify", wires, passes, udp, writers, engs, [&](int fd, icsum::BatchEngine& eng, size_t& accepted, auto start) {
         icsum::DatagramRing ring(eng, fd, 3, size_t(32) << 20, kBatch);
         start();
         size_t n = 0;
