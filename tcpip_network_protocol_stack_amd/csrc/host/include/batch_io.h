@@ -97,12 +97,18 @@ class DatagramBatch
 // stream (read_from returns 0: the peer closed).  The destructor stops and
 // joins the reader within one 50 ms poll interval, and leaves the fd as it
 // was.  Only the reader thread touches the fd; only the caller's thread
-// touches the engine.
+// touches the engine.  With several fds there is one reader thread per fd.
 class DatagramRing
 {
   public:
     DatagramRing(BatchEngine& engine, int fd, size_t slots = 3, size_t capacity_bytes = size_t(32) << 20,
                  size_t max_datagrams = 1 << 14);
+    // several fds (e.g. SO_REUSEPORT sockets), one reader thread each, sharing
+    // the arenas: next() returns filled arenas from any of them, so one caller
+    // and one engine serve every socket; slots = 0 means 2 * fds + 1.  The
+    // stream ends when every fd has ended.
+    DatagramRing(BatchEngine& engine, const std::vector<int>& fds, size_t slots = 0,
+                 size_t capacity_bytes = size_t(32) << 20, size_t max_datagrams = 1 << 14);
     ~DatagramRing();
     DatagramRing(const DatagramRing&) = delete;
     DatagramRing& operator=(const DatagramRing&) = delete;
@@ -114,17 +120,18 @@ class DatagramRing
     void release(DatagramBatch* batch);
 
   private:
-    void reader();
+    void start(BatchEngine& engine, size_t slots, size_t capacity_bytes);
+    void reader(int fd);
 
-    int fd_;
-    size_t max_n_;
+    std::vector<int> fds_;
+    size_t max_n_, live_ = 0;
     std::vector<std::unique_ptr<DatagramBatch>> arenas_;
     std::deque<DatagramBatch*> free_, ready_;
     std::mutex mu_;
     std::condition_variable cv_;
     bool eof_ = false, stop_ = false, waiting_ = false;
     std::exception_ptr error_;
-    std::thread thread_;
+    std::vector<std::thread> threads_;
 };
 
 }  // namespace icsum

@@ -173,14 +173,30 @@ void DatagramBatch::patch()
 }
 
 DatagramRing::DatagramRing(BatchEngine& engine, int fd, size_t slots, size_t capacity_bytes, size_t max_datagrams)
-    : fd_(fd), max_n_(max_datagrams)
+    : fds_{fd}, max_n_(max_datagrams)
 {
-    if (slots < 2) throw std::invalid_argument("DatagramRing needs at least 2 slots");
+    start(engine, slots, capacity_bytes);
+}
+
+DatagramRing::DatagramRing(BatchEngine& engine, const std::vector<int>& fds, size_t slots, size_t capacity_bytes,
+                           size_t max_datagrams)
+    : fds_(fds), max_n_(max_datagrams)
+{
+    if (fds.empty()) throw std::invalid_argument("DatagramRing needs at least one fd");
+    start(engine, slots ? slots : 2 * fds.size() + 1, capacity_bytes);
+}
+
+void DatagramRing::start(BatchEngine& engine, size_t slots, size_t capacity_bytes)
+{
+    // every reader holds one arena while it fills it; one more keeps a
+    // filled arena moving to the caller
+    if (slots < fds_.size() + 1) throw std::invalid_argument("DatagramRing needs more slots than fds");
     for (size_t k = 0; k < slots; ++k) {
-        arenas_.push_back(std::make_unique<DatagramBatch>(engine, capacity_bytes, max_datagrams));
+        arenas_.push_back(std::make_unique<DatagramBatch>(engine, capacity_bytes, max_n_));
         free_.push_back(arenas_.back().get());
     }
-    thread_ = std::thread([this] { reader(); });
+    live_ = fds_.size();
+    for (int fd : fds_) threads_.emplace_back([this, fd] { reader(fd); });
 }
 
 DatagramRing::~DatagramRing()
@@ -190,10 +206,10 @@ DatagramRing::~DatagramRing()
         stop_ = true;
     }
     cv_.notify_all();
-    thread_.join();  // the reader polls the fd and checks stop_ every 50 ms
+    for (auto& t : threads_) t.join();  // each reader polls its fd and checks stop_ every 50 ms
 }
 
-void DatagramRing::reader()
+void DatagramRing::reader(int fd)
 {
     for (;;) {
         DatagramBatch* b = nullptr;
@@ -216,11 +232,11 @@ void DatagramRing::reader()
                     std::lock_guard<std::mutex> lock(mu_);
                     if (stop_ || (b->size() && waiting_)) break;
                 }
-                pollfd p{fd_, POLLIN, 0};
+                pollfd p{fd, POLLIN, 0};
                 const int r = ::poll(&p, 1, b->size() ? 1 : 50);
                 if (r < 0 && errno != EINTR) sys_fail("poll");
                 if (r <= 0) continue;
-                b->read_from(fd_, max_n_ - b->size());
+                b->read_from(fd, max_n_ - b->size());
                 if (b->ended()) {
                     end = true;
                     break;
@@ -229,7 +245,8 @@ void DatagramRing::reader()
             }
         } catch (...) {
             std::lock_guard<std::mutex> lock(mu_);
-            error_ = std::current_exception();
+            if (!error_) error_ = std::current_exception();
+            stop_ = true;  // the other readers stop too
             end = true;
         }
         std::lock_guard<std::mutex> lock(mu_);
@@ -241,7 +258,7 @@ void DatagramRing::reader()
         if (end || stop_) break;
     }
     std::lock_guard<std::mutex> lock(mu_);
-    eof_ = true;
+    if (--live_ == 0) eof_ = true;  // the stream ends with the last fd
     cv_.notify_all();
 }
 

@@ -3,6 +3,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <map>
 #include <random>
 #include <string>
 #include <thread>
@@ -288,6 +289,54 @@ int main()
         close(rxfd);
         EXPECT(ordered);
         EXPECT(seen > 0 && seen <= kPasses * rx.size());
+    }
+    // one DatagramRing over two SOCK_SEQPACKET streams (one reader thread
+    // each, shared arenas, one engine): every datagram of both streams
+    // arrives exactly once, with the status verify_raw() gave its bytes
+    {
+        int a[2], c[2];
+        EXPECT(socketpair(AF_UNIX, SOCK_SEQPACKET, 0, a) == 0);
+        EXPECT(socketpair(AF_UNIX, SOCK_SEQPACKET, 0, c) == 0);
+        constexpr size_t kPasses = 4;
+        auto send_all = [&](int fd) {
+            icsum::DatagramBatch txb(size_t(1) << 20);
+            for (size_t p = 0; p < kPasses; ++p)
+                for (size_t i = 0; i < rx.size();) {
+                    txb.clear();
+                    size_t j = i;
+                    for (; j < rx.size() && j - i < 64 && txb.push(rx[j]); ++j) {
+                    }
+                    txb.write_to(fd);
+                    i = j;
+                }
+            close(fd);
+        };
+        std::thread wa(send_all, a[0]), wc(send_all, c[0]);
+        std::map<std::string, long> left;
+        std::map<std::string, uint8_t> status;
+        for (size_t i = 0; i < rx.size(); ++i) {
+            left[rx[i]] += 2 * kPasses;
+            status[rx[i]] = st[i];
+        }
+        size_t seen = 0;
+        {
+            icsum::DatagramRing ring(eng, std::vector<int>{a[1], c[1]}, 0, size_t(2) << 20, 300);
+            while (icsum::DatagramBatch* b = ring.next()) {
+                const auto vs = b->verify();
+                for (size_t k = 0; k < vs.size(); ++k, ++seen) {
+                    const std::string w((*b)[k]);
+                    EXPECT(left.count(w) && --left[w] >= 0);
+                    EXPECT(vs[k] == status[w]);
+                }
+                ring.release(b);
+            }
+        }
+        wa.join();
+        wc.join();
+        close(a[1]);
+        close(c[1]);
+        EXPECT(seen == 2 * kPasses * rx.size());
+        for (const auto& [w, n] : left) EXPECT(n == 0);
     }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);

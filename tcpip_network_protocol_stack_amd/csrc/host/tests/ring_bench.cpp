@@ -118,11 +118,13 @@ void big_buffers(int fd)
 
 // `readers` receiving sockets (one receive() call each, on its own thread
 // when readers > 1), writer k sending to socket k % readers
+// shared: ONE receive() call on all sockets (one engine, one caller thread)
 template <class Receive>
 void run(const char* mode, const std::vector<std::string>& wires, size_t passes, bool udp, size_t writers,
-         std::vector<std::unique_ptr<icsum::BatchEngine>>& engs, Receive receive)
+         std::vector<std::unique_ptr<icsum::BatchEngine>>& engs, bool shared, Receive receive)
 {
     const size_t readers = engs.size();
+    const size_t callers = shared ? 1 : readers;
     std::vector<Lane> lanes(readers);
     int rcvbuf = 0;
     for (auto& l : lanes) {
@@ -152,18 +154,22 @@ void run(const char* mode, const std::vector<std::string>& wires, size_t passes,
         cv.notify_all();
         cv.wait(lock, [&] { return go; });
     };
-    std::vector<size_t> got(readers, 0), accepted(readers, 0);
+    std::vector<size_t> got(callers, 0), accepted(callers, 0);
     std::vector<std::thread> rs;
-    for (size_t r = 0; r < readers; ++r)
+    for (size_t r = 0; r < callers; ++r)
         rs.emplace_back([&, r] {
-            got[r] = receive(lanes[r].rx, *engs[r], accepted[r], start);
-            lanes[r].rx_done = true;
+            std::vector<int> fds;
+            for (size_t k = 0; k < readers; ++k)
+                if (shared || k == r) fds.push_back(lanes[k].rx);
+            got[r] = receive(fds, *engs[r], accepted[r], start);
+            for (size_t k = 0; k < readers; ++k)
+                if (shared || k == r) lanes[k].rx_done = true;
         });
     std::chrono::steady_clock::time_point t0;
     std::vector<std::thread> ws;
     {
         std::unique_lock<std::mutex> lock(mu);
-        cv.wait(lock, [&] { return ready == readers; });
+        cv.wait(lock, [&] { return ready == callers; });
         t0 = std::chrono::steady_clock::now();
         for (size_t k = 0; k < writers; ++k)
             ws.emplace_back(writer, std::ref(lanes[k % readers]), std::cref(wires),
@@ -177,7 +183,7 @@ void run(const char* mode, const std::vector<std::string>& wires, size_t passes,
     for (auto& l : lanes) close(l.rx);
     const double s = std::chrono::duration<double>(t1 - t0).count();
     size_t n = 0, acc = 0;
-    for (size_t r = 0; r < readers; ++r) {
+    for (size_t r = 0; r < callers; ++r) {
         n += got[r];
         acc += accepted[r];
     }
@@ -207,7 +213,9 @@ int main(int argc, char** argv)
     const auto wires = make_wires(*engs[0], size_t(1) << 16);
     constexpr size_t kBatch = 1 << 14;  // datagrams per arena (24 MB of 1500-byte datagrams)
 
-    run("read_only", wires, passes, udp, writers, engs, [&](int fd, icsum::BatchEngine& eng, size_t&, auto start) {
+    using Fds = const std::vector<int>&;
+    run("read_only", wires, passes, udp, writers, engs, false, [&](Fds fds, icsum::BatchEngine& eng, size_t&, auto start) {
+        const int fd = fds[0];
         icsum::DatagramBatch rxb(eng, size_t(32) << 20, kBatch);
         start();
         size_t n = 0;
@@ -219,7 +227,9 @@ int main(int argc, char** argv)
         }
         return n;
     });
-    run("read_then_verify", wires, passes, udp, writers, engs, [&](int fd, icsum::BatchEngine& eng, size_t& accepted, auto start) {
+    run("read_then_verify", wires, passes, udp, writers, engs, false,
+        [&](Fds fds, icsum::BatchEngine& eng, size_t& accepted, auto start) {
+        const int fd = fds[0];
         icsum::DatagramBatch rxb(eng, size_t(32) << 20, kBatch);
         start();
         size_t n = 0;
@@ -234,8 +244,11 @@ int main(int argc, char** argv)
         }
         return n;
     });
-    run("ring_3x_verify", wires, passes, udp, writers, engs, [&](int fd, icsum::BatchEngine& eng, size_t& accepted, auto start) {
-        icsum::DatagramRing ring(eng, fd, 3, size_t(32) << 20, kBatch);
+    // one ring per socket (3 arenas, its own engine and caller thread), then
+    // with several sockets one ring over all of them (2 * sockets + 1 arenas,
+    // one engine, one caller)
+    auto ring_receive = [&](Fds fds, icsum::BatchEngine& eng, size_t& accepted, auto start) {
+        icsum::DatagramRing ring(eng, fds, 0, size_t(32) << 20, kBatch);
         start();
         size_t n = 0;
         while (icsum::DatagramBatch* b = ring.next()) {
@@ -244,6 +257,8 @@ int main(int argc, char** argv)
             ring.release(b);
         }
         return n;
-    });
+    };
+    run("ring_3x_verify", wires, passes, udp, writers, engs, false, ring_receive);
+    if (readers > 1) run("ring_shared_verify", wires, passes, udp, writers, engs, true, ring_receive);
     return 0;
 }
