@@ -134,6 +134,45 @@ class DatagramRing
     std::vector<std::thread> threads_;
 };
 
+// The transmit side (the reference wraps each segment with wrap_tcp_in_ip,
+// util/tcp_over_ip/tcp_over_ip.cpp:69-88, and writes it to the TUN fd, one
+// write per datagram: util/tuntap/tuntap_adapter.h:39): the caller fills a
+// page-locked arena with serialized datagrams, submit() patches both checksum
+// fields of every datagram on the GPU (ICS_MODE_PATCH) on the caller's
+// thread and queues the arena; a writer thread sends queued arenas with
+// sendmmsg / write() while the caller fills and patches the next one.
+class DatagramTxRing
+{
+  public:
+    DatagramTxRing(BatchEngine& engine, int fd, size_t slots = 3, size_t capacity_bytes = size_t(32) << 20,
+                   size_t max_datagrams = 1 << 14);
+    ~DatagramTxRing();  // flushes what was submitted, then stops the writer
+    DatagramTxRing(const DatagramTxRing&) = delete;
+    DatagramTxRing& operator=(const DatagramTxRing&) = delete;
+
+    // an empty arena to fill (blocks while every arena is queued or being
+    // sent); rethrows a writer error
+    DatagramBatch* acquire();
+    // patch (when `patch`) and queue an arena taken with acquire()
+    void submit(DatagramBatch* batch, bool patch = true);
+    // wait until every submitted datagram was written; rethrows a writer error
+    void flush();
+    size_t sent() const;  // datagrams written so far
+
+  private:
+    void writer();
+
+    int fd_;
+    std::vector<std::unique_ptr<DatagramBatch>> arenas_;
+    std::deque<DatagramBatch*> free_, queued_;
+    mutable std::mutex mu_;
+    std::condition_variable cv_;
+    bool stop_ = false, busy_ = false;
+    size_t sent_ = 0;
+    std::exception_ptr error_;
+    std::thread thread_;
+};
+
 }  // namespace icsum
 
 #endif

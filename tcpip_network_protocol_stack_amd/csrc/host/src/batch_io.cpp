@@ -138,7 +138,7 @@ size_t DatagramBatch::write_to(int fd) const
                 msgs[j].msg_hdr.msg_iov = &iov[j];
                 msgs[j].msg_hdr.msg_iovlen = 1;
             }
-            const int r = sendmmsg(fd, msgs.data(), static_cast<unsigned>(k), 0);
+            const int r = sendmmsg(fd, msgs.data(), static_cast<unsigned>(k), MSG_NOSIGNAL);  // EPIPE, not SIGPIPE
             if (r < 0) {
                 if (errno == EINTR) continue;
                 sys_fail("sendmmsg");
@@ -284,6 +284,94 @@ void DatagramRing::release(DatagramBatch* batch)
         free_.push_back(batch);
     }
     cv_.notify_all();
+}
+
+DatagramTxRing::DatagramTxRing(BatchEngine& engine, int fd, size_t slots, size_t capacity_bytes,
+                               size_t max_datagrams)
+    : fd_(fd)
+{
+    if (slots < 2) throw std::invalid_argument("DatagramTxRing needs at least 2 slots");
+    for (size_t k = 0; k < slots; ++k) {
+        arenas_.push_back(std::make_unique<DatagramBatch>(engine, capacity_bytes, max_datagrams));
+        free_.push_back(arenas_.back().get());
+    }
+    thread_ = std::thread([this] { writer(); });
+}
+
+DatagramTxRing::~DatagramTxRing()
+{
+    {
+        std::unique_lock<std::mutex> lock(mu_);
+        cv_.wait(lock, [this] { return (queued_.empty() && !busy_) || error_; });
+        stop_ = true;
+    }
+    cv_.notify_all();
+    thread_.join();
+}
+
+DatagramBatch* DatagramTxRing::acquire()
+{
+    std::unique_lock<std::mutex> lock(mu_);
+    cv_.wait(lock, [this] { return !free_.empty() || error_; });
+    if (error_) std::rethrow_exception(error_);
+    DatagramBatch* b = free_.front();
+    free_.pop_front();
+    b->clear();
+    return b;
+}
+
+void DatagramTxRing::submit(DatagramBatch* batch, bool patch)
+{
+    if (patch && batch->size()) batch->patch();  // the engine stays on the caller's thread
+    {
+        std::lock_guard<std::mutex> lock(mu_);
+        queued_.push_back(batch);
+    }
+    cv_.notify_all();
+}
+
+void DatagramTxRing::flush()
+{
+    std::unique_lock<std::mutex> lock(mu_);
+    cv_.wait(lock, [this] { return (queued_.empty() && !busy_) || error_; });
+    if (error_) std::rethrow_exception(error_);
+}
+
+size_t DatagramTxRing::sent() const
+{
+    std::lock_guard<std::mutex> lock(mu_);
+    return sent_;
+}
+
+void DatagramTxRing::writer()
+{
+    for (;;) {
+        DatagramBatch* b = nullptr;
+        {
+            std::unique_lock<std::mutex> lock(mu_);
+            cv_.wait(lock, [this] { return stop_ || !queued_.empty(); });
+            if (queued_.empty()) break;  // stop_ with nothing left to send
+            b = queued_.front();
+            queued_.pop_front();
+            busy_ = true;
+        }
+        size_t n = 0;
+        std::exception_ptr err;
+        try {
+            n = b->write_to(fd_);
+        } catch (...) {
+            err = std::current_exception();
+        }
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            sent_ += n;
+            busy_ = false;
+            free_.push_back(b);
+            if (err && !error_) error_ = err;
+        }
+        cv_.notify_all();
+        if (err) break;
+    }
 }
 
 }  // namespace icsum

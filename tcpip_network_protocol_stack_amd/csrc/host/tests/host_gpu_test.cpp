@@ -338,6 +338,50 @@ int main()
         EXPECT(seen == 2 * kPasses * rx.size());
         for (const auto& [w, n] : left) EXPECT(n == 0);
     }
+    // DatagramTxRing: arenas of wires with both checksum fields zeroed are
+    // patched on the GPU at submit() and sent by the ring's writer thread
+    // over a SOCK_SEQPACKET socketpair; the peer reads exactly wrap_tcp_in_ip's
+    // wires, in order
+    {
+        int sv[2];
+        EXPECT(socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) == 0);
+        constexpr size_t kPasses = 4, kPerArena = 50;
+        std::vector<std::string> heard;
+        std::thread peer([&] {
+            icsum::DatagramBatch rxb(size_t(4) << 20, 1024);
+            for (;;) {
+                rxb.clear();
+                const size_t k = rxb.read_from(sv[1], 1024);
+                for (size_t i = 0; i < k; ++i) heard.emplace_back(rxb[i]);
+                if (k == 0 || rxb.ended()) break;
+            }
+        });
+        size_t sent = 0, arenas = 0;
+        {
+            icsum::DatagramTxRing tx(eng, sv[0], 3, size_t(1) << 20, kPerArena);
+            for (size_t p = 0; p < kPasses; ++p)
+                for (size_t i = 0; i < wires.size();) {
+                    icsum::DatagramBatch* b = tx.acquire();
+                    for (; i < wires.size() && b->size() < kPerArena; ++i) {
+                        std::string z = wires[i];
+                        z[10] = z[11] = 0;
+                        z[36] = z[37] = 0;
+                        EXPECT(b->push(z));
+                    }
+                    tx.submit(b);
+                    ++arenas;
+                }
+            tx.flush();
+            sent = tx.sent();
+        }
+        close(sv[0]);
+        peer.join();
+        close(sv[1]);
+        EXPECT(sent == kPasses * wires.size());
+        EXPECT(arenas > 3);
+        EXPECT(heard.size() == kPasses * wires.size());
+        for (size_t i = 0; i < heard.size() && i < kPasses * wires.size(); ++i) EXPECT(heard[i] == wires[i % wires.size()]);
+    }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);
     return failures ? 1 : 0;

@@ -18,7 +18,9 @@
 // thread (writer k sends to socket k % readers; one port per socket stands in
 // for SO_REUSEPORT's flow hashing, which would not let the bench end each
 // socket's stream), to see whether the host side scales with reading threads.
-//   build/ring_bench [passes] [seqpacket|udp] [writers] [readers]
+// `tx` measures the transmit side instead (patch on the GPU, then send):
+// one arena at a time vs a DatagramTxRing.
+//   build/ring_bench [passes] [seqpacket|udp|tx] [writers] [readers]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
@@ -198,12 +200,80 @@ void run(const char* mode, const std::vector<std::string>& wires, size_t passes,
     if ((udp ? n > sent : n != sent) || (acc != 0 && acc != n)) std::exit(2);
 }
 
+// transmit side over a SOCK_SEQPACKET socketpair: the caller fills arenas
+// with serialized datagrams whose checksum fields are zero, patches them on
+// the GPU and sends them, either in turn (patch_then_send) or through a
+// DatagramTxRing whose writer thread sends arena k while the caller fills and
+// patches arena k+1; a peer thread reads and checks every datagram
+void tx_run(icsum::BatchEngine& eng, const std::vector<std::string>& wires, size_t passes, bool ring)
+{
+    constexpr size_t kBatch = 1 << 14;
+    std::vector<std::string> zeroed(wires);
+    for (auto& z : zeroed) z[10] = z[11] = z[36] = z[37] = 0;
+    int sv[2];
+    if (socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) != 0) {
+        std::perror("socketpair");
+        std::exit(1);
+    }
+    big_buffers(sv[0]);
+    big_buffers(sv[1]);
+    size_t heard = 0, same = 0;
+    std::thread peer([&] {
+        icsum::DatagramBatch rxb(size_t(32) << 20, kBatch);
+        for (;;) {
+            rxb.clear();
+            const size_t k = rxb.read_from(sv[1], kBatch);
+            for (size_t i = 0; i < k; ++i, ++heard) same += rxb[i] == wires[heard % wires.size()];
+            if (k == 0 || rxb.ended()) break;
+        }
+    });
+    std::unique_ptr<icsum::DatagramTxRing> tx;
+    std::unique_ptr<icsum::DatagramBatch> one;
+    if (ring)
+        tx = std::make_unique<icsum::DatagramTxRing>(eng, sv[0], 3, size_t(32) << 20, kBatch);
+    else
+        one = std::make_unique<icsum::DatagramBatch>(eng, size_t(32) << 20, kBatch);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (size_t p = 0; p < passes; ++p)
+        for (size_t i = 0; i < zeroed.size();) {
+            icsum::DatagramBatch* b = ring ? tx->acquire() : one.get();
+            if (!ring) b->clear();
+            for (; i < zeroed.size() && b->push(zeroed[i]); ++i) {
+            }
+            if (ring) {
+                tx->submit(b);
+            } else {
+                b->patch();
+                b->write_to(sv[0]);
+            }
+        }
+    if (ring) tx->flush();
+    const double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+    tx.reset();
+    close(sv[0]);
+    peer.join();
+    close(sv[1]);
+    const size_t sent = wires.size() * passes;
+    std::printf("{\"transport\": \"seqpacket_socketpair\", \"mode\": \"%s\", \"sent\": %zu, \"datagrams\": %zu, "
+                "\"intact\": %zu, \"seconds\": %.4f, \"Mdgram_s\": %.3f, \"GB_s\": %.3f}\n",
+                ring ? "tx_ring_3x" : "patch_then_send", sent, heard, same, s, sent / s / 1e6,
+                double(sent) * double(wires[0].size()) / s / 1e9);
+    if (heard != sent || same != sent) std::exit(2);
+}
+
 }  // namespace
 
 int main(int argc, char** argv)
 {
     const size_t passes = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 4;
     const bool udp = argc > 2 && std::string(argv[2]) == "udp";
+    if (argc > 2 && std::string(argv[2]) == "tx") {
+        icsum::BatchEngine eng(0);
+        const auto wires = make_wires(eng, size_t(1) << 16);
+        tx_run(eng, wires, passes, false);
+        tx_run(eng, wires, passes, true);
+        return 0;
+    }
     const size_t readers = std::max<size_t>(1, argc > 4 ? std::strtoul(argv[4], nullptr, 10) : 1);
     // every socket needs a writer to end its stream
     const size_t writers = std::max<size_t>(readers, argc > 3 ? std::strtoul(argv[3], nullptr, 10) : 1);
