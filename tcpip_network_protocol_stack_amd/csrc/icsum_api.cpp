@@ -78,6 +78,9 @@ struct ics_ctx {
   int nslots = 3;  // 3 x 32 MiB: pageable 49.2 -> 51.4 GB/s over 2 x 64 MiB, pinned equal (tools/ab_host.py)
   size_t slot_bytes = size_t(32) << 20;
   bool staged = false;
+  // ICSUM_HOST_BLOCKING_SYNC: the host path's waits sleep (interrupt) instead
+  // of polling, for many host threads driving engines at once
+  bool blocking_sync = false;
   hipStream_t st[kMaxSlots] = {};
   hipEvent_t ev[kMaxSlots] = {};
   uint8_t* h_in[kMaxSlots] = {};
@@ -189,7 +192,8 @@ int ensure_staging(ics_ctx* ctx) {
   if (ctx->staged) return ICS_OK;
   for (int k = 0; k < ctx->nslots; ++k) {
     ICS_HIP(hipStreamCreateWithFlags(&ctx->st[k], hipStreamNonBlocking));
-    ICS_HIP(hipEventCreateWithFlags(&ctx->ev[k], hipEventDisableTiming));
+    ICS_HIP(hipEventCreateWithFlags(&ctx->ev[k], hipEventDisableTiming |
+                                                     (ctx->blocking_sync ? hipEventBlockingSync : 0)));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_in[k]), ctx->slot_bytes, 0));
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_in[k]), ctx->slot_bytes));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_off[k]), (ics_ctx::kSlotSegs + 1) * 8, 0));
@@ -413,6 +417,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin_debug = std::getenv("ICSUM_BIN_DEBUG") != nullptr;
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
+  ctx->blocking_sync = env_u32("ICSUM_HOST_BLOCKING_SYNC", 0) != 0;
   if (std::getenv("ICSUM_XCD_REMAP")) icsum::set_xcd_remap(env_u32("ICSUM_XCD_REMAP", 0));
   *out = ctx;
   return ICS_OK;
