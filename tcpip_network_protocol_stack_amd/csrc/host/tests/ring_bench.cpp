@@ -328,6 +328,18 @@ int main(int argc, char** argv)
         }
         return n;
     };
+    // the ring alone (no GPU pass): its own hand-off cost against read_only
+    run("ring_3x_only", wires, passes, udp, writers, engs, false,
+        [&](Fds fds, icsum::BatchEngine& eng, size_t&, auto start) {
+            icsum::DatagramRing ring(eng, fds, 0, size_t(32) << 20, kBatch);
+            start();
+            size_t n = 0;
+            while (icsum::DatagramBatch* b = ring.next()) {
+                n += b->size();
+                ring.release(b);
+            }
+            return n;
+        });
     run("ring_3x_verify", wires, passes, udp, writers, engs, false, ring_receive);
     if (readers > 1) run("ring_shared_verify", wires, passes, udp, writers, engs, true, ring_receive);
     return 0;
