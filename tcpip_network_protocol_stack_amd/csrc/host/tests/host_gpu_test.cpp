@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <map>
 #include <random>
+#include <stdexcept>
 #include <string>
 #include <thread>
 #include <vector>
@@ -381,6 +382,29 @@ int main()
         EXPECT(arenas > 3);
         EXPECT(heard.size() == kPasses * wires.size());
         for (size_t i = 0; i < heard.size() && i < kPasses * wires.size(); ++i) EXPECT(heard[i] == wires[i % wires.size()]);
+    }
+    // DatagramTxRing whose peer is gone: the writer's EPIPE (no SIGPIPE)
+    // comes back from flush() / acquire(), and the destructor does not hang
+    {
+        int sv[2];
+        EXPECT(socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) == 0);
+        close(sv[1]);
+        bool threw = false;
+        const auto t0 = std::chrono::steady_clock::now();
+        {
+            icsum::DatagramTxRing tx(eng, sv[0], 2, size_t(1) << 20, 64);
+            try {
+                icsum::DatagramBatch* b = tx.acquire();
+                EXPECT(b->push(wires[0]));
+                tx.submit(b, false);
+                tx.flush();
+            } catch (const std::runtime_error&) {
+                threw = true;
+            }
+        }
+        EXPECT(threw);
+        EXPECT(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2));
+        close(sv[0]);
     }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);
