@@ -524,6 +524,37 @@ def test_router_random(engine, orc):
     assert 0 < sum(want) < len(segs)
 
 
+@pytest.mark.parametrize("stride", [1500, 1502, 64])
+def test_router_fixed_stride(engine, orc, stride):
+    """Fixed-stride router batches: stride 1500 / 64 keep every header
+    dword-aligned (one 8-byte store rewrites wire bytes 4..11), 1502 mixes
+    aligned and 2-byte-offset headers (narrow stores); reserved flag bits set
+    on some headers must be dropped, every ttl from 0 to 255 appears."""
+    rng = np.random.default_rng(7)
+    n = 2048
+    buf = rng.integers(0, 256, n * stride, dtype=np.uint8)
+    for i in range(n):
+        b = bytearray(buf[i * stride:(i + 1) * stride].tobytes())
+        b[0] = 0x45
+        b[2], b[3] = stride >> 8, stride & 0xFF
+        b[6] = (b[6] | 0x80) if i % 3 == 0 else (b[6] & 0x7F)
+        b[8] = i % 256
+        if i % 5 != 4:  # every fifth header keeps a wrong checksum (dropped)
+            _, _, _, b = orc.ipv4_tcp(bytes(b), 2)
+        buf[i * stride:(i + 1) * stride] = np.frombuffer(bytes(b), dtype=np.uint8)
+    d = _t(buf)
+    st = engine.router_ttl_batch(d, n=n, stride=stride, dgram_len=stride).cpu().numpy()
+    hb = buf.copy()
+    want = []
+    for i in range(n):
+        f, out = orc.router_ttl(hb[i * stride:(i + 1) * stride].tobytes())
+        hb[i * stride:(i + 1) * stride] = np.frombuffer(out, dtype=np.uint8)
+        want.append(f)
+    assert st.tolist() == want
+    assert (d.cpu().numpy() == hb).all()
+    assert 0 < sum(want) < n
+
+
 @pytest.mark.parametrize("run", [0, 1, 3, 10])
 def test_xcd_block_order_is_a_permutation(run, orc):
     """block_order (k_checksum / k_ipv4_tcp) only permutes blocks: every run

@@ -3,7 +3,7 @@
 (PCIe) rate — the numbers DESIGN.md §Measurements quotes.  bench.py stays the
 driver's single headline line (north star); this is the wider table.
 
-    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host] [--iters 20]
+    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k] [--iters 20]
 
 Batches that fit the 256 MiB Infinity Cache (ipv4 98 MB, tcp64 67 MB) are
 rotated over >= 4 distinct copies (>= 393 / 268 MB) so every launch reads HBM.
@@ -92,6 +92,49 @@ def main():
                                                      ip_ck=ip, tcp_ck=tcp, status=st), args.iters * 3)
             emit(f"ipv4_64Kix1500_{nm}", n * L, t, n * 5, entry="ics_ipv4_tcp_batch", rotation=R)
         assert (st.cpu().numpy() == 0x0F).all()
+        del bufs
+
+    if "router" in only:  # router TTL batch (ttl-- + header checksum) over 1 M x 1500 B
+        # Each call forwards a datagram once (TTL 64 -> 63 ...), so the batch
+        # cannot be re-run for the usual 150 ms settle: the chip is settled on
+        # the NS workload instead, then 6 rotating copies (63 forwards each)
+        # take 5 rounds of `iters` calls; every datagram must still forward.
+        n, L, seed, R = 1 << 20, 1500, 0x10710003, 6
+        bufs = []
+        for r in range(R):
+            d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+            eng.ipv4_tcp_headers(d, n, L, L, seed, index0=r * n)
+            eng.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)  # PATCH: valid header checksums
+            bufs.append(d)
+        st = torch.empty(n, dtype=torch.uint8, device=dev)
+        warm = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed)
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) < 0.15:
+            for _ in range(8):
+                eng.checksum_batch(warm, n=n, stride=L, seg_len=L)
+            torch.cuda.synchronize()
+        del warm
+        iters = min(args.iters, (63 * R - R) // 5)
+        for i in range(R):
+            eng.router_ttl_batch(bufs[i], n=n, stride=L, dgram_len=L, status=st)
+        ts = []
+        for _ in range(5):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for i in range(iters):
+                eng.router_ttl_batch(bufs[i % R], n=n, stride=L, dgram_len=L, status=st)
+            b.record()
+            torch.cuda.synchronize()
+            ts.append(a.elapsed_time(b) / 1e3 / iters)
+        assert (st.cpu().numpy() == 1).all(), "router batch stopped forwarding"
+        t = statistics.median(ts)
+        # algorithmic: 20 header bytes read + 4 written per datagram; the
+        # memory system moves at least one 128-B line per datagram
+        print(json.dumps({"config": "router_ttl_1Mx1500", "datagrams": n, "us": round(t * 1e6, 2),
+                          "Mdgram_s": round(n / t / 1e6, 1), "header_GB_s": round(n * 24 / t / 1e9, 1),
+                          "line_GB_s": round(n * 128 / t / 1e9, 1),
+                          "frac_hbm_peak_lines": round(n * 128 / t / 1e9 / PEAK, 4),
+                          "entry": "ics_router_ttl_batch", "rotation": R}), flush=True)
         del bufs
 
     if "ns64k" in only:  # reference point for config 2: plain checksum over the same 64 Ki x 1500 B, rotated
