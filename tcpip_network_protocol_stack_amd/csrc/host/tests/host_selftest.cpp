@@ -12,6 +12,8 @@
 #include <thread>
 #include <vector>
 
+#include <arpa/inet.h>
+#include <netinet/in.h>
 #include <sys/socket.h>
 #include <unistd.h>
 
@@ -139,6 +141,44 @@ int main()
             close(sv[0]);
             close(sv[1]);
             std::cout << sent << " " << got << " " << same << " " << rx.bytes() << "\n";
+        } else if (cmd == "ioudp") {
+            // UDP on 127.0.0.1: every wire, then an empty datagram (the end
+            // marker DatagramRing's readers stop at), then one more wire;
+            // read_from takes the wires before the marker, sets ended(), and
+            // leaves the wire after it for the next read
+            std::vector<std::string> ws;
+            std::string h;
+            while (in >> h) ws.push_back(unhex(h));
+            sockaddr_in a{};
+            a.sin_family = AF_INET;
+            a.sin_addr.s_addr = htonl(INADDR_LOOPBACK);
+            socklen_t alen = sizeof a;
+            const int tx = socket(AF_INET, SOCK_DGRAM, 0), rxfd = socket(AF_INET, SOCK_DGRAM, 0);
+            if (tx < 0 || rxfd < 0 || bind(rxfd, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0 ||
+                getsockname(rxfd, reinterpret_cast<sockaddr*>(&a), &alen) != 0 ||
+                connect(tx, reinterpret_cast<sockaddr*>(&a), sizeof a) != 0)
+                return 3;
+            const int buf = 4 << 20;
+            (void)setsockopt(rxfd, SOL_SOCKET, SO_RCVBUF, &buf, sizeof buf);
+            icsum::DatagramBatch txb(size_t(1) << 20), rx(size_t(1) << 22, 4096);
+            for (const auto& w : ws) txb.push(w);
+            const size_t sent = txb.write_to(tx);
+            (void)send(tx, "", 0, 0);
+            (void)send(tx, ws[0].data(), ws[0].size(), 0);
+            size_t got = 0;
+            bool same = true;
+            while (!rx.ended() && got < ws.size()) {
+                const size_t before = rx.size();
+                got += rx.read_from(rxfd, ws.size() + 1);
+                for (size_t k = before; k < rx.size(); ++k) same = same && rx[k] == ws[k];
+            }
+            const bool ended = rx.ended();
+            rx.clear();
+            const size_t after = rx.read_from(rxfd, 8);
+            const bool next_ok = after == 1 && rx[0] == ws[0] && !rx.ended();
+            close(tx);
+            close(rxfd);
+            std::cout << sent << " " << got << " " << same << " " << ended << " " << next_ok << "\n";
         } else if (cmd == "ioseq") {
             // SOCK_SEQPACKET stream: a writer thread sends every wire 4 times
             // and closes its end; read_from(64) until it returns 0

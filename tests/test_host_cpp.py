@@ -118,3 +118,13 @@ def test_datagram_batch_seqpacket_end_of_stream(selftest):
     line = "ioseq " + " ".join(c["wire"] for c in cases)
     sent, got, same, several, ended = (int(x) for x in selftest([line])[0].split())
     assert sent == got == 4 * len(cases) and same == 1 and several == 1 and ended == 1
+
+
+def test_datagram_batch_udp_end_marker(selftest):
+    # UDP over 127.0.0.1 has no end of stream: an empty datagram is the
+    # marker (DatagramRing, ring_bench); read_from stops at it with ended()
+    # set and leaves what follows for the next read
+    cases = wires("tcp_wrap.json")[:64]  # well inside any default socket buffer
+    line = "ioudp " + " ".join(c["wire"] for c in cases)
+    sent, got, same, ended, next_ok = (int(x) for x in selftest([line])[0].split())
+    assert sent == got == len(cases) and same == 1 and ended == 1 and next_ok == 1
