@@ -20,7 +20,9 @@
 // socket's stream), to see whether the host side scales with reading threads.
 // `tx` measures the transmit side instead (patch on the GPU, then send):
 // one arena at a time vs a DatagramTxRing.
-//   build/ring_bench [passes] [seqpacket|udp|tx] [writers] [readers]
+// `verify` times the engine side alone: [readers] threads verifying their
+// own 24 MB arena `passes` times (how concurrent engines share PCIe).
+//   build/ring_bench [passes] [seqpacket|udp|tx|verify] [writers] [readers]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
@@ -267,6 +269,36 @@ int main(int argc, char** argv)
 {
     const size_t passes = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 4;
     const bool udp = argc > 2 && std::string(argv[2]) == "udp";
+    if (argc > 2 && std::string(argv[2]) == "verify") {
+        // engine side alone: `readers` threads, each with its own engine and
+        // a page-locked arena of 16 Ki datagrams, verify it `passes` times
+        const size_t threads = std::max<size_t>(1, argc > 4 ? std::strtoul(argv[4], nullptr, 10) : 1);
+        std::vector<std::unique_ptr<icsum::BatchEngine>> es;
+        std::vector<std::unique_ptr<icsum::DatagramBatch>> bs;
+        for (size_t r = 0; r < threads; ++r) es.push_back(std::make_unique<icsum::BatchEngine>(0));
+        const auto wires = make_wires(*es[0], size_t(1) << 14);
+        for (size_t r = 0; r < threads; ++r) {
+            bs.push_back(std::make_unique<icsum::DatagramBatch>(*es[r], size_t(32) << 20, size_t(1) << 14));
+            for (const auto& w : wires) bs[r]->push(w);
+            (void)bs[r]->verify();  // staging allocated before the clock
+        }
+        std::atomic<size_t> bad{0};
+        const auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> ts;
+        for (size_t r = 0; r < threads; ++r)
+            ts.emplace_back([&, r] {
+                for (size_t p = 0; p < passes; ++p)
+                    for (uint8_t st : bs[r]->verify()) bad += st != ICS_ST_ACCEPT;
+            });
+        for (auto& t : ts) t.join();
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        const double bytes = double(threads) * double(passes) * double(bs[0]->bytes());
+        std::printf("{\"mode\": \"verify_only\", \"threads\": %zu, \"passes\": %zu, \"arena_MB\": %.1f, "
+                    "\"ms_per_verify\": %.3f, \"GB_s\": %.3f}\n",
+                    threads, passes, bs[0]->bytes() / 1e6, sec * 1e3 / double(passes),
+                    bytes / sec / 1e9);
+        return bad ? 2 : 0;
+    }
     if (argc > 2 && std::string(argv[2]) == "tx") {
         icsum::BatchEngine eng(0);
         const auto wires = make_wires(eng, size_t(1) << 16);
