@@ -283,6 +283,35 @@ void par_memcpy(void* dst, const void* src, size_t n) {
   for (auto& x : th) x.join();
 }
 
+// ICS_MODE_PATCH's stores (k_ipv4_tcp, mode 2) applied on the host from a
+// COMPUTE pass's results: for every datagram of >= 20 bytes the IPv4
+// checksum goes to bytes 10..11; when >= 18 bytes follow the header
+// (4 * hlen clamped to [20, len]) the TCP checksum goes to bytes 16..17 of
+// the TCP header.  Both big-endian.  `res` = the slot's results: m ip u16,
+// m tcp u16, m status bytes.
+void host_patch_fields(uint8_t* bytes, const uint64_t* offsets, uint64_t stride, uint64_t dlen, const Chunk& c,
+                       const uint8_t* res) {
+  const uint64_t m = c.i1 - c.i0;
+  const uint16_t* ip = reinterpret_cast<const uint16_t*>(res);
+  const uint16_t* tcp = ip + m;
+  for (uint64_t j = 0; j < m; ++j) {
+    const uint64_t i = c.i0 + j;
+    const uint64_t s = offsets ? offsets[i] : i * stride;
+    const uint64_t len = offsets ? offsets[i + 1] - s : dlen;
+    if (len < 20) continue;
+    uint8_t* d = bytes + s;
+    d[10] = uint8_t(ip[j] >> 8);
+    d[11] = uint8_t(ip[j]);
+    uint64_t off = 4u * (d[0] & 0x0fu);
+    if (off < 20) off = 20;
+    if (off > len) off = len;
+    if (len - off >= 18) {
+      d[off + 16] = uint8_t(tcp[j] >> 8);
+      d[off + 17] = uint8_t(tcp[j]);
+    }
+  }
+}
+
 // kind 0: checksum batch (u16 out); kind 1: ipv4_tcp batch (ip u16, tcp u16, status u8).
 // The slots take turns, one stream each: while the GPU moves and sums chunk
 // k, the host prepares chunk k+1.  Pinned user buffers are DMA'd directly (no
@@ -306,8 +335,8 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       if (out_a) std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
       if (out_b) std::memcpy(out_b + c.i0, ctx->h_out[k] + m * 2, m * 2);
       if (out_c) std::memcpy(out_c + c.i0, ctx->h_out[k] + m * 4, m);
-      if (mode == ICS_MODE_PATCH && !direct)
-        par_memcpy(static_cast<uint8_t*>(h_bytes) + c.b0, ctx->h_in[k], c.b1 - c.b0);
+      if (mode == ICS_MODE_PATCH)
+        host_patch_fields(static_cast<uint8_t*>(h_bytes), h_offsets, stride, seg_len, c, ctx->h_out[k]);
     }
     busy[k] = false;
     return ICS_OK;
@@ -348,11 +377,13 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       uint16_t* a = reinterpret_cast<uint16_t*>(ctx->d_out[slot]);
       uint16_t* b = a + m;
       uint8_t* s = ctx->d_out[slot] + m * 4;
-      ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, a, b, s, ipv4_geometry(g), ctx->max_blocks, ctx->patch_wt, st));
+      // PATCH from host memory: the device computes (COMPUTE gives the very
+      // values PATCH stores) and only the 5-byte results come back; the two
+      // fields are written into the caller's bytes on the host at retire,
+      // instead of copying every patched byte back over PCIe
+      const int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;
+      ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, ipv4_geometry(g), ctx->max_blocks, ctx->patch_wt, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 5, hipMemcpyDeviceToHost, st));
-      if (mode == ICS_MODE_PATCH)
-        ICS_HIP(hipMemcpyAsync(direct ? static_cast<uint8_t*>(h_bytes) + c.b0 : ctx->h_in[slot], ctx->d_in[slot],
-                               nb, hipMemcpyDeviceToHost, st));
     }
     ICS_HIP(hipEventRecord(ctx->ev[slot], st));
     pending[slot] = c;

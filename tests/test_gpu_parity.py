@@ -482,6 +482,49 @@ def _random_datagrams(rng, n):
     return segs
 
 
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("lead", [0, 3])
+def test_host_path_ipv4_random_all_modes(engine, orc, pinned, lead):
+    """ics_ipv4_tcp_batch_host on every header shape, from pageable and from
+    page-locked memory: PATCH from host memory writes the two fields on the
+    host from a device COMPUTE pass; bytes, checksums and statuses must equal
+    the oracle's (and the device-memory path's) in every mode."""
+    import torch
+
+    rng = np.random.default_rng(131 + lead)
+    segs = _random_datagrams(rng, 1500)
+    buf, off = pack_contiguous(segs, lead)
+    for mode in (0, 1, 2):
+        h = torch.empty(buf.size, dtype=torch.uint8, pin_memory=pinned).numpy()
+        h[:] = buf
+        ip, tcp, st = engine.ipv4_tcp_batch_host(h, len(segs), mode, offsets=off)
+        hb = buf.copy()
+        w = orc.ipv4_tcp_batch(hb, len(segs), mode, offsets=off)
+        assert (ip == w[0]).all(), mode
+        assert (tcp == w[1]).all(), mode
+        assert (st == w[2]).all(), mode
+        assert (h == hb).all(), mode
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_path_ipv4_patch_fixed_stride(engine, orc, pinned):
+    """Fixed-stride PATCH from host memory over more datagrams than one
+    staging slot holds (several chunks in flight)."""
+    import torch
+
+    n, L = 40_000, 1500
+    data = orc.fill_bytes(0x10710002, 0, n * L)
+    h = torch.empty(n * L, dtype=torch.uint8, pin_memory=pinned).numpy()
+    h[:] = data
+    for i in range(0, n, 7):  # some headers with options, some with short hlen
+        h[i * L] = 0x40 | (5 + (i % 3) * 2 if i % 2 else i % 5)
+    hb = h.copy()
+    ip, tcp, st = engine.ipv4_tcp_batch_host(h, n, 2, stride=L, dgram_len=L)
+    w = orc.ipv4_tcp_batch(hb, n, 2, stride=L, dgram_len=L)
+    assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all()
+    assert (h == hb).all()
+
+
 @pytest.mark.parametrize("lead", [0, 1, 2, 3])
 def test_ipv4_tcp_random_all_modes(geo_engine, orc, lead):
     rng = np.random.default_rng(97 + lead)

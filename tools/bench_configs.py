@@ -3,7 +3,7 @@
 (PCIe) rate — the numbers DESIGN.md §Measurements quotes.  bench.py stays the
 driver's single headline line (north star); this is the wider table.
 
-    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k] [--iters 20]
+    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch] [--iters 20]
 
 Batches that fit the 256 MiB Infinity Cache (ipv4 98 MB, tcp64 67 MB) are
 rotated over >= 4 distinct copies (>= 393 / 268 MB) so every launch reads HBM.
@@ -136,6 +136,25 @@ def main():
                           "frac_hbm_peak_lines": round(n * 128 / t / 1e9 / PEAK, 4),
                           "entry": "ics_router_ttl_batch", "rotation": R}), flush=True)
         del bufs
+
+    if "hostpatch" in only:  # PATCH from host memory (the transmit side): 256 Ki x 1500 B IPv4/TCP datagrams
+        n, L, seed = 1 << 18, 1500, 0x10710002
+        d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed)
+        eng.ipv4_tcp_headers(d, n, L, L, seed)
+        src = d.cpu().numpy()
+        del d
+        for pinned in (True, False):
+            h = torch.empty(n * L, dtype=torch.uint8, pin_memory=pinned).numpy()
+            h[:] = src
+            eng.ipv4_tcp_batch_host(h, n, 2, stride=L, dgram_len=L)  # warm (staging allocated)
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                _, _, st = eng.ipv4_tcp_batch_host(h, n, 2, stride=L, dgram_len=L)
+                ts.append(time.perf_counter() - t0)
+            assert (st == 0x0F).all()
+            emit(f"host_patch_256Kix1500_{'pinned' if pinned else 'pageable'}", n * L, statistics.median(ts),
+                 n * 5, entry="ics_ipv4_tcp_batch_host(PATCH)")
 
     if "ns64k" in only:  # reference point for config 2: plain checksum over the same 64 Ki x 1500 B, rotated
         n, L, seed, R = 1 << 16, 1500, 0x10710002, 6
