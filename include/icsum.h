@@ -151,9 +151,12 @@ int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets
                          uint8_t* d_status, void* stream);
 
 /* ---- host-memory variants (PCIe-inclusive path) ------------------------ */
-/* Same semantics as ics_checksum_batch on host buffers.  The engine stages
- * through pinned memory in chunks and pipelines H2D / kernel / D2H on two
- * streams; returns when h_out is complete. */
+/* Same semantics as ics_checksum_batch / ics_ipv4_tcp_batch on host
+ * buffers.  The engine stages through pinned memory in chunks (page-locked
+ * caller buffers are DMA'd directly) and pipelines H2D / kernel / D2H on its
+ * slot streams; returns when the outputs are complete.  PATCH on host
+ * memory: the device computes the two checksums and the engine writes the
+ * two fields into h_dgrams on the host (same bytes as the device PATCH). */
 int ics_checksum_batch_host(ics_ctx* ctx, const void* h_bytes, const uint64_t* h_offsets,
                             uint64_t stride, uint64_t seg_len, const uint32_t* h_init,
                             uint16_t* h_out, uint64_t n);
