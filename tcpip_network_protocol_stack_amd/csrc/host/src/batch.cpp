@@ -2,7 +2,9 @@
 // contiguous wire buffer + offsets, runs one engine call, scatters results.
 #include "batch.h"
 
+#include <algorithm>
 #include <stdexcept>
+#include <thread>
 
 #include "icsum.h"
 #include "wire_internal.h"
@@ -208,41 +210,74 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_packed(TCPOverIPv4Ada
     // receive path from raw wire datagrams (a TUN / socket read batch):
     // IPv4 parse + TCP checksum verified on the GPU, fields parsed on the host
     const std::vector<uint8_t> st = verify_packed(bytes, offsets, n);
+    // 1) field parse of every verified datagram: pure, so it runs on up to 8
+    //    threads (contiguous ranges); 2) the adapter's gates in datagram
+    //    order on this thread (tcp_gate's listen -> connected transition
+    //    changes what ip_gate lets through for every later datagram)
+    struct Parsed
+    {
+        bool ok = false;
+        IPv4Header ip;
+        TCPSegment seg;
+    };
+    std::vector<Parsed> parsed(n);
+    auto parse_range = [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            if ((st[i] & (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) !=
+                (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK))
+                continue;
+            const std::string_view wire{reinterpret_cast<const char*>(bytes) + offsets[i],
+                                        static_cast<size_t>(offsets[i + 1] - offsets[i])};
+            IPv4Header& h = parsed[i].ip;
+            // only the 20 fixed header bytes are copied for the field parse
+            // (IPV4_OK implies at least 20 bytes); fields only, the GPU
+            // already compared the header checksum
+            Parser ipp{std::vector<std::string>{std::string{wire.substr(0, IPv4Header::LENGTH)}}};
+            uint8_t first = 0;
+            ipp.integer(first);
+            h.ver = first >> 4;
+            h.hlen = first & 0x0f;
+            ipp.integer(h.tos);
+            ipp.integer(h.len);
+            ipp.integer(h.id);
+            uint16_t fo = 0;
+            ipp.integer(fo);
+            h.df = (fo & 0x4000) != 0;
+            h.mf = (fo & 0x2000) != 0;
+            h.offset = fo & 0x1fff;
+            ipp.integer(h.ttl);
+            ipp.integer(h.proto);
+            ipp.integer(h.cksum);
+            ipp.integer(h.src);
+            ipp.integer(h.dst);
+            // all bytes after the options (ipv4_header.cpp:50, then the
+            // datagram's remaining buffer as the TCP segment); a header
+            // longer than the datagram leaves nothing, and the TCP parse fails
+            const size_t hdr_bytes = static_cast<size_t>(h.hlen) * 4;
+            Parser tp{std::vector<std::string>{
+                std::string{hdr_bytes <= wire.size() ? wire.substr(hdr_bytes) : std::string_view{}}}};
+            detail::parse_tcp_fields(tp, parsed[i].seg);
+            parsed[i].ok = !tp.has_error();
+        }
+    };
+    const size_t threads = std::min<size_t>({size_t(8), std::max(1u, std::thread::hardware_concurrency()),
+                                             std::max<size_t>(1, n / 2048)});
+    if (threads <= 1) {
+        parse_range(0, n);
+    } else {
+        std::vector<std::thread> pool;
+        for (size_t t = 1; t < threads; ++t) pool.emplace_back(parse_range, n * t / threads, n * (t + 1) / threads);
+        parse_range(0, n / threads);
+        for (auto& th : pool) th.join();
+    }
     std::vector<std::optional<TCPMessage>> out(n);
     for (size_t i = 0; i < n; ++i) {
-        const std::string_view wire{reinterpret_cast<const char*>(bytes) + offsets[i],
-                                    static_cast<size_t>(offsets[i + 1] - offsets[i])};
         if ((st[i] & (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) !=
             (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK))
             continue;
-        IPv4Datagram dg;
-        Parser ipp{std::vector<std::string>{std::string{wire}}};
-        // fields only: the GPU already compared the header checksum
-        uint8_t first = 0;
-        ipp.integer(first);
-        dg.header.ver = first >> 4;
-        dg.header.hlen = first & 0x0f;
-        ipp.integer(dg.header.tos);
-        ipp.integer(dg.header.len);
-        ipp.integer(dg.header.id);
-        uint16_t fo = 0;
-        ipp.integer(fo);
-        dg.header.df = (fo & 0x4000) != 0;
-        dg.header.mf = (fo & 0x2000) != 0;
-        dg.header.offset = fo & 0x1fff;
-        ipp.integer(dg.header.ttl);
-        ipp.integer(dg.header.proto);
-        ipp.integer(dg.header.cksum);
-        ipp.integer(dg.header.src);
-        ipp.integer(dg.header.dst);
-        ipp.remove_prefix(static_cast<uint64_t>(dg.header.hlen) * 4 - IPv4Header::LENGTH);
-        ipp.all_remaining(dg.payload);
-        if (!detail::ip_gate(adapter, dg.header)) continue;
-        TCPSegment seg;
-        Parser tp{dg.payload};
-        detail::parse_tcp_fields(tp, seg);
-        if (tp.has_error()) continue;
-        out[i] = detail::tcp_gate(adapter, dg.header, seg);
+        if (!detail::ip_gate(adapter, parsed[i].ip)) continue;
+        if (!parsed[i].ok) continue;
+        out[i] = detail::tcp_gate(adapter, parsed[i].ip, parsed[i].seg);
     }
     return out;
 }

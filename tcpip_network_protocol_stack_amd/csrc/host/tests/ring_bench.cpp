@@ -269,6 +269,44 @@ int main(int argc, char** argv)
 {
     const size_t passes = argc > 1 ? std::strtoul(argv[1], nullptr, 10) : 4;
     const bool udp = argc > 2 && std::string(argv[2]) == "udp";
+    if (argc > 2 && std::string(argv[2]) == "unwrap") {
+        // receive side without a socket: one thread unwraps (GPU verify +
+        // host field parse + the adapter's gates) a page-locked arena of
+        // 16 Ki datagrams addressed to it, `passes` times
+        icsum::BatchEngine eng(0);
+        TCPOverIPv4Adapter a, b;
+        a.config_mut().source = Address{"10.1.2.3", 4321};
+        a.config_mut().destination = Address{"10.9.8.7", 80};
+        b.config_mut().source = Address{"10.9.8.7", 80};
+        b.config_mut().destination = Address{"10.1.2.3", 4321};
+        std::mt19937_64 rng(0x1072);
+        std::vector<TCPMessage> msgs(size_t(1) << 14);
+        for (auto& m : msgs) {
+            m.sender.seqno = Wrap32{static_cast<uint32_t>(rng())};
+            m.sender.payload.resize(1460);
+            for (auto& c : m.sender.payload) c = static_cast<char>(rng());
+            m.receiver.ackno = Wrap32{static_cast<uint32_t>(rng())};
+            m.receiver.window_size = 65535;
+        }
+        icsum::DatagramBatch arena(eng, size_t(32) << 20, msgs.size());
+        for (const auto& d : eng.wrap(a, msgs)) {
+            std::string w;
+            for (const auto& piece : serialize(d)) w += piece;
+            arena.push(w);
+        }
+        size_t ok = 0;
+        for (const auto& m : arena.unwrap(b)) ok += m.has_value();  // staging allocated before the clock
+        const auto t0 = std::chrono::steady_clock::now();
+        for (size_t p = 0; p < passes; ++p)
+            for (const auto& m : arena.unwrap(b)) ok += m.has_value();
+        const double sec = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("{\"mode\": \"unwrap_only\", \"passes\": %zu, \"arena_MB\": %.1f, \"ms_per_unwrap\": %.3f, "
+                    "\"Mdgram_s\": %.3f, \"GB_s\": %.3f, \"accepted\": %zu}\n",
+                    passes, arena.bytes() / 1e6, sec * 1e3 / double(passes),
+                    double(passes) * double(arena.size()) / sec / 1e6,
+                    double(passes) * double(arena.bytes()) / sec / 1e9, ok);
+        return ok == (passes + 1) * arena.size() ? 0 : 2;
+    }
     if (argc > 2 && std::string(argv[2]) == "verify") {
         // engine side alone: `readers` threads, each with its own engine and
         // a page-locked arena of 16 Ki datagrams, verify it `passes` times
