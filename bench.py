@@ -10,10 +10,15 @@ At N>1 (torchrun, one process per GPU) every rank owns its own 1 M-segment
 shard of one global spec stream — weak scaling, no data-path collective; the
 only collectives are the timing barrier and the max-over-ranks reduction.
 
+`--gpus N` without an outer launcher starts the N ranks itself (one process
+per GPU via torch.distributed.run on 127.0.0.1; this parent never touches the
+GPU); under a launcher, WORLD_SIZE must equal --gpus.
+
 Prints ONE JSON line (rank 0) with `roofline` (HIP-event kernel time vs the
 8 TB/s HBM peak; PMC traffic from a rocprofv3 child pass) and `cpu_baseline`
 (the reference's own InternetChecksum, compiled from /root/reference into
-oracle/_ref/, on a bounded sample of the same bytes, all host threads).
+oracle/_ref/, over the same bytes — the whole NS batch — on every CPU this
+process may use, outputs compared with the GPU's).
 """
 import argparse
 import csv
@@ -55,7 +60,45 @@ def parse():
                     help="minimum untimed warm-up (ms of back-to-back launches) after --warmup")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 PMC child pass")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-threads", type=int, default=0,
+                    help="CPU-baseline threads (0 = every CPU this process may run on)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="ranks report their rank/world wiring over gloo and exit (no GPU use)")
     return ap.parse_args()
+
+
+# ------------------------------------------------------------ rank launcher -
+def _free_port():
+    import socket
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(args):
+    """`--gpus N` without an outer launcher: start N ranks, one process per GPU,
+    through torch.distributed.run on 127.0.0.1.  This parent never touches the
+    GPU (nothing here imports torch), and the ranks are children, not an exec."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
+    return subprocess.call(cmd, env=env)
+
+
+def launch_check(rank, world):
+    """Every rank joins a gloo group and rank 0 prints what each one saw."""
+    import torch.distributed as dist
+
+    dist.init_process_group("gloo")
+    seen = [None] * world
+    dist.all_gather_object(seen, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "-1")),
+                                  "world_size": dist.get_world_size(),
+                                  "master_addr": os.environ.get("MASTER_ADDR"), "pid": os.getpid()})
+    if rank == 0:
+        print(json.dumps({"launch_check": seen}), flush=True)
+    dist.destroy_process_group()
 
 
 # ------------------------------------------------------------ PMC traffic --
@@ -90,52 +133,79 @@ def pmc_traffic(args):
 
 
 # ------------------------------------------------------------ CPU baseline -
-def cpu_baseline(n_total, seg, seed, budget_s, gpu_out_head):
-    """Reference InternetChecksum (oracle/_ref) — or the oracle port if the
-    reference build is absent — on the first `sample` segments of the same
-    byte stream, repeated until `budget_s` of wall time; all host threads."""
+def cpu_share():
+    """(threads, how) — every CPU this process may run on: its affinity mask,
+    capped by a cgroup CPU quota when one is set (on the GPU box the machine
+    shows all its CPUs while one GPU's job gets a share of them)."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    how = f"affinity {n} of {os.cpu_count()} host CPUs"
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                quota, period = f.read().split()[:2]
+            if quota != "max":
+                q = max(1, int(int(quota) // int(period)))
+                if q < n:
+                    n, how = q, f"cgroup quota {quota}/{period} = {q} CPUs ({how})"
+        except (OSError, ValueError):
+            pass
+    return n, how
+
+
+def cpu_baseline(data_d, init_d, out_d, seg, budget_s, threads=0):
+    """The reference's own InternetChecksum (oracle/_ref, compiled from
+    /root/reference) — or the oracle port when that build is absent — over the
+    whole batch of this run (its first 2 GiB for the larger workloads) (the same bytes and inits, copied back from HBM),
+    on every CPU this process may use, repeated until ~budget_s; its outputs
+    are compared with the GPU's for every segment.  Plus a 1-core figure."""
     import numpy as np
 
     from oracle import oracle as orc
 
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
-    sample = min(n_total, max(threads * 4096, (256 << 20) // seg))
-    data = orc.fill_bytes(seed, 0, sample * seg)
-    init = np.array([orc.pseudo_init(seed, i, seg) for i in range(sample)], dtype=np.uint32)
-    out = np.empty(sample, dtype=np.uint16)
+    n = min(init_d.numel(), (2 << 30) // seg)  # the whole batch up to 2 GiB (NS: all 1.47 GiB)
+    data = data_d[: n * seg].cpu().numpy()
+    init = init_d[:n].cpu().numpy().view(np.uint32)
+    gpu = out_d[:n].cpu().numpy().view(np.uint16)
+    out = np.empty(n, dtype=np.uint16)
+    share, how = cpu_share()
+    threads = threads or share
     ref = orc.ref_lib()
     kind = "reference" if ref is not None else "port"
 
+    def one(count, nthreads):
+        if ref is not None:
+            ref.ref_checksum_batch(data.ctypes.data, None, seg, seg, init.ctypes.data, out.ctypes.data,
+                                   count, nthreads)
+        else:
+            out[:count] = orc.checksum_batch(data[: count * seg], count, stride=seg, seg_len=seg,
+                                             init=init[:count], threads=nthreads)
+
     def timed(nthreads, budget, count):
         """passes of `count` segments on `nthreads` threads until `budget` s"""
-        def one():
-            if ref is not None:
-                ref.ref_checksum_batch(data.ctypes.data, None, seg, seg, init.ctypes.data, out.ctypes.data,
-                                       count, nthreads)
-            else:
-                out[:count] = orc.checksum_batch(data[: count * seg], count, stride=seg, seg_len=seg,
-                                                 init=init[:count], threads=nthreads)
-        one()  # warm
         passes, t0 = 0, time.perf_counter()
         while True:
-            one()
+            one(count, nthreads)
             passes += 1
             el = time.perf_counter() - t0
             if el >= budget:
                 return passes, el
 
-    passes, el = timed(threads, 0.75 * budget_s, sample)
-    gib = passes * sample * seg / el / 2**30
-    match = bool((out[: len(gpu_out_head)] == gpu_out_head).all())
-    # one core on a smaller slice, same bytes (SURVEY.md §8d: all cores plus a 1-core number)
-    one_n = max(1, sample // threads)
-    p1, el1 = timed(1, 0.25 * budget_s, one_n)
+    one(n, threads)  # warm, and the full-batch comparison
+    match = bool((out == gpu).all())
+    passes, el = timed(threads, 0.8 * budget_s, n)
+    gib = passes * n * seg / el / 2**30
+    one_n = max(1, min(n, (256 << 20) // seg))  # 1 core: a 256 MiB prefix
+    p1, el1 = timed(1, 0.2 * budget_s, one_n)
     gib1 = p1 * one_n * seg / el1 / 2**30
     return {"value": round(gib, 3), "unit": "GiB/s", "cores": threads, "kind": kind,
             "value_1core": round(gib1, 3), "cpu_model": _cpu_model(), "host_cpus": os.cpu_count(),
-            "sample": f"first {sample} segments x {seg} B of the same batch, {passes} passes "
-                      f"in {el:.1f} s on {threads} threads ({one_n} segments, {p1} passes in {el1:.1f} s "
-                      f"on 1); outputs bit-identical to the GPU: {match}"}
+            "cores_basis": how,
+            "sample": f"{'the whole batch' if n == init_d.numel() else 'a prefix of the batch'} ({n} segments x {seg} B = {n * seg / 2**30:.2f} GiB), {passes} passes "
+                      f"in {el:.1f} s on {threads} threads; 1 core: first {one_n} segments, {p1} passes "
+                      f"in {el1:.1f} s; all {n} outputs bit-identical to the GPU's: {match}"}
 
 
 def _cpu_model():
@@ -151,10 +221,18 @@ def _cpu_model():
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus:
+        print(f"bench.py: WORLD_SIZE={world} but --gpus {args.gpus}", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     n_cfg, seg, seed, scaling = WORKLOADS[args.workload]
+    if args.launch_check:
+        launch_check(rank, world)
+        return
 
     # the PMC child pass runs before this process touches the GPU
     traffic, traffic_src = (None, "skipped")
@@ -239,10 +317,9 @@ def main():
     value = n_total * seg * args.steps / elapsed / 2**30  # all ranks' bytes / max-over-ranks time
     achieved = bytes_step / kern_s / 1e9  # GB/s, decimal like the 8 TB/s peak
 
-    head = out[:4096].cpu().numpy().view(np.uint16).copy()
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(n, seg, seed, args.cpu_seconds, head)
+        cpu = cpu_baseline(data, init, out, seg, args.cpu_seconds, args.cpu_threads)
 
     if rank == 0:
         line = {

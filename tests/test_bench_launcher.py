@@ -1,0 +1,53 @@
+"""CPU: bench.py's own rank launcher (`--gpus N` with no outer torchrun) and
+its world-size check — the wiring the driver's 1/2/4/8-GPU scaling runs use.
+`--launch-check` makes every rank join a gloo group and report what it saw,
+without touching a GPU."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+from conftest import ROOT
+
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _env(**kw):
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT")}
+    env.update(kw)
+    return env
+
+
+@pytest.mark.parametrize("n", [2, 3])
+def test_gpus_n_starts_n_ranks(n):
+    r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--launch-check"], env=_env(),
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    seen = lines[0]["launch_check"]
+    assert sorted(s["rank"] for s in seen) == list(range(n))
+    assert sorted(s["local_rank"] for s in seen) == list(range(n))
+    assert {s["world_size"] for s in seen} == {n}
+    assert {s["master_addr"] for s in seen} == {"127.0.0.1"}
+    assert len({s["pid"] for s in seen}) == n  # one process per rank
+
+
+def test_world_size_must_match_gpus():
+    r = subprocess.run([sys.executable, BENCH, "--gpus", "1", "--launch-check"],
+                       env=_env(WORLD_SIZE="2", RANK="0", LOCAL_RANK="0"),
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "WORLD_SIZE=2 but --gpus 1" in r.stderr
+
+
+def test_cpu_share_reports_usable_cpus():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    n, how = bench.cpu_share()
+    assert 1 <= n <= (os.cpu_count() or 1)
+    assert "host CPUs" in how

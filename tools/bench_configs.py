@@ -61,7 +61,15 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--modes", default="compute,patch,verify", help="ipv4 rows: which ics_ipv4_tcp_batch modes")
+    ap.add_argument("--settle-ms", type=float, default=150.0,
+                    help="untimed warm-up per row (0 for counter passes, which serialise every dispatch)")
+    ap.add_argument("--rounds", type=int, default=5)
     args = ap.parse_args()
+    global timed
+    _timed = timed
+    timed = lambda fn, iters, **kw: _timed(fn, iters, **{"rounds": args.rounds,  # noqa: E731
+                                                          "settle_ms": args.settle_ms, **kw})
     only = set(args.only.split(","))
     eng = Engine(0)
     eng_nobin = Engine(0)
@@ -88,6 +96,8 @@ def main():
         tcp = torch.empty(n, dtype=torch.int16, device=dev)
         st = torch.empty(n, dtype=torch.uint8, device=dev)
         for mode, nm in ((0, "compute"), (2, "patch"), (1, "verify")):
+            if nm not in args.modes.split(","):
+                continue
             t = timed(lambda i=0: eng.ipv4_tcp_batch(bufs[i % R], mode, n=n, stride=L, dgram_len=L,
                                                      ip_ck=ip, tcp_ck=tcp, status=st), args.iters * 3)
             emit(f"ipv4_64Kix1500_{nm}", n * L, t, n * 5, entry="ics_ipv4_tcp_batch", rotation=R)
