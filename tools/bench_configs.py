@@ -95,6 +95,9 @@ def main():
         ip = torch.empty(n, dtype=torch.int16, device=dev)
         tcp = torch.empty(n, dtype=torch.int16, device=dev)
         st = torch.empty(n, dtype=torch.uint8, device=dev)
+        if "patch" not in args.modes.split(","):  # VERIFY rows need valid checksum fields
+            for d in bufs:
+                eng.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)
         for mode, nm in ((0, "compute"), (2, "patch"), (1, "verify")):
             if nm not in args.modes.split(","):
                 continue
