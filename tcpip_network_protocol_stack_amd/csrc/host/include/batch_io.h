@@ -123,15 +123,15 @@ class DatagramRing
     void start(BatchEngine& engine, size_t slots, size_t capacity_bytes);
     void reader(int fd);
 
-    std::vector<int> fds_;
+    std::vector<int> fds_{};
     size_t max_n_, live_ = 0;
-    std::vector<std::unique_ptr<DatagramBatch>> arenas_;
-    std::deque<DatagramBatch*> free_, ready_;
-    std::mutex mu_;
-    std::condition_variable cv_;
+    std::vector<std::unique_ptr<DatagramBatch>> arenas_{};
+    std::deque<DatagramBatch*> free_{}, ready_{};
+    std::mutex mu_{};
+    std::condition_variable cv_{};
     bool eof_ = false, stop_ = false, waiting_ = false;
-    std::exception_ptr error_;
-    std::vector<std::thread> threads_;
+    std::exception_ptr error_{};
+    std::vector<std::thread> threads_{};
 };
 
 // The transmit side (the reference wraps each segment with wrap_tcp_in_ip,
@@ -163,14 +163,14 @@ class DatagramTxRing
     void writer();
 
     int fd_;
-    std::vector<std::unique_ptr<DatagramBatch>> arenas_;
-    std::deque<DatagramBatch*> free_, queued_;
-    mutable std::mutex mu_;
-    std::condition_variable cv_;
+    std::vector<std::unique_ptr<DatagramBatch>> arenas_{};
+    std::deque<DatagramBatch*> free_{}, queued_{};
+    mutable std::mutex mu_{};
+    std::condition_variable cv_{};
     bool stop_ = false, busy_ = false;
     size_t sent_ = 0;
-    std::exception_ptr error_;
-    std::thread thread_;
+    std::exception_ptr error_{};
+    std::thread thread_{};
 };
 
 }  // namespace icsum

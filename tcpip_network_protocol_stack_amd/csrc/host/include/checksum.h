@@ -11,8 +11,8 @@
 // at even offsets sum to the four 16-bit lanes of (w & 0x00FF00FF00FF00FF) and
 // the odd ones to those of ((w >> 8) & ...); partial lane sums are folded into
 // sum_ before they can overflow, so sum_ matches the byte loop exactly.
-#ifndef ICSUM_HOST_CHECKSUM_H
-#define ICSUM_HOST_CHECKSUM_H
+#ifndef CHECKSUM_H  // the reference header's guard
+#define CHECKSUM_H
 
 #include <cstdint>
 #include <cstring>

@@ -1,8 +1,8 @@
 // ipv4_header.h — drop-in IPv4Header (reference: util/ipv4_header/ipv4_header.h:10-70).
 // Same fields, defaults and methods; parse() verifies the header checksum with
 // the reference's exact rules (see ipv4_header.cpp).
-#ifndef ICSUM_HOST_IPV4_HEADER_H
-#define ICSUM_HOST_IPV4_HEADER_H
+#ifndef IPV4_HEADER_H  // the reference header's guard
+#define IPV4_HEADER_H
 
 #include <cstddef>
 #include <cstdint>

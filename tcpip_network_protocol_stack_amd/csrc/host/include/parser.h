@@ -18,8 +18,8 @@
 // current piece take one memcpy + byte swap instead of a byte loop.  The
 // reference's nested BufferList and Parser::input() accessor are not part of
 // this surface: nothing on the stack's path uses them.
-#ifndef ICSUM_HOST_PARSER_H
-#define ICSUM_HOST_PARSER_H
+#ifndef PARSER_H  // the reference header's guard
+#define PARSER_H
 
 #include <algorithm>
 #include <concepts>
@@ -44,7 +44,7 @@ constexpr T from_big_endian(T v)
 
 class Parser
 {
-    std::vector<std::string> chunks_;
+    std::vector<std::string> chunks_{};
     size_t cur_ = 0;         // index of the chunk the cursor is in
     size_t pos_ = 0;         // cursor offset inside chunks_[cur_]
     uint64_t remaining_ = 0; // unread bytes across all chunks
@@ -81,7 +81,7 @@ class Parser
     }
 
   public:
-    explicit Parser(const std::vector<std::string>& input)
+    explicit Parser(const std::vector<std::string>& input) : chunks_()
     {
         chunks_.reserve(input.size());
         for (const std::string& s : input) {

@@ -20,7 +20,7 @@ void check(int rc, const char* what)
 // contiguous wire bytes of many pieces-lists with n+1 offsets
 struct Packed
 {
-    std::string bytes;
+    std::string bytes{};
     std::vector<uint64_t> off{0};
 
     void begin() {}
@@ -217,8 +217,8 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_packed(TCPOverIPv4Ada
     struct Parsed
     {
         bool ok = false;
-        IPv4Header ip;
-        TCPSegment seg;
+        IPv4Header ip{};
+        TCPSegment seg{};
     };
     std::vector<Parsed> parsed(n);
     auto parse_range = [&](size_t i0, size_t i1) {

@@ -6,7 +6,7 @@
 #include <cstdint>
 #include <optional>
 
-#include "icsum_wire.h"
+#include "tcp_over_ip.h"
 
 namespace icsum::detail {
 

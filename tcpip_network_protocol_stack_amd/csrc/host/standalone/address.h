@@ -1,9 +1,12 @@
-// address.h — the part of the reference's Address (util/address/address.h)
-// that the TCP-over-IPv4 adapter needs: an IPv4 address + port value type.
-// Socket/DNS resolution is the runtime's business and out of this engine's
-// scope; only numeric IPv4 literals are accepted here.
-#ifndef ICSUM_HOST_ADDRESS_H
-#define ICSUM_HOST_ADDRESS_H
+// address.h — standalone stand-in for the reference's Address
+// (util/address/address.h:14-70), used only when this layer is built WITHOUT
+// the reference tree (here and on the GPU box; see udinfo.h in this
+// directory).  It is the part the TCP-over-IPv4 adapter needs: an IPv4
+// address + port value type with the reference's signatures.  Integrated into
+// the reference, the reference's own Address (sockaddr storage, resolution,
+// Raw) is the one found and linked: the engine replaces nothing in it.
+#ifndef ADDRESS_H  // the reference header's guard
+#define ADDRESS_H
 
 #include <cstdint>
 #include <string>
