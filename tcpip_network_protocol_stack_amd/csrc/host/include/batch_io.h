@@ -109,6 +109,13 @@ class DatagramRing
     // stream ends when every fd has ended.
     DatagramRing(BatchEngine& engine, const std::vector<int>& fds, size_t slots = 0,
                  size_t capacity_bytes = size_t(32) << 20, size_t max_datagrams = 1 << 14);
+    // the same ring over ordinary-memory arenas, without an engine (I/O only:
+    // the batches' verify / unwrap / patch throw); the host-only stress tests
+    // and sanitizer builds run the ring's threading this way
+    explicit DatagramRing(int fd, size_t slots = 3, size_t capacity_bytes = size_t(32) << 20,
+                          size_t max_datagrams = 1 << 14);
+    explicit DatagramRing(const std::vector<int>& fds, size_t slots = 0, size_t capacity_bytes = size_t(32) << 20,
+                          size_t max_datagrams = 1 << 14);
     ~DatagramRing();
     DatagramRing(const DatagramRing&) = delete;
     DatagramRing& operator=(const DatagramRing&) = delete;
@@ -120,7 +127,7 @@ class DatagramRing
     void release(DatagramBatch* batch);
 
   private:
-    void start(BatchEngine& engine, size_t slots, size_t capacity_bytes);
+    void start(BatchEngine* engine, size_t slots, size_t capacity_bytes);
     void reader(int fd);
 
     std::vector<int> fds_{};
@@ -146,6 +153,9 @@ class DatagramTxRing
   public:
     DatagramTxRing(BatchEngine& engine, int fd, size_t slots = 3, size_t capacity_bytes = size_t(32) << 20,
                    size_t max_datagrams = 1 << 14);
+    // ordinary-memory arenas, no engine: submit(batch, false) only
+    explicit DatagramTxRing(int fd, size_t slots = 3, size_t capacity_bytes = size_t(32) << 20,
+                            size_t max_datagrams = 1 << 14);
     ~DatagramTxRing();  // flushes what was submitted, then stops the writer
     DatagramTxRing(const DatagramTxRing&) = delete;
     DatagramTxRing& operator=(const DatagramTxRing&) = delete;
@@ -153,13 +163,15 @@ class DatagramTxRing
     // an empty arena to fill (blocks while every arena is queued or being
     // sent); rethrows a writer error
     DatagramBatch* acquire();
-    // patch (when `patch`) and queue an arena taken with acquire()
+    // patch (when `patch`) and queue an arena taken with acquire(); if the
+    // patch throws, the arena returns to the free list and the error propagates
     void submit(DatagramBatch* batch, bool patch = true);
     // wait until every submitted datagram was written; rethrows a writer error
     void flush();
     size_t sent() const;  // datagrams written so far
 
   private:
+    void start(BatchEngine* engine, size_t slots, size_t capacity_bytes, size_t max_datagrams);
     void writer();
 
     int fd_;

@@ -7,6 +7,7 @@
 #include <thread>
 
 #include "icsum.h"
+#include "par_for.h"
 #include "wire_internal.h"
 
 namespace icsum {
@@ -262,14 +263,7 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_packed(TCPOverIPv4Ada
     };
     const size_t threads = std::min<size_t>({size_t(8), std::max(1u, std::thread::hardware_concurrency()),
                                              std::max<size_t>(1, n / 2048)});
-    if (threads <= 1) {
-        parse_range(0, n);
-    } else {
-        std::vector<std::thread> pool;
-        for (size_t t = 1; t < threads; ++t) pool.emplace_back(parse_range, n * t / threads, n * (t + 1) / threads);
-        parse_range(0, n / threads);
-        for (auto& th : pool) th.join();
-    }
+    detail::parallel_ranges(n, threads, parse_range);  // joins every worker, rethrows a worker's exception
     std::vector<std::optional<TCPMessage>> out(n);
     for (size_t i = 0; i < n; ++i) {
         if ((st[i] & (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) !=

@@ -172,10 +172,18 @@ void DatagramBatch::patch()
     engine_->patch_packed(arena_, off_.data(), size());
 }
 
+namespace {
+std::unique_ptr<DatagramBatch> make_arena(BatchEngine* engine, size_t capacity_bytes, size_t max_datagrams)
+{
+    return engine ? std::make_unique<DatagramBatch>(*engine, capacity_bytes, max_datagrams)
+                  : std::make_unique<DatagramBatch>(capacity_bytes, max_datagrams);
+}
+}  // namespace
+
 DatagramRing::DatagramRing(BatchEngine& engine, int fd, size_t slots, size_t capacity_bytes, size_t max_datagrams)
     : fds_{fd}, max_n_(max_datagrams)
 {
-    start(engine, slots, capacity_bytes);
+    start(&engine, slots, capacity_bytes);
 }
 
 DatagramRing::DatagramRing(BatchEngine& engine, const std::vector<int>& fds, size_t slots, size_t capacity_bytes,
@@ -183,20 +191,43 @@ DatagramRing::DatagramRing(BatchEngine& engine, const std::vector<int>& fds, siz
     : fds_(fds), max_n_(max_datagrams)
 {
     if (fds.empty()) throw std::invalid_argument("DatagramRing needs at least one fd");
-    start(engine, slots ? slots : 2 * fds.size() + 1, capacity_bytes);
+    start(&engine, slots ? slots : 2 * fds.size() + 1, capacity_bytes);
 }
 
-void DatagramRing::start(BatchEngine& engine, size_t slots, size_t capacity_bytes)
+DatagramRing::DatagramRing(int fd, size_t slots, size_t capacity_bytes, size_t max_datagrams)
+    : fds_{fd}, max_n_(max_datagrams)
+{
+    start(nullptr, slots, capacity_bytes);
+}
+
+DatagramRing::DatagramRing(const std::vector<int>& fds, size_t slots, size_t capacity_bytes, size_t max_datagrams)
+    : fds_(fds), max_n_(max_datagrams)
+{
+    if (fds.empty()) throw std::invalid_argument("DatagramRing needs at least one fd");
+    start(nullptr, slots ? slots : 2 * fds.size() + 1, capacity_bytes);
+}
+
+void DatagramRing::start(BatchEngine* engine, size_t slots, size_t capacity_bytes)
 {
     // every reader holds one arena while it fills it; one more keeps a
     // filled arena moving to the caller
     if (slots < fds_.size() + 1) throw std::invalid_argument("DatagramRing needs more slots than fds");
     for (size_t k = 0; k < slots; ++k) {
-        arenas_.push_back(std::make_unique<DatagramBatch>(engine, capacity_bytes, max_n_));
+        arenas_.push_back(make_arena(engine, capacity_bytes, max_n_));
         free_.push_back(arenas_.back().get());
     }
     live_ = fds_.size();
-    for (int fd : fds_) threads_.emplace_back([this, fd] { reader(fd); });
+    try {
+        for (int fd : fds_) threads_.emplace_back([this, fd] { reader(fd); });
+    } catch (...) {  // a thread failed to start: stop and join the ones that did
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            stop_ = true;
+        }
+        cv_.notify_all();
+        for (auto& t : threads_) t.join();
+        throw;
+    }
 }
 
 DatagramRing::~DatagramRing()
@@ -290,9 +321,19 @@ DatagramTxRing::DatagramTxRing(BatchEngine& engine, int fd, size_t slots, size_t
                                size_t max_datagrams)
     : fd_(fd)
 {
+    start(&engine, slots, capacity_bytes, max_datagrams);
+}
+
+DatagramTxRing::DatagramTxRing(int fd, size_t slots, size_t capacity_bytes, size_t max_datagrams) : fd_(fd)
+{
+    start(nullptr, slots, capacity_bytes, max_datagrams);
+}
+
+void DatagramTxRing::start(BatchEngine* engine, size_t slots, size_t capacity_bytes, size_t max_datagrams)
+{
     if (slots < 2) throw std::invalid_argument("DatagramTxRing needs at least 2 slots");
     for (size_t k = 0; k < slots; ++k) {
-        arenas_.push_back(std::make_unique<DatagramBatch>(engine, capacity_bytes, max_datagrams));
+        arenas_.push_back(make_arena(engine, capacity_bytes, max_datagrams));
         free_.push_back(arenas_.back().get());
     }
     thread_ = std::thread([this] { writer(); });
@@ -322,7 +363,18 @@ DatagramBatch* DatagramTxRing::acquire()
 
 void DatagramTxRing::submit(DatagramBatch* batch, bool patch)
 {
-    if (patch && batch->size()) batch->patch();  // the engine stays on the caller's thread
+    try {
+        if (patch && batch->size()) batch->patch();  // the engine stays on the caller's thread
+    } catch (...) {
+        // the arena goes back to the free list, so a failed patch does not
+        // leak it (acquire() would otherwise block once every slot was lost)
+        {
+            std::lock_guard<std::mutex> lock(mu_);
+            free_.push_back(batch);
+        }
+        cv_.notify_all();
+        throw;
+    }
     {
         std::lock_guard<std::mutex> lock(mu_);
         queued_.push_back(batch);

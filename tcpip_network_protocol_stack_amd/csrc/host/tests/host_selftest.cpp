@@ -5,8 +5,17 @@
 //   tcpv HEX                       -> "ip_ok tcp_ok tcp_value ip_computed proto" (datagram parse path)
 //   wrap SRC SPORT DST DPORT SEQ SYN FIN RST HASACK ACK WIN PAYLOADHEX -> wire hex
 //   unwrap SRC SPORT DST DPORT HEX -> "1" if the adapter (source=SRC:SPORT) accepts, else "0"
+//   io / ioudp / ioseq HEX...      -> DatagramBatch socket round trips (see below)
+//   ringstress F P N               -> engine-less DatagramRing over F SEQPACKET streams, P passes of N
+//                                     datagrams each: "got same_order lost_none"
+//   txstress P N                   -> engine-less DatagramTxRing to a SEQPACKET stream:
+//                                     "sent got same_order failed_patch_recovered"
+// The two stress commands run the rings' reader / writer threads with no GPU,
+// so the ASan+UBSan and TSan builds (make asan / make tsan) cover their locking.
+#include <algorithm>
 #include <cstdio>
 #include <iostream>
+#include <stdexcept>
 #include <sstream>
 #include <string>
 #include <thread>
@@ -48,6 +57,16 @@ std::string joined(const std::vector<std::string>& v)
     return r;
 }
 std::string ipstr(uint32_t a) { return Address::from_ipv4_numeric(a).ip(); }
+
+// datagram k of stream f: [f][k, 4 bytes LE][(k*7+f) % 200 bytes of a pattern]
+std::string stress_dgram(uint32_t f, uint32_t k)
+{
+    std::string d(5 + (k * 7 + f) % 200, '\0');
+    d[0] = static_cast<char>(f);
+    for (int b = 0; b < 4; ++b) d[1 + b] = static_cast<char>(k >> (8 * b));
+    for (size_t i = 5; i < d.size(); ++i) d[i] = static_cast<char>(i * 31 + k);
+    return d;
+}
 }  // namespace
 
 int main()
@@ -215,6 +234,108 @@ int main()
             // ended() is set by the read that meets the end, never before
             std::cout << sent << " " << got << " " << same << " " << (reads > 1) << " "
                       << (rx.ended() && !ended_early) << "\n";
+        } else if (cmd == "ringstress") {
+            uint32_t F = 0, P = 0, N = 0;
+            in >> F >> P >> N;
+            std::vector<int> rd, wr;
+            for (uint32_t f = 0; f < F; ++f) {
+                int sv[2];
+                if (socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) != 0) return 3;
+                wr.push_back(sv[0]);
+                rd.push_back(sv[1]);
+            }
+            std::vector<uint32_t> next(F, 0);
+            bool same = true;
+            size_t got = 0;
+            {
+                // small arenas and few datagrams per arena: many hand-overs
+                icsum::DatagramRing ring(rd, 0, size_t(64) << 10, 64);
+                std::vector<std::thread> ws;
+                for (uint32_t f = 0; f < F; ++f)
+                    ws.emplace_back([&, f] {
+                        icsum::DatagramBatch tx(size_t(1) << 20, 256);
+                        uint32_t k = 0;
+                        for (uint32_t p = 0; p < P; ++p) {
+                            for (uint32_t i = 0; i < N; i += 64) {
+                                tx.clear();
+                                for (uint32_t j = i; j < std::min(N, i + 64); ++j) tx.push(stress_dgram(f, k++));
+                                tx.write_to(wr[f]);
+                            }
+                        }
+                        close(wr[f]);
+                    });
+                while (icsum::DatagramBatch* b = ring.next()) {
+                    for (size_t i = 0; i < b->size(); ++i) {
+                        const std::string_view d = (*b)[i];
+                        const uint32_t f = static_cast<uint8_t>(d[0]);
+                        uint32_t k = 0;
+                        for (int q = 0; q < 4; ++q) k |= uint32_t(static_cast<uint8_t>(d[1 + q])) << (8 * q);
+                        same = same && f < F && k == next[f] && d == stress_dgram(f, k);
+                        if (f < F) next[f] = k + 1;
+                        ++got;
+                    }
+                    ring.release(b);
+                }
+                for (auto& t : ws) t.join();
+            }
+            bool all = true;
+            for (uint32_t f = 0; f < F; ++f) all = all && next[f] == P * N;
+            for (int fd : rd) close(fd);
+            std::cout << got << " " << same << " " << all << "\n";
+        } else if (cmd == "txstress") {
+            uint32_t P = 0, N = 0;
+            in >> P >> N;
+            int sv[2];
+            if (socketpair(AF_UNIX, SOCK_SEQPACKET, 0, sv) != 0) return 3;
+            size_t got = 0;
+            bool same = true;
+            std::thread r([&] {
+                icsum::DatagramBatch rx(size_t(1) << 20, 256);
+                for (;;) {
+                    rx.clear();
+                    const size_t k = rx.read_from(sv[1], 256);
+                    if (k == 0) break;
+                    for (size_t i = 0; i < k; ++i) same = same && rx[i] == stress_dgram(0, static_cast<uint32_t>(got + i));
+                    got += k;
+                }
+            });
+            size_t sent = 0;
+            bool recovered = false;
+            {
+                icsum::DatagramTxRing tx(sv[0], 3, size_t(64) << 10, 64);
+                // an engine-less arena cannot patch: submit() throws and the
+                // arena goes back to the free list (4 more acquires than slots
+                // would block forever if it leaked)
+                int threw = 0;
+                for (int t = 0; t < 4; ++t) {
+                    icsum::DatagramBatch* b = tx.acquire();
+                    b->push(stress_dgram(9, 9));
+                    try {
+                        tx.submit(b, true);
+                    } catch (const std::logic_error&) {
+                        ++threw;
+                    }
+                }
+                recovered = threw == 4;
+                uint32_t k = 0;
+                for (uint32_t p = 0; p < P; ++p) {
+                    for (uint32_t i = 0; i < N;) {
+                        icsum::DatagramBatch* b = tx.acquire();
+                        while (i < N && b->push(stress_dgram(0, k))) {
+                            ++i;
+                            ++k;
+                        }
+                        tx.submit(b, false);
+                    }
+                }
+                tx.flush();
+                sent = tx.sent();
+            }
+            shutdown(sv[0], SHUT_WR);
+            r.join();
+            close(sv[0]);
+            close(sv[1]);
+            std::cout << sent << " " << got << " " << same << " " << recovered << "\n";
         } else if (!cmd.empty()) {
             std::cerr << "unknown command " << cmd << "\n";
             return 1;

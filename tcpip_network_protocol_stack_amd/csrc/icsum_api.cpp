@@ -19,6 +19,7 @@
 
 #include "icsum.h"
 #include "icsum_workload.h"
+#include "common/par_for.h"
 #include "kernels/icsum_launch.h"
 
 namespace {
@@ -273,14 +274,9 @@ void par_memcpy(void* dst, const void* src, size_t n) {
     std::memcpy(dst, src, n);
     return;
   }
-  std::vector<std::thread> th;
-  th.reserve(t - 1);
-  for (size_t k = 1; k < t; ++k) {
-    const size_t a = n * k / t, b = n * (k + 1) / t;
-    th.emplace_back([=] { std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, b - a); });
-  }
-  std::memcpy(dst, src, n / t);
-  for (auto& x : th) x.join();
+  icsum::detail::parallel_ranges(n, t, [=](size_t a, size_t b) {
+    std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, b - a);
+  });
 }
 
 // ICS_MODE_PATCH's stores (k_ipv4_tcp, mode 2) applied on the host from a

@@ -1,0 +1,78 @@
+"""CPU: the host layer and the oracle under sanitizers (the
+reference builds ASan/UBSan variants of every library, test and app,
+etc/cflags.cmake:8, etc/tests.cmake:8-26 — and this layer adds threads, so
+TSan too).
+
+* csrc/host `make asan` / `make tsan`: host_selftest over every golden-vector
+  command (KATs, IPv4 parse, TCP verify, wrap, unwrap), the socket round trips
+  (io / ioseq / ioudp) and an engine-less DatagramRing (4 SEQPACKET streams,
+  one reader thread each) / DatagramTxRing (writer thread) stress; output must
+  equal the plain build's and the sanitizers must stay silent.
+* oracle `make asan` / `make tsan`: every oracle entry point on exact-size heap
+  buffers plus its threaded batch; the digest must equal the plain build's."""
+import os
+import subprocess
+
+import pytest
+
+from conftest import ROOT
+from helpers import kat_cases, wires
+
+HOST = os.path.join(ROOT, "tcpip_network_protocol_stack_amd", "csrc", "host")
+ORACLE = os.path.join(ROOT, "oracle")
+SAN_MARKS = ("ERROR: AddressSanitizer", "runtime error:", "WARNING: ThreadSanitizer", "ERROR: LeakSanitizer")
+
+
+def _selftest_lines():
+    lines = [f"kat {init} " + " ".join(p.hex() or "-" for p in pieces)
+             for init, pieces, _, _ in kat_cases()[:200]]
+    lines += [f"ipv4 {c['bytes']}" for c in wires("ipv4_cases.json")]
+    tw = wires("tcp_wrap.json")
+    lines += [f"tcpv {c['wire']}" for c in tw]
+    for c in wires("tcp_wrap.json", {"wrap"}):
+        payload = c["wire"][80:80 + 2 * c["payload_len"]] or "-"
+        lines.append(f"wrap {c['src']} {c['sport']} {c['dst']} {c['dport']} {c['seqno']} {c['syn']} {c['fin']} "
+                     f"{c['rst']} {c['has_ack']} {c['ackno']} {c['window']} {payload}")
+        lines.append(f"unwrap {c['dst']} {c['dport']} {c['src']} {c['sport']} {c['wire']}")
+    lines.append("io " + " ".join(c["wire"] for c in tw))
+    lines.append("ioseq " + " ".join(c["wire"] for c in tw))
+    lines.append("ioudp " + " ".join(c["wire"] for c in tw[:64]))
+    lines.append("ringstress 4 3 2000")
+    lines.append("txstress 3 3000")
+    return "\n".join(lines) + "\n"
+
+
+@pytest.fixture(scope="module")
+def host_builds():
+    subprocess.check_call(["make", "-s", "-j8", "-C", HOST], stdout=subprocess.DEVNULL)
+    subprocess.check_call(["make", "-s", "-C", HOST, "asan", "tsan"], stdout=subprocess.DEVNULL)
+    return {k: os.path.join(HOST, d, "host_selftest")
+            for k, d in (("plain", "build"), ("asan", "build-asan"), ("tsan", "build-tsan"))}
+
+
+def _clean(r):
+    return r.returncode == 0 and not any(m in r.stderr for m in SAN_MARKS)
+
+
+def test_host_selftest_under_asan_and_tsan(host_builds):
+    stdin = _selftest_lines()
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0",
+               TSAN_OPTIONS="halt_on_error=1:second_deadlock_stack=1")
+    runs = {k: subprocess.run([exe], input=stdin, capture_output=True, text=True, timeout=600, env=env)
+            for k, exe in host_builds.items()}
+    assert runs["plain"].returncode == 0, runs["plain"].stderr[-2000:]
+    last = runs["plain"].stdout.strip().splitlines()[-2:]
+    assert last[0] == "24000 1 1" and last[1] == "9000 9000 1 1", last
+    for k in ("asan", "tsan"):
+        assert _clean(runs[k]), (k, runs[k].stderr[-4000:])
+        assert runs[k].stdout == runs["plain"].stdout, k
+
+
+def test_oracle_under_asan_and_tsan():
+    subprocess.check_call(["make", "-s", "-C", ORACLE, "check", "asan", "tsan"], stdout=subprocess.DEVNULL)
+    outs = {}
+    for k in ("oracle_check", "oracle_check_asan", "oracle_check_tsan"):
+        r = subprocess.run([os.path.join(ORACLE, "_build", k)], capture_output=True, text=True, timeout=300)
+        assert _clean(r), (k, r.stderr[-4000:])
+        outs[k] = r.stdout
+    assert len(set(outs.values())) == 1 and outs["oracle_check"].startswith("oracle-check "), outs
