@@ -150,6 +150,71 @@ int main()
     }
     EXPECT(accepted >= wires.size() / 2);
 
+    // unwrap_raw() at a batch size that takes the threaded field parse (8
+    // ranges at >= 16 Ki datagrams, batch.cpp) with the adapter's gates in
+    // datagram order: 20 000 wires from two peers and strangers, a third
+    // one-bit corrupted, to a LISTENING adapter whose first clean SYN (from
+    // peer 2) sits mid-batch; then to a connected adapter.  Every result must
+    // equal the per-object unwrap_tcp_in_ip in the same order, field by field.
+    {
+        auto same_msg = [](const TCPMessage& a, const TCPMessage& b) {
+            return a.sender.seqno == b.sender.seqno && a.sender.SYN == b.sender.SYN &&
+                   a.sender.payload == b.sender.payload && a.sender.FIN == b.sender.FIN &&
+                   a.sender.RST == b.sender.RST && a.receiver.ackno == b.receiver.ackno &&
+                   a.receiver.window_size == b.receiver.window_size && a.receiver.RST == b.receiver.RST;
+        };
+        TCPOverIPv4Adapter p1, p2, stranger, wrongport;
+        p1.config_mut().source = Address{"10.9.8.7", 80};
+        p2.config_mut().source = Address{"10.5.5.5", 8080};
+        stranger.config_mut().source = Address{"10.7.7.7", 80};
+        wrongport.config_mut().source = Address{"10.9.8.7", 80};
+        for (auto* a : {&p1, &p2, &stranger}) a->config_mut().destination = Address{"10.1.2.3", 4321};
+        wrongport.config_mut().destination = Address{"10.1.2.3", 4322};
+        const size_t N = 20000, kSyn = 8191;
+        std::vector<std::string> big;
+        for (size_t i = 0; i < N; ++i) {
+            TCPMessage m;
+            m.sender.seqno = Wrap32{static_cast<uint32_t>(rng())};
+            m.sender.SYN = i == kSyn || (i > kSyn && rng() % 5 == 0);
+            m.sender.RST = i != kSyn && rng() % 11 == 0;
+            m.sender.FIN = rng() % 7 == 0;
+            m.sender.payload = bytes(rng() % 600);
+            if (rng() % 3) m.receiver.ackno = Wrap32{static_cast<uint32_t>(rng())};
+            m.receiver.window_size = static_cast<uint16_t>(rng());
+            const unsigned pick = static_cast<unsigned>(rng() % 20);
+            TCPOverIPv4Adapter& from =
+                i == kSyn ? p2 : (pick < 12 ? p1 : (pick < 16 ? p2 : (pick < 18 ? stranger : wrongport)));
+            std::string w = joined(serialize(from.wrap_tcp_in_ip(m)));
+            if (i != kSyn && i % 3 == 1) w[rng() % w.size()] ^= static_cast<char>(1u << (rng() % 8));
+            big.push_back(w);
+        }
+        std::vector<std::string_view> bigv(big.begin(), big.end());
+        TCPOverIPv4Adapter L;
+        L.config_mut().source = Address{"0", 4321};
+        L.set_listening(true);
+        TCPOverIPv4Adapter C = A;  // 10.1.2.3:4321 connected to 10.9.8.7:80 (peer 1)
+        for (int pass = 0; pass < 2; ++pass) {
+            TCPOverIPv4Adapter Agpu = pass ? C : L, Acpu = pass ? C : L;
+            const auto gotb = eng.unwrap_raw(Agpu, bigv);
+            size_t acc = 0, before_syn = 0;
+            for (size_t i = 0; i < N; ++i) {
+                InternetDatagram d;
+                std::optional<TCPMessage> want;
+                if (parse(d, std::vector<std::string>{big[i]})) want = Acpu.unwrap_tcp_in_ip(d);
+                EXPECT(gotb[i].has_value() == want.has_value());
+                if (want && gotb[i]) {
+                    EXPECT(same_msg(*gotb[i], *want));
+                    ++acc;
+                    if (i < kSyn) ++before_syn;
+                }
+            }
+            EXPECT(Agpu.listening() == Acpu.listening());
+            EXPECT(Agpu.config().destination == Acpu.config().destination);
+            EXPECT(acc > N / 10);
+            if (pass == 0) EXPECT(before_syn == 0 && !Agpu.listening());  // nothing before the first SYN
+        }
+    }
+
     // batched datagram I/O: the same received wires through
     // a SOCK_DGRAM socketpair into a page-locked arena, unwrapped in place
     {

@@ -225,21 +225,35 @@ void free_staging(ics_ctx* ctx) {
   ctx->staged = false;
 }
 
-// One staged chunk of segments [i0, i1) covering bytes [b0, b1).
+// One staged chunk of segments [i0, i1) covering bytes [b0, b1).  A segment
+// longer than a staging slot goes through the slots as PIECES: chunks with
+// piece = true, i1 = i0 + 1 and [b0, b1) a slot-sized part of that one
+// segment (pos = the part's offset inside it).
 struct Chunk {
   uint64_t i0, i1, b0, b1;
+  bool piece = false, last = false;
+  uint64_t pos = 0;
 };
 
-// Next chunk starting at segment i0 that fits the slot (a single segment
-// larger than a slot is an error for the host path).
+// Next chunk starting at segment i0 (whose first `pos` bytes were already
+// staged as pieces) that fits the slot.
 int next_chunk(const ics_ctx* ctx, const uint64_t* offsets, uint64_t stride, uint64_t seg_len, uint64_t n,
-               uint64_t i0, Chunk* c) {
+               uint64_t i0, uint64_t pos, bool allow_pieces, Chunk* c) {
   const uint64_t cap_b = ctx->slot_bytes, cap_n = ics_ctx::kSlotSegs;
+  const uint64_t s0 = offsets ? offsets[i0] : i0 * stride;
+  const uint64_t len0 = offsets ? offsets[i0 + 1] - s0 : seg_len;
+  if (pos || len0 > cap_b) {  // segment i0 does not fit a slot: its next piece
+    if (!allow_pieces)
+      return fail(ICS_ERR_INVALID, "datagram %llu (%llu bytes) exceeds the %zu-byte staging slot",
+                  (unsigned long long)i0, (unsigned long long)len0, ctx->slot_bytes);
+    const uint64_t take = std::min<uint64_t>(cap_b, len0 - pos);
+    *c = {i0, i0 + 1, s0 + pos, s0 + pos + take, true, pos + take == len0, pos};
+    return ICS_OK;
+  }
   if (!offsets) {
     const uint64_t per = std::max<uint64_t>(stride, seg_len);
     uint64_t k = per ? cap_b / per : cap_n;
-    if (k == 0) return fail(ICS_ERR_INVALID, "segment of %llu bytes exceeds the %zu-byte staging slot",
-                            (unsigned long long)per, ctx->slot_bytes);
+    if (k == 0) k = 1;  // stride > slot but the segment itself fits
     k = std::min<uint64_t>({k, cap_n, n - i0});
     *c = {i0, i0 + k, i0 * stride, (i0 + k - 1) * stride + seg_len};
     return ICS_OK;
@@ -247,12 +261,20 @@ int next_chunk(const ics_ctx* ctx, const uint64_t* offsets, uint64_t stride, uin
   const uint64_t b0 = offsets[i0];
   uint64_t i1 = i0;
   while (i1 < n && i1 - i0 < cap_n && offsets[i1 + 1] - b0 <= cap_b) ++i1;
-  if (i1 == i0)
-    return fail(ICS_ERR_INVALID, "segment %llu (%llu bytes) exceeds the staging slot",
-                (unsigned long long)i0, (unsigned long long)(offsets[i0 + 1] - offsets[i0]));
   *c = {i0, i1, b0, offsets[i1]};
   return ICS_OK;
 }
+
+// InternetChecksum::value() of a raw sum (util/tools/checksum.h:31-41)
+uint16_t fold_value(uint32_t sum) {
+  while (sum > 0xFFFFu) sum = (sum >> 16) + (sum & 0xFFFFu);
+  return uint16_t(~sum & 0xFFFFu);
+}
+
+// A piece is summed on the device as sub-pieces of this many bytes (one lane
+// group each, so a 32 MiB piece is 512 segments of work, not one long one);
+// even, so every sub-piece starts with the piece's parity.
+constexpr uint64_t kSubPiece = uint64_t(64) << 10;
 
 // Is [p, p+bytes) page-locked host memory the DMA engines can read directly?
 bool host_pinned(const void* p) {
@@ -320,12 +342,24 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   const bool direct = host_pinned(h_bytes);
   Chunk pending[ics_ctx::kMaxSlots];
   bool busy[ics_ctx::kMaxSlots] = {};
+  uint32_t piece_sum = 0;  // running sum of the long segment whose pieces are in flight
   auto retire = [&](int k) -> int {
     if (!busy[k]) return ICS_OK;
     ICS_HIP(hipEventSynchronize(ctx->ev[k]));
     const Chunk& c = pending[k];
     const uint64_t m = c.i1 - c.i0;
-    if (kind == 0) {
+    if (c.piece) {
+      // raw u32 sums of the piece's sub-pieces; uint32 addition is
+      // associative, so sum_ of the whole segment = init + every part's sum
+      // (each summed with its own start parity), wrap included
+      const uint64_t parts = (c.b1 - c.b0 + kSubPiece - 1) / kSubPiece;
+      const uint32_t* raw = reinterpret_cast<const uint32_t*>(ctx->h_out[k]);
+      for (uint64_t j = 0; j < parts; ++j) piece_sum += raw[j];
+      if (c.last) {
+        out_a[c.i0] = fold_value((h_init ? h_init[c.i0] : 0u) + piece_sum);
+        piece_sum = 0;
+      }
+    } else if (kind == 0) {
       std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
     } else {
       if (out_a) std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
@@ -337,11 +371,11 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
     busy[k] = false;
     return ICS_OK;
   };
-  uint64_t i0 = 0;
+  uint64_t i0 = 0, pos = 0;
   int slot = 0;
   while (i0 < n) {
     Chunk c;
-    if (int rc = next_chunk(ctx, h_offsets, stride, seg_len, n, i0, &c)) return rc;
+    if (int rc = next_chunk(ctx, h_offsets, stride, seg_len, n, i0, pos, kind == 0, &c)) return rc;
     if (int rc = retire(slot)) return rc;
     const uint64_t m = c.i1 - c.i0, nb = c.b1 - c.b0;
     uint8_t* src = static_cast<uint8_t*>(h_bytes) + c.b0;
@@ -351,6 +385,31 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
     }
     hipStream_t st = ctx->st[slot];
     ICS_HIP(hipMemcpyAsync(ctx->d_in[slot], src, nb, hipMemcpyHostToDevice, st));
+    if (c.piece) {
+      // ics_sum_batch over the piece's sub-pieces: raw sums, parity = the
+      // piece's offset in its segment (checksum.h:24-26 carried across add()s)
+      const uint64_t parts = (nb + kSubPiece - 1) / kSubPiece;
+      for (uint64_t j = 0; j <= parts; ++j) ctx->h_off[slot][j] = std::min<uint64_t>(j * kSubPiece, nb);
+      uint8_t* odd = reinterpret_cast<uint8_t*>(ctx->h_init[slot]);
+      std::memset(odd, int(c.pos & 1), parts);
+      ICS_HIP(hipMemcpyAsync(ctx->d_off[slot], ctx->h_off[slot], (parts + 1) * 8, hipMemcpyHostToDevice, st));
+      ICS_HIP(hipMemcpyAsync(ctx->d_init[slot], odd, parts, hipMemcpyHostToDevice, st));
+      const icsum::SegSpec sp{ctx->d_in[slot], ctx->d_off[slot], 0, 0, parts, ctx->d_zero};
+      ICS_HIP(icsum::launch_checksum(sp, nullptr, reinterpret_cast<const uint8_t*>(ctx->d_init[slot]),
+                                     ctx->d_out[slot], 1, geometry_for(ctx, kSubPiece), ctx->max_blocks, st));
+      ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], parts * 4, hipMemcpyDeviceToHost, st));
+      ICS_HIP(hipEventRecord(ctx->ev[slot], st));
+      pending[slot] = c;
+      busy[slot] = true;
+      if (c.last) {
+        i0 = c.i1;
+        pos = 0;
+      } else {
+        pos = c.pos + nb;
+      }
+      slot = (slot + 1) % ctx->nslots;
+      continue;
+    }
     const uint64_t* d_off = nullptr;
     if (h_offsets) {
       for (uint64_t j = 0; j <= m; ++j) ctx->h_off[slot][j] = h_offsets[c.i0 + j] - c.b0;
