@@ -210,7 +210,7 @@ int main()
             }
             EXPECT(Agpu.listening() == Acpu.listening());
             EXPECT(Agpu.config().destination == Acpu.config().destination);
-            EXPECT(acc > N / 10);
+            EXPECT(acc > N / 20);  // listening: only peer 2 (1/5 of the wires) after its SYN
             if (pass == 0) EXPECT(before_syn == 0 && !Agpu.listening());  // nothing before the first SYN
         }
     }
