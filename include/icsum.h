@@ -150,9 +150,45 @@ int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets
                          uint64_t stride, uint64_t dgram_len, uint64_t n,
                          uint8_t* d_status, void* stream);
 
+/* ---- a14 / §8(f) rank 2: device-side wrap_tcp_in_ip -------------------- */
+/* The fields of one TCPMessage as TCPOverIPv4Adapter::wrap_tcp_in_ip
+ * (util/tcp_over_ip/tcp_over_ip.cpp:69-88) puts them on the wire.  28 bytes. */
+typedef struct ics_tcp_msg {
+  uint32_t src, dst;   /* IPv4Header::src / dst, host order (FdAdapterConfig source / destination) */
+  uint32_t seqno;      /* TCPSenderMessage::seqno, raw Wrap32 value */
+  uint32_t ackno;      /* raw ackno; 0 when the message has none (tcp_segment.cpp:86) */
+  uint16_t src_port, dst_port;
+  uint16_t window;     /* TCPReceiverMessage::window_size */
+  uint8_t flags;       /* ICS_TCP_* bits, as tcp_segment.cpp:92-97 derives them */
+  uint8_t ttl;         /* IPv4Header::ttl (DEFAULT_TTL = 128 in wrap_tcp_in_ip) */
+  uint16_t id;         /* IPv4Header::id (0 in wrap_tcp_in_ip) */
+  uint16_t reserved;   /* 0 */
+} ics_tcp_msg;
+#define ICS_TCP_FIN 0x01u
+#define ICS_TCP_SYN 0x02u
+#define ICS_TCP_RST 0x04u /* sender.RST || receiver.RST */
+#define ICS_TCP_ACK 0x10u /* receiver.ackno present */
+
+/* Datagram i = bytes [off_i, off_i+1) (or fixed stride / dgram_len) holds 40
+ * bytes of room for the headers followed by message i's payload, already in
+ * place.  In one pass per datagram the engine sums the payload and writes the
+ * serialized IPv4 header (ipv4_header.cpp:62-86: ver 4, hlen 5, tos 0,
+ * len = datagram length mod 2^16, id, DF, ttl, proto 6, checksum, src, dst)
+ * and TCP header (tcp_segment.cpp:76-106: ports, seqno, ackno, data offset 5,
+ * flags, window, checksum, urgent 0) with both checksums
+ * (TCPSegment::compute_checksum(pseudo_checksum()), then
+ * IPv4Header::compute_checksum(), tcp_over_ip.cpp:83-84): the wire bytes of
+ * serialize(wrap_tcp_in_ip(msg)), with no host-side serialization.
+ * Datagrams shorter than 40 bytes are left untouched (checksums 0).
+ * d_ip_ck / d_tcp_ck (optional) receive the two checksums. */
+int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,
+                       uint64_t dgram_len, uint64_t n, const ics_tcp_msg* d_msgs, uint16_t* d_ip_ck,
+                       uint16_t* d_tcp_ck, void* stream);
+
 /* ---- host-memory variants (PCIe-inclusive path) ------------------------ */
 /* Same semantics as ics_checksum_batch / ics_ipv4_tcp_batch on host
- * buffers.  The engine stages through pinned memory in chunks (page-locked
+ * buffers; ics_checksum_batch_host takes segments of any length (longer than
+ * a staging slot: summed piecewise, parity carried, as add() chains do).  The engine stages through pinned memory in chunks (page-locked
  * caller buffers are DMA'd directly) and pipelines H2D / kernel / D2H on its
  * slot streams; returns when the outputs are complete.  PATCH on host
  * memory: the device computes the two checksums and the engine writes the
@@ -163,6 +199,12 @@ int ics_checksum_batch_host(ics_ctx* ctx, const void* h_bytes, const uint64_t* h
 int ics_ipv4_tcp_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offsets,
                             uint64_t stride, uint64_t dgram_len, uint64_t n, int mode,
                             uint16_t* h_ip_ck, uint16_t* h_tcp_ck, uint8_t* h_status);
+/* ics_tcp_wrap_batch on host memory (e.g. a page-locked DatagramBatch arena
+ * the payloads were copied into once): the payload bytes go to the device,
+ * only the 40 header bytes per datagram come back and are written into
+ * h_dgrams.  Synchronous. */
+int ics_tcp_wrap_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offsets, uint64_t stride,
+                            uint64_t dgram_len, uint64_t n, const ics_tcp_msg* h_msgs);
 
 /* ---- device memory helpers for FFI callers without an allocator -------- */
 int ics_malloc(ics_ctx* ctx, void** d_ptr, size_t bytes);

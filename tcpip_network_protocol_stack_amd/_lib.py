@@ -15,6 +15,19 @@ ICS_MODE_COMPUTE, ICS_MODE_VERIFY, ICS_MODE_PATCH = 0, 1, 2
 ICS_ST_IPV4_OK, ICS_ST_TCP_CKSUM_OK, ICS_ST_TCP_HDR_OK, ICS_ST_PROTO_TCP = 0x01, 0x02, 0x04, 0x08
 ICS_ST_ACCEPT = 0x0F
 ICS_BINNING_AUTO, ICS_BINNING_SINGLE, ICS_BINNING_BINNED = -1, 0, 1
+ICS_TCP_FIN, ICS_TCP_SYN, ICS_TCP_RST, ICS_TCP_ACK = 0x01, 0x02, 0x04, 0x10
+
+
+class TcpMsg(ctypes.Structure):
+    """struct ics_tcp_msg (include/icsum.h), 28 bytes: the fields
+    wrap_tcp_in_ip puts on the wire (util/tcp_over_ip/tcp_over_ip.cpp:69-88)."""
+    _fields_ = [("src", ctypes.c_uint32), ("dst", ctypes.c_uint32), ("seqno", ctypes.c_uint32),
+                ("ackno", ctypes.c_uint32), ("src_port", ctypes.c_uint16), ("dst_port", ctypes.c_uint16),
+                ("window", ctypes.c_uint16), ("flags", ctypes.c_uint8), ("ttl", ctypes.c_uint8),
+                ("id", ctypes.c_uint16), ("reserved", ctypes.c_uint16)]
+
+
+assert ctypes.sizeof(TcpMsg) == 28
 
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -36,6 +49,8 @@ SIGNATURES = {
     "ics_fold_batch": (_int, [_p, _p, _p, _u64, _p]),
     "ics_ipv4_tcp_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p, _p]),
     "ics_router_ttl_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p]),
+    "ics_tcp_wrap_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p, _p, _p]),
+    "ics_tcp_wrap_batch_host": (_int, [_p, _p, _p, _u64, _u64, _u64, _p]),
     "ics_checksum_batch_host": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _u64]),
     "ics_ipv4_tcp_batch_host": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p]),
     "ics_malloc": (_int, [_p, ctypes.POINTER(_p), ctypes.c_size_t]),

@@ -7,6 +7,8 @@
 //                         IPv4Header::compute_checksum() per header        ipv4_header.cpp:113-123
 //   verify_raw()          IPv4Header::parse + TCPSegment::parse checks     ipv4_header.cpp:9-59, tcp_segment.cpp:11-65
 //   wrap()                TCPOverIPv4Adapter::wrap_tcp_in_ip per message   tcp_over_ip.cpp:69-88
+//                         (headers + both checksums serialized on the GPU;
+//                         payloads copied once, into the DMA arena)
 //   unwrap()/unwrap_raw() TCPOverIPv4Adapter::unwrap_tcp_in_ip per datagram tcp_over_ip.cpp:10-67
 //
 // Results are bit-identical to the per-object calls.  All checksum arithmetic
@@ -22,14 +24,18 @@
 #include <string_view>
 #include <vector>
 
+#include "icsum.h"
 #include "ipv4_datagram.h"
 #include "ipv4_header.h"
 #include "tcp_over_ip.h"
 #include "tcp_segment.h"
 
-struct ics_ctx;
-
 namespace icsum {
+
+// The fields wrap_tcp_in_ip puts on the wire for `msg` from an adapter with
+// configuration `cfg` (tcp_over_ip.cpp:71-80, tcp_segment.cpp:76-106): the
+// record the device-side wrap (ics_tcp_wrap_batch) serializes.
+ics_tcp_msg wrap_fields(const FdAdapterConfig& cfg, const TCPMessage& msg);
 
 class BatchEngine
 {
@@ -45,6 +51,9 @@ class BatchEngine
     // ICS_ST_* status bits per raw wire datagram (ICS_ST_ACCEPT = all parse checks pass)
     std::vector<uint8_t> verify_raw(std::span<const std::string_view> wires);
     std::vector<InternetDatagram> wrap(TCPOverIPv4Adapter& adapter, std::span<const TCPMessage> msgs);
+    // the same, consuming the messages: each payload string is moved into its
+    // datagram after the one copy into the arena
+    std::vector<InternetDatagram> wrap(TCPOverIPv4Adapter& adapter, std::vector<TCPMessage>&& msgs);
     std::vector<std::optional<TCPMessage>> unwrap(TCPOverIPv4Adapter& adapter,
                                                   std::span<const InternetDatagram> dgrams);
     std::vector<std::optional<TCPMessage>> unwrap_raw(TCPOverIPv4Adapter& adapter,
@@ -54,6 +63,9 @@ class BatchEngine
     // e.g. a DatagramBatch arena in page-locked memory: no packing copy
     std::vector<uint8_t> verify_packed(const uint8_t* bytes, const uint64_t* offsets, size_t n);
     void patch_packed(uint8_t* bytes, const uint64_t* offsets, size_t n);  // compute + store both checksums
+    // device-side wrap of a packed batch: datagram i = [40 B room][payload i],
+    // headers + both checksums written into `bytes` (ics_tcp_wrap_batch_host)
+    void wrap_packed(uint8_t* bytes, const uint64_t* offsets, const ics_tcp_msg* msgs, size_t n);
     std::vector<std::optional<TCPMessage>> unwrap_packed(TCPOverIPv4Adapter& adapter, const uint8_t* bytes,
                                                          const uint64_t* offsets, size_t n);
 
@@ -64,8 +76,14 @@ class BatchEngine
     int device() const { return device_; }
 
   private:
+    template <typename Msgs, typename Take>
+    std::vector<InternetDatagram> wrap_impl(const TCPOverIPv4Adapter& adapter, Msgs& msgs, Take take_payload);
+    uint8_t* scratch(size_t bytes);  // page-locked arena reused across calls
+
     ics_ctx* ctx_ = nullptr;
     int device_ = 0;
+    uint8_t* scratch_ = nullptr;
+    size_t scratch_cap_ = 0;
 };
 
 }  // namespace icsum

@@ -44,6 +44,7 @@ class DatagramBatch
     void clear()
     {
         off_.assign(1, 0);
+        msgs_.clear();
         ended_ = false;
     }
     size_t size() const { return off_.size() - 1; }
@@ -61,6 +62,14 @@ class DatagramBatch
     const uint64_t* offsets() const { return off_.data(); }
 
     bool push(std::string_view wire);  // false when the arena is full
+    // the transmit side without host serialization: 40 bytes of header room +
+    // msg's payload (its only copy) appended; wrap() then has the engine write
+    // both headers and checksums of every such datagram (wrap_tcp_in_ip,
+    // tcp_over_ip.cpp:69-88, from `adapter`'s configuration).  False when full.
+    bool push_tcp(const TCPOverIPv4Adapter& adapter, const TCPMessage& msg);
+    // datagrams added by push_tcp are waiting for wrap() (which requires that
+    // every datagram of the batch came from push_tcp)
+    bool wrap_pending() const { return !msgs_.empty(); }
 
     // up to `max` datagrams from `fd` (non-blocking fds stop at EAGAIN;
     // blocking ones wait for the first datagram, then take what is queued);
@@ -74,12 +83,14 @@ class DatagramBatch
     std::vector<uint8_t> verify();
     std::vector<std::optional<TCPMessage>> unwrap(TCPOverIPv4Adapter& adapter);
     void patch();
+    void wrap();
 
   private:
     BatchEngine* engine_ = nullptr;
     uint8_t* arena_ = nullptr;
     size_t cap_ = 0, max_n_ = 0;
     std::vector<uint64_t> off_{0};
+    std::vector<ics_tcp_msg> msgs_{};  // one per push_tcp datagram
     bool ended_ = false;
     bool room(size_t n) const { return size() < max_n_ && bytes() + n <= cap_; }
 };
@@ -163,8 +174,10 @@ class DatagramTxRing
     // an empty arena to fill (blocks while every arena is queued or being
     // sent); rethrows a writer error
     DatagramBatch* acquire();
-    // patch (when `patch`) and queue an arena taken with acquire(); if the
-    // patch throws, the arena returns to the free list and the error propagates
+    // queue an arena taken with acquire(): an arena filled with push_tcp is
+    // wrapped on the GPU (headers + both checksums), one filled with push()
+    // is patched (both checksum fields) when `patch`; if that throws, the
+    // arena returns to the free list and the error propagates
     void submit(DatagramBatch* batch, bool patch = true);
     // wait until every submitted datagram was written; rethrows a writer error
     void flush();

@@ -3,6 +3,7 @@
 #include "batch.h"
 
 #include <algorithm>
+#include <cstring>
 #include <stdexcept>
 #include <thread>
 
@@ -30,22 +31,49 @@ struct Packed
     uint64_t n() const { return off.size() - 1; }
 };
 
-// the 40 header bytes wrap_tcp_in_ip serializes (checksum fields 0) + payload
-void append_wire(Packed& p, const IPv4Header& h, const TCPSegment& seg)
+}  // namespace
+
+ics_tcp_msg wrap_fields(const FdAdapterConfig& cfg, const TCPMessage& msg)
 {
-    p.add(serialize(h).front());
-    for (const auto& piece : serialize(seg)) p.add(piece);
-    p.end();
+    ics_tcp_msg m{};
+    m.src = cfg.source.ipv4_numeric();
+    m.dst = cfg.destination.ipv4_numeric();
+    m.seqno = detail::raw_of(msg.sender.seqno);
+    m.ackno = detail::raw_of(msg.receiver.ackno.value_or(Wrap32{0}));  // tcp_segment.cpp:86
+    m.src_port = cfg.source.port();
+    m.dst_port = cfg.destination.port();
+    m.window = msg.receiver.window_size;
+    m.flags = static_cast<uint8_t>((msg.receiver.ackno.has_value() ? ICS_TCP_ACK : 0U) |
+                                   (msg.sender.RST || msg.receiver.RST ? ICS_TCP_RST : 0U) |
+                                   (msg.sender.SYN ? ICS_TCP_SYN : 0U) | (msg.sender.FIN ? ICS_TCP_FIN : 0U));
+    m.ttl = IPv4Header::DEFAULT_TTL;  // wrap_tcp_in_ip keeps the header defaults
+    m.id = 0;
+    return m;
 }
 
-}  // namespace
+uint8_t* BatchEngine::scratch(size_t bytes)
+{
+    if (bytes > scratch_cap_) {
+        const size_t cap = std::max(bytes, scratch_cap_ * 2);
+        if (scratch_) host_free(scratch_);
+        scratch_ = nullptr;
+        scratch_cap_ = 0;
+        scratch_ = static_cast<uint8_t*>(host_alloc(cap));
+        scratch_cap_ = cap;
+    }
+    return scratch_;
+}
 
 BatchEngine::BatchEngine(int device) : device_(device)
 {
     check(ics_create(device, &ctx_), "ics_create");
 }
 
-BatchEngine::~BatchEngine() { ics_destroy(ctx_); }
+BatchEngine::~BatchEngine()
+{
+    if (scratch_) ics_host_free(ctx_, scratch_);
+    ics_destroy(ctx_);
+}
 
 std::vector<uint16_t> BatchEngine::checksum(std::span<const std::string_view> segs, std::span<const uint32_t> init)
 {
@@ -112,32 +140,55 @@ std::vector<uint8_t> BatchEngine::verify_raw(std::span<const std::string_view> w
     return st;
 }
 
-std::vector<InternetDatagram> BatchEngine::wrap(TCPOverIPv4Adapter& adapter, std::span<const TCPMessage> msgs)
+template <typename Msgs, typename Take>
+std::vector<InternetDatagram> BatchEngine::wrap_impl(const TCPOverIPv4Adapter& adapter, Msgs& msgs, Take take_payload)
 {
-    // tcp_over_ip.cpp:69-88 for every message; both checksums in one device pass
-    std::vector<InternetDatagram> out(msgs.size());
-    std::vector<TCPSegment> segs(msgs.size());
-    Packed p;
-    for (size_t i = 0; i < msgs.size(); ++i) {
-        TCPSegment& seg = segs[i];
-        IPv4Header& h = out[i].header;
-        detail::stamp_outgoing(adapter.config(), msgs[i], h, seg);
-        h.cksum = 0;
-        append_wire(p, h, seg);
+    // tcp_over_ip.cpp:69-88 for every message: each payload is copied ONCE,
+    // to its final offset in a page-locked arena (after 40 bytes of header
+    // room); one device pass sums it and serializes both headers with both
+    // checksums (ics_tcp_wrap_batch_host) — no host-side serialize().
+    const size_t n = msgs.size();
+    std::vector<uint64_t> off(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) off[i + 1] = off[i] + 40 + msgs[i].sender.payload.size();
+    uint8_t* arena = scratch(std::max<uint64_t>(off[n], 1));
+    std::vector<ics_tcp_msg> rec(n);
+    const FdAdapterConfig& cfg = adapter.config();
+    for (size_t i = 0; i < n; ++i) {
+        const std::string& pl = msgs[i].sender.payload;
+        if (!pl.empty()) std::memcpy(arena + off[i] + 40, pl.data(), pl.size());
+        rec[i] = wrap_fields(cfg, msgs[i]);
     }
-    std::vector<uint16_t> ip(msgs.size()), tcp(msgs.size());
-    if (!msgs.empty())
-        check(ics_ipv4_tcp_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, p.n(), ICS_MODE_COMPUTE, ip.data(),
-                                      tcp.data(), nullptr),
-              "ics_ipv4_tcp_batch_host");
-    for (size_t i = 0; i < msgs.size(); ++i) {
-        out[i].header.cksum = ip[i];
-        segs[i].udinfo.cksum = tcp[i];
-        out[i].payload = serialize(segs[i]);
+    if (n) wrap_packed(arena, off.data(), rec.data(), n);
+    std::vector<InternetDatagram> out(n);
+    for (size_t i = 0; i < n; ++i) {
+        IPv4Header& h = out[i].header;  // the defaults wrap_tcp_in_ip keeps (ipv4_header.h)
+        const uint8_t* w = arena + off[i];
+        h.len = static_cast<uint16_t>((w[2] << 8) | w[3]);
+        h.cksum = static_cast<uint16_t>((w[10] << 8) | w[11]);
+        h.src = rec[i].src;
+        h.dst = rec[i].dst;
+        // serialize(seg)'s pieces: the 20-byte TCP header, then the payload
+        // (Serializer::buffer, parser.h) when there is one
+        out[i].payload.emplace_back(reinterpret_cast<const char*>(w) + 20, 20);
+        if (!msgs[i].sender.payload.empty()) out[i].payload.push_back(take_payload(msgs[i]));
     }
     return out;
 }
 
+std::vector<InternetDatagram> BatchEngine::wrap(TCPOverIPv4Adapter& adapter, std::span<const TCPMessage> msgs)
+{
+    return wrap_impl(adapter, msgs, [](const TCPMessage& m) { return m.sender.payload; });
+}
+
+std::vector<InternetDatagram> BatchEngine::wrap(TCPOverIPv4Adapter& adapter, std::vector<TCPMessage>&& msgs)
+{
+    return wrap_impl(adapter, msgs, [](TCPMessage& m) { return std::move(m.sender.payload); });
+}
+
+void BatchEngine::wrap_packed(uint8_t* bytes, const uint64_t* offsets, const ics_tcp_msg* msgs, size_t n)
+{
+    if (n) check(ics_tcp_wrap_batch_host(ctx_, bytes, offsets, 0, 0, n, msgs), "ics_tcp_wrap_batch_host");
+}
 
 std::vector<std::optional<TCPMessage>> BatchEngine::unwrap(TCPOverIPv4Adapter& adapter,
                                                            std::span<const InternetDatagram> dgrams)

@@ -166,6 +166,25 @@ std::vector<std::optional<TCPMessage>> DatagramBatch::unwrap(TCPOverIPv4Adapter&
     return engine_->unwrap_packed(adapter, arena_, off_.data(), size());
 }
 
+bool DatagramBatch::push_tcp(const TCPOverIPv4Adapter& adapter, const TCPMessage& msg)
+{
+    const std::string& pl = msg.sender.payload;
+    if (!room(40 + pl.size())) return false;
+    const uint64_t at = off_.back();
+    if (!pl.empty()) std::memcpy(arena_ + at + 40, pl.data(), pl.size());
+    off_.push_back(at + 40 + pl.size());
+    msgs_.push_back(wrap_fields(adapter.config(), msg));
+    return true;
+}
+
+void DatagramBatch::wrap()
+{
+    if (!engine_) throw std::logic_error("DatagramBatch::wrap needs an engine");
+    if (msgs_.size() != size()) throw std::logic_error("DatagramBatch::wrap: datagrams not added by push_tcp");
+    engine_->wrap_packed(arena_, off_.data(), msgs_.data(), size());
+    msgs_.clear();
+}
+
 void DatagramBatch::patch()
 {
     if (!engine_) throw std::logic_error("DatagramBatch::patch needs an engine");
@@ -364,7 +383,10 @@ DatagramBatch* DatagramTxRing::acquire()
 void DatagramTxRing::submit(DatagramBatch* batch, bool patch)
 {
     try {
-        if (patch && batch->size()) batch->patch();  // the engine stays on the caller's thread
+        if (batch->wrap_pending())
+            batch->wrap();  // the engine stays on the caller's thread
+        else if (patch && batch->size())
+            batch->patch();
     } catch (...) {
         // the arena goes back to the free list, so a failed patch does not
         // leak it (acquire() would otherwise block once every slot was lost)

@@ -83,9 +83,35 @@ int main()
     const auto dgs = eng.wrap(A, msgs);
     std::vector<std::string> wires;
     for (size_t i = 0; i < msgs.size(); ++i) {
-        const auto want = joined(serialize(A.wrap_tcp_in_ip(msgs[i])));
+        const InternetDatagram ref = A.wrap_tcp_in_ip(msgs[i]);
+        const auto want = joined(serialize(ref));
         wires.push_back(joined(serialize(dgs[i])));
         EXPECT(wires.back() == want);
+        EXPECT(dgs[i].payload == ref.payload);  // the same pieces serialize(seg) gives
+        EXPECT(dgs[i].header.len == ref.header.len && dgs[i].header.cksum == ref.header.cksum);
+    }
+    // device-side wrap through the other entry points: consuming the messages
+    // (payloads moved, not copied), and the arena path (push_tcp + wrap, the
+    // transmit ring's), both byte-equal to wrap_tcp_in_ip
+    {
+        std::vector<TCPMessage> moved = msgs;
+        const auto dgs2 = eng.wrap(A, std::move(moved));
+        for (size_t i = 0; i < msgs.size(); ++i) EXPECT(joined(serialize(dgs2[i])) == wires[i]);
+        icsum::DatagramBatch tb(eng, size_t(8) << 20);
+        for (const auto& m : msgs) EXPECT(tb.push_tcp(A, m));
+        EXPECT(tb.wrap_pending());
+        tb.wrap();
+        EXPECT(!tb.wrap_pending());
+        for (size_t i = 0; i < msgs.size(); ++i) EXPECT(tb[i] == wires[i]);
+        icsum::DatagramBatch mixed(eng, size_t(1) << 20);
+        EXPECT(mixed.push_tcp(A, msgs[0]) && mixed.push(wires[1]));
+        bool threw = false;
+        try {
+            mixed.wrap();
+        } catch (const std::logic_error&) {
+            threw = true;
+        }
+        EXPECT(threw);
     }
 
     // compute_checksums(): TCP and IPv4 header batches
@@ -405,7 +431,9 @@ int main()
         for (const auto& [w, n] : left) EXPECT(n == 0);
     }
     // DatagramTxRing: arenas of wires with both checksum fields zeroed are
-    // patched on the GPU at submit() and sent by the ring's writer thread
+    // patched on the GPU at submit(), arenas of messages (push_tcp) are
+    // wrapped there (headers + checksums), and the ring's writer thread sends
+    // them
     // over a SOCK_SEQPACKET socketpair; the peer reads exactly wrap_tcp_in_ip's
     // wires, in order
     {
@@ -429,6 +457,10 @@ int main()
                 for (size_t i = 0; i < wires.size();) {
                     icsum::DatagramBatch* b = tx.acquire();
                     for (; i < wires.size() && b->size() < kPerArena; ++i) {
+                        if (p % 2) {  // odd passes: messages, wrapped on the GPU at submit()
+                            EXPECT(b->push_tcp(A, msgs[i]));
+                            continue;
+                        }
                         std::string z = wires[i];
                         z[10] = z[11] = 0;
                         z[36] = z[37] = 0;

@@ -92,6 +92,14 @@ struct ics_ctx {
   uint32_t* d_init[kMaxSlots] = {};
   uint8_t* h_out[kMaxSlots] = {};   // u16 outputs or 5-byte ipv4 results
   uint8_t* d_out[kMaxSlots] = {};
+  // wrap from host memory (allocated on first use): per slot up to
+  // kWrapSlotSegs messages in, 40 header bytes per datagram back
+  static constexpr size_t kWrapSlotSegs = size_t(1) << 18;
+  bool wrap_staged = false;
+  uint8_t* h_msg[kMaxSlots] = {};
+  uint8_t* d_msg[kMaxSlots] = {};
+  uint8_t* h_hdr[kMaxSlots] = {};
+  uint8_t* d_hdr[kMaxSlots] = {};
 };
 
 namespace {
@@ -208,6 +216,18 @@ int ensure_staging(ics_ctx* ctx) {
   return ICS_OK;
 }
 
+int ensure_wrap_staging(ics_ctx* ctx) {
+  if (ctx->wrap_staged) return ICS_OK;
+  for (int k = 0; k < ctx->nslots; ++k) {
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_msg[k]), ics_ctx::kWrapSlotSegs * sizeof(ics_tcp_msg), 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_msg[k]), ics_ctx::kWrapSlotSegs * sizeof(ics_tcp_msg)));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_hdr[k]), ics_ctx::kWrapSlotSegs * 40, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_hdr[k]), ics_ctx::kWrapSlotSegs * 40));
+  }
+  ctx->wrap_staged = true;
+  return ICS_OK;
+}
+
 void free_staging(ics_ctx* ctx) {
   for (int k = 0; k < ics_ctx::kMaxSlots; ++k) {
     if (ctx->st[k]) (void)hipStreamSynchronize(ctx->st[k]);
@@ -219,10 +239,15 @@ void free_staging(ics_ctx* ctx) {
     if (ctx->d_init[k]) (void)hipFree(ctx->d_init[k]);
     if (ctx->h_out[k]) (void)hipHostFree(ctx->h_out[k]);
     if (ctx->d_out[k]) (void)hipFree(ctx->d_out[k]);
+    if (ctx->h_msg[k]) (void)hipHostFree(ctx->h_msg[k]);
+    if (ctx->d_msg[k]) (void)hipFree(ctx->d_msg[k]);
+    if (ctx->h_hdr[k]) (void)hipHostFree(ctx->h_hdr[k]);
+    if (ctx->d_hdr[k]) (void)hipFree(ctx->d_hdr[k]);
     if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
     if (ctx->st[k]) (void)hipStreamDestroy(ctx->st[k]);
   }
   ctx->staged = false;
+  ctx->wrap_staged = false;
 }
 
 // One staged chunk of segments [i0, i1) covering bytes [b0, b1).  A segment
@@ -238,8 +263,8 @@ struct Chunk {
 // Next chunk starting at segment i0 (whose first `pos` bytes were already
 // staged as pieces) that fits the slot.
 int next_chunk(const ics_ctx* ctx, const uint64_t* offsets, uint64_t stride, uint64_t seg_len, uint64_t n,
-               uint64_t i0, uint64_t pos, bool allow_pieces, Chunk* c) {
-  const uint64_t cap_b = ctx->slot_bytes, cap_n = ics_ctx::kSlotSegs;
+               uint64_t i0, uint64_t pos, bool allow_pieces, uint64_t cap_n, Chunk* c) {
+  const uint64_t cap_b = ctx->slot_bytes;
   const uint64_t s0 = offsets ? offsets[i0] : i0 * stride;
   const uint64_t len0 = offsets ? offsets[i0 + 1] - s0 : seg_len;
   if (pos || len0 > cap_b) {  // segment i0 does not fit a slot: its next piece
@@ -330,15 +355,18 @@ void host_patch_fields(uint8_t* bytes, const uint64_t* offsets, uint64_t stride,
   }
 }
 
-// kind 0: checksum batch (u16 out); kind 1: ipv4_tcp batch (ip u16, tcp u16, status u8).
+// kind 0: checksum batch (u16 out); kind 1: ipv4_tcp batch (ip u16, tcp u16, status u8);
+// kind 2: tcp wrap (40 header bytes per datagram back, written into h_bytes).
 // The slots take turns, one stream each: while the GPU moves and sums chunk
 // k, the host prepares chunk k+1.  Pinned user buffers are DMA'd directly (no
 // host copy); pageable ones are staged through the pinned slots by par_memcpy.
 int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets,
                   uint64_t stride, uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode,
-                  uint16_t* out_a, uint16_t* out_b, uint8_t* out_c) {
+                  uint16_t* out_a, uint16_t* out_b, uint8_t* out_c, const ics_tcp_msg* h_msgs = nullptr) {
   std::lock_guard<std::mutex> lock(ctx->mu);
   if (int rc = ensure_staging(ctx)) return rc;
+  if (kind == 2)
+    if (int rc = ensure_wrap_staging(ctx)) return rc;
   const bool direct = host_pinned(h_bytes);
   Chunk pending[ics_ctx::kMaxSlots];
   bool busy[ics_ctx::kMaxSlots] = {};
@@ -361,6 +389,14 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       }
     } else if (kind == 0) {
       std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
+    } else if (kind == 2) {
+      uint8_t* bytes = static_cast<uint8_t*>(h_bytes);
+      for (uint64_t j = 0; j < m; ++j) {
+        const uint64_t i = c.i0 + j;
+        const uint64_t s0 = h_offsets ? h_offsets[i] : i * stride;
+        const uint64_t len = h_offsets ? h_offsets[i + 1] - s0 : seg_len;
+        if (len >= 40) std::memcpy(bytes + s0, ctx->h_hdr[k] + 40 * j, 40);
+      }
     } else {
       if (out_a) std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
       if (out_b) std::memcpy(out_b + c.i0, ctx->h_out[k] + m * 2, m * 2);
@@ -375,7 +411,9 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   int slot = 0;
   while (i0 < n) {
     Chunk c;
-    if (int rc = next_chunk(ctx, h_offsets, stride, seg_len, n, i0, pos, kind == 0, &c)) return rc;
+    if (int rc = next_chunk(ctx, h_offsets, stride, seg_len, n, i0, pos, kind == 0,
+                            kind == 2 ? ics_ctx::kWrapSlotSegs : ics_ctx::kSlotSegs, &c))
+      return rc;
     if (int rc = retire(slot)) return rc;
     const uint64_t m = c.i1 - c.i0, nb = c.b1 - c.b0;
     uint8_t* src = static_cast<uint8_t*>(h_bytes) + c.b0;
@@ -419,7 +457,14 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
     const icsum::SegSpec sp{ctx->d_in[slot], d_off, stride, seg_len, m, ctx->d_zero};
     const uint64_t avg = h_offsets ? nb / m : seg_len;
     const icsum::Geometry g = geometry_for(ctx, avg);
-    if (kind == 0) {
+    if (kind == 2) {
+      std::memcpy(ctx->h_msg[slot], h_msgs + c.i0, m * sizeof(ics_tcp_msg));
+      ICS_HIP(hipMemcpyAsync(ctx->d_msg[slot], ctx->h_msg[slot], m * sizeof(ics_tcp_msg), hipMemcpyHostToDevice, st));
+      ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(ctx->d_msg[slot]),
+                                     reinterpret_cast<uint32_t*>(ctx->d_hdr[slot]), nullptr, nullptr,
+                                     ipv4_geometry(g), ctx->max_blocks, st));
+      ICS_HIP(hipMemcpyAsync(ctx->h_hdr[slot], ctx->d_hdr[slot], m * 40, hipMemcpyDeviceToHost, st));
+    } else if (kind == 0) {
       const uint32_t* d_init = nullptr;
       if (h_init) {
         std::memcpy(ctx->h_init[slot], h_init + c.i0, m * 4);
@@ -576,6 +621,30 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt,
                                  static_cast<hipStream_t>(stream)));
   return ICS_OK;
+}
+
+int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,
+                       uint64_t dgram_len, uint64_t n, const ics_tcp_msg* d_msgs, uint16_t* d_ip_ck,
+                       uint16_t* d_tcp_ck, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!d_dgrams || !d_msgs) return fail(ICS_ERR_INVALID, "null device buffer");
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
+  // the stack's segments are <= 1000 B of payload (TCPConfig::MAX_PAYLOAD_SIZE): the
+  // 16-lane line grid of MTU-sized datagrams unless a fixed length says otherwise
+  const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1040 : dgram_len));
+  ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), nullptr, d_ip_ck, d_tcp_ck,
+                                 g, ctx->max_blocks, static_cast<hipStream_t>(stream)));
+  return ICS_OK;
+}
+
+int ics_tcp_wrap_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offsets, uint64_t stride,
+                            uint64_t dgram_len, uint64_t n, const ics_tcp_msg* h_msgs) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!h_dgrams || !h_msgs) return fail(ICS_ERR_INVALID, "null host buffer");
+  return host_pipeline(ctx, 2, h_dgrams, h_offsets, stride, dgram_len, nullptr, n, 0, nullptr, nullptr, nullptr,
+                       h_msgs);
 }
 
 int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,

@@ -764,6 +764,85 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
   }
 }
 
+// ------------------------------------------- device-side wrap (f2) -------
+// TCPOverIPv4Adapter::wrap_tcp_in_ip (tcp_over_ip.cpp:69-88) for a batch:
+// datagram i = [40 header bytes][payload], the payload already in place (laid
+// once at its final offset by the caller).  One pass per datagram sums the
+// payload; the lanes of its group then write the serialized IPv4 header
+// (ipv4_header.cpp:62-86: ver 4, hlen 5, tos 0, len, id, DF, ttl, proto 6,
+// checksum, src, dst) and TCP header (tcp_segment.cpp:76-106: ports, seqno,
+// ackno, data offset 5, flags, window, checksum, urgent 0) with both
+// checksums: TCPSegment::compute_checksum seeded with the pseudo sum (len =
+// 40 + payload, uint16 like the reference's field), then
+// IPv4Header::compute_checksum.  hdr_out != nullptr: the 40 bytes go to
+// hdr_out[40 i ..] instead of in place (the host-memory path copies only them
+// back).  Datagrams shorter than 40 bytes are left as they are.
+template <int LPS, int UNROLL, bool NT, int MODE>
+__global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
+                                                     const uint64_t* __restrict__ offsets,
+                                                     uint64_t stride, uint64_t dlen, uint64_t n,
+                                                     const TcpMsg* __restrict__ msgs,
+                                                     uint32_t* __restrict__ hdr_out,
+                                                     uint16_t* __restrict__ ip_ck,
+                                                     uint16_t* __restrict__ tcp_ck, uint32_t remap) {
+  constexpr uint32_t kGroups = kBlock / LPS;
+  const uint32_t lane = threadIdx.x & (LPS - 1);
+  const uint64_t step = uint64_t(gridDim.x) * kGroups;
+  for (uint64_t g0 = uint64_t(block_order(remap)) * kGroups; g0 < n; g0 += step) {
+    const uint64_t seg = g0 + threadIdx.x / LPS;
+    const bool valid = seg < n;
+    const uint64_t idx = valid ? seg : n - 1;  // clamped index: every load unconditional
+    uint64_t s, e;
+    seg_bounds(offsets, stride, dlen, idx, s, e);
+    if (!valid) e = s;
+    const bool ok = e - s >= 40;
+    const TcpMsg m = msgs[idx];  // same address across the group: one request per wave instruction
+    const uint64_t p0 = ok ? s + 40 : e;  // payload [p0, e)
+    uint32_t ev = 0, od = 0;
+    seg_sums<LPS, UNROLL, NT, MODE>(dg, p0, e, lane, ev, od);
+    uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(p0) & 1u));
+    if (LPS > 16) tot = __shfl(tot, int((threadIdx.x & 63u) | (LPS - 1)) & 63, 64);  // to every lane of the group
+    // both checksums (16-bit big-endian words of the serialized headers)
+    const uint32_t len = uint32_t(e - s) & 0xffffu;  // IPv4Header::len is uint16
+    const uint32_t flags_ttl = (uint32_t(m.ttl) << 8) | 6u;
+    const uint32_t addr = (m.src >> 16) + (m.src & 0xffffu) + (m.dst >> 16) + (m.dst & 0xffffu);
+    const uint32_t ipc = fold_value(0x4500u + len + m.id + 0x4000u + flags_ttl + addr);
+    const uint32_t pseudo = addr + 6u + ((len - 20u) & 0xffffu);  // ipv4_header.cpp:103-110
+    const uint32_t thdr = uint32_t(m.sport) + m.dport + (m.seqno >> 16) + (m.seqno & 0xffffu) + (m.ackno >> 16) +
+                          (m.ackno & 0xffffu) + (0x5000u | m.flags) + m.window;
+    const uint32_t tcv = fold_value(pseudo + thdr + tot);
+    if (valid && ok && lane < 10) {
+      auto be16 = [](uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); };
+      uint32_t w;  // dword `lane` of the 40 wire bytes, little-endian
+      switch (lane) {
+        case 0: w = 0x45u | (be16(len) << 16); break;
+        case 1: w = be16(m.id) | (0x40u << 16); break;
+        case 2: w = flags_ttl | (be16(ipc) << 16); break;  // ttl, proto, checksum
+        case 3: w = bswap32(m.src); break;
+        case 4: w = bswap32(m.dst); break;
+        case 5: w = be16(m.sport) | (be16(m.dport) << 16); break;
+        case 6: w = bswap32(m.seqno); break;
+        case 7: w = bswap32(m.ackno); break;
+        case 8: w = 0x50u | (uint32_t(m.flags) << 8) | (be16(m.window) << 16); break;
+        default: w = be16(tcv); break;  // checksum, urgent pointer 0
+      }
+      uint8_t* h = dg + s;
+      if (hdr_out)
+        hdr_out[seg * 10 + lane] = w;
+      else if ((reinterpret_cast<uintptr_t>(h) & 3u) == 0)
+        reinterpret_cast<uint32_t*>(h)[lane] = w;
+      else {
+#pragma unroll
+        for (int b = 0; b < 4; ++b) h[4 * lane + b] = uint8_t(w >> (8 * b));
+      }
+    }
+    if (valid && lane == 0) {
+      if (ip_ck) ip_ck[seg] = ok ? uint16_t(ipc) : uint16_t(0);
+      if (tcp_ck) tcp_ck[seg] = ok ? uint16_t(tcv) : uint16_t(0);
+    }
+  }
+}
+
 // --------------------------------------------------- router batch -------
 __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
                                                        const uint64_t* __restrict__ offsets,
@@ -1063,6 +1142,16 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
   return hipGetLastError();
 }
 
+template <int LPS, int UNROLL, bool NT, int MODE>
+hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
+                         uint16_t* tcp_ck, uint32_t max_blocks, hipStream_t st) {
+  const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
+  hipLaunchKernelGGL((k_tcp_wrap<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
+                     const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, msgs, hdr_out,
+                     ip_ck, tcp_ck, g_xcd_remap);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 // Geometry choice from the (average) segment length, measured on MI355X
@@ -1204,6 +1293,17 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 #define ICS_CASE(L, U, T, A)                                      \
   if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
     return launch_ipv4_t<L, U, T, A>(sp, mode, ip_ck, tcp_ck, status, max_blocks, patch_wt, st);
+  ICS_GEOMETRIES(ICS_CASE)
+#undef ICS_CASE
+  return hipErrorInvalidValue;
+}
+
+hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
+                           uint16_t* tcp_ck, Geometry g, uint32_t max_blocks, hipStream_t st) {
+  if (sp.n == 0) return hipSuccess;
+#define ICS_CASE(L, U, T, A)                                      \
+  if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
+    return launch_wrap_t<L, U, T, A>(sp, msgs, hdr_out, ip_ck, tcp_ck, max_blocks, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;

@@ -89,6 +89,20 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
                            uint8_t* status, Geometry g, uint32_t max_blocks, bool patch_wt, hipStream_t st);
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
 
+// Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg
+// (include/icsum.h), 28 bytes.
+struct TcpMsg {
+  uint32_t src, dst, seqno, ackno;
+  uint16_t sport, dport, window;
+  uint8_t flags, ttl;
+  uint16_t id, reserved;
+};
+static_assert(sizeof(TcpMsg) == 28, "ics_tcp_msg layout");
+// wrap_tcp_in_ip for a batch (k_tcp_wrap): headers + both checksums written in
+// place, or to hdr_out (40 bytes per datagram) when it is not null
+hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
+                           uint16_t* tcp_ck, Geometry g, uint32_t max_blocks, hipStream_t st);
+
 // synthetic workloads (icsum_workload.h)
 hipError_t launch_fill_bytes(uint8_t* d, uint64_t nbytes, uint64_t seed, uint64_t pos0,
                              hipStream_t st);

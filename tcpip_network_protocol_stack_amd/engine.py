@@ -18,6 +18,13 @@ from ._lib import check
 
 MODE_COMPUTE, MODE_VERIFY, MODE_PATCH = _lib.ICS_MODE_COMPUTE, _lib.ICS_MODE_VERIFY, _lib.ICS_MODE_PATCH
 ST_ACCEPT = _lib.ICS_ST_ACCEPT
+TCP_FIN, TCP_SYN, TCP_RST, TCP_ACK = _lib.ICS_TCP_FIN, _lib.ICS_TCP_SYN, _lib.ICS_TCP_RST, _lib.ICS_TCP_ACK
+
+# struct ics_tcp_msg (include/icsum.h) as a numpy record
+TCP_MSG_DTYPE = np.dtype([("src", "<u4"), ("dst", "<u4"), ("seqno", "<u4"), ("ackno", "<u4"),
+                          ("src_port", "<u2"), ("dst_port", "<u2"), ("window", "<u2"), ("flags", "u1"),
+                          ("ttl", "u1"), ("id", "<u2"), ("reserved", "<u2")])
+assert TCP_MSG_DTYPE.itemsize == 28
 
 
 def _ptr(t):
@@ -102,6 +109,24 @@ class Engine:
                                           mode, _ptr(ip_ck), _ptr(tcp_ck), _ptr(status),
                                           _stream(stream, self.device)))
         return ip_ck, tcp_ck, status
+
+    # ---- device-side wrap (wrap_tcp_in_ip, tcp_over_ip.cpp:69-88) ----------
+    def tcp_wrap_batch(self, dgrams, msgs, n=None, offsets=None, stride=0, dgram_len=0, ip_ck=None,
+                       tcp_ck=None, stream=None):
+        """Headers + both checksums of every datagram written in place on the
+        device; `msgs` is a device tensor holding n ics_tcp_msg records."""
+        if n is None:
+            n = offsets.numel() - 1 if offsets is not None else dgrams.numel() // max(stride, 1)
+        check(self.lib.ics_tcp_wrap_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+                                          _ptr(msgs), _ptr(ip_ck), _ptr(tcp_ck), _stream(stream, self.device)))
+        return dgrams
+
+    def tcp_wrap_batch_host(self, dgrams, msgs, n, offsets=None, stride=0, dgram_len=0):
+        """The same on host memory (numpy uint8 datagrams, TCP_MSG_DTYPE records)."""
+        msgs = np.ascontiguousarray(msgs, dtype=TCP_MSG_DTYPE)
+        check(self.lib.ics_tcp_wrap_batch_host(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+                                               msgs.ctypes.data))
+        return dgrams
 
     def router_ttl_batch(self, dgrams, n=None, offsets=None, stride=0, dgram_len=0, status=None,
                          stream=None):

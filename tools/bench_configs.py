@@ -3,7 +3,7 @@
 (PCIe) rate — the numbers DESIGN.md §Measurements quotes.  bench.py stays the
 driver's single headline line (north star); this is the wider table.
 
-    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch] [--iters 20]
+    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch,wrap] [--iters 20]
 
 Batches that fit the 256 MiB Infinity Cache (ipv4 98 MB, tcp64 67 MB) are
 rotated over >= 4 distinct copies (>= 393 / 268 MB) so every launch reads HBM.
@@ -266,6 +266,35 @@ def main():
                 emit("pcie_h2d_copy_256Kix1500_pinned", n * L, statistics.median(ts), 0, entry="torch copy_ (hipMemcpyAsync)",
                      note="reference ceiling for the host-inclusive rows: H2D only")
                 del d
+    if "wrap" in only:  # device-side wrap_tcp_in_ip (headers + both checksums written)
+        from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE
+
+        # the stack's segments: MSS 1000 B payload (TCPConfig::MAX_PAYLOAD_SIZE) -> 1040-byte datagrams
+        n, L, seed, R = 1 << 20, 1040, 0x10710006, 2
+        rng = np.random.default_rng(6)
+        m = np.zeros(n, dtype=TCP_MSG_DTYPE)
+        for f, hi in (("src", 2**32), ("dst", 2**32), ("seqno", 2**32), ("ackno", 2**32), ("src_port", 2**16),
+                      ("dst_port", 2**16), ("window", 2**16)):
+            m[f] = rng.integers(0, hi, n, dtype=np.uint64)
+        m["flags"], m["ttl"] = 0x10, 128
+        dm = torch.from_numpy(m.view(np.uint8).copy()).to(dev)
+        ds = [eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L) for r in range(R)]
+        t = timed(lambda i=0: eng.tcp_wrap_batch(ds[i % R], dm, n=n, stride=L, dgram_len=L), args.iters)
+        emit("wrap_1Mx1040_device", n * L, t, n * 28, entry="ics_tcp_wrap_batch", rotation=R,
+             note="bytes = datagram bytes (payload read once, 40 header bytes written per datagram)")
+        del ds
+        nh = 1 << 18
+        for pinned in (True, False):
+            h = torch.empty(nh * L, dtype=torch.uint8, pin_memory=pinned).numpy()
+            h[:] = 7
+            eng.tcp_wrap_batch_host(h, m[:nh], nh, stride=L, dgram_len=L)
+            ts = []
+            for _ in range(5):
+                t0 = time.perf_counter()
+                eng.tcp_wrap_batch_host(h, m[:nh], nh, stride=L, dgram_len=L)
+                ts.append(time.perf_counter() - t0)
+            emit(f"wrap_host_256Kix1040_{'pinned' if pinned else 'pageable'}", nh * L, statistics.median(ts), nh * 68,
+                 entry="ics_tcp_wrap_batch_host", note="H2D payloads + kernel + D2H of the 40 header bytes")
     eng.close()
 
 
