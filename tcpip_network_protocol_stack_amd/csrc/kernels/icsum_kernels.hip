@@ -804,9 +804,9 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
     if (LPS > 16) tot = __shfl(tot, int((threadIdx.x & 63u) | (LPS - 1)) & 63, 64);  // to every lane of the group
     // both checksums (16-bit big-endian words of the serialized headers)
     const uint32_t len = uint32_t(e - s) & 0xffffu;  // IPv4Header::len is uint16
-    const uint32_t flags_ttl = (uint32_t(m.ttl) << 8) | 6u;
+    const uint32_t ttl_proto = (uint32_t(m.ttl) << 8) | 6u;  // big-endian word 4 of the IPv4 header
     const uint32_t addr = (m.src >> 16) + (m.src & 0xffffu) + (m.dst >> 16) + (m.dst & 0xffffu);
-    const uint32_t ipc = fold_value(0x4500u + len + m.id + 0x4000u + flags_ttl + addr);
+    const uint32_t ipc = fold_value(0x4500u + len + m.id + 0x4000u + ttl_proto + addr);
     const uint32_t pseudo = addr + 6u + ((len - 20u) & 0xffffu);  // ipv4_header.cpp:103-110
     const uint32_t thdr = uint32_t(m.sport) + m.dport + (m.seqno >> 16) + (m.seqno & 0xffffu) + (m.ackno >> 16) +
                           (m.ackno & 0xffffu) + (0x5000u | m.flags) + m.window;
@@ -817,7 +817,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
       switch (lane) {
         case 0: w = 0x45u | (be16(len) << 16); break;
         case 1: w = be16(m.id) | (0x40u << 16); break;
-        case 2: w = flags_ttl | (be16(ipc) << 16); break;  // ttl, proto, checksum
+        case 2: w = uint32_t(m.ttl) | (6u << 8) | (be16(ipc) << 16); break;  // ttl, proto, checksum
         case 3: w = bswap32(m.src); break;
         case 4: w = bswap32(m.dst); break;
         case 5: w = be16(m.sport) | (be16(m.dport) << 16); break;
