@@ -68,7 +68,7 @@ int main(int argc, char** argv)
     for (auto& c : up) c = static_cast<char>(rng());
     for (auto& c : down) c = static_cast<char>(rng());
     std::string got_up, got_down;
-    size_t up_off = 0, down_off = 0, wires = 0, dropped = 0;
+    size_t up_off = 0, down_off = 0, wires = 0, dropped = 0, wrap_mismatch = 0;
 
     for (int round = 0; round < 200000; ++round) {
         // application writes
@@ -95,6 +95,18 @@ int main(int argc, char** argv)
 #ifndef ICSUM_REFERENCE_UTIL
             if (gpu) {
                 for (auto& d : eng->wrap(p.adapter, msgs)) out.push_back(joined(serialize(d)));
+                // every GPU-wrapped datagram must equal the per-object wrap_tcp_in_ip's
+                for (size_t i = 0; i < msgs.size(); ++i) {
+                    const std::string want = joined(serialize(p.adapter.wrap_tcp_in_ip(msgs[i])));
+                    if (out[i] != want && ++wrap_mismatch == 1) {
+                        std::fprintf(stderr, "wrap mismatch (n=%zu, i=%zu, %zu vs %zu bytes)\n", msgs.size(), i,
+                                     out[i].size(), want.size());
+                        for (size_t k = 0; k < 48 && k < out[i].size(); ++k)
+                            std::fprintf(stderr, "%02x%s", static_cast<unsigned char>(out[i][k]), k == 47 ? "\n" : "");
+                        for (size_t k = 0; k < 48 && k < want.size(); ++k)
+                            std::fprintf(stderr, "%02x%s", static_cast<unsigned char>(want[k]), k == 47 ? "\n" : "");
+                    }
+                }
                 return out;
             }
 #endif
@@ -146,7 +158,7 @@ int main(int argc, char** argv)
         if (b.receiver.reader().is_finished() && a.receiver.reader().is_finished()) break;
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-    const bool ok = got_up == up && got_down == down;
+    const bool ok = got_up == up && got_down == down && wrap_mismatch == 0;
 #ifdef ICSUM_REFERENCE_UTIL
     const char* path = "reference util";
 #else

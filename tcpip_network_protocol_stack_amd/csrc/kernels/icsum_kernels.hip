@@ -811,10 +811,14 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
     const uint32_t thdr = uint32_t(m.sport) + m.dport + (m.seqno >> 16) + (m.seqno & 0xffffu) + (m.ackno >> 16) +
                           (m.ackno & 0xffffu) + (0x5000u | m.flags) + m.window;
     const uint32_t tcv = fold_value(pseudo + thdr + tot);
-    if (valid && ok && lane < 10) {
-      auto be16 = [](uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); };
-      uint32_t w;  // dword `lane` of the 40 wire bytes, little-endian
-      switch (lane) {
+    // the 10 header dwords over the group's lanes (groups of 4 or 8 lanes
+    // write two or three each)
+    auto be16 = [](uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); };
+    uint8_t* h = dg + s;
+    const bool aligned = (reinterpret_cast<uintptr_t>(h) & 3u) == 0;
+    for (uint32_t k = lane; valid && ok && k < 10; k += LPS) {
+      uint32_t w;  // dword k of the 40 wire bytes, little-endian
+      switch (k) {
         case 0: w = 0x45u | (be16(len) << 16); break;
         case 1: w = be16(m.id) | (0x40u << 16); break;
         case 2: w = uint32_t(m.ttl) | (6u << 8) | (be16(ipc) << 16); break;  // ttl, proto, checksum
@@ -826,14 +830,13 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
         case 8: w = 0x50u | (uint32_t(m.flags) << 8) | (be16(m.window) << 16); break;
         default: w = be16(tcv); break;  // checksum, urgent pointer 0
       }
-      uint8_t* h = dg + s;
       if (hdr_out)
-        hdr_out[seg * 10 + lane] = w;
-      else if ((reinterpret_cast<uintptr_t>(h) & 3u) == 0)
-        reinterpret_cast<uint32_t*>(h)[lane] = w;
+        hdr_out[seg * 10 + k] = w;
+      else if (aligned)
+        reinterpret_cast<uint32_t*>(h)[k] = w;
       else {
 #pragma unroll
-        for (int b = 0; b < 4; ++b) h[4 * lane + b] = uint8_t(w >> (8 * b));
+        for (int b = 0; b < 4; ++b) h[4 * k + b] = uint8_t(w >> (8 * b));
       }
     }
     if (valid && lane == 0) {
