@@ -70,6 +70,7 @@ struct ics_ctx {
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
   int bin_plan = -1;        // -1: decided on the device per batch; forced (tests): 0 whole, 1 split, 2 whole16, 3 wholeS
   bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
+  bool wrap_split = false;  // ICSUM_WRAP_SPLIT: device wrap as compact headers + an address-ordered scatter launch
   bool bin_debug = false;   // ICSUM_BIN_DEBUG: dump the binning pass's meta words after each binned call (dev)
   std::mutex mu;
   // host path: nslots slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each
@@ -545,6 +546,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
   if (ctx->bin_plan > 3) ctx->bin_plan = -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
+  ctx->wrap_split = env_u32("ICSUM_WRAP_SPLIT", 0) != 0;
   ctx->bin_debug = std::getenv("ICSUM_BIN_DEBUG") != nullptr;
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
@@ -633,8 +635,20 @@ int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   // the stack's segments are <= 1000 B of payload (TCPConfig::MAX_PAYLOAD_SIZE): the
   // 16-lane line grid of MTU-sized datagrams unless a fixed length says otherwise
   const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1040 : dgram_len));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (ctx->wrap_split) {  // measurement variant: headers to a compact array, then one scatter launch
+    void* hdr = nullptr;
+    ICS_HIP(hipMallocAsync(&hdr, n * 40, st));
+    hipError_t e = icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs),
+                                          static_cast<uint32_t*>(hdr), d_ip_ck, d_tcp_ck, g, ctx->max_blocks, st);
+    if (e == hipSuccess) e = icsum::launch_hdr_scatter(sp, static_cast<const uint32_t*>(hdr), st);
+    const hipError_t f = hipFreeAsync(hdr, st);
+    ICS_HIP(e);
+    ICS_HIP(f);
+    return ICS_OK;
+  }
   ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), nullptr, d_ip_ck, d_tcp_ck,
-                                 g, ctx->max_blocks, static_cast<hipStream_t>(stream)));
+                                 g, ctx->max_blocks, st));
   return ICS_OK;
 }
 

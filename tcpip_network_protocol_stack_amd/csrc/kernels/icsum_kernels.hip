@@ -846,6 +846,30 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
   }
 }
 
+// Second half of the split wrap (measurement variant, ICSUM_WRAP_SPLIT=1):
+// copy each datagram's 40 header bytes from the compact array k_tcp_wrap
+// wrote (hdr_out) to the datagram start, datagrams in address order, one lane
+// per header dword.
+__global__ __launch_bounds__(kBlock) void k_hdr_scatter(uint8_t* __restrict__ dg,
+                                                        const uint64_t* __restrict__ offsets,
+                                                        uint64_t stride, uint64_t dlen, uint64_t n,
+                                                        const uint32_t* __restrict__ hdr) {
+  ICS_GRID_STRIDE(t, n * 10) {
+    const uint64_t i = t / 10;
+    const uint32_t k = uint32_t(t - i * 10);
+    uint64_t s, e;
+    seg_bounds(offsets, stride, dlen, i, s, e);
+    if (e - s >= 40) {
+      const uint32_t w = hdr[t];
+      uint8_t* h = dg + s;
+      if ((reinterpret_cast<uintptr_t>(h) & 3u) == 0)
+        reinterpret_cast<uint32_t*>(h)[k] = w;
+      else
+        for (int b = 0; b < 4; ++b) h[4 * k + b] = uint8_t(w >> (8 * b));
+    }
+  }
+}
+
 // --------------------------------------------------- router batch -------
 __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
                                                        const uint64_t* __restrict__ offsets,
@@ -1299,6 +1323,13 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_hdr_scatter(const SegSpec& sp, const uint32_t* hdr, hipStream_t st) {
+  if (sp.n == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_hdr_scatter, dim3(ew_blocks(sp.n * 10)), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes),
+                     sp.offsets, sp.stride, sp.seg_len, sp.n, hdr);
+  return hipGetLastError();
 }
 
 hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,

@@ -102,6 +102,8 @@ static_assert(sizeof(TcpMsg) == 28, "ics_tcp_msg layout");
 // place, or to hdr_out (40 bytes per datagram) when it is not null
 hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
                            uint16_t* tcp_ck, Geometry g, uint32_t max_blocks, hipStream_t st);
+// copy 40-byte headers from a compact array to the datagram starts (split wrap)
+hipError_t launch_hdr_scatter(const SegSpec& sp, const uint32_t* hdr, hipStream_t st);
 
 // synthetic workloads (icsum_workload.h)
 hipError_t launch_fill_bytes(uint8_t* d, uint64_t nbytes, uint64_t seed, uint64_t pos0,
