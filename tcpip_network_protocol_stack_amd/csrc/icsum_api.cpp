@@ -72,6 +72,19 @@ struct ics_ctx {
   bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
   bool wrap_split = false;  // ICSUM_WRAP_SPLIT: device wrap as compact headers + an address-ordered scatter launch
   bool bin_debug = false;   // ICSUM_BIN_DEBUG: dump the binning pass's meta words after each binned call (dev)
+  // plan cache of the AUTO dispatch (ICSUM_PLAN_CACHE, default on): the plan
+  // kernel reports (n << 8) | plan into page-locked host memory; a batch with
+  // the same offsets pointer and n as the last binned one whose plan came back
+  // as "whole batch" skips the binning passes (their 4 dispatches, ~25 us)
+  // and runs as that plan's single launch, re-binned every kPlanRefresh calls
+  static constexpr uint32_t kPlanRefresh = 16;
+  bool plan_cache = true;
+  uint64_t* plan_host = nullptr;      // host view
+  uint64_t* plan_host_dev = nullptr;  // the device's pointer to it
+  std::mutex plan_mu;
+  const uint64_t* plan_key = nullptr;
+  uint64_t plan_key_n = 0;
+  uint32_t plan_hits = 0;
   std::mutex mu;
   // host path: nslots slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each
   // (ICSUM_HOST_SLOT_MB), each with pinned in/out staging, device buffers and a stream
@@ -163,18 +176,43 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
     return ICS_OK;
   }
+  // the whole-batch plan's launch geometry: one lane group per segment of the
+  // batch; above 1 M segments 32-lane groups halve the waves an empty last bin
+  // costs to dispatch
+  icsum::Geometry g_last = icsum::bin_geometry(icsum::kBins - 1);
+  const uint32_t lps = ctx->last_bin_lps ? ctx->last_bin_lps : (sp.n > (uint64_t(1) << 20) ? 32u : 64u);
+  if (lps == 32) g_last = {32, 8, true, 3, 1};
+  const uint32_t last_blocks = ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks;
+  const bool cacheable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_cache && ctx->plan_host;
+  if (cacheable) {
+    bool hit = false;
+    {
+      std::lock_guard<std::mutex> lock(ctx->plan_mu);
+      const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
+      if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && (v >> 8) == sp.n &&
+          (v & 0xffu) == icsum::kPlanWholeBatch && ctx->plan_hits + 1 < ics_ctx::kPlanRefresh) {
+        ++ctx->plan_hits;
+        hit = true;
+      } else {
+        ctx->plan_key = sp.offsets;
+        ctx->plan_key_n = sp.n;
+        ctx->plan_hits = 0;
+      }
+    }
+    if (hit) {  // the plan the device chose for this batch last time: its single launch
+      ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_last, last_blocks, st));
+      return ICS_OK;
+    }
+  }
   void* ws = nullptr;
   const size_t meta_bytes = (icsum::kBinMetaBytesTotal + 255) & ~size_t(255);
   ICS_HIP(hipMallocAsync(&ws, meta_bytes + sp.n * 16 * icsum::kBins, st));
   uint32_t* meta = static_cast<uint32_t*>(ws);
   void* list = static_cast<uint8_t*>(ws) + meta_bytes;
   // the last bin's launch dispatches one lane group per segment of the whole
-  // batch (whatever the plan); above 1 M segments 32-lane groups halve the
-  // waves an empty last bin costs to dispatch
-  icsum::Geometry g_last = icsum::bin_geometry(icsum::kBins - 1);
-  const uint32_t lps = ctx->last_bin_lps ? ctx->last_bin_lps : (sp.n > (uint64_t(1) << 20) ? 32u : 64u);
-  if (lps == 32) g_last = {32, 8, true, 3, 1};
-  hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, ctx->bin_plan, lps, st);
+  // batch (whatever the plan)
+  hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, ctx->bin_plan, lps,
+                                            cacheable ? ctx->plan_host_dev : nullptr, st);
   // bins 0..3: one launch, a capped grid striding over each bin; the last
   // bin: one lane group per segment of the batch (it takes the whole batch
   // under the whole-batch plans)
@@ -183,7 +221,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
                                     ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks, st);
   if (e == hipSuccess)
     e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, icsum::kBins - 1), d_init, d_odd, d_out, out_kind,
-                               g_last, ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks, st);
+                               g_last, last_blocks, st);
   if (e == hipSuccess && ctx->bin_debug) {  // dev: dump the binning pass's meta words
     uint32_t h[icsum::kBinMetaWords];
     if (hipMemcpyAsync(h, meta, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess) {
@@ -547,6 +585,22 @@ int ics_create(int device, ics_ctx** out) {
   if (ctx->bin_plan > 3) ctx->bin_plan = -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
   ctx->wrap_split = env_u32("ICSUM_WRAP_SPLIT", 0) != 0;
+  ctx->plan_cache = env_u32("ICSUM_PLAN_CACHE", 1) != 0;
+  if (ctx->plan_cache) {  // coherent: the plan kernel's store reaches host memory without a flush
+    void* p = nullptr;
+    if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess) {
+      ctx->plan_host = static_cast<uint64_t*>(p);
+      *ctx->plan_host = ~uint64_t(0);
+      void* dp = nullptr;
+      if (hipHostGetDevicePointer(&dp, p, 0) == hipSuccess) {
+        ctx->plan_host_dev = static_cast<uint64_t*>(dp);
+      } else {
+        (void)hipHostFree(p);
+        ctx->plan_host = nullptr;
+      }
+    }
+    (void)hipGetLastError();
+  }
   ctx->bin_debug = std::getenv("ICSUM_BIN_DEBUG") != nullptr;
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
@@ -561,6 +615,7 @@ int ics_destroy(ics_ctx* ctx) {
   if (bind(ctx) == ICS_OK) {
     free_staging(ctx);
     if (ctx->d_zero) (void)hipFree(ctx->d_zero);
+    if (ctx->plan_host) (void)hipHostFree(ctx->plan_host);
   }
   delete ctx;
   return ICS_OK;

@@ -119,7 +119,7 @@ constexpr uint32_t kPlanWhole = 0, kPlanSplit = 1, kPlanWhole16 = 2, kPlanWholeS
 
 __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta, const uint32_t* __restrict__ cnt_part,
                                                      const uint64_t* __restrict__ by_part, uint32_t parts, uint64_t n,
-                                                     int force, uint32_t last_lps) {
+                                                     int force, uint32_t last_lps, uint64_t* __restrict__ plan_out) {
   // totals per bin from the stats pass's per-block partials (parts <= kBlock:
   // one partial per thread, all loads in flight together)
   __shared__ uint32_t wc[kBlock / 64][kBins];
@@ -184,6 +184,9 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       if (t_small < best) plan = kPlanWholeSmall;
     }
     meta[kBinMetaPlan] = plan;
+    // the host's plan cache (icsum_api.cpp): batch size and plan, one 8-byte
+    // store to page-locked host memory
+    if (plan_out) *plan_out = (n << 8) | plan;
   }
 }
 
@@ -1256,7 +1259,7 @@ hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* 
 }
 
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
-                               uint32_t last_lps, hipStream_t st) {
+                               uint32_t last_lps, uint64_t* plan_out, hipStream_t st) {
   if (!offsets || n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   uint32_t* cnt_part = meta + kBinMetaWords;
   uint64_t* by_part = reinterpret_cast<uint64_t*>(cnt_part + kBins * kBinStatBlocks);
@@ -1265,7 +1268,7 @@ hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, 
   hipLaunchKernelGGL(k_bin_stats, dim3(parts), dim3(kBlock), 0, st, offsets, n, cnt_part, by_part);
   if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(kBlock), 0, st, meta, cnt_part, by_part, parts, n, force_plan,
-                     last_lps);
+                     last_lps, plan_out);
   if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL(k_bin_scatter, dim3(uint32_t(tiles < 2048 ? tiles : 2048)), dim3(kBlock), 0, st,
                      offsets, n, meta, static_cast<u32x4*>(list));

@@ -61,8 +61,11 @@ constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks
 // force_plan: -1 the device plan decides, 0 whole batch, 1 split, 2 whole
 // batch in 16-lane groups, 3 whole batch through the small-segment body (tests); last_lps: lanes per segment of the last
 // bin's launch (its wave count enters the plan's cost model)
+// plan_out (nullable, device-visible page-locked host memory): the plan
+// kernel stores (n << 8) | plan there for the host's plan cache
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
-                               uint32_t last_lps, hipStream_t st);
+                               uint32_t last_lps, uint64_t* plan_out, hipStream_t st);
+constexpr uint32_t kPlanWholeBatch = 0;  // k_bin_plan's whole-batch plan
 Geometry bin_geometry(int bin);
 // bins 0..kBins-2 in one launch (sp = bin_spec(whole, list, meta, 0)),
 // blocks_per_bin blocks striding over each bin

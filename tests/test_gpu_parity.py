@@ -234,6 +234,36 @@ def test_set_binning_modes(engine, orc):
         engine.set_binning(-1)
 
 
+def test_auto_plan_cache_repeated_and_changed_mix(engine, orc):
+    """AUTO dispatch with the plan cache: the same long-segment batch (the
+    device plans "whole batch") called repeatedly — the cached calls skip the
+    binning passes and run that plan's single launch — then the SAME offsets
+    buffer rewritten in place with a bimodal mix of the same n (a stale cache
+    entry): every call's output equals the oracle's."""
+    import torch
+
+    rng = np.random.default_rng(0xCAC)
+    n = 70_000
+    lens = rng.integers(2048, 16384, n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    want = orc.checksum_batch(buf, n, offsets=off)
+    dbuf, doff = _t(buf), _t(off)
+    for k in range(40):
+        out = engine.checksum_batch(dbuf, offsets=doff)
+        if k % 7 == 0:
+            torch.cuda.synchronize()
+        assert (_u16(out) == want).all(), k
+    lens2 = np.where(rng.random(n) < 0.5, 40, 1460)
+    off2 = np.zeros(n + 1, dtype=np.uint64)
+    off2[1:] = np.cumsum(lens2)
+    doff.copy_(_t(off2))
+    want2 = orc.checksum_batch(buf, n, offsets=off2)
+    for k in range(20):
+        assert (_u16(engine.checksum_batch(dbuf, offsets=doff)) == want2).all(), k
+
+
 @pytest.mark.parametrize("stride,seg_len", [(1500, 1500), (1501, 1497), (64, 64), (9000, 9000),
                                             (16, 0), (24, 1), (9216, 9000), (7, 7)])
 def test_fixed_stride(engine, orc, stride, seg_len):

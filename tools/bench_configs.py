@@ -74,6 +74,9 @@ def main():
     eng = Engine(0)
     eng_nobin = Engine(0)
     eng_nobin.set_binning(0)  # ICS_BINNING_SINGLE: single-geometry dispatch of offsets batches, for comparison
+    os.environ["ICSUM_PLAN_CACHE"] = "0"
+    eng_nocache = Engine(0)  # AUTO without the plan cache: every call runs the binning passes
+    del os.environ["ICSUM_PLAN_CACHE"]
     dev = torch.device("cuda", 0)
 
     if "ns" in only:  # north star: 1 M x 1500 B, pseudo-header inits
@@ -196,10 +199,11 @@ def main():
         doff = torch.from_numpy(off.view(np.int64)).to(dev)
         init = eng.pseudo_inits(n, seed, offsets=doff)
         out = torch.empty(n, dtype=torch.int16, device=dev)
-        for tag, e in (("", eng), ("_unbinned", eng_nobin)):
+        for tag, e in (("", eng), ("_unbinned", eng_nobin), ("_auto_nocache", eng_nocache)):
             t = timed(lambda i=0: e.checksum_batch(d, offsets=doff, init=init, out=out), args.iters // 2 or 1)
             emit("mixed_1M_64B_64KiB" + tag, int(off[-1]), t, n * 14, entry="ics_checksum_batch(offsets)",
-                 binned=not tag)
+                 dispatch={"": "auto (default, plan cache)", "_unbinned": "single launch",
+                           "_auto_nocache": "auto, binning passes every call"}[tag])
         del d
 
     if "bimodal" in only:  # ACK-sized and MSS-sized TCP segments interleaved, packed offsets
@@ -212,10 +216,11 @@ def main():
         doff = torch.from_numpy(off.view(np.int64)).to(dev)
         init = eng.pseudo_inits(n, seed, offsets=doff)
         out = torch.empty(n, dtype=torch.int16, device=dev)
-        for tag, e in (("", eng), ("_unbinned", eng_nobin)):
+        for tag, e in (("", eng), ("_unbinned", eng_nobin), ("_auto_nocache", eng_nocache)):
             t = timed(lambda i=0: e.checksum_batch(d, offsets=doff, init=init, out=out), args.iters)
             emit("bimodal_2M_40B_1460B" + tag, int(off[-1]), t, n * 14, entry="ics_checksum_batch(offsets)",
-                 binned=not tag)
+                 dispatch={"": "auto (default, plan cache)", "_unbinned": "single launch",
+                           "_auto_nocache": "auto, binning passes every call"}[tag])
         del d
 
     if "jumbo" in only:  # config 5 per-GPU shard (weak scaling unit): 1 M x 9000 B
