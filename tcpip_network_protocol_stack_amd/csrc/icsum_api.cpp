@@ -76,7 +76,9 @@ struct ics_ctx {
   // kernel reports (n << 8) | plan into page-locked host memory; a batch with
   // the same offsets pointer and n as the last binned one whose plan came back
   // as "whole batch" skips the binning passes (their 4 dispatches, ~25 us)
-  // and runs as that plan's single launch, re-binned every kPlanRefresh calls
+  // and runs as that plan's single launch; every kPlanRefresh-th such call
+  // re-plans behind its launch (stats + plan kernels), so a changed mix is
+  // noticed within kPlanRefresh calls
   static constexpr uint32_t kPlanRefresh = 16;
   bool plan_cache = true;
   uint64_t* plan_host = nullptr;      // host view
@@ -185,14 +187,14 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   const uint32_t last_blocks = ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks;
   const bool cacheable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_cache && ctx->plan_host;
   if (cacheable) {
-    bool hit = false;
+    bool hit = false, refresh = false;
     {
       std::lock_guard<std::mutex> lock(ctx->plan_mu);
       const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
       if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && (v >> 8) == sp.n &&
-          (v & 0xffu) == icsum::kPlanWholeBatch && ctx->plan_hits + 1 < ics_ctx::kPlanRefresh) {
-        ++ctx->plan_hits;
+          (v & 0xffu) == icsum::kPlanWholeBatch) {
         hit = true;
+        refresh = ++ctx->plan_hits % ics_ctx::kPlanRefresh == 0;
       } else {
         ctx->plan_key = sp.offsets;
         ctx->plan_key_n = sp.n;
@@ -201,6 +203,18 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     }
     if (hit) {  // the plan the device chose for this batch last time: its single launch
       ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_last, last_blocks, st));
+      if (refresh) {
+        // re-plan behind it (stats + plan kernels only, no lists): a batch
+        // whose mix changed under the same pointer and size is re-binned
+        // from the next call on
+        void* meta = nullptr;
+        ICS_HIP(hipMallocAsync(&meta, (icsum::kBinMetaBytesTotal + 255) & ~size_t(255), st));
+        const hipError_t e = icsum::launch_bin_plan(sp.offsets, sp.n, static_cast<uint32_t*>(meta), lps,
+                                                    ctx->plan_host_dev, st);
+        const hipError_t f = hipFreeAsync(meta, st);
+        ICS_HIP(e);
+        ICS_HIP(f);
+      }
       return ICS_OK;
     }
   }

@@ -1275,6 +1275,20 @@ hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, 
   return hipGetLastError();
 }
 
+hipError_t launch_bin_plan(const uint64_t* offsets, uint64_t n, uint32_t* meta, uint32_t last_lps,
+                           uint64_t* plan_out, hipStream_t st) {
+  if (!offsets || n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
+  uint32_t* cnt_part = meta + kBinMetaWords;
+  uint64_t* by_part = reinterpret_cast<uint64_t*>(cnt_part + kBins * kBinStatBlocks);
+  const uint64_t tiles = (n + kBinTile - 1) / kBinTile;
+  const uint32_t parts = uint32_t(tiles < kBinStatBlocks ? tiles : kBinStatBlocks);
+  hipLaunchKernelGGL(k_bin_stats, dim3(parts), dim3(kBlock), 0, st, offsets, n, cnt_part, by_part);
+  if (hipError_t e = hipGetLastError()) return e;
+  hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(kBlock), 0, st, meta, cnt_part, by_part, parts, n, -1, last_lps,
+                     plan_out);
+  return hipGetLastError();
+}
+
 // geometries k_checksum_bins hard-codes for bins 0..kBins-2
 constexpr Geometry kBinGeometry[kBins - 1] = {{4, 2, true, 2, 2}, {16, 4, true, 3, 1}, {16, 8, true, 3, 1},
                                               {32, 4, true, 3, 1}};

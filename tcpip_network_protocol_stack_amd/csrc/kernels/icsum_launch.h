@@ -66,6 +66,9 @@ constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
                                uint32_t last_lps, uint64_t* plan_out, hipStream_t st);
 constexpr uint32_t kPlanWholeBatch = 0;  // k_bin_plan's whole-batch plan
+// the stats + plan passes alone (no bin lists): a re-plan for the plan cache
+hipError_t launch_bin_plan(const uint64_t* offsets, uint64_t n, uint32_t* meta, uint32_t last_lps,
+                           uint64_t* plan_out, hipStream_t st);
 Geometry bin_geometry(int bin);
 // bins 0..kBins-2 in one launch (sp = bin_spec(whole, list, meta, 0)),
 // blocks_per_bin blocks striding over each bin
