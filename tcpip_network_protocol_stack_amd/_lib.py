@@ -9,6 +9,9 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libicsum.so")
+# the same engine with every device load bounds-checked (slower,
+# synchronises after each call; ICS_ERR_INVALID "bounds check: ..." on a fault)
+DEBUG_LIB_PATH = os.path.join(_HERE, "libicsum_debug.so")
 
 ICS_OK = 0
 ICS_MODE_COMPUTE, ICS_MODE_VERIFY, ICS_MODE_PATCH = 0, 1, 2
@@ -72,31 +75,36 @@ class IcsumError(RuntimeError):
     pass
 
 
-_lib = None
+_libs = {}
+_current = None  # the library check() reads ics_last_error() from
 
 
-def load():
-    """Load libicsum.so (built by __graft_entry__.build()); raise if absent."""
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
+def load(path=None):
+    """Load libicsum.so (or `path`, e.g. DEBUG_LIB_PATH), built by
+    __graft_entry__.build(); raise if absent.  Each path is loaded once."""
+    global _current
+    path = path or LIB_PATH
+    if path in _libs:
+        return _libs[path]
+    if not os.path.exists(path):
         raise IcsumError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
             "(the checksum engine has no CPU fallback)")
     # torch (if imported) already holds the process's libamdhip64.so.7; the
     # engine binds to the same runtime by soname.
-    lib = ctypes.CDLL(LIB_PATH)
+    lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
-    _lib = lib
+    _libs[path] = lib
+    if path == LIB_PATH or _current is None:
+        _current = lib
     return lib
 
 
-def check(rc):
+def check(rc, lib=None):
     if rc != ICS_OK:
-        msg = load().ics_last_error().decode(errors="replace")
+        msg = (lib or _current or load()).ics_last_error().decode(errors="replace")
         raise IcsumError(f"icsum error {rc}: {msg}")
     return rc

@@ -127,6 +127,21 @@ int bind(ics_ctx* ctx) {
   return ICS_OK;
 }
 
+// Bounds-checked build only: wait for the call's kernels and turn a device
+// violation record into ICS_ERR_INVALID (the release build returns rc as is).
+int bounds_verdict(hipStream_t st, int rc) {
+  if (rc != ICS_OK || !icsum::bounds_checked_build()) return rc;
+  uint32_t flags = 0;
+  uint64_t what = 0;
+  ICS_HIP(icsum::bounds_take(st, &flags, &what));
+  if (flags)
+    return fail(ICS_ERR_INVALID,
+                "bounds check: %s%s%s (first: %s 0x%llx)", (flags & 1u) ? "load outside a segment's envelope " : "",
+                (flags & 2u) ? "offsets not monotone " : "", (flags & 4u) ? "header load past a datagram " : "",
+                (flags & 2u) && !(flags & 5u) ? "segment" : "address", (unsigned long long)what);
+  return ICS_OK;
+}
+
 icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
   icsum::Geometry g = icsum::pick_geometry(avg_len);
   if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll, g.nt, g.mode, 1};
@@ -546,14 +561,16 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   }
   for (int k = 0; k < ctx->nslots; ++k)  // oldest first
     if (int rc = retire((slot + k) % ctx->nslots)) return rc;
-  return ICS_OK;
+  return bounds_verdict(ctx->st[0], ICS_OK);
 }
 
 }  // namespace
 
 extern "C" {
 
-const char* ics_version(void) { return "icsum 0.1.0 (gfx950)"; }
+const char* ics_version(void) {
+  return icsum::bounds_checked_build() ? "icsum 0.2.0 (gfx950, bounds-checked debug build)" : "icsum 0.2.0 (gfx950)";
+}
 int ics_abi_version(void) { return ICS_ABI_VERSION; }
 const char* ics_last_error(void) { return g_err.c_str(); }
 
@@ -648,7 +665,8 @@ int ics_checksum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offs
   if (n == 0) return ICS_OK;
   if (!d_bytes || !d_out) return fail(ICS_ERR_INVALID, "null device buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n, ctx->d_zero};
-  return checksum_device(ctx, sp, d_init, nullptr, d_out, 0, static_cast<hipStream_t>(stream));
+  return bounds_verdict(static_cast<hipStream_t>(stream),
+                        checksum_device(ctx, sp, d_init, nullptr, d_out, 0, static_cast<hipStream_t>(stream)));
 }
 
 int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets, uint64_t stride,
@@ -658,7 +676,8 @@ int ics_sum_batch(ics_ctx* ctx, const void* d_bytes, const uint64_t* d_offsets, 
   if (n == 0) return ICS_OK;
   if (!d_bytes || !d_sum) return fail(ICS_ERR_INVALID, "null device buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_bytes), d_offsets, stride, seg_len, n, ctx->d_zero};
-  return checksum_device(ctx, sp, d_init, d_odd, d_sum, 1, static_cast<hipStream_t>(stream));
+  return bounds_verdict(static_cast<hipStream_t>(stream),
+                        checksum_device(ctx, sp, d_init, d_odd, d_sum, 1, static_cast<hipStream_t>(stream)));
 }
 
 int ics_set_binning(ics_ctx* ctx, int mode) {
@@ -691,7 +710,7 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1500 : dgram_len));
   ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt,
                                  static_cast<hipStream_t>(stream)));
-  return ICS_OK;
+  return bounds_verdict(static_cast<hipStream_t>(stream), ICS_OK);
 }
 
 int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,
@@ -718,7 +737,7 @@ int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   }
   ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), nullptr, d_ip_ck, d_tcp_ck,
                                  g, ctx->max_blocks, st));
-  return ICS_OK;
+  return bounds_verdict(st, ICS_OK);
 }
 
 int ics_tcp_wrap_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offsets, uint64_t stride,
@@ -737,7 +756,7 @@ int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets
   if (!d_dgrams || !d_status) return fail(ICS_ERR_INVALID, "null device buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
   ICS_HIP(icsum::launch_router_ttl(sp, d_status, static_cast<hipStream_t>(stream)));
-  return ICS_OK;
+  return bounds_verdict(static_cast<hipStream_t>(stream), ICS_OK);
 }
 
 int ics_checksum_batch_host(ics_ctx* ctx, const void* h_bytes, const uint64_t* h_offsets,

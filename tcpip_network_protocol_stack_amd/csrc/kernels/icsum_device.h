@@ -21,6 +21,35 @@ namespace icsum {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
+// ---- bounds-checked build (libicsum_debug.so, -DICSUM_BOUNDS_CHECK) --------
+// SURVEY §5's device bounds-check variant.  Every 16-byte payload load is
+// checked against its segment's envelope (the aligned blocks that hold the
+// segment's bytes: the documented read set), every
+// offsets pair for e >= s, and every IPv4 header dword against the
+// datagram's last dword.  A violation sets a bit in a device word (vector
+// atomics) with the first offending address; the C-ABI synchronises after
+// each call, reads it and returns ICS_ERR_INVALID.  The release build
+// compiles all of it away.
+#ifdef ICSUM_BOUNDS_CHECK
+struct BoundsState {
+  unsigned int flags;  // ICS_BOUNDS_* bits
+  unsigned int pad;
+  unsigned long long addr;  // first offending address (or segment index for an offsets fault)
+};
+extern __device__ BoundsState g_icsum_bounds;
+constexpr unsigned kBoundsLoad = 1u, kBoundsOffsets = 2u, kBoundsHeader = 4u;
+__device__ __forceinline__ void bounds_fail(unsigned bit, unsigned long long what) {
+  if (atomicOr(&g_icsum_bounds.flags, bit) == 0u) atomicExch(&g_icsum_bounds.addr, what);
+}
+__device__ __forceinline__ void bounds_check16(const void* p, const uint8_t* lo, const uint8_t* hi) {
+  const uint8_t* q = static_cast<const uint8_t*>(p);
+  if (q < lo || q + 16 > hi) bounds_fail(kBoundsLoad, reinterpret_cast<unsigned long long>(p));
+}
+#define ICS_CHECK16(p, lo, hi) ::icsum::bounds_check16((p), (lo), (hi))
+#else
+#define ICS_CHECK16(p, lo, hi) ((void)0)
+#endif
+
 constexpr uint32_t kEvenBytes = 0x00010001u;  // bytes 0 and 2 of a dword
 constexpr uint32_t kOddBytes = 0x01000100u;   // bytes 1 and 3 of a dword
 
@@ -83,6 +112,8 @@ __device__ __forceinline__ void range_sums(const uint8_t* __restrict__ base, uin
   const uint64_t span = e > a0 ? e - a0 : 0;  // bytes from the first chunk start to the end
   const uint32_t nch = uint32_t((span + 15) >> 4);
   const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  [[maybe_unused]] const uint8_t* env_lo = base + a0;
+  [[maybe_unused]] const uint8_t* env_hi = base + ((e + 15) & ~uint64_t(15));
   // boundary chunks 0 and nch-1 are loaded FIRST so that their latency
   // overlaps the interior stream: lane 0 -> chunk 0, lane 1 -> chunk nch-1
   // (when distinct), other lanes re-load chunk 0 and mask it to nothing.
@@ -93,11 +124,14 @@ __device__ __forceinline__ void range_sums(const uint8_t* __restrict__ base, uin
   uint32_t blo = 0, bhi = 0;
   if (LPS == 1) {
     if (nch) {
+      ICS_CHECK16(p, env_lo, env_hi);
+      ICS_CHECK16(p + lastc, env_lo, env_hi);
       bh = load16<NT>(p);
       bt = load16<NT>(p + lastc);
     }
   } else if (nch) {
     const bool is_tail = lane == 1 && nch >= 2;
+    ICS_CHECK16(p + (is_tail ? lastc : 0u), env_lo, env_hi);
     bh = load16<NT>(p + (is_tail ? lastc : 0u));
     blo = is_tail ? 0u : lo0;
     bhi = (is_tail || nch == 1) ? tail : 16u;
@@ -110,6 +144,7 @@ __device__ __forceinline__ void range_sums(const uint8_t* __restrict__ base, uin
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const uint32_t cc = c + uint32_t(u * LPS);
+      ICS_CHECK16(p + (cc <= last_in ? cc : last_in), env_lo, env_hi);
       v[u] = load16<NT>(p + (cc <= last_in ? cc : last_in));
     }
 #pragma unroll
@@ -147,12 +182,15 @@ __device__ __forceinline__ void range_sums_line(const uint8_t* __restrict__ base
   const uint32_t cs = uint32_t(s - a0) >> 4;   // head chunk (0..7)
   const uint32_t lastc = nch ? nch - 1 : 0u;   // tail chunk
   const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  [[maybe_unused]] const uint8_t* env_lo = base + a0;
+  [[maybe_unused]] const uint8_t* env_hi = base + ((e + 15) & ~uint64_t(15));
   u32x4 hd = {0u, 0u, 0u, 0u}, td = {0u, 0u, 0u, 0u};
   for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
     u32x4 v[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const uint32_t cc = c + uint32_t(u * LPS);
+      ICS_CHECK16(p + (cc < lastc ? cc : lastc), env_lo, env_hi);
       v[u] = load16<NT>(p + (cc < lastc ? cc : lastc));
     }
 #pragma unroll
@@ -188,23 +226,30 @@ __device__ __forceinline__ void range_sums_line_primed(const uint8_t* __restrict
   const uint32_t cs = uint32_t(s - a0) >> 4;  // head chunk (0..7)
   const uint32_t lastc = nch ? nch - 1 : 0u;  // tail chunk
   const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  [[maybe_unused]] const uint8_t* env_lo = base + a0;
+  [[maybe_unused]] const uint8_t* env_hi = base + ((e + 15) & ~uint64_t(15));
   const uint32_t tail = nch ? uint32_t(span - (uint64_t(lastc) << 4)) : 0u;
   u32x4 bnd = {0u, 0u, 0u, 0u};
   uint32_t blo = 0, bhi = 0;
   if (nch) {
     const bool is_tail = (LPS == 1 ? false : lane == 1) && lastc != cs;
+    ICS_CHECK16(p + (is_tail ? lastc : cs), env_lo, env_hi);
     bnd = load16<false>(p + (is_tail ? lastc : cs));
     blo = is_tail ? 0u : (uint32_t(s) & 15u);
     bhi = (is_tail || lastc == cs) ? tail : 16u;
     if (LPS > 1 && (lane >= 2 || (lane == 1 && lastc == cs))) bhi = 0u;
   }
   u32x4 bt = {0u, 0u, 0u, 0u};
-  if (LPS == 1 && nch && lastc != cs) bt = load16<false>(p + lastc);
+  if (LPS == 1 && nch && lastc != cs) {
+    ICS_CHECK16(p + lastc, env_lo, env_hi);
+    bt = load16<false>(p + lastc);
+  }
   for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
     u32x4 v[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const uint32_t cc = c + uint32_t(u * LPS);
+      ICS_CHECK16(p + (cc < lastc ? cc : lastc), env_lo, env_hi);
       v[u] = load16<NT>(p + (cc < lastc ? cc : lastc));
     }
 #pragma unroll
@@ -232,11 +277,14 @@ __device__ __forceinline__ void range_sums_masked(const uint8_t* __restrict__ ba
   const uint32_t nch = uint32_t((span + 15) >> 4);
   const uint32_t lo0 = uint32_t(s - a0);
   const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
+  [[maybe_unused]] const uint8_t* env_lo = base + a0;
+  [[maybe_unused]] const uint8_t* env_hi = base + ((e + 15) & ~uint64_t(15));
   for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
     u32x4 v[UNROLL];
 #pragma unroll
     for (int u = 0; u < UNROLL; ++u) {
       const uint32_t cc = c + uint32_t(u * LPS);
+      ICS_CHECK16(p + (cc < nch ? cc : nch - 1), env_lo, env_hi);
       v[u] = load16<NT>(p + (cc < nch ? cc : nch - 1));
     }
 #pragma unroll

@@ -21,6 +21,10 @@
 
 namespace icsum {
 
+#ifdef ICSUM_BOUNDS_CHECK
+__device__ BoundsState g_icsum_bounds;
+#endif
+
 namespace {
 
 constexpr int kBlock = 256;
@@ -31,6 +35,9 @@ __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets,
   if (offsets) {
     s = offsets[i];
     e = offsets[i + 1];
+#ifdef ICSUM_BOUNDS_CHECK
+    if (e < s) bounds_fail(kBoundsOffsets, i);  // offsets must be monotone
+#endif
   } else {
     s = i * stride;
     e = s + seg_len;
@@ -437,6 +444,7 @@ __device__ __forceinline__ void checksum_small_body(const uint8_t* __restrict__ 
         const uint32_t cc = lane + uint32_t(u * LPS);
         // unconditional load from a valid address (empty segment -> zero16)
         const u32x4* q = nch[k] ? p + (cc < nch[k] ? cc : nch[k] - 1) : zero16;
+        if (nch[k]) ICS_CHECK16(q, bytes + a0, bytes + a0 + (uint64_t(nch[k]) << 4));
         v[k][u] = __builtin_nontemporal_load(q);
       }
     }
@@ -457,6 +465,8 @@ __device__ __forceinline__ void checksum_small_body(const uint8_t* __restrict__ 
         for (uint32_t cc = lane + kSlots; cc < nch[k]; cc += LPS) {
           const uint64_t at = uint64_t(cc) << 4;
           const uint32_t hi = span[k] - at >= 16 ? 16u : uint32_t(span[k] - at);
+          ICS_CHECK16(p + cc, reinterpret_cast<const uint8_t*>(p),
+                      reinterpret_cast<const uint8_t*>(p) + (uint64_t(nch[k]) << 4));
           acc_chunk(__builtin_nontemporal_load(p + cc) & byte_range_mask(0u, hi), ev, od);
         }
       }
@@ -510,6 +520,8 @@ __global__ __launch_bounds__(kBlock) void k_checksum_dense(const u32x4* __restri
   for (int k = 0; k < SEGS; ++k) {
     const uint64_t seg = seg0 + uint64_t(k) * kSegsPerWave;
     const uint64_t c = seg * LPS + lane;
+    ICS_CHECK16(chunks + (c < nch ? c : nch - 1), reinterpret_cast<const uint8_t*>(chunks),
+                reinterpret_cast<const uint8_t*>(chunks + nch));
     v[k] = __builtin_nontemporal_load(chunks + (c < nch ? c : nch - 1));
     i0[k] = INIT ? init[seg < n ? seg : n - 1] : 0u;
   }
@@ -595,6 +607,9 @@ __device__ __forceinline__ Hdr load_hdr(const uint8_t* p, const uint32_t* last) 
   const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
   const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
   uint32_t d[6];
+#ifdef ICSUM_BOUNDS_CHECK
+  if (q + 4 > last) bounds_fail(kBoundsHeader, reinterpret_cast<unsigned long long>(q + 4));
+#endif
 #pragma unroll
   for (int k = 0; k < 5; ++k) d[k] = q[k];
   d[5] = *(q + 5 < last ? q + 5 : last);
@@ -644,6 +659,9 @@ __device__ __forceinline__ void load_tcp_fields(const uint8_t* t, const uint32_t
   const uint8_t* p = t + 12;
   const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
   const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
+#ifdef ICSUM_BOUNDS_CHECK
+  if (q + 1 > last) bounds_fail(kBoundsHeader, reinterpret_cast<unsigned long long>(q + 1));
+#endif
   const uint32_t d0 = q[0], d1 = q[1];
   const uint32_t d2 = *(q + 2 < last ? q + 2 : last);
   tf0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
@@ -1317,6 +1335,33 @@ hipError_t launch_checksum_bins(const SegSpec& sp, const uint32_t* init, const u
 }
 
 void set_xcd_remap(uint32_t run_log2) { g_xcd_remap = run_log2 < 31 ? run_log2 : 31; }
+
+bool bounds_checked_build() {
+#ifdef ICSUM_BOUNDS_CHECK
+  return true;
+#else
+  return false;
+#endif
+}
+
+hipError_t bounds_take(hipStream_t st, uint32_t* flags, uint64_t* what) {
+  *flags = 0;
+  *what = 0;
+#ifdef ICSUM_BOUNDS_CHECK
+  BoundsState b{};
+  if (hipError_t e = hipStreamSynchronize(st)) return e;
+  if (hipError_t e = hipMemcpyFromSymbol(&b, HIP_SYMBOL(g_icsum_bounds), sizeof b)) return e;
+  if (b.flags) {
+    const BoundsState z{};
+    if (hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(g_icsum_bounds), &z, sizeof z)) return e;
+  }
+  *flags = b.flags;
+  *what = b.addr;
+#else
+  (void)st;
+#endif
+  return hipSuccess;
+}
 
 Geometry bin_geometry(int bin) {
   // the upper edge of the bin (the last bin: a long segment)

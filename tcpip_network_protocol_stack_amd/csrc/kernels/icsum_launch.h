@@ -111,6 +111,12 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
 // copy 40-byte headers from a compact array to the datagram starts (split wrap)
 hipError_t launch_hdr_scatter(const SegSpec& sp, const uint32_t* hdr, hipStream_t st);
 
+// bounds-checked build (libicsum_debug.so): synchronise `st` and take (read
+// and clear) the device's violation record; flags 0 = clean.  No-op returning
+// flags 0 in the release build.
+bool bounds_checked_build();
+hipError_t bounds_take(hipStream_t st, uint32_t* flags, uint64_t* what);
+
 // synthetic workloads (icsum_workload.h)
 hipError_t launch_fill_bytes(uint8_t* d, uint64_t nbytes, uint64_t seed, uint64_t pos0,
                              hipStream_t st);

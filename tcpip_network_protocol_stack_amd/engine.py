@@ -43,17 +43,21 @@ def _stream(stream, device):
 class Engine:
     """One engine context bound to one GPU (ics_create / ics_destroy)."""
 
-    def __init__(self, device=0):
-        self.lib = _lib.load()
+    def __init__(self, device=0, debug=False):
+        """debug=True: the bounds-checked build (libicsum_debug.so)."""
+        self.lib = _lib.load(_lib.DEBUG_LIB_PATH if debug else None)
         self.device = torch.device("cuda", device) if isinstance(device, int) else torch.device(device)
         ctx = ctypes.c_void_p()
-        check(self.lib.ics_create(self.device.index or 0, ctypes.byref(ctx)))
+        self._check(self.lib.ics_create(self.device.index or 0, ctypes.byref(ctx)))
         self.ctx = ctx
+
+    def _check(self, rc):
+        return check(rc, self.lib)
 
     def set_binning(self, mode):
         """Dispatch of offsets batches: _lib.ICS_BINNING_AUTO / SINGLE / BINNED
         (ics_set_binning)."""
-        check(self.lib.ics_set_binning(self.ctx, int(mode)))
+        self._check(self.lib.ics_set_binning(self.ctx, int(mode)))
 
     def close(self):
         if self.ctx:
@@ -74,7 +78,7 @@ class Engine:
             n = offsets.numel() - 1 if offsets is not None else data.numel() // max(stride, 1)
         if out is None:
             out = torch.empty(n, dtype=torch.int16, device=self.device)
-        check(self.lib.ics_checksum_batch(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len,
+        self._check(self.lib.ics_checksum_batch(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len,
                                           _ptr(init), _ptr(out), n, _stream(stream, self.device)))
         return out
 
@@ -85,7 +89,7 @@ class Engine:
             n = offsets.numel() - 1 if offsets is not None else data.numel() // max(stride, 1)
         if out is None:
             out = torch.empty(n, dtype=torch.int32, device=self.device)
-        check(self.lib.ics_sum_batch(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len, _ptr(init),
+        self._check(self.lib.ics_sum_batch(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len, _ptr(init),
                                      _ptr(odd), _ptr(out), n, _stream(stream, self.device)))
         return out
 
@@ -93,7 +97,7 @@ class Engine:
         n = sums.numel()
         if out is None:
             out = torch.empty(n, dtype=torch.int16, device=self.device)
-        check(self.lib.ics_fold_batch(self.ctx, _ptr(sums), _ptr(out), n, _stream(stream, self.device)))
+        self._check(self.lib.ics_fold_batch(self.ctx, _ptr(sums), _ptr(out), n, _stream(stream, self.device)))
         return out
 
     # ---- fused IPv4 + TCP --------------------------------------------------
@@ -105,7 +109,7 @@ class Engine:
         ip_ck = mk(torch.int16) if ip_ck is None else ip_ck
         tcp_ck = mk(torch.int16) if tcp_ck is None else tcp_ck
         status = mk(torch.uint8) if status is None else status
-        check(self.lib.ics_ipv4_tcp_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+        self._check(self.lib.ics_ipv4_tcp_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
                                           mode, _ptr(ip_ck), _ptr(tcp_ck), _ptr(status),
                                           _stream(stream, self.device)))
         return ip_ck, tcp_ck, status
@@ -117,14 +121,14 @@ class Engine:
         device; `msgs` is a device tensor holding n ics_tcp_msg records."""
         if n is None:
             n = offsets.numel() - 1 if offsets is not None else dgrams.numel() // max(stride, 1)
-        check(self.lib.ics_tcp_wrap_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+        self._check(self.lib.ics_tcp_wrap_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
                                           _ptr(msgs), _ptr(ip_ck), _ptr(tcp_ck), _stream(stream, self.device)))
         return dgrams
 
     def tcp_wrap_batch_host(self, dgrams, msgs, n, offsets=None, stride=0, dgram_len=0):
         """The same on host memory (numpy uint8 datagrams, TCP_MSG_DTYPE records)."""
         msgs = np.ascontiguousarray(msgs, dtype=TCP_MSG_DTYPE)
-        check(self.lib.ics_tcp_wrap_batch_host(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+        self._check(self.lib.ics_tcp_wrap_batch_host(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
                                                msgs.ctypes.data))
         return dgrams
 
@@ -133,14 +137,14 @@ class Engine:
         if n is None:
             n = offsets.numel() - 1 if offsets is not None else dgrams.numel() // max(stride, 1)
         status = torch.empty(n, dtype=torch.uint8, device=self.device) if status is None else status
-        check(self.lib.ics_router_ttl_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+        self._check(self.lib.ics_router_ttl_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
                                             _ptr(status), _stream(stream, self.device)))
         return status
 
     # ---- host-memory (PCIe-inclusive) variants -----------------------------
     def checksum_batch_host(self, data, n, offsets=None, stride=0, seg_len=0, init=None):
         out = np.empty(n, dtype=np.uint16)
-        check(self.lib.ics_checksum_batch_host(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len,
+        self._check(self.lib.ics_checksum_batch_host(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len,
                                                _ptr(init), _ptr(out), n))
         return out
 
@@ -148,24 +152,24 @@ class Engine:
         ip = np.empty(n, dtype=np.uint16)
         tcp = np.empty(n, dtype=np.uint16)
         st = np.empty(n, dtype=np.uint8)
-        check(self.lib.ics_ipv4_tcp_batch_host(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len,
+        self._check(self.lib.ics_ipv4_tcp_batch_host(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len,
                                                n, mode, _ptr(ip), _ptr(tcp), _ptr(st)))
         return ip, tcp, st
 
     # ---- synthetic workloads (include/icsum_workload.h) -------------------
     def fill_bytes(self, t, seed, pos0=0, stream=None):
-        check(self.lib.icsw_fill_bytes(self.ctx, _ptr(t), t.numel() * t.element_size(), seed, pos0,
+        self._check(self.lib.icsw_fill_bytes(self.ctx, _ptr(t), t.numel() * t.element_size(), seed, pos0,
                                        _stream(stream, self.device)))
         return t
 
     def pseudo_inits(self, n, seed, offsets=None, seg_len=0, index0=0, out=None, stream=None):
         out = torch.empty(n, dtype=torch.int32, device=self.device) if out is None else out
-        check(self.lib.icsw_pseudo_inits(self.ctx, _ptr(out), _ptr(offsets), seg_len, n, seed, index0,
+        self._check(self.lib.icsw_pseudo_inits(self.ctx, _ptr(out), _ptr(offsets), seg_len, n, seed, index0,
                                          _stream(stream, self.device)))
         return out
 
     def ipv4_tcp_headers(self, dgrams, n, stride, dgram_len, seed, index0=0, stream=None):
-        check(self.lib.icsw_ipv4_tcp_headers(self.ctx, _ptr(dgrams), stride, dgram_len, n, seed, index0,
+        self._check(self.lib.icsw_ipv4_tcp_headers(self.ctx, _ptr(dgrams), stride, dgram_len, n, seed, index0,
                                              _stream(stream, self.device)))
         return dgrams
 

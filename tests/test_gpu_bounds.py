@@ -1,0 +1,128 @@
+"""GPU: the bounds-checked build (libicsum_debug.so, -DICSUM_BOUNDS_CHECK;
+SURVEY §5's device bounds-check variant).  Every kernel family runs clean
+under it with results identical to the release library's, and a batch that
+breaks the C-ABI contract (non-monotone offsets) is reported as
+ICS_ERR_INVALID "bounds check: ..." instead of being silently read."""
+import numpy as np
+import pytest
+
+from helpers import pack_contiguous, wires
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dbg():
+    import torch
+
+    from tcpip_network_protocol_stack_amd.engine import Engine
+
+    e = Engine(0, debug=True)
+    yield e
+    torch.cuda.synchronize()
+    e.close()
+
+
+def _t(a):
+    import torch
+
+    a = np.ascontiguousarray(a)
+    if a.dtype == np.uint64:
+        a = a.view(np.int64)
+    if a.dtype == np.uint32:
+        a = a.view(np.int32)
+    if a.dtype == np.uint16:
+        a = a.view(np.int16)
+    return torch.from_numpy(a.copy()).cuda()
+
+
+def _u(t, dt):
+    return t.cpu().numpy().view(dt)
+
+
+def test_debug_build_identifies_itself(dbg):
+    assert b"bounds-checked" in dbg.lib.ics_version()
+
+
+@pytest.mark.parametrize("stride,seg_len", [(1500, 1500), (1501, 1497), (64, 64), (7, 7), (9000, 9000), (16, 0)])
+def test_fixed_stride_clean_and_identical(dbg, engine, stride, seg_len):
+    rng = np.random.default_rng(stride + seg_len)
+    n = 3001
+    buf = rng.integers(0, 256, n * stride + 64, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    d, di = _t(buf), _t(init)
+    a = dbg.checksum_batch(d, n=n, stride=stride, seg_len=seg_len, init=di)
+    b = engine.checksum_batch(d, n=n, stride=stride, seg_len=seg_len, init=di)
+    assert (_u(a, np.uint16) == _u(b, np.uint16)).all()
+
+
+def test_offsets_all_dispatches_clean_and_identical(dbg, engine):
+    import torch
+
+    rng = np.random.default_rng(11)
+    for n, hi in ((5000, 70000), (70000, 3000), (100000, 64)):
+        lens = rng.integers(0, hi, n)
+        lens[::13] = 0
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        off += 3
+        buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+        d, do = _t(buf), _t(off)
+        odd = _t(rng.integers(0, 2, n).astype(np.uint8))
+        for mode in (1, 0, -1):
+            dbg.set_binning(mode)
+            a = dbg.checksum_batch(d, offsets=do)
+            s = dbg.sum_batch(d, offsets=do, odd=odd)
+            assert (_u(a, np.uint16) == _u(engine.checksum_batch(d, offsets=do), np.uint16)).all(), (n, mode)
+            assert (_u(s, np.uint32) == _u(engine.sum_batch(d, offsets=do, odd=odd), np.uint32)).all(), (n, mode)
+        dbg.set_binning(-1)
+    torch.cuda.synchronize()
+
+
+def test_ipv4_router_wrap_host_clean_and_identical(dbg, engine):
+    from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE
+
+    cases = wires("tcp_wrap.json")
+    segs = [bytes.fromhex(c["wire"]) for c in cases] + [b"", b"\x45" * 19, b"\x46" * 23]
+    buf, off = pack_contiguous(segs, 1)
+    for mode in (0, 1, 2):
+        d1, d2, do = _t(buf), _t(buf), _t(off)
+        r1 = dbg.ipv4_tcp_batch(d1, mode, offsets=do)
+        r2 = engine.ipv4_tcp_batch(d2, mode, offsets=do)
+        for x, y in zip(r1, r2):
+            assert (x.cpu().numpy() == y.cpu().numpy()).all(), mode
+        assert (d1.cpu().numpy() == d2.cpu().numpy()).all(), mode
+    d1, d2, do = _t(buf), _t(buf), _t(off)
+    assert (dbg.router_ttl_batch(d1, offsets=do).cpu().numpy() ==
+            engine.router_ttl_batch(d2, offsets=do).cpu().numpy()).all()
+    wcases = wires("tcp_wrap.json", {"wrap"})
+    arena, woff = pack_contiguous([b"\0" * 40 + bytes.fromhex(c["wire"][80:]) for c in wcases], 2)
+    m = np.zeros(len(wcases), dtype=TCP_MSG_DTYPE)
+    m["ttl"] = 128
+    d1, d2 = _t(arena), _t(arena)
+    dm = _t(m.view(np.uint8))
+    dbg.tcp_wrap_batch(d1, dm, n=len(wcases), offsets=_t(woff))
+    engine.tcp_wrap_batch(d2, dm, n=len(wcases), offsets=_t(woff))
+    assert (d1.cpu().numpy() == d2.cpu().numpy()).all()
+    h = np.frombuffer(b"".join(bytes.fromhex(c["wire"]) for c in cases), dtype=np.uint8).copy()
+    hoff = np.concatenate([[0], np.cumsum([len(c["wire"]) // 2 for c in cases])]).astype(np.uint64)
+    assert (dbg.checksum_batch_host(h, len(cases), offsets=hoff) ==
+            engine.checksum_batch_host(h, len(cases), offsets=hoff)).all()
+
+
+def test_non_monotone_offsets_are_reported(dbg, engine):
+    from tcpip_network_protocol_stack_amd._lib import IcsumError
+
+    rng = np.random.default_rng(3)
+    buf = rng.integers(0, 256, 100_000, dtype=np.uint8)
+    off = np.array([0, 100, 50, 900, 1000], dtype=np.uint64)  # segment 1 ends before it starts
+    d, do = _t(buf), _t(off)
+    engine.checksum_batch(d, offsets=do)  # release build: an empty segment, no check
+    with pytest.raises(IcsumError, match="bounds check: .*offsets not monotone"):
+        dbg.checksum_batch(d, offsets=do)
+    # the record was cleared: the next good call is clean
+    good = _t(np.array([0, 100, 150, 900, 1000], dtype=np.uint64))
+    assert (_u(dbg.checksum_batch(d, offsets=good), np.uint16) ==
+            _u(engine.checksum_batch(d, offsets=good), np.uint16)).all()
+    with pytest.raises(IcsumError, match="bounds check"):
+        dbg.ipv4_tcp_batch(d, 1, offsets=do)
