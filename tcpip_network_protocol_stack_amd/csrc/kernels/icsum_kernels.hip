@@ -269,6 +269,9 @@ __device__ __forceinline__ void src_decode(const SegSrc& src, const Work& w, uin
     if (src.offsets) {
       s = m.a;
       e = m.b;
+#ifdef ICSUM_BOUNDS_CHECK
+      if (e < s) bounds_fail(kBoundsOffsets, gi);  // offsets must be monotone
+#endif
     } else {
       s = gi * src.stride;
       e = s + src.seg_len;
