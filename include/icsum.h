@@ -185,6 +185,17 @@ int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
                        uint64_t dgram_len, uint64_t n, const ics_tcp_msg* d_msgs, uint16_t* d_ip_ck,
                        uint16_t* d_tcp_ck, void* stream);
 
+/* The same wrap with the headers kept apart — the two pieces an
+ * InternetDatagram holds (util/tools/ipv4_datagram.h:10-34: header, then the
+ * serialized segment) and what a writev/sendmmsg iovec pair sends: segment i
+ * of d_payloads is message i's payload ALONE (no header room); the 40 header
+ * bytes of datagram i go to d_hdrs + 40*i (4-byte aligned), written as one
+ * coalesced array instead of into the payload stream.  Datagram i on the wire
+ * = d_hdrs[40 i .. 40 i + 40) followed by payload i. */
+int ics_tcp_wrap_headers(ics_ctx* ctx, const void* d_payloads, const uint64_t* d_offsets, uint64_t stride,
+                         uint64_t payload_len, uint64_t n, const ics_tcp_msg* d_msgs, void* d_hdrs,
+                         uint16_t* d_ip_ck, uint16_t* d_tcp_ck, void* stream);
+
 /* ---- host-memory variants (PCIe-inclusive path) ------------------------ */
 /* Same semantics as ics_checksum_batch / ics_ipv4_tcp_batch on host
  * buffers; ics_checksum_batch_host takes segments of any length (longer than
@@ -205,6 +216,10 @@ int ics_ipv4_tcp_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offs
  * h_dgrams.  Synchronous. */
 int ics_tcp_wrap_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offsets, uint64_t stride,
                             uint64_t dgram_len, uint64_t n, const ics_tcp_msg* h_msgs);
+/* ics_tcp_wrap_headers on host memory: payloads in, 40 header bytes per
+ * datagram out into h_hdrs.  Synchronous. */
+int ics_tcp_wrap_headers_host(ics_ctx* ctx, const void* h_payloads, const uint64_t* h_offsets, uint64_t stride,
+                              uint64_t payload_len, uint64_t n, const ics_tcp_msg* h_msgs, void* h_hdrs);
 
 /* ---- device memory helpers for FFI callers without an allocator -------- */
 int ics_malloc(ics_ctx* ctx, void** d_ptr, size_t bytes);

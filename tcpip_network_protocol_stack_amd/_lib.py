@@ -54,6 +54,8 @@ SIGNATURES = {
     "ics_router_ttl_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p]),
     "ics_tcp_wrap_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p, _p, _p]),
     "ics_tcp_wrap_batch_host": (_int, [_p, _p, _p, _u64, _u64, _u64, _p]),
+    "ics_tcp_wrap_headers": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p, _p, _p, _p]),
+    "ics_tcp_wrap_headers_host": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p]),
     "ics_checksum_batch_host": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _u64]),
     "ics_ipv4_tcp_batch_host": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p]),
     "ics_malloc": (_int, [_p, ctypes.POINTER(_p), ctypes.c_size_t]),

@@ -457,6 +457,8 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       }
     } else if (kind == 0) {
       std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
+    } else if (kind == 2 && mode == 1) {  // payload-only: headers to the caller's array
+      std::memcpy(reinterpret_cast<uint8_t*>(out_c) + 40 * c.i0, ctx->h_hdr[k], m * 40);
     } else if (kind == 2) {
       uint8_t* bytes = static_cast<uint8_t*>(h_bytes);
       for (uint64_t j = 0; j < m; ++j) {
@@ -529,7 +531,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       std::memcpy(ctx->h_msg[slot], h_msgs + c.i0, m * sizeof(ics_tcp_msg));
       ICS_HIP(hipMemcpyAsync(ctx->d_msg[slot], ctx->h_msg[slot], m * sizeof(ics_tcp_msg), hipMemcpyHostToDevice, st));
       ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(ctx->d_msg[slot]),
-                                     reinterpret_cast<uint32_t*>(ctx->d_hdr[slot]), nullptr, nullptr,
+                                     reinterpret_cast<uint32_t*>(ctx->d_hdr[slot]), nullptr, nullptr, mode == 1,
                                      ipv4_geometry(g), ctx->max_blocks, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_hdr[slot], ctx->d_hdr[slot], m * 40, hipMemcpyDeviceToHost, st));
     } else if (kind == 0) {
@@ -728,7 +730,7 @@ int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
     void* hdr = nullptr;
     ICS_HIP(hipMallocAsync(&hdr, n * 40, st));
     hipError_t e = icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs),
-                                          static_cast<uint32_t*>(hdr), d_ip_ck, d_tcp_ck, g, ctx->max_blocks, st);
+                                          static_cast<uint32_t*>(hdr), d_ip_ck, d_tcp_ck, false, g, ctx->max_blocks, st);
     if (e == hipSuccess) e = icsum::launch_hdr_scatter(sp, static_cast<const uint32_t*>(hdr), st);
     const hipError_t f = hipFreeAsync(hdr, st);
     ICS_HIP(e);
@@ -736,8 +738,32 @@ int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
     return ICS_OK;
   }
   ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), nullptr, d_ip_ck, d_tcp_ck,
-                                 g, ctx->max_blocks, st));
+                                 false, g, ctx->max_blocks, st));
   return bounds_verdict(st, ICS_OK);
+}
+
+int ics_tcp_wrap_headers(ics_ctx* ctx, const void* d_payloads, const uint64_t* d_offsets, uint64_t stride,
+                         uint64_t payload_len, uint64_t n, const ics_tcp_msg* d_msgs, void* d_hdrs,
+                         uint16_t* d_ip_ck, uint16_t* d_tcp_ck, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!d_payloads || !d_msgs || !d_hdrs) return fail(ICS_ERR_INVALID, "null device buffer");
+  if (reinterpret_cast<uintptr_t>(d_hdrs) & 3u) return fail(ICS_ERR_INVALID, "header array not 4-byte aligned");
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_payloads), d_offsets, stride, payload_len, n, ctx->d_zero};
+  const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1000 : payload_len));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), static_cast<uint32_t*>(d_hdrs),
+                                 d_ip_ck, d_tcp_ck, true, g, ctx->max_blocks, st));
+  return bounds_verdict(st, ICS_OK);
+}
+
+int ics_tcp_wrap_headers_host(ics_ctx* ctx, const void* h_payloads, const uint64_t* h_offsets, uint64_t stride,
+                              uint64_t payload_len, uint64_t n, const ics_tcp_msg* h_msgs, void* h_hdrs) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!h_payloads || !h_msgs || !h_hdrs) return fail(ICS_ERR_INVALID, "null host buffer");
+  return host_pipeline(ctx, 2, const_cast<void*>(h_payloads), h_offsets, stride, payload_len, nullptr, n, 1,
+                       nullptr, nullptr, static_cast<uint8_t*>(h_hdrs), h_msgs);
 }
 
 int ics_tcp_wrap_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offsets, uint64_t stride,

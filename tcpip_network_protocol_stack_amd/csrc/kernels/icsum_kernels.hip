@@ -808,7 +808,8 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
                                                      const TcpMsg* __restrict__ msgs,
                                                      uint32_t* __restrict__ hdr_out,
                                                      uint16_t* __restrict__ ip_ck,
-                                                     uint16_t* __restrict__ tcp_ck, uint32_t remap) {
+                                                     uint16_t* __restrict__ tcp_ck, uint32_t remap,
+                                                     int payload_only) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
@@ -819,15 +820,16 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
     uint64_t s, e;
     seg_bounds(offsets, stride, dlen, idx, s, e);
     if (!valid) e = s;
-    const bool ok = e - s >= 40;
+    // payload_only: segment i is the payload alone, its headers go to hdr_out
+    const bool ok = valid && (payload_only || e - s >= 40);
     const TcpMsg m = msgs[idx];  // same address across the group: one request per wave instruction
-    const uint64_t p0 = ok ? s + 40 : e;  // payload [p0, e)
+    const uint64_t p0 = ok ? (payload_only ? s : s + 40) : e;  // payload [p0, e)
     uint32_t ev = 0, od = 0;
     seg_sums<LPS, UNROLL, NT, MODE>(dg, p0, e, lane, ev, od);
     uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(p0) & 1u));
     if (LPS > 16) tot = __shfl(tot, int((threadIdx.x & 63u) | (LPS - 1)) & 63, 64);  // to every lane of the group
     // both checksums (16-bit big-endian words of the serialized headers)
-    const uint32_t len = uint32_t(e - s) & 0xffffu;  // IPv4Header::len is uint16
+    const uint32_t len = uint32_t(e - p0 + 40) & 0xffffu;  // IPv4Header::len is uint16
     const uint32_t ttl_proto = (uint32_t(m.ttl) << 8) | 6u;  // big-endian word 4 of the IPv4 header
     const uint32_t addr = (m.src >> 16) + (m.src & 0xffffu) + (m.dst >> 16) + (m.dst & 0xffffu);
     const uint32_t ipc = fold_value(0x4500u + len + m.id + 0x4000u + ttl_proto + addr);
@@ -840,7 +842,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
     auto be16 = [](uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); };
     uint8_t* h = dg + s;
     const bool aligned = (reinterpret_cast<uintptr_t>(h) & 3u) == 0;
-    for (uint32_t k = lane; valid && ok && k < 10; k += LPS) {
+    for (uint32_t k = lane; ok && k < 10; k += LPS) {
       uint32_t w;  // dword k of the 40 wire bytes, little-endian
       switch (k) {
         case 0: w = 0x45u | (be16(len) << 16); break;
@@ -1195,11 +1197,11 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
 
 template <int LPS, int UNROLL, bool NT, int MODE>
 hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                         uint16_t* tcp_ck, uint32_t max_blocks, hipStream_t st) {
+                         uint16_t* tcp_ck, bool payload_only, uint32_t max_blocks, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
   hipLaunchKernelGGL((k_tcp_wrap<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, msgs, hdr_out,
-                     ip_ck, tcp_ck, g_xcd_remap);
+                     ip_ck, tcp_ck, g_xcd_remap, int(payload_only));
   return hipGetLastError();
 }
 
@@ -1398,11 +1400,12 @@ hipError_t launch_hdr_scatter(const SegSpec& sp, const uint32_t* hdr, hipStream_
 }
 
 hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                           uint16_t* tcp_ck, Geometry g, uint32_t max_blocks, hipStream_t st) {
+                           uint16_t* tcp_ck, bool payload_only, Geometry g, uint32_t max_blocks, hipStream_t st) {
   if (sp.n == 0) return hipSuccess;
+  if (payload_only && !hdr_out) return hipErrorInvalidValue;
 #define ICS_CASE(L, U, T, A)                                      \
   if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
-    return launch_wrap_t<L, U, T, A>(sp, msgs, hdr_out, ip_ck, tcp_ck, max_blocks, st);
+    return launch_wrap_t<L, U, T, A>(sp, msgs, hdr_out, ip_ck, tcp_ck, payload_only, max_blocks, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;

@@ -105,9 +105,10 @@ struct TcpMsg {
 };
 static_assert(sizeof(TcpMsg) == 28, "ics_tcp_msg layout");
 // wrap_tcp_in_ip for a batch (k_tcp_wrap): headers + both checksums written in
-// place, or to hdr_out (40 bytes per datagram) when it is not null
+// place, or to hdr_out (40 bytes per datagram) when it is not null;
+// payload_only: segment i is the payload alone (no header room), hdr_out required
 hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                           uint16_t* tcp_ck, Geometry g, uint32_t max_blocks, hipStream_t st);
+                           uint16_t* tcp_ck, bool payload_only, Geometry g, uint32_t max_blocks, hipStream_t st);
 // copy 40-byte headers from a compact array to the datagram starts (split wrap)
 hipError_t launch_hdr_scatter(const SegSpec& sp, const uint32_t* hdr, hipStream_t st);
 

@@ -125,6 +125,23 @@ class Engine:
                                           _ptr(msgs), _ptr(ip_ck), _ptr(tcp_ck), _stream(stream, self.device)))
         return dgrams
 
+    def tcp_wrap_headers(self, payloads, msgs, hdrs, n=None, offsets=None, stride=0, payload_len=0, ip_ck=None,
+                         tcp_ck=None, stream=None):
+        """Payload-only batch; the 40 header bytes of datagram i go to hdrs[40 i:]."""
+        if n is None:
+            n = offsets.numel() - 1 if offsets is not None else payloads.numel() // max(stride, 1)
+        self._check(self.lib.ics_tcp_wrap_headers(self.ctx, _ptr(payloads), _ptr(offsets), stride, payload_len, n,
+                                                  _ptr(msgs), _ptr(hdrs), _ptr(ip_ck), _ptr(tcp_ck),
+                                                  _stream(stream, self.device)))
+        return hdrs
+
+    def tcp_wrap_headers_host(self, payloads, msgs, n, offsets=None, stride=0, payload_len=0):
+        msgs = np.ascontiguousarray(msgs, dtype=TCP_MSG_DTYPE)
+        hdrs = np.empty(n * 40, dtype=np.uint8)
+        self._check(self.lib.ics_tcp_wrap_headers_host(self.ctx, _ptr(payloads), _ptr(offsets), stride, payload_len,
+                                                       n, msgs.ctypes.data, hdrs.ctypes.data))
+        return hdrs
+
     def tcp_wrap_batch_host(self, dgrams, msgs, n, offsets=None, stride=0, dgram_len=0):
         """The same on host memory (numpy uint8 datagrams, TCP_MSG_DTYPE records)."""
         msgs = np.ascontiguousarray(msgs, dtype=TCP_MSG_DTYPE)

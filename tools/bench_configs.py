@@ -288,6 +288,14 @@ def main():
         emit("wrap_1Mx1040_device", n * L, t, n * 28, entry="ics_tcp_wrap_batch", rotation=R,
              note="bytes = datagram bytes (payload read once, 40 header bytes written per datagram)")
         del ds
+        # headers kept apart (iovec form): payload-only batch, 40-byte headers to one coalesced array
+        P = L - 40
+        ps = [eng.fill_bytes(torch.empty(n * P, dtype=torch.uint8, device=dev), seed, pos0=r * n * P) for r in range(R)]
+        hd = torch.empty(n * 40, dtype=torch.uint8, device=dev)
+        t = timed(lambda i=0: eng.tcp_wrap_headers(ps[i % R], dm, hd, n=n, stride=P, payload_len=P), args.iters)
+        emit("wrap_headers_apart_1Mx1000_device", n * (P + 40), t, n * 28, entry="ics_tcp_wrap_headers",
+             rotation=R, note="bytes = datagram bytes (1000-byte payloads read, 40-byte headers written coalesced)")
+        del ps
         nh = 1 << 18
         for pinned in (True, False):
             h = torch.empty(nh * L, dtype=torch.uint8, pin_memory=pinned).numpy()
