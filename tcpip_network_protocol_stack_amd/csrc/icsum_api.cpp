@@ -75,8 +75,8 @@ struct ics_ctx {
   // plan cache of the AUTO dispatch (ICSUM_PLAN_CACHE, default on): the plan
   // kernel reports (n << 8) | plan into page-locked host memory; a batch with
   // the same offsets pointer and n as the last binned one whose plan came back
-  // as "whole batch" skips the binning passes (their 4 dispatches, ~25 us)
-  // and runs as that plan's single launch; every kPlanRefresh-th such call
+  // as one of the whole-batch plans skips the binning passes (their 4
+  // dispatches, ~25 us) and runs as that plan's single launch; every kPlanRefresh-th such call
   // re-plans behind its launch (stats + plan kernels), so a changed mix is
   // noticed within kPlanRefresh calls
   static constexpr uint32_t kPlanRefresh = 16;
@@ -203,12 +203,15 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   const bool cacheable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_cache && ctx->plan_host;
   if (cacheable) {
     bool hit = false, refresh = false;
+    uint32_t hit_plan = 0;
     {
       std::lock_guard<std::mutex> lock(ctx->plan_mu);
       const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
+      const uint32_t plan = uint32_t(v & 0xffu);
       if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && (v >> 8) == sp.n &&
-          (v & 0xffu) == icsum::kPlanWholeBatch) {
+          (plan == icsum::kPlanWholeBatch || plan == icsum::kPlanWholeBatch16 || plan == icsum::kPlanWholeBatchSmall)) {
         hit = true;
+        hit_plan = plan;
         refresh = ++ctx->plan_hits % ics_ctx::kPlanRefresh == 0;
       } else {
         ctx->plan_key = sp.offsets;
@@ -216,8 +219,15 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
         ctx->plan_hits = 0;
       }
     }
-    if (hit) {  // the plan the device chose for this batch last time: its single launch
-      ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_last, last_blocks, st));
+    if (hit) {
+      // the whole-batch plan the device chose for this batch last time, as
+      // its single launch: the last bin's geometry (whole), 16-lane groups
+      // (whole16) or the small-segment body (wholeS) over every segment
+      const icsum::Geometry g_hit = hit_plan == icsum::kPlanWholeBatch16      ? icsum::Geometry{16, 8, true, 3, 1}
+                                    : hit_plan == icsum::kPlanWholeBatchSmall ? icsum::Geometry{4, 2, true, 2, 2}
+                                                                              : g_last;
+      ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_hit,
+                                     hit_plan == icsum::kPlanWholeBatch ? last_blocks : ctx->max_blocks, st));
       if (refresh) {
         // re-plan behind it (stats + plan kernels only, no lists): a batch
         // whose mix changed under the same pointer and size is re-binned

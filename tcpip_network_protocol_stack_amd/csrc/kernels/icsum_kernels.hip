@@ -123,6 +123,8 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total)
 // 1429 / 1622 / 1682, 2 M bimodal 40+1460 B 525 / 473 / 364, 2 M x 4-6 KiB
 // 1515 / 1589 / 1593, 1 M x 1460 B 520 / 429 / 296, 1 M x 40 B 451 / 168 / 205.
 constexpr uint32_t kPlanWhole = 0, kPlanSplit = 1, kPlanWhole16 = 2, kPlanWholeSmall = 3;
+static_assert(kPlanWhole == kPlanWholeBatch && kPlanWhole16 == kPlanWholeBatch16 &&
+              kPlanWholeSmall == kPlanWholeBatchSmall, "plan ids shared with the host's plan cache");
 
 __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta, const uint32_t* __restrict__ cnt_part,
                                                      const uint64_t* __restrict__ by_part, uint32_t parts, uint64_t n,

@@ -65,7 +65,8 @@ constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks
 // kernel stores (n << 8) | plan there for the host's plan cache
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
                                uint32_t last_lps, uint64_t* plan_out, hipStream_t st);
-constexpr uint32_t kPlanWholeBatch = 0;  // k_bin_plan's whole-batch plan
+// k_bin_plan's whole-batch plans (the split plan is 1)
+constexpr uint32_t kPlanWholeBatch = 0, kPlanWholeBatch16 = 2, kPlanWholeBatchSmall = 3;
 // the stats + plan passes alone (no bin lists): a re-plan for the plan cache
 hipError_t launch_bin_plan(const uint64_t* offsets, uint64_t n, uint32_t* meta, uint32_t last_lps,
                            uint64_t* plan_out, hipStream_t st);

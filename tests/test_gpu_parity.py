@@ -264,6 +264,28 @@ def test_auto_plan_cache_repeated_and_changed_mix(engine, orc):
         assert (_u16(engine.checksum_batch(dbuf, offsets=doff)) == want2).all(), k
 
 
+@pytest.mark.parametrize("mix", ["bimodal", "acks", "mtu", "long"])
+def test_auto_plan_cache_every_whole_plan(engine, orc, mix):
+    """Batches whose device plan is each of the whole-batch plans (whole,
+    whole16, small body) and the split plan, called 40 times back to back:
+    cached calls run the plan's single launch; every output equals the oracle's."""
+    rng = np.random.default_rng(len(mix))
+    n = 300_000
+    lens = {"bimodal": np.where(rng.random(n) < 0.5, 40, 1460) + rng.integers(0, 4, n),
+            "acks": rng.integers(40, 44, n), "mtu": rng.integers(1460, 1464, n),
+            "long": rng.integers(4096, 9000, n)}[mix]
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    off += 5
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = orc.checksum_batch(buf, n, offsets=off, init=init)
+    dbuf, doff, dinit = _t(buf), _t(off), _t(init)
+    outs = [engine.checksum_batch(dbuf, offsets=doff, init=dinit) for _ in range(40)]
+    for k, o in enumerate(outs):
+        assert (_u16(o) == want).all(), k
+
+
 @pytest.mark.parametrize("stride,seg_len", [(1500, 1500), (1501, 1497), (64, 64), (9000, 9000),
                                             (16, 0), (24, 1), (9216, 9000), (7, 7)])
 def test_fixed_stride(engine, orc, stride, seg_len):
