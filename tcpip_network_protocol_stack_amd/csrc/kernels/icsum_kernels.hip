@@ -28,6 +28,12 @@ __device__ BoundsState g_icsum_bounds;
 namespace {
 
 constexpr int kBlock = 256;
+// ICSUM_OCC8 builds (A/B): hold the fused kernels to 8 waves per SIMD (<= 64 VGPRs)
+#ifdef ICSUM_OCC8
+#define ICS_OCC8 __attribute__((amdgpu_waves_per_eu(ICSUM_OCC8, 8)))
+#else
+#define ICS_OCC8
+#endif
 
 __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets, uint64_t stride,
                                            uint64_t seg_len, uint64_t i, uint64_t& s,
@@ -700,7 +706,7 @@ __device__ __forceinline__ uint32_t ipv4_pseudo(const Hdr& h) {
 
 // --------------------------------------------- fused IPv4 + TCP ----------
 template <int LPS, int UNROLL, bool NT, int MODE>
-__global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
+__global__ __launch_bounds__(kBlock) ICS_OCC8 void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
                                                      int mode, uint16_t* __restrict__ ip_ck,
@@ -804,7 +810,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
 // hdr_out[40 i ..] instead of in place (the host-memory path copies only them
 // back).  Datagrams shorter than 40 bytes are left as they are.
 template <int LPS, int UNROLL, bool NT, int MODE>
-__global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
+__global__ __launch_bounds__(kBlock) ICS_OCC8 void k_tcp_wrap(uint8_t* __restrict__ dg,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
                                                      const TcpMsg* __restrict__ msgs,
@@ -1219,14 +1225,25 @@ hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_ou
 // with slots >= chunks + 8 so one step covers a segment (1500 B -> 16 lanes x
 // 8 loads), and 64 x 8 (8 KiB per wave step) looping for long segments.
 // Interior chunks stream non-temporally (read once).
+//
+// Round 2 (tools/sweep_geometry.py, profiles/r2_sweep_mtu.jsonl,
+// r2_sweep_mid.jsonl; 1 M segments, GB/s of the best vs the round-1 pick):
+// slots close above the chunks a line-anchored segment spans win — 1000 B
+// (16,5) 7569 vs (16,8) 6577, 1040 B (16,5) 7526 vs 6394, 1200 B (16,6) 7571
+// vs 7133, 2000 B (16,4) 7477 vs (32,4) 7107, 2500 B (32,8) 7486 vs 7359,
+// 3000 B (32,8) 7416 vs 7294, 4096 B (64,8) 7561 vs 7324; 600/800 B keep
+// (16,4), 1460/1500 B (16,8).
 Geometry pick_geometry(uint64_t avg_len) {
   const uint64_t m = (avg_len + 15) / 16;  // 16-byte chunks of the payload
   if (m <= 5) return {4, 1, true, 2, 2};   // small-segment kernel, 2 segments per group in flight
   if (m <= 9) return {4, 2, true, 2, 2};
   if (m <= 17) return {8, 2, true, 2, 2};
   if (m <= 56) return {16, 4, true, 3, 1};
+  if (m <= 69) return {16, 5, true, 3, 1};
+  if (m <= 82) return {16, 6, true, 3, 1};
   if (m <= 120) return {16, 8, true, 3, 1};
-  if (m <= 256) return {32, 4, true, 3, 1};
+  if (m <= 140) return {16, 4, true, 3, 1};
+  if (m <= 220) return {32, 8, true, 3, 1};
   return {64, 8, true, 3, 1};
 }
 
@@ -1240,7 +1257,8 @@ Geometry pick_geometry(uint64_t avg_len) {
   X(32, 4, true, 1) X(64, 4, true, 1) X(64, 8, true, 1) X(16, 6, false, 1)                 \
   X(1, 4, true, 2) X(1, 8, true, 2) X(2, 4, true, 2) X(4, 1, true, 2) X(4, 2, true, 2)     \
   X(8, 1, true, 2) X(8, 2, true, 2) X(16, 2, true, 2) X(16, 8, false, 1) X(64, 8, false, 1)    \
-  X(16, 8, true, 3) X(32, 4, true, 3) X(64, 8, true, 3) X(16, 4, true, 3) X(32, 8, true, 3)
+  X(16, 8, true, 3) X(32, 4, true, 3) X(64, 8, true, 3) X(16, 4, true, 3) X(32, 8, true, 3)   \
+  X(16, 6, true, 3) X(32, 3, true, 3) X(8, 8, true, 3) X(16, 5, true, 3)
 
 // small-segment kernel instantiations (LPS, UNROLL, SEGS); Geometry::segs > 1
 #define ICS_SMALL_GEOMETRIES(X) \
@@ -1371,9 +1389,9 @@ hipError_t bounds_take(hipStream_t st, uint32_t* flags, uint64_t* what) {
 }
 
 Geometry bin_geometry(int bin) {
-  // the upper edge of the bin (the last bin: a long segment)
-  const uint64_t len = bin < kBins - 1 ? kBinMaxChunks[bin] * 16 : uint64_t(1) << 16;
-  return pick_geometry(len);
+  // bins 0..kBins-2: the geometries k_checksum_bins hard-codes (kBinGeometry,
+  // chosen by the round-1 binning A/B); the last bin: a long segment
+  return bin < kBins - 1 ? kBinGeometry[bin] : pick_geometry(uint64_t(1) << 16);
 }
 
 SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, int bin) {

@@ -21,7 +21,8 @@ GEOMETRIES = [(1, 4, 0), (1, 8, 0), (2, 4, 0), (4, 1, 0), (4, 2, 0), (8, 2, 0), 
               (16, 6, 0), (16, 8, 0), (32, 3, 0), (32, 4, 0), (64, 2, 0), (64, 3, 0), (64, 4, 0),
               (64, 8, 0), (8, 4, 1), (16, 4, 1), (16, 6, 1), (16, 8, 1), (32, 3, 1), (32, 4, 1),
               (64, 4, 1), (64, 8, 1), (1, 4, 2), (1, 8, 2), (2, 4, 2), (4, 1, 2), (4, 2, 2), (8, 1, 2),
-              (8, 2, 2), (16, 2, 2), (16, 8, 3), (32, 4, 3), (64, 8, 3), (16, 4, 3), (32, 8, 3)]
+              (8, 2, 2), (16, 2, 2), (16, 8, 3), (32, 4, 3), (64, 8, 3), (16, 4, 3), (32, 8, 3),
+              (16, 6, 3), (32, 3, 3), (8, 8, 3), (16, 5, 3)]
 # small-segment kernel (k_checksum_small): (LPS, UNROLL, MODE unused, SEGS) — ICS_SMALL_GEOMETRIES
 SMALL_GEOMETRIES = [(4, 1, 0, 2), (4, 1, 0, 4), (4, 1, 0, 8), (4, 2, 0, 2), (4, 2, 0, 4), (8, 1, 0, 4),
                     (8, 2, 0, 2), (8, 2, 0, 4), (16, 2, 0, 2)]

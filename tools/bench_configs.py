@@ -295,6 +295,10 @@ def main():
         t = timed(lambda i=0: eng.tcp_wrap_headers(ps[i % R], dm, hd, n=n, stride=P, payload_len=P), args.iters)
         emit("wrap_headers_apart_1Mx1000_device", n * (P + 40), t, n * 28, entry="ics_tcp_wrap_headers",
              rotation=R, note="bytes = datagram bytes (1000-byte payloads read, 40-byte headers written coalesced)")
+        out = torch.empty(n, dtype=torch.int16, device=dev)
+        t = timed(lambda i=0: eng.checksum_batch(ps[i % R], n=n, stride=P, seg_len=P, out=out), args.iters)
+        emit("plain_1Mx1000_reference_point", n * P, t, n * 2, entry="ics_checksum_batch", rotation=R,
+             note="the same payload batch through the plain checksum kernel (no headers, no records)")
         del ps
         nh = 1 << 18
         for pinned in (True, False):
