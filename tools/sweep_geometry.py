@@ -24,7 +24,8 @@ WL = {"ns": (1 << 20, 1500), "tcp64": (1 << 20, 64), "jumbo": (1 << 20, 9000), "
       "s128": (1 << 20, 128), "s256": (1 << 20, 256), "s576": (1 << 20, 576), "s3000": (1 << 19, 3000),
       "s600": (1 << 20, 600), "s800": (1 << 20, 800), "s1000": (1 << 20, 1000), "s1040": (1 << 20, 1040),
       "s1200": (1 << 20, 1200), "s1460": (1 << 20, 1460), "s2000": (1 << 20, 2000),
-      "s2500": (1 << 19, 2500), "s4096": (1 << 19, 4096), "s6000": (1 << 18, 6000)}
+      "s2500": (1 << 19, 2500), "s4096": (1 << 19, 4096), "s6000": (1 << 18, 6000),
+      "s1400": (1 << 20, 1400), "s1536": (1 << 20, 1536), "s1600": (1 << 20, 1600), "s1800": (1 << 20, 1800)}
 
 
 def make_engine(lps, unroll, nt, line, segs, cap):
