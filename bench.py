@@ -239,7 +239,6 @@ def main():
     if not args.pmc_child and not args.no_pmc and world == 1:
         traffic, traffic_src = pmc_traffic(args)
 
-    import numpy as np
     import torch
 
     from tcpip_network_protocol_stack_amd.engine import Engine
