@@ -65,6 +65,7 @@ def main():
     ap.add_argument("--settle-ms", type=float, default=150.0,
                     help="untimed warm-up per row (0 for counter passes, which serialise every dispatch)")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--wrap-device-only", action="store_true", help="wrap rows: skip the host-memory rows")
     args = ap.parse_args()
     global timed
     _timed = timed
@@ -301,7 +302,7 @@ def main():
              note="the same payload batch through the plain checksum kernel (no headers, no records)")
         del ps
         nh = 1 << 18
-        for pinned in (True, False):
+        for pinned in (() if args.wrap_device_only else (True, False)):
             h = torch.empty(nh * L, dtype=torch.uint8, pin_memory=pinned).numpy()
             h[:] = 7
             eng.tcp_wrap_batch_host(h, m[:nh], nh, stride=L, dgram_len=L)
