@@ -1,0 +1,172 @@
+// router_probe.hip — dev tool: the router TTL batch (k_router_ttl,
+// src/router/router.cpp:43-50) on 1 M x 1500 B datagrams, 6 rotated copies,
+// variants timed interleaved in one process.  The memory-side counters show
+// ~1.9 128-byte read requests per datagram where the header needs ~1.16
+// lines: the six dword loads of one lane per datagram are six wave
+// instructions, each touching 64 different lines.  Variants:
+//   engine  the shipped kernel (one lane per datagram, six dword loads)
+//   c4      four lanes per datagram: lane j loads dwords j (and j+4 for j<2),
+//           the group assembles the header with DPP (two instructions touch
+//           16 lines each)
+//   c2      two lanes per datagram, three dwords each
+//   rd      reads only (one lane per datagram, no store) — the read floor
+// Every variant forwards (ttl--, checksum recomputed) the same datagrams, so
+// the copies start at ttl 255 and each is forwarded at most 120 times.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include router_probe.hip -o router_probe
+#include "../../tcpip_network_protocol_stack_amd/csrc/kernels/icsum_kernels.hip"
+
+#include <stdio.h>
+
+#include <algorithm>
+#include <functional>
+#include <vector>
+
+namespace icsum {
+namespace {
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    hipError_t e_ = (x);                                                        \
+    if (e_ != hipSuccess) {                                                     \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                  \
+    }                                                                           \
+  } while (0)
+
+constexpr uint64_t kN = 1 << 20, kL = 1500;
+constexpr int kCopies = 6;
+
+// ttl := 255 on every datagram, then PATCH recomputes both checksums
+__global__ void k_ttl255(uint8_t* dg, uint64_t n, uint64_t stride) {
+  ICS_GRID_STRIDE(i, n) dg[i * stride + 8] = 255;
+}
+
+// forward the datagram whose (aligned) header dwords are d[0..5]
+__device__ __forceinline__ uint8_t forward(uint8_t* p, const uint32_t* d, uint32_t sh) {
+  Hdr h;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+  const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu, ttl = h.byte(8);
+  if (!(ver == 4 && hlen >= 5 && fold_value(ipv4_header_sum(h)) == h.be16(10) && ttl > 1)) return 0;
+  h.w[2] = (h.w[2] & ~0xffu) | (ttl - 1);
+  const uint32_t c = fold_value(ipv4_header_sum(h));
+  if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0) {
+    const uint32_t w1 = h.w[1] & ~0x00800000u;
+    const uint32_t w2 = (h.w[2] & 0x0000ffffu) | ((c >> 8) << 16) | ((c & 0xffu) << 24);
+    uint32_t* q = reinterpret_cast<uint32_t*>(p + 4);
+    q[0] = w1;
+    q[1] = w2;
+  } else {
+    p[6] = uint8_t(h.byte(6) & 0x7fu);
+    p[8] = uint8_t(ttl - 1);
+    store_be16(p + 10, c);
+  }
+  return 1;
+}
+
+// LPS lanes per datagram; lane j loads dwords j, j+LPS, ... of the 6
+template <int LPS, bool STORE>
+__global__ __launch_bounds__(kBlock) void k_coop(uint8_t* __restrict__ dg, uint64_t stride, uint64_t n,
+                                                 uint8_t* __restrict__ status) {
+  constexpr uint32_t kG = kBlock / LPS;
+  const uint32_t lane = threadIdx.x & (LPS - 1);
+  for (uint64_t i = uint64_t(blockIdx.x) * kG + threadIdx.x / LPS; i - threadIdx.x / LPS < n;
+       i += uint64_t(gridDim.x) * kG) {
+    const bool valid = i < n;
+    const uint64_t s = (valid ? i : n - 1) * stride;
+    uint8_t* p = dg + s;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
+    const uint32_t* last = last_dword(p + stride);
+    uint32_t mine[(6 + LPS - 1) / LPS];
+#pragma unroll
+    for (int k = 0; k < (6 + LPS - 1) / LPS; ++k) {
+      const uint32_t idx = lane + uint32_t(k * LPS);
+      const uint32_t* a = q + (idx < 6 ? idx : 5);
+      mine[k] = *(a < last ? a : last);
+    }
+    uint32_t d[6];
+#pragma unroll
+    for (int w = 0; w < 6; ++w) {  // dword w lives in lane w % LPS, slot w / LPS
+      const int src = int(threadIdx.x & 63u & ~uint32_t(LPS - 1)) + (w % LPS);
+      d[w] = LPS == 1 ? mine[w] : uint32_t(__shfl(int(mine[w / LPS]), src, 64));
+    }
+    if (valid && lane == 0) {
+      if (STORE) {
+        status[i] = forward(p, d, sh);
+      } else {
+        Hdr h;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        status[i] = uint8_t(fold_value(ipv4_header_sum(h)) == h.be16(10));
+      }
+    }
+  }
+}
+
+}  // namespace
+}  // namespace icsum
+
+using namespace icsum;
+
+int main() {
+  std::vector<uint8_t*> d(kCopies);
+  uint8_t *st = nullptr, *zero = nullptr;
+  for (int c = 0; c < kCopies; ++c) {
+    CK(hipMalloc(&d[c], kN * kL + 64));
+    CK(launch_fill_bytes(d[c], kN * kL, 0x10710003, c * kN * kL, nullptr));
+    CK(launch_ipv4_tcp_headers(d[c], kL, kL, kN, 0x10710003, c * kN, nullptr));
+    hipLaunchKernelGGL(k_ttl255, dim3(4096), dim3(256), 0, nullptr, d[c], kN, kL);
+  }
+  CK(hipMalloc(&st, kN));
+  CK(hipMalloc(&zero, 64));
+  CK(hipMemset(zero, 0, 64));
+  for (int c = 0; c < kCopies; ++c) {
+    const SegSpec sp{d[c], nullptr, kL, kL, kN, zero};
+    CK(launch_ipv4_tcp(sp, 2, nullptr, nullptr, nullptr, pick_geometry(kL), 0, false, nullptr));
+  }
+  CK(hipDeviceSynchronize());
+  struct V {
+    const char* name;
+    std::function<void(int)> fn;
+  };
+  std::vector<V> vs;
+  vs.push_back({"engine", [&](int c) {
+                  const SegSpec sp{d[c], nullptr, kL, kL, kN, zero};
+                  CK(launch_router_ttl(sp, st, nullptr));
+                }});
+  vs.push_back({"c1", [&](int c) { hipLaunchKernelGGL((k_coop<1, true>), dim3(4096), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  vs.push_back({"c2", [&](int c) { hipLaunchKernelGGL((k_coop<2, true>), dim3(8192), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  vs.push_back({"c4", [&](int c) { hipLaunchKernelGGL((k_coop<4, true>), dim3(16384), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  vs.push_back({"c8", [&](int c) { hipLaunchKernelGGL((k_coop<8, true>), dim3(32768), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  vs.push_back({"rd1", [&](int c) { hipLaunchKernelGGL((k_coop<1, false>), dim3(4096), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  vs.push_back({"rd4", [&](int c) { hipLaunchKernelGGL((k_coop<4, false>), dim3(16384), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  // settle on reads (no forwarding) for ~150 ms
+  for (int k = 0; k < 400; ++k) hipLaunchKernelGGL((k_coop<4, false>), dim3(16384), dim3(256), 0, nullptr, d[k % kCopies], kL, kN, st);
+  CK(hipDeviceSynchronize());
+  std::vector<std::vector<float>> t(vs.size());
+  for (int r = 0; r < 4; ++r) {
+    for (size_t v = 0; v < vs.size(); ++v) {
+      CK(hipEventRecord(a, nullptr));
+      for (int k = 0; k < 6; ++k) vs[v].fn(k % kCopies);
+      CK(hipEventRecord(b, nullptr));
+      CK(hipEventSynchronize(b));
+      float ms = 0;
+      CK(hipEventElapsedTime(&ms, a, b));
+      t[v].push_back(ms * 1e3f / 6);
+    }
+  }
+  std::vector<uint8_t> h(kN);
+  CK(hipMemcpy(h.data(), st, kN, hipMemcpyDeviceToHost));
+  size_t ok = 0;
+  for (auto x : h) ok += x;
+  for (size_t v = 0; v < vs.size(); ++v) {
+    std::sort(t[v].begin(), t[v].end());
+    printf("{\"variant\": \"%s\", \"med_us\": %.2f, \"min_us\": %.2f}\n", vs[v].name, t[v][t[v].size() / 2], t[v][0]);
+  }
+  printf("{\"last_status_ok\": %zu}\n", ok);
+  return 0;
+}
