@@ -905,42 +905,80 @@ __global__ __launch_bounds__(kBlock) void k_hdr_scatter(uint8_t* __restrict__ dg
 }
 
 // --------------------------------------------------- router batch -------
+// Two lanes per datagram: lane 0 loads header dwords 0, 2, 4 and lane 1
+// dwords 1, 3, 5, so each wave instruction touches 32 header lines with two
+// neighbouring dwords each instead of 64 lines with one (one lane loading all
+// six dwords: six instructions of 64 lines; the memory side then saw ~1.9
+// 128-byte read requests per datagram for ~1.16 lines of header).  Measured
+// (tools/probe/router_probe.hip, profiles/r2_router_probe.jsonl): 1 M x 1500 B
+// 59.8 -> 57.3 us; the read-only floor of the same headers is 35-41 us, the
+// rest is the scattered 8-byte write-back of every forwarded header.
 __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
                                                        const uint64_t* __restrict__ offsets,
                                                        uint64_t stride, uint64_t dlen, uint64_t n,
-                                                       uint8_t* __restrict__ status) {
-  ICS_GRID_STRIDE(i, n) {
-  uint64_t s, e;
-  seg_bounds(offsets, stride, dlen, i, s, e);
-  uint8_t st = 0;
-  if (e - s >= 20) {
-    Hdr h = load_hdr(dg + s, last_dword(dg + e));
-    const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu, ttl = h.byte(8);
-    // NetworkInterface::recv_frame parse (network_interface.cpp:51) then
-    // Router::route: ttl <= 1 dropped, else ttl-- and compute_checksum()
-    if (ver == 4 && hlen >= 5 && fold_value(ipv4_header_sum(h)) == h.be16(10) && ttl > 1) {
-      h.w[2] = (h.w[2] & ~0xffu) | (ttl - 1);
-      const uint32_t c = fold_value(ipv4_header_sum(h));
-      uint8_t* p = dg + s;
-      if ((reinterpret_cast<uintptr_t>(p) & 3u) == 0) {
-        // dword-aligned header (every fixed stride that is a multiple of 4):
-        // wire bytes 4..11 rewritten by ONE 8-byte store instead of three
-        // narrow ones — id and fragment offset as read, the flags byte
-        // re-serialized (reserved bit dropped), ttl - 1, protocol, checksum
-        const uint32_t w1 = h.w[1] & ~0x00800000u;
-        const uint32_t w2 = (h.w[2] & 0x0000ffffu) | ((c >> 8) << 16) | ((c & 0xffu) << 24);
-        uint32_t* q = reinterpret_cast<uint32_t*>(p + 4);  // 4-byte aligned: merged to one dwordx2 store
-        q[0] = w1;
-        q[1] = w2;
-      } else {
-        p[6] = uint8_t(h.byte(6) & 0x7fu);  // re-serialized flags word
-        p[8] = uint8_t(ttl - 1);
-        store_be16(p + 10, c);
-      }
-      st = 1;
+                                                       uint8_t* __restrict__ status,
+                                                       const uint32_t* __restrict__ zpad) {
+  constexpr uint32_t kG = kBlock / 2;
+  const uint32_t lane = threadIdx.x & 1u;
+  const uint64_t step = uint64_t(gridDim.x) * kG;
+  // the loop bound is uniform per block (group base index), so both lanes of
+  // every pair reach the shuffles together
+  for (uint64_t g0 = uint64_t(blockIdx.x) * kG; g0 < n; g0 += step) {
+    const uint64_t i = g0 + threadIdx.x / 2;
+    const bool valid = i < n;
+    uint64_t s, e;
+    seg_bounds(offsets, stride, dlen, valid ? i : n - 1, s, e);
+    const bool hdr = valid && e - s >= 20;
+    uint8_t* p = dg + s;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+    // a datagram too short for a header (or an idle pair) reads the zero pad
+    const uint32_t* q = hdr ? reinterpret_cast<const uint32_t*>(p - sh) : zpad;
+    const uint32_t* last = hdr ? last_dword(dg + e) : zpad + 7;
+    uint32_t mine[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t* a = q + (lane + 2u * k);
+#ifdef ICSUM_BOUNDS_CHECK
+      if (hdr && k < 2 && a > last) bounds_fail(kBoundsHeader, reinterpret_cast<unsigned long long>(a));
+#endif
+      mine[k] = *(a < last ? a : last);
     }
-  }
-  status[i] = st;
+    const int pair = int(threadIdx.x & 63u & ~1u);
+    uint32_t d[6];
+#pragma unroll
+    for (int w = 0; w < 6; ++w) d[w] = uint32_t(__shfl(int(mine[w / 2]), pair + (w & 1), 64));
+    if (valid && lane == 0) {
+      uint8_t st = 0;
+      if (hdr) {
+        Hdr h;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu, ttl = h.byte(8);
+        // NetworkInterface::recv_frame parse (network_interface.cpp:51) then
+        // Router::route: ttl <= 1 dropped, else ttl-- and compute_checksum()
+        if (ver == 4 && hlen >= 5 && fold_value(ipv4_header_sum(h)) == h.be16(10) && ttl > 1) {
+          h.w[2] = (h.w[2] & ~0xffu) | (ttl - 1);
+          const uint32_t c = fold_value(ipv4_header_sum(h));
+          if (sh == 0) {
+            // dword-aligned header (every fixed stride that is a multiple of 4):
+            // wire bytes 4..11 rewritten by ONE 8-byte store instead of three
+            // narrow ones — id and fragment offset as read, the flags byte
+            // re-serialized (reserved bit dropped), ttl - 1, protocol, checksum
+            const uint32_t w1 = h.w[1] & ~0x00800000u;
+            const uint32_t w2 = (h.w[2] & 0x0000ffffu) | ((c >> 8) << 16) | ((c & 0xffu) << 24);
+            uint32_t* o = reinterpret_cast<uint32_t*>(p + 4);  // 4-byte aligned: merged to one dwordx2 store
+            o[0] = w1;
+            o[1] = w2;
+          } else {
+            p[6] = uint8_t(h.byte(6) & 0x7fu);  // re-serialized flags word
+            p[8] = uint8_t(ttl - 1);
+            store_be16(p + 10, c);
+          }
+          st = 1;
+        }
+      }
+      status[i] = st;
+    }
   }
 }
 
@@ -1452,8 +1490,9 @@ hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream
 }
 
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st) {
-  hipLaunchKernelGGL(k_router_ttl, dim3(ew_blocks(sp.n)), dim3(kBlock), 0, st,
-                     const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, status);
+  hipLaunchKernelGGL(k_router_ttl, dim3(ew_blocks(sp.n * 2)), dim3(kBlock), 0, st,
+                     const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, status,
+                     static_cast<const uint32_t*>(sp.zero16));
   return hipGetLastError();
 }
 
