@@ -70,7 +70,13 @@ struct ics_ctx {
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
   int bin_plan = -1;        // -1: decided on the device per batch; forced (tests): 0 whole, 1 split, 2 whole16, 3 wholeS
   bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
-  bool wrap_split = false;  // ICSUM_WRAP_SPLIT: device wrap as compact headers + an address-ordered scatter launch
+  // ICSUM_WRAP_PASSES: 0 = two passes (payload sums, then a header launch)
+  // when the headers go to an array of their own and the batch has at least
+  // kWrapTwoPassMin datagrams, otherwise one pass (headers stored inside the
+  // payload stream) — each the faster there (tools/ab_wrap_twopass.py,
+  // DESIGN.md §6); 1 / 2 = always one / two (A/B)
+  static constexpr uint64_t kWrapTwoPassMin = uint64_t(1) << 18;
+  uint32_t wrap_passes = 0;
   bool bin_debug = false;   // ICSUM_BIN_DEBUG: dump the binning pass's meta words after each binned call (dev)
   // plan cache of the AUTO dispatch (ICSUM_PLAN_CACHE, default on): the plan
   // kernel reports (n << 8) | plan into page-locked host memory; a batch with
@@ -87,6 +93,18 @@ struct ics_ctx {
   const uint64_t* plan_key = nullptr;
   uint64_t plan_key_n = 0;
   uint32_t plan_hits = 0;
+  // Device scratch of the binned dispatch and the two-pass wrap, kept across
+  // calls (hipMallocAsync + hipFreeAsync per call cost ≈5 us between the
+  // kernels).  A Scratch lease holds scratch_mu while the call enqueues its
+  // kernels, then records scratch_ev on its stream; a call on another stream
+  // first makes its stream wait for that event, and growing the buffer waits
+  // for it on the host.
+  std::mutex scratch_mu;
+  void* scratch = nullptr;
+  size_t scratch_cap = 0;
+  hipEvent_t scratch_ev = nullptr;
+  hipStream_t scratch_owner = nullptr;
+  bool scratch_used = false;
   std::mutex mu;
   // host path: nslots slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each
   // (ICSUM_HOST_SLOT_MB), each with pinned in/out staging, device buffers and a stream
@@ -116,6 +134,7 @@ struct ics_ctx {
   uint8_t* d_msg[kMaxSlots] = {};
   uint8_t* h_hdr[kMaxSlots] = {};
   uint8_t* d_hdr[kMaxSlots] = {};
+  uint32_t* d_sums[kMaxSlots] = {};  // the two-pass wrap's payload sums
 };
 
 namespace {
@@ -126,6 +145,51 @@ int bind(ics_ctx* ctx) {
   if (hipGetDevice(&cur) != hipSuccess || cur != ctx->device) ICS_HIP(hipSetDevice(ctx->device));
   return ICS_OK;
 }
+
+bool wrap_two_pass(const ics_ctx* ctx, bool headers_apart, uint64_t n) {
+  return ctx->wrap_passes == 2 || (ctx->wrap_passes == 0 && headers_apart && n >= ics_ctx::kWrapTwoPassMin);
+}
+
+// Scratch for the kernels one call enqueues on `st` (see ics_ctx::scratch).
+class Scratch {
+ public:
+  Scratch(ics_ctx* ctx, size_t bytes, hipStream_t st) : ctx_(ctx), lock_(ctx->scratch_mu), st_(st) {
+    if (ctx->scratch_used && ctx->scratch_owner != st) err_ = hipStreamWaitEvent(st, ctx->scratch_ev, 0);
+    if (err_ == hipSuccess && bytes > ctx->scratch_cap) {
+      if (ctx->scratch) {
+        if (ctx->scratch_used) err_ = hipEventSynchronize(ctx->scratch_ev);
+        if (err_ == hipSuccess) err_ = hipFree(ctx->scratch);
+        ctx->scratch = nullptr;
+        ctx->scratch_cap = 0;
+      }
+      const size_t cap = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
+      if (err_ == hipSuccess) err_ = hipMalloc(&ctx->scratch, cap);
+      if (err_ == hipSuccess) ctx->scratch_cap = cap;
+      else ctx->scratch = nullptr;
+    }
+  }
+  ~Scratch() {
+    if (err_ != hipSuccess) return;
+    if (hipEventRecord(ctx_->scratch_ev, st_) == hipSuccess) {
+      ctx_->scratch_owner = st_;
+      ctx_->scratch_used = true;
+    } else {  // cannot track this call's use: the next one waits for the device
+      (void)hipDeviceSynchronize();
+      ctx_->scratch_used = false;
+    }
+  }
+  Scratch(const Scratch&) = delete;
+  Scratch& operator=(const Scratch&) = delete;
+  hipError_t error() const { return err_; }
+  void* get() const { return ctx_->scratch; }
+
+ private:
+  ics_ctx* ctx_;
+  std::lock_guard<std::mutex> lock_;
+  hipStream_t st_;
+  hipError_t err_ = hipSuccess;
+};
+
 
 // Bounds-checked build only: wait for the call's kernels and turn a device
 // violation record into ICS_ERR_INVALID (the release build returns rc as is).
@@ -232,22 +296,19 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
         // re-plan behind it (stats + plan kernels only, no lists): a batch
         // whose mix changed under the same pointer and size is re-binned
         // from the next call on
-        void* meta = nullptr;
-        ICS_HIP(hipMallocAsync(&meta, (icsum::kBinMetaBytesTotal + 255) & ~size_t(255), st));
-        const hipError_t e = icsum::launch_bin_plan(sp.offsets, sp.n, static_cast<uint32_t*>(meta), lps,
-                                                    ctx->plan_host_dev, st);
-        const hipError_t f = hipFreeAsync(meta, st);
-        ICS_HIP(e);
-        ICS_HIP(f);
+        Scratch meta(ctx, (icsum::kBinMetaBytesTotal + 255) & ~size_t(255), st);
+        ICS_HIP(meta.error());
+        ICS_HIP(icsum::launch_bin_plan(sp.offsets, sp.n, static_cast<uint32_t*>(meta.get()), lps,
+                                       ctx->plan_host_dev, st));
       }
       return ICS_OK;
     }
   }
-  void* ws = nullptr;
   const size_t meta_bytes = (icsum::kBinMetaBytesTotal + 255) & ~size_t(255);
-  ICS_HIP(hipMallocAsync(&ws, meta_bytes + sp.n * 16 * icsum::kBins, st));
-  uint32_t* meta = static_cast<uint32_t*>(ws);
-  void* list = static_cast<uint8_t*>(ws) + meta_bytes;
+  Scratch ws(ctx, meta_bytes + sp.n * 16 * icsum::kBins, st);
+  ICS_HIP(ws.error());
+  uint32_t* meta = static_cast<uint32_t*>(ws.get());
+  void* list = static_cast<uint8_t*>(ws.get()) + meta_bytes;
   // the last bin's launch dispatches one lane group per segment of the whole
   // batch (whatever the plan)
   hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, ctx->bin_plan, lps,
@@ -269,9 +330,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
       std::fprintf(stderr, "\n");
     }
   }
-  const hipError_t f = hipFreeAsync(ws, st);
   ICS_HIP(e);
-  ICS_HIP(f);
   return ICS_OK;
 }
 
@@ -301,6 +360,7 @@ int ensure_wrap_staging(ics_ctx* ctx) {
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_msg[k]), ics_ctx::kWrapSlotSegs * sizeof(ics_tcp_msg)));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_hdr[k]), ics_ctx::kWrapSlotSegs * 40, 0));
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_hdr[k]), ics_ctx::kWrapSlotSegs * 40));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_sums[k]), ics_ctx::kWrapSlotSegs * 4));
   }
   ctx->wrap_staged = true;
   return ICS_OK;
@@ -321,6 +381,7 @@ void free_staging(ics_ctx* ctx) {
     if (ctx->d_msg[k]) (void)hipFree(ctx->d_msg[k]);
     if (ctx->h_hdr[k]) (void)hipHostFree(ctx->h_hdr[k]);
     if (ctx->d_hdr[k]) (void)hipFree(ctx->d_hdr[k]);
+    if (ctx->d_sums[k]) (void)hipFree(ctx->d_sums[k]);
     if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
     if (ctx->st[k]) (void)hipStreamDestroy(ctx->st[k]);
   }
@@ -542,7 +603,8 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       ICS_HIP(hipMemcpyAsync(ctx->d_msg[slot], ctx->h_msg[slot], m * sizeof(ics_tcp_msg), hipMemcpyHostToDevice, st));
       ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(ctx->d_msg[slot]),
                                      reinterpret_cast<uint32_t*>(ctx->d_hdr[slot]), nullptr, nullptr, mode == 1,
-                                     ipv4_geometry(g), ctx->max_blocks, st));
+                                     wrap_two_pass(ctx, true, m) ? ctx->d_sums[slot] : nullptr, ipv4_geometry(g),
+                                     ctx->max_blocks, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_hdr[slot], ctx->d_hdr[slot], m * 40, hipMemcpyDeviceToHost, st));
     } else if (kind == 0) {
       const uint32_t* d_init = nullptr;
@@ -627,7 +689,12 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
   if (ctx->bin_plan > 3) ctx->bin_plan = -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
-  ctx->wrap_split = env_u32("ICSUM_WRAP_SPLIT", 0) != 0;
+  ctx->wrap_passes = env_u32("ICSUM_WRAP_PASSES", 0);
+  if (hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess) {
+    (void)hipFree(ctx->d_zero);
+    delete ctx;
+    return fail(ICS_ERR_HIP, "event creation failed");
+  }
   ctx->plan_cache = env_u32("ICSUM_PLAN_CACHE", 1) != 0;
   if (ctx->plan_cache) {  // coherent: the plan kernel's store reaches host memory without a flush
     void* p = nullptr;
@@ -659,6 +726,11 @@ int ics_destroy(ics_ctx* ctx) {
     free_staging(ctx);
     if (ctx->d_zero) (void)hipFree(ctx->d_zero);
     if (ctx->plan_host) (void)hipHostFree(ctx->plan_host);
+    if (ctx->scratch) {
+      if (ctx->scratch_used) (void)hipEventSynchronize(ctx->scratch_ev);
+      (void)hipFree(ctx->scratch);
+    }
+    if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
   }
   delete ctx;
   return ICS_OK;
@@ -725,30 +797,34 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   return bounds_verdict(static_cast<hipStream_t>(stream), ICS_OK);
 }
 
+namespace {
+// The device wrap: two passes (payload sums into n words of scratch, then the
+// header launch) or one (ics_ctx::wrap_passes)
+hipError_t device_wrap(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* msgs, uint32_t* hdr_out,
+                       uint16_t* ip_ck, uint16_t* tcp_ck, bool payload_only, icsum::Geometry g, hipStream_t st) {
+  const icsum::TcpMsg* m = reinterpret_cast<const icsum::TcpMsg*>(msgs);
+  if (!wrap_two_pass(ctx, hdr_out != nullptr, sp.n))
+    return icsum::launch_tcp_wrap(sp, m, hdr_out, ip_ck, tcp_ck, payload_only, nullptr, g, ctx->max_blocks, st);
+  Scratch sums(ctx, sp.n * 4, st);
+  if (sums.error() != hipSuccess) return sums.error();
+  return icsum::launch_tcp_wrap(sp, m, hdr_out, ip_ck, tcp_ck, payload_only, static_cast<uint32_t*>(sums.get()), g,
+                                ctx->max_blocks, st);
+}
+}  // namespace
+
 int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,
                        uint64_t dgram_len, uint64_t n, const ics_tcp_msg* d_msgs, uint16_t* d_ip_ck,
                        uint16_t* d_tcp_ck, void* stream) {
   if (int rc = bind(ctx)) return rc;
   if (n == 0) return ICS_OK;
   if (!d_dgrams || !d_msgs) return fail(ICS_ERR_INVALID, "null device buffer");
+  if (reinterpret_cast<uintptr_t>(d_msgs) & 3u) return fail(ICS_ERR_INVALID, "message records not 4-byte aligned");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
   // the stack's segments are <= 1000 B of payload (TCPConfig::MAX_PAYLOAD_SIZE): the
   // 16-lane line grid of MTU-sized datagrams unless a fixed length says otherwise
   const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1040 : dgram_len));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  if (ctx->wrap_split) {  // measurement variant: headers to a compact array, then one scatter launch
-    void* hdr = nullptr;
-    ICS_HIP(hipMallocAsync(&hdr, n * 40, st));
-    hipError_t e = icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs),
-                                          static_cast<uint32_t*>(hdr), d_ip_ck, d_tcp_ck, false, g, ctx->max_blocks, st);
-    if (e == hipSuccess) e = icsum::launch_hdr_scatter(sp, static_cast<const uint32_t*>(hdr), st);
-    const hipError_t f = hipFreeAsync(hdr, st);
-    ICS_HIP(e);
-    ICS_HIP(f);
-    return ICS_OK;
-  }
-  ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), nullptr, d_ip_ck, d_tcp_ck,
-                                 false, g, ctx->max_blocks, st));
+  ICS_HIP(device_wrap(ctx, sp, d_msgs, nullptr, d_ip_ck, d_tcp_ck, false, g, st));
   return bounds_verdict(st, ICS_OK);
 }
 
@@ -758,12 +834,12 @@ int ics_tcp_wrap_headers(ics_ctx* ctx, const void* d_payloads, const uint64_t* d
   if (int rc = bind(ctx)) return rc;
   if (n == 0) return ICS_OK;
   if (!d_payloads || !d_msgs || !d_hdrs) return fail(ICS_ERR_INVALID, "null device buffer");
+  if (reinterpret_cast<uintptr_t>(d_msgs) & 3u) return fail(ICS_ERR_INVALID, "message records not 4-byte aligned");
   if (reinterpret_cast<uintptr_t>(d_hdrs) & 3u) return fail(ICS_ERR_INVALID, "header array not 4-byte aligned");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_payloads), d_offsets, stride, payload_len, n, ctx->d_zero};
   const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1000 : payload_len));
   hipStream_t st = static_cast<hipStream_t>(stream);
-  ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), static_cast<uint32_t*>(d_hdrs),
-                                 d_ip_ck, d_tcp_ck, true, g, ctx->max_blocks, st));
+  ICS_HIP(device_wrap(ctx, sp, d_msgs, static_cast<uint32_t*>(d_hdrs), d_ip_ck, d_tcp_ck, true, g, st));
   return bounds_verdict(st, ICS_OK);
 }
 

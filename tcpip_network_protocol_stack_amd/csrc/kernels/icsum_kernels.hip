@@ -809,7 +809,7 @@ __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_ipv4_tcp(uint8_t* __restric
 // IPv4Header::compute_checksum.  hdr_out != nullptr: the 40 bytes go to
 // hdr_out[40 i ..] instead of in place (the host-memory path copies only them
 // back).  Datagrams shorter than 40 bytes are left as they are.
-template <int LPS, int UNROLL, bool NT, int MODE>
+template <int LPS, int UNROLL, bool NT, int MODE, bool SUMS>
 __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_tcp_wrap(uint8_t* __restrict__ dg,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
@@ -817,7 +817,7 @@ __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_tcp_wrap(uint8_t* __restric
                                                      uint32_t* __restrict__ hdr_out,
                                                      uint16_t* __restrict__ ip_ck,
                                                      uint16_t* __restrict__ tcp_ck, uint32_t remap,
-                                                     int payload_only) {
+                                                     int payload_only, uint32_t* __restrict__ sums) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
@@ -830,11 +830,16 @@ __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_tcp_wrap(uint8_t* __restric
     if (!valid) e = s;
     // payload_only: segment i is the payload alone, its headers go to hdr_out
     const bool ok = valid && (payload_only || e - s >= 40);
-    const TcpMsg m = msgs[idx];  // same address across the group: one request per wave instruction
+    TcpMsg m{};
+    if (!SUMS) m = msgs[idx];  // same address across the group: one request per wave instruction
     const uint64_t p0 = ok ? (payload_only ? s : s + 40) : e;  // payload [p0, e)
     uint32_t ev = 0, od = 0;
     seg_sums<LPS, UNROLL, NT, MODE>(dg, p0, e, lane, ev, od);
     uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(p0) & 1u));
+    if (SUMS) {  // pass 1 of the two-pass wrap: the payload sums only (k_tcp_hdr writes the headers)
+      if (valid && lane == LPS - 1) sums[seg] = tot;
+      continue;
+    }
     if (LPS > 16) tot = __shfl(tot, int((threadIdx.x & 63u) | (LPS - 1)) & 63, 64);  // to every lane of the group
     // both checksums (16-bit big-endian words of the serialized headers)
     const uint32_t len = uint32_t(e - p0 + 40) & 0xffffu;  // IPv4Header::len is uint16
@@ -880,27 +885,94 @@ __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_tcp_wrap(uint8_t* __restric
   }
 }
 
-// Second half of the split wrap (measurement variant, ICSUM_WRAP_SPLIT=1):
-// copy each datagram's 40 header bytes from the compact array k_tcp_wrap
-// wrote (hdr_out) to the datagram start, datagrams in address order, one lane
-// per header dword.
-__global__ __launch_bounds__(kBlock) void k_hdr_scatter(uint8_t* __restrict__ dg,
-                                                        const uint64_t* __restrict__ offsets,
-                                                        uint64_t stride, uint64_t dlen, uint64_t n,
-                                                        const uint32_t* __restrict__ hdr) {
-  ICS_GRID_STRIDE(t, n * 10) {
-    const uint64_t i = t / 10;
-    const uint32_t k = uint32_t(t - i * 10);
+// Pass 2 of the device wrap when the headers go to an array of their own and
+// the batch is large (in place, and for short batches, the one-pass k_tcp_wrap
+// above is faster): the headers of 64 datagrams per wave from their 28-byte
+// records and the payload sums pass 1 left in `sums`.  Lane d builds datagram
+// d's 10 dwords and both checksums (the same arithmetic as k_tcp_wrap); LDS
+// turns them around so each store instruction writes 64 consecutive header
+// dwords — 256 contiguous bytes of hdr_out, or the headers of 6-7
+// neighbouring datagrams in place.  Header stores inside the payload stream
+// cost ≈40 ps per datagram apart and ≈85 ps in place
+// (profiles/r2_ab_wrap_variant.jsonl); here the apart ones are a
+// 14 us launch of their own per 1 M datagrams.
+__global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
+                                                    const uint64_t* __restrict__ offsets, uint64_t stride,
+                                                    uint64_t dlen, uint64_t n, const TcpMsg* __restrict__ msgs,
+                                                    const uint32_t* __restrict__ sums,
+                                                    uint32_t* __restrict__ hdr_out, uint16_t* __restrict__ ip_ck,
+                                                    uint16_t* __restrict__ tcp_ck, int payload_only) {
+  __shared__ uint32_t stage[kBlock / 64][64 * 10];  // 10 KiB: each wave's 640 header dwords
+  const uint32_t lane64 = threadIdx.x & 63u;
+  uint32_t* const sw = stage[threadIdx.x >> 6];
+  auto be16 = [](uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); };
+  for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock; b0 < n; b0 += uint64_t(gridDim.x) * kBlock) {
+    const uint64_t base = b0 + (threadIdx.x & ~63u);  // the wave's first datagram
+    if (base >= n) continue;                          // wave-uniform
+    const uint64_t i = base + lane64;
+    const bool valid = i < n;
+    const uint64_t idx = valid ? i : n - 1;
     uint64_t s, e;
-    seg_bounds(offsets, stride, dlen, i, s, e);
-    if (e - s >= 40) {
-      const uint32_t w = hdr[t];
-      uint8_t* h = dg + s;
-      if ((reinterpret_cast<uintptr_t>(h) & 3u) == 0)
-        reinterpret_cast<uint32_t*>(h)[k] = w;
-      else
-        for (int b = 0; b < 4; ++b) h[4 * k + b] = uint8_t(w >> (8 * b));
+    seg_bounds(offsets, stride, dlen, idx, s, e);
+    const bool ok = valid && (payload_only || e - s >= 40);
+    // the record as dwordx4 + dwordx3 (ics_tcp_msg: src, dst, seqno, ackno;
+    // sport | dport << 16; window | flags << 16 | ttl << 24; id)
+    const uint32_t* r = reinterpret_cast<const uint32_t*>(msgs + idx);
+    u32x4 a;
+    __builtin_memcpy(&a, r, 16);
+    const uint32_t r4 = r[4], r5 = r[5], r6 = r[6] & 0xffffu;
+    const uint32_t tot = sums[idx];
+    const uint32_t sport = r4 & 0xffffu, dport = r4 >> 16, window = r5 & 0xffffu;
+    const uint32_t flags = (r5 >> 16) & 0xffu, ttl = r5 >> 24;
+    const uint64_t p0 = payload_only ? s : s + 40;
+    const uint32_t len = uint32_t(e - p0 + 40) & 0xffffu;  // IPv4Header::len is uint16
+    const uint32_t addr = (a.x >> 16) + (a.x & 0xffffu) + (a.y >> 16) + (a.y & 0xffffu);
+    const uint32_t ipc = fold_value(0x4500u + len + r6 + 0x4000u + ((ttl << 8) | 6u) + addr);
+    const uint32_t pseudo = addr + 6u + ((len - 20u) & 0xffffu);  // ipv4_header.cpp:103-110
+    const uint32_t thdr = sport + dport + (a.z >> 16) + (a.z & 0xffffu) + (a.w >> 16) + (a.w & 0xffffu) +
+                          (0x5000u | flags) + window;
+    const uint32_t tcv = fold_value(pseudo + thdr + tot);
+    uint32_t* const my = sw + lane64 * 10;
+    my[0] = 0x45u | (be16(len) << 16);
+    my[1] = be16(r6) | (0x40u << 16);                     // id, DF
+    my[2] = ttl | (6u << 8) | (be16(ipc) << 16);          // ttl, proto, checksum
+    my[3] = bswap32(a.x);
+    my[4] = bswap32(a.y);
+    my[5] = be16(sport) | (be16(dport) << 16);
+    my[6] = bswap32(a.z);
+    my[7] = bswap32(a.w);
+    my[8] = 0x50u | (flags << 8) | (be16(window) << 16);  // data offset 5, flags, window
+    my[9] = be16(tcv);                                    // checksum, urgent pointer 0
+    if (valid) {
+      if (ip_ck) ip_ck[i] = ok ? uint16_t(ipc) : uint16_t(0);
+      if (tcp_ck) tcp_ck[i] = ok ? uint16_t(tcv) : uint16_t(0);
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // store j: the wave's header dword t = 64 j + lane64 = dword t % 10 of datagram t / 10
+    const int s_lo = int(uint32_t(s)), s_hi = int(uint32_t(s >> 32)), ok_i = int(ok);
+#pragma unroll
+    for (uint32_t j = 0; j < 10; ++j) {
+      const uint32_t t = j * 64 + lane64, d = t / 10, k = t - d * 10;
+      const uint32_t w = sw[t];
+      const bool dok = __shfl(ok_i, int(d), 64) != 0;
+      if (hdr_out) {
+        if (dok) hdr_out[base * 10 + t] = w;
+      } else {
+        const uint64_t ds = (uint64_t(uint32_t(__shfl(s_hi, int(d), 64))) << 32) | uint32_t(__shfl(s_lo, int(d), 64));
+        uint8_t* h = dg + ds + 4 * k;
+        if (dok) {
+          if ((reinterpret_cast<uintptr_t>(h) & 3u) == 0)
+            *reinterpret_cast<uint32_t*>(h) = w;
+          else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) h[b] = uint8_t(w >> (8 * b));
+          }
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();  // the next step rewrites sw
   }
 }
 
@@ -1243,11 +1315,16 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
 
 template <int LPS, int UNROLL, bool NT, int MODE>
 hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                         uint16_t* tcp_ck, bool payload_only, uint32_t max_blocks, hipStream_t st) {
+                         uint16_t* tcp_ck, bool payload_only, uint32_t* sums, uint32_t max_blocks, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
-  hipLaunchKernelGGL((k_tcp_wrap<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
-                     const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, msgs, hdr_out,
-                     ip_ck, tcp_ck, g_xcd_remap, int(payload_only));
+  if (sums)
+    hipLaunchKernelGGL((k_tcp_wrap<LPS, UNROLL, NT, MODE, true>), dim3(blocks), dim3(kBlock), 0, st,
+                       const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, msgs, hdr_out,
+                       ip_ck, tcp_ck, g_xcd_remap, int(payload_only), sums);
+  else
+    hipLaunchKernelGGL((k_tcp_wrap<LPS, UNROLL, NT, MODE, false>), dim3(blocks), dim3(kBlock), 0, st,
+                       const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, msgs, hdr_out,
+                       ip_ck, tcp_ck, g_xcd_remap, int(payload_only), sums);
   return hipGetLastError();
 }
 
@@ -1450,23 +1527,23 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_hdr_scatter(const SegSpec& sp, const uint32_t* hdr, hipStream_t st) {
-  if (sp.n == 0) return hipSuccess;
-  hipLaunchKernelGGL(k_hdr_scatter, dim3(ew_blocks(sp.n * 10)), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes),
-                     sp.offsets, sp.stride, sp.seg_len, sp.n, hdr);
-  return hipGetLastError();
-}
-
 hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                           uint16_t* tcp_ck, bool payload_only, Geometry g, uint32_t max_blocks, hipStream_t st) {
+                           uint16_t* tcp_ck, bool payload_only, uint32_t* sums, Geometry g, uint32_t max_blocks,
+                           hipStream_t st) {
   if (sp.n == 0) return hipSuccess;
   if (payload_only && !hdr_out) return hipErrorInvalidValue;
-#define ICS_CASE(L, U, T, A)                                      \
-  if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
-    return launch_wrap_t<L, U, T, A>(sp, msgs, hdr_out, ip_ck, tcp_ck, payload_only, max_blocks, st);
+  hipError_t e = hipErrorInvalidValue;
+#define ICS_CASE(L, U, T, A)                                                                         \
+  if (e == hipErrorInvalidValue && g.lps == L && g.unroll == U && g.nt == T && g.mode == A)        \
+    e = launch_wrap_t<L, U, T, A>(sp, msgs, hdr_out, ip_ck, tcp_ck, payload_only, sums, max_blocks, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
-  return hipErrorInvalidValue;
+  if (e != hipSuccess || !sums) return e;
+  const uint64_t blocks = (sp.n + kBlock - 1) / kBlock;  // one datagram per lane
+  hipLaunchKernelGGL(k_tcp_hdr, dim3(uint32_t(blocks < (uint64_t(1) << 22) ? blocks : (uint64_t(1) << 22))),
+                     dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n,
+                     msgs, sums, hdr_out, ip_ck, tcp_ck, int(payload_only));
+  return hipGetLastError();
 }
 
 bool geometry_supported(Geometry g) {

@@ -105,13 +105,15 @@ struct TcpMsg {
   uint16_t id, reserved;
 };
 static_assert(sizeof(TcpMsg) == 28, "ics_tcp_msg layout");
-// wrap_tcp_in_ip for a batch (k_tcp_wrap): headers + both checksums written in
-// place, or to hdr_out (40 bytes per datagram) when it is not null;
-// payload_only: segment i is the payload alone (no header room), hdr_out required
+// wrap_tcp_in_ip for a batch: headers + both checksums written in place, or
+// to hdr_out (40 bytes per datagram) when it is not null; payload_only:
+// segment i is the payload alone (no header room), hdr_out required.
+// sums != nullptr (n words of scratch): two passes, the payload sums
+// (k_tcp_wrap, pass-1 mode) then the headers (k_tcp_hdr); nullptr: the
+// one-pass k_tcp_wrap
 hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                           uint16_t* tcp_ck, bool payload_only, Geometry g, uint32_t max_blocks, hipStream_t st);
-// copy 40-byte headers from a compact array to the datagram starts (split wrap)
-hipError_t launch_hdr_scatter(const SegSpec& sp, const uint32_t* hdr, hipStream_t st);
+                           uint16_t* tcp_ck, bool payload_only, uint32_t* sums, Geometry g, uint32_t max_blocks,
+                           hipStream_t st);
 
 // bounds-checked build (libicsum_debug.so): synchronise `st` and take (read
 // and clear) the device's violation record; flags 0 = clean.  No-op returning
