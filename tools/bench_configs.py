@@ -3,12 +3,14 @@
 (PCIe) rate — the numbers DESIGN.md §Measurements quotes.  bench.py stays the
 driver's single headline line (north star); this is the wider table.
 
-    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch,wrap] [--iters 20]
+    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch,wrap,streams] [--iters 20]
 
 Batches that fit the 256 MiB Infinity Cache (ipv4 98 MB, tcp64 67 MB) are
 rotated over >= 4 distinct copies (>= 393 / 268 MB) so every launch reads HBM.
 Times are HIP events on the launch stream around `iters` back-to-back launches
-(median of 5 rounds).  GiB = 2^30 B of algorithmic bytes (segment bytes, each
+(median of 5 rounds); the `streams` rows issue a stream of short batches
+(configs 2, 3) on two HIP streams in turn, so one batch's drain overlaps the
+next one's ramp.  GiB = 2^30 B of algorithmic bytes (segment bytes, each
 read once); metadata (inits, offsets, outputs) is reported separately.
 """
 import argparse
@@ -50,6 +52,29 @@ def timed(fn, iters, rounds=5, settle_ms=150.0):
     return statistics.median(ts)
 
 
+def timed_streams(fn, iters, k, rounds=5):
+    """Per-batch seconds of `iters` batches issued on k streams in turn:
+    fn(i, stream, slot); first event to the last stream's end, median of
+    `rounds` after one settling round."""
+    main = torch.cuda.current_stream()
+    streams = [torch.cuda.Stream(main.device) for _ in range(k)]
+    ts = []
+    for r in range(rounds + 1):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(main)
+        for s in streams:
+            s.wait_stream(main)
+        for i in range(iters):
+            fn(i, streams[i % k], i % k)
+        for s in streams:
+            main.wait_stream(s)
+        b.record(main)
+        torch.cuda.synchronize()
+        if r:
+            ts.append(a.elapsed_time(b) / 1e3 / iters)
+    return statistics.median(ts)
+
+
 def emit(name, nbytes, t, meta_bytes=0, **kw):
     gbs = nbytes / t / 1e9
     print(json.dumps({"config": name, "bytes": nbytes, "us": round(t * 1e6, 2),
@@ -59,7 +84,7 @@ def emit(name, nbytes, t, meta_bytes=0, **kw):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--only", default="ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host")
+    ap.add_argument("--only", default="ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,streams")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--modes", default="compute,patch,verify", help="ipv4 rows: which ics_ipv4_tcp_batch modes")
     ap.add_argument("--settle-ms", type=float, default=150.0,
@@ -180,6 +205,37 @@ def main():
         out = torch.empty(n, dtype=torch.int16, device=dev)
         t = timed(lambda i=0: eng.checksum_batch(ds[i % R], n=n, stride=L, seg_len=L, out=out), args.iters * 3)
         emit("plain_64Kix1500", n * L, t, n * 2, entry="ics_checksum_batch", rotation=R)
+        del ds
+
+    if "streams" in only:  # a stream of short batches on two HIP streams in turn (configs 2, 3)
+        K = 2
+        n, L, seed, R = 1 << 16, 1500, 0x10710002, 6
+        bufs = []
+        for r in range(R):
+            d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+            eng.ipv4_tcp_headers(d, n, L, L, seed, index0=r * n)
+            eng.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)
+            bufs.append(d)
+        outs = [(torch.empty(n, dtype=torch.int16, device=dev), torch.empty(n, dtype=torch.int16, device=dev),
+                 torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(K)]
+        for mode, nm in ((0, "compute"), (2, "patch"), (1, "verify")):
+            t = timed_streams(lambda i, s, j: eng.ipv4_tcp_batch(bufs[i % R], mode, n=n, stride=L, dgram_len=L,
+                                                                ip_ck=outs[j][0], tcp_ck=outs[j][1],
+                                                                status=outs[j][2], stream=s), args.iters * 3, K)
+            emit(f"ipv4_64Kix1500_{nm}_2streams", n * L, t, n * 5, entry="ics_ipv4_tcp_batch", rotation=R, streams=K)
+        assert all((o[2].cpu().numpy() == 0x0F).all() for o in outs)
+        t = timed_streams(lambda i, s, j: eng.checksum_batch(bufs[i % R], n=n, stride=L, seg_len=L, out=outs[j][0],
+                                                            stream=s), args.iters * 3, K)
+        emit("plain_64Kix1500_2streams", n * L, t, n * 2, entry="ics_checksum_batch", rotation=R, streams=K)
+        del bufs
+        n, L, seed = 1 << 20, 64, 0x10710003
+        ds = [eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+              for r in range(R)]
+        inits = [eng.pseudo_inits(n, seed, seg_len=L, index0=r * n) for r in range(R)]
+        o16 = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(K)]
+        t = timed_streams(lambda i, s, j: eng.checksum_batch(ds[i % R], n=n, stride=L, seg_len=L, init=inits[i % R],
+                                                            out=o16[j], stream=s), args.iters * 3, K)
+        emit("tcp_1Mx64_2streams", n * L, t, n * 6, entry="ics_checksum_batch", rotation=R, streams=K)
         del ds
 
     if "tcp64" in only:  # config 3: 1 M x 64 B TCP segments with pseudo inits
