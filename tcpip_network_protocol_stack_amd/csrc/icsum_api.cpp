@@ -98,7 +98,9 @@ struct ics_ctx {
   // kernels).  A Scratch lease holds scratch_mu while the call enqueues its
   // kernels, then records scratch_ev on its stream; a call on another stream
   // first makes its stream wait for that event, and growing the buffer waits
-  // for it on the host.
+  // for it on the host.  It grows to the largest call's need (a binned batch
+  // of n segments: 80 n bytes + 16 KiB; a two-pass wrap: 4 n) and lives until
+  // ics_destroy.
   std::mutex scratch_mu;
   void* scratch = nullptr;
   size_t scratch_cap = 0;
