@@ -679,6 +679,67 @@ __device__ __forceinline__ void load_tcp_fields(const uint8_t* t, const uint32_t
   tf1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
 }
 
+// The header dwords and the TCP fields with ONE load instruction for a lane
+// group of >= 16 lanes: lane k (< 9) of the group loads header dword k (k <
+// 6: the aligned window at p, the sixth clamped to `last`) or TCP-field dword
+// k - 6 (the window at t + 12, the third clamped to `tlast`), the other lanes
+// repeat lane 0's address.  group_hdr_take, called after the byte stream has
+// been summed (loads return in order, so waiting for the stream covers this
+// load too), hands every lane the nine dwords from the group's lanes —
+// row_newbcast DPP for 16-lane groups (one DPP row), readlane for 64,
+// ds_bpermute for 32 — and aligns them: the values of load_hdr +
+// load_tcp_fields, which take 9 load instructions per lane.
+struct GroupHdr {
+  uint32_t v, sh, tsh;
+};
+
+template <int LPS>
+__device__ __forceinline__ GroupHdr group_hdr_load(const uint8_t* p, const uint32_t* last, const uint8_t* t,
+                                                   const uint32_t* tlast) {
+  static_assert(LPS >= 16, "nine dwords need nine lanes of the group");
+  const uint32_t k = threadIdx.x & (LPS - 1);
+  GroupHdr g;
+  g.sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p - g.sh);
+  const uint8_t* tp = t + 12;
+  g.tsh = uint32_t(reinterpret_cast<uintptr_t>(tp) & 3u);
+  const uint32_t* tq = reinterpret_cast<const uint32_t*>(tp - g.tsh);
+#ifdef ICSUM_BOUNDS_CHECK
+  if (k == 0 && q + 4 > last) bounds_fail(kBoundsHeader, reinterpret_cast<unsigned long long>(q + 4));
+  if (k == 0 && tq + 1 > tlast) bounds_fail(kBoundsHeader, reinterpret_cast<unsigned long long>(tq + 1));
+#endif
+  const uint32_t* a = q;
+  if (k < 5) a = q + k;
+  else if (k == 5) a = q + 5 < last ? q + 5 : last;
+  else if (k < 8) a = tq + (k - 6);
+  else if (k == 8) a = tq + 2 < tlast ? tq + 2 : tlast;
+  g.v = *a;
+  return g;
+}
+
+template <int LPS>
+__device__ __forceinline__ void group_hdr_take(const GroupHdr& g, Hdr& h, uint32_t& tf0, uint32_t& tf1) {
+  uint32_t d[9];
+  if constexpr (LPS == 16) {
+#define ICS_NEWBCAST(j) d[j] = __builtin_amdgcn_update_dpp(0u, g.v, 0x150 + (j), 0xF, 0xF, false);  // row_newbcast:j
+    ICS_NEWBCAST(0) ICS_NEWBCAST(1) ICS_NEWBCAST(2) ICS_NEWBCAST(3) ICS_NEWBCAST(4)
+    ICS_NEWBCAST(5) ICS_NEWBCAST(6) ICS_NEWBCAST(7) ICS_NEWBCAST(8)
+#undef ICS_NEWBCAST
+  } else {
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      if (LPS == 64)
+        d[j] = __builtin_amdgcn_readlane(g.v, j);
+      else
+        d[j] = uint32_t(__shfl(int(g.v), int((threadIdx.x & 63u & ~(LPS - 1u)) + j), 64));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < 5; ++j) h.w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], g.sh);
+  tf0 = __builtin_amdgcn_alignbyte(d[7], d[6], g.tsh);
+  tf1 = __builtin_amdgcn_alignbyte(d[8], d[7], g.tsh);
+}
+
 // IPv4Header::compute_checksum (ipv4_header.cpp:113-123): the 20 serialized
 // bytes equal the wire bytes with cksum = 0 and the reserved flag bit (0x8000
 // of the flags word, wire byte 6 bit 7) dropped (serialize, :78); options are
@@ -734,12 +795,19 @@ __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_ipv4_tcp(uint8_t* __restric
     // A datagram with options (rare) redoes its stream below.
     uint64_t t0 = hdr ? s + 20 : e;  // TCP part: [t0, e)
     const uint32_t* last = hdr ? last_dword(dg + e) : zlast;
-    Hdr h = load_hdr(hdr ? dg + s : zpad, last);
+    Hdr h;
     uint32_t tf0 = 0, tf1 = 0;  // TCP bytes 12..15 and 16..19 (little-endian)
     const bool tcpf = hdr && e - t0 >= 18;
-    load_tcp_fields(tcpf ? dg + t0 : zpad, tcpf ? last : zlast, tf0, tf1);
+    GroupHdr gh{};
+    if constexpr (LPS >= 16) {
+      gh = group_hdr_load<LPS>(hdr ? dg + s : zpad, last, tcpf ? dg + t0 : zpad, tcpf ? last : zlast);
+    } else {
+      h = load_hdr(hdr ? dg + s : zpad, last);
+      load_tcp_fields(tcpf ? dg + t0 : zpad, tcpf ? last : zlast, tf0, tf1);
+    }
     uint32_t ev = 0, od = 0;
     seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
+    if constexpr (LPS >= 16) group_hdr_take<LPS>(gh, h, tf0, tf1);
     bool redo = false;
     if (hdr) {
       uint64_t off = 4u * (h.byte(0) & 0x0fu);  // options skipped (ipv4_header.cpp:50)

@@ -1,0 +1,96 @@
+#!/usr/bin/env python3
+"""Dev A/B between two builds of libicsum.so in ONE process (interleaved
+rounds on the same box and buffers): the in-tree library ("new") and another
+build ("old", e.g. the previous commit's, built into build_ab/).  Both are
+loaded side by side (ctypes, RTLD_LOCAL); each engine uses its own.
+
+    python3 tools/ab_two_libs.py build_ab/libicsum_old.so --cases ipv4,ipv4_off,ipv4_mix
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tcpip_network_protocol_stack_amd import _lib  # noqa: E402
+from tcpip_network_protocol_stack_amd.engine import Engine  # noqa: E402
+
+
+def old_engine(path):
+    saved = _lib.DEBUG_LIB_PATH
+    _lib.DEBUG_LIB_PATH = os.path.abspath(path)
+    try:
+        return Engine(0, debug=True)  # the "debug" slot of Engine loads `path`
+    finally:
+        _lib.DEBUG_LIB_PATH = saved
+
+
+def cases_for(names, engines, dev):
+    from ab_ipv4_mix import batch
+
+    cases = {}
+    keep = []
+    o = [torch.empty(1 << 20, dtype=torch.int16, device=dev), torch.empty(1 << 20, dtype=torch.int16, device=dev),
+         torch.empty(1 << 20, dtype=torch.uint8, device=dev)]
+    new = engines["new"]
+    if "ipv4" in names:  # config 2, rotated over 6 copies
+        n, L, seed, R = 1 << 16, 1500, 0x10710002, 6
+        bufs = []
+        for r in range(R):
+            d = new.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+            new.ipv4_tcp_headers(d, n, L, L, seed, index0=r * n)
+            new.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)
+            bufs.append(d)
+        keep.append(bufs)
+        for tag, e in engines.items():
+            for mode, mn in ((0, "compute"), (1, "verify")):
+                cases[f"cfg2_{mn}_{tag}"] = (lambda e, mode: lambda i: e.ipv4_tcp_batch(
+                    bufs[i % R], mode, n=n, stride=L, dgram_len=L, ip_ck=o[0], tcp_ck=o[1], status=o[2]))(e, mode)
+    for nm, af in (("ipv4_off", 0.0), ("ipv4_mix", 0.5)):
+        if nm in names:
+            d, doff, _ = batch(new, 1 << 20, af, 7)
+            keep.append((d, doff))
+            for tag, e in engines.items():
+                cases[f"{nm}_verify_{tag}"] = (lambda e, d, doff: lambda i: e.ipv4_tcp_batch(
+                    d, 1, n=1 << 20, offsets=doff, ip_ck=o[0], tcp_ck=o[1], status=o[2]))(e, d, doff)
+    return cases, keep
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("old")
+    ap.add_argument("--cases", default="ipv4,ipv4_off,ipv4_mix")
+    ap.add_argument("--rounds", type=int, default=7)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    engines = {"new": Engine(0), "old": old_engine(args.old)}
+    cases, _keep = cases_for(set(args.cases.split(",")), engines, dev)
+    res = {k: [] for k in cases}
+    for _ in range(args.rounds):
+        for k, fn in cases.items():
+            t0 = time.perf_counter()
+            while time.perf_counter() - t0 < 0.03:
+                for i in range(4):
+                    fn(i)
+                torch.cuda.synchronize()
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            for i in range(30):
+                fn(i)
+            b.record()
+            torch.cuda.synchronize()
+            res[k].append(a.elapsed_time(b) * 1e3 / 30)
+    for k, v in res.items():
+        print(json.dumps({"case": k, "us": round(float(np.median(v)), 2), "min": round(min(v), 2),
+                          "max": round(max(v), 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
