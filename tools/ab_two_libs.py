@@ -60,6 +60,17 @@ def cases_for(names, engines, dev):
             for tag, e in engines.items():
                 cases[f"{nm}_verify_{tag}"] = (lambda e, d, doff: lambda i: e.ipv4_tcp_batch(
                     d, 1, n=1 << 20, offsets=doff, ip_ck=o[0], tcp_ck=o[1], status=o[2]))(e, d, doff)
+    for nm, L in (("dense32", 32), ("tcp64", 64), ("dense128", 128)):  # fixed-stride short segments + inits
+        if nm in names:
+            n, R = (64 << 20) // L, 6
+            ds = [new.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), 0x10710003, pos0=r * n * L)
+                  for r in range(R)]
+            inits = [new.pseudo_inits(n, 0x10710003, seg_len=L, index0=r * n) for r in range(R)]
+            out16 = torch.empty(n, dtype=torch.int16, device=dev)
+            keep.append((ds, inits, out16))
+            for tag, e in engines.items():
+                cases[f"{nm}_{tag}"] = (lambda e, ds, inits, out16, n, L: lambda i: e.checksum_batch(
+                    ds[i % R], n=n, stride=L, seg_len=L, init=inits[i % R], out=out16))(e, ds, inits, out16, n, L)
     return cases, keep
 
 
