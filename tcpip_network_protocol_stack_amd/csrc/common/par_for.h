@@ -1,14 +1,16 @@
 // par_for.h — not installed.  Split [0, n) into `threads` contiguous ranges and
 // run fn(i0, i1) on each, the first range on the calling thread.  Exception
-// safe: every worker thread that started is joined on every path, an
-// exception thrown inside fn (or by a thread that fails to start) is carried
-// out and rethrown on the calling thread after the join, instead of
-// terminating the process.
+// safe: every worker thread that started is joined on every path, and an
+// exception thrown inside fn is carried out and rethrown on the calling thread
+// after the join, instead of terminating the process.  A range whose thread
+// fails to start (EAGAIN) runs on the calling thread instead — the work is
+// done, so that is not an error.
 #pragma once
 
 #include <cstddef>
 #include <exception>
 #include <mutex>
+#include <system_error>
 #include <thread>
 #include <vector>
 
@@ -35,11 +37,9 @@ void parallel_ranges(size_t n, size_t threads, Fn&& fn)
     pool.reserve(threads - 1);
     try {
         for (size_t t = 1; t < threads; ++t) pool.emplace_back(guarded, n * t / threads, n * (t + 1) / threads);
-    } catch (...) {  // std::thread failed to start (EAGAIN): the caller runs what is left
-        std::lock_guard<std::mutex> lock(mu);
-        if (!err) err = std::current_exception();
+    } catch (const std::system_error&) {  // a thread failed to start: the caller runs what is left
     }
-    // ranges whose thread did not start run here, so no work is skipped silently
+    // ranges whose thread did not start run here
     for (size_t t = pool.size() + 1; t < threads; ++t) guarded(n * t / threads, n * (t + 1) / threads);
     guarded(0, n / threads);
     for (auto& th : pool) th.join();

@@ -10,9 +10,13 @@
 //                                     datagrams each: "got same_order lost_none"
 //   txstress P N                   -> engine-less DatagramTxRing to a SEQPACKET stream:
 //                                     "sent got same_order failed_patch_recovered"
-// The two stress commands run the rings' reader / writer threads with no GPU,
-// so the ASan+UBSan and TSan builds (make asan / make tsan) cover their locking.
+//   parfor N T                     -> detail::parallel_ranges over [0, N) on T threads: "covered_once
+//                                     worker_throw_seen caller_throw_seen"
+// The stress commands run the rings' reader / writer threads (and parfor the
+// thread pool) with no GPU, so the ASan+UBSan and TSan builds (make asan /
+// make tsan) cover their locking.
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <iostream>
 #include <stdexcept>
@@ -29,6 +33,7 @@
 #include "batch_io.h"
 #include "checksum.h"
 #include "ipv4_datagram.h"
+#include "par_for.h"
 #include "parser.h"
 #include "tcp_over_ip.h"
 #include "tcp_segment.h"
@@ -76,7 +81,33 @@ int main()
         std::istringstream in(line);
         std::string cmd;
         in >> cmd;
-        if (cmd == "kat") {
+        if (cmd == "parfor") {
+            size_t n = 0, t = 0;
+            in >> n >> t;
+            std::vector<std::atomic<int>> hits(n);
+            icsum::detail::parallel_ranges(n, t, [&](size_t i0, size_t i1) {
+                for (size_t i = i0; i < i1; ++i) hits[i].fetch_add(1, std::memory_order_relaxed);
+            });
+            bool once = std::all_of(hits.begin(), hits.end(), [](const std::atomic<int>& h) { return h.load() == 1; });
+            // an exception in a worker's range and one in the caller's own
+            // range (the first) both reach the caller, after every join
+            bool worker = false, caller = false;
+            try {
+                icsum::detail::parallel_ranges(n, t, [&](size_t i0, size_t) {
+                    if (i0 > 0) throw std::runtime_error("worker");
+                });
+            } catch (const std::runtime_error& e) {
+                worker = std::string(e.what()) == "worker";
+            }
+            try {
+                icsum::detail::parallel_ranges(n, t, [&](size_t i0, size_t) {
+                    if (i0 == 0) throw std::runtime_error("caller");
+                });
+            } catch (const std::runtime_error& e) {
+                caller = std::string(e.what()) == "caller";
+            }
+            std::cout << once << " " << (worker || t <= 1 || n < 2) << " " << caller << "\n";
+        } else if (cmd == "kat") {
             uint64_t init = 0;
             in >> init;
             std::vector<std::string> pieces;
