@@ -191,7 +191,10 @@ int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
  * of d_payloads is message i's payload ALONE (no header room); the 40 header
  * bytes of datagram i go to d_hdrs + 40*i (4-byte aligned), written as one
  * coalesced array instead of into the payload stream.  Datagram i on the wire
- * = d_hdrs[40 i .. 40 i + 40) followed by payload i. */
+ * = d_hdrs[40 i .. 40 i + 40) followed by payload i.  From 2^18 datagrams up
+ * the engine runs two launches on `stream` (payload sums, then the headers),
+ * faster than storing headers inside the payload stream;
+ * d_msgs must be 4-byte aligned (both wrap calls). */
 int ics_tcp_wrap_headers(ics_ctx* ctx, const void* d_payloads, const uint64_t* d_offsets, uint64_t stride,
                          uint64_t payload_len, uint64_t n, const ics_tcp_msg* d_msgs, void* d_hdrs,
                          uint16_t* d_ip_ck, uint16_t* d_tcp_ck, void* stream);
