@@ -21,7 +21,7 @@ def _env(**kw):
     return env
 
 
-@pytest.mark.parametrize("n", [2, 3])
+@pytest.mark.parametrize("n", [2, 3, 8])
 def test_gpus_n_starts_n_ranks(n):
     r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--launch-check"], env=_env(),
                        capture_output=True, text=True, timeout=240)
@@ -34,6 +34,26 @@ def test_gpus_n_starts_n_ranks(n):
     assert {s["world_size"] for s in seen} == {n}
     assert {s["master_addr"] for s in seen} == {"127.0.0.1"}
     assert len({s["pid"] for s in seen}) == n  # one process per rank
+
+
+def test_driver_style_outer_launcher():
+    """The driver's own form: torch.distributed.run starts the ranks and each
+    runs `bench.py --gpus N`; bench.py must not launch again."""
+    import socket
+
+    n = 4
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", str(n),
+                        "--launch-check"], env=_env(), capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    seen = lines[0]["launch_check"]
+    assert sorted(s["rank"] for s in seen) == list(range(n)) and {s["world_size"] for s in seen} == {n}
+    assert len({s["pid"] for s in seen}) == n
 
 
 def test_world_size_must_match_gpus():
