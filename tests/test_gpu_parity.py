@@ -38,6 +38,8 @@ def _t(a, dev="cuda:0"):
     a = np.ascontiguousarray(a)
     if a.dtype in _SIGNED:
         a = a.view(_SIGNED[a.dtype])
+    if not a.flags.writeable:  # e.g. np.frombuffer over bytes: torch wants a writable array
+        a = a.copy()
     return torch.from_numpy(a).to(dev)
 
 
