@@ -12,6 +12,8 @@
 //                                     "sent got same_order failed_patch_recovered"
 //   parfor N T                     -> detail::parallel_ranges over [0, N) on T threads: "covered_once
 //                                     worker_throw_seen caller_throw_seen"
+//   pool N T J                     -> detail::WorkerPool(T - 1), J jobs of N items in T ranges each:
+//                                     "covered_once_every_job worker_throw_seen caller_throw_seen"
 // The stress commands run the rings' reader / writer threads (and parfor the
 // thread pool) with no GPU, so the ASan+UBSan and TSan builds (make asan /
 // make tsan) cover their locking.
@@ -81,7 +83,36 @@ int main()
         std::istringstream in(line);
         std::string cmd;
         in >> cmd;
-        if (cmd == "parfor") {
+        if (cmd == "pool") {
+            size_t n = 0, t = 0, jobs = 0;
+            in >> n >> t >> jobs;
+            icsum::detail::WorkerPool pool(t > 0 ? t - 1 : 0);
+            bool once = true;
+            std::vector<std::atomic<int>> hits(n);
+            for (size_t j = 0; j < jobs; ++j) {
+                for (auto& h : hits) h.store(0, std::memory_order_relaxed);
+                pool.run(n, t, [&](size_t i0, size_t i1) {
+                    for (size_t i = i0; i < i1; ++i) hits[i].fetch_add(1, std::memory_order_relaxed);
+                });
+                once = once && std::all_of(hits.begin(), hits.end(), [](const std::atomic<int>& h) { return h.load() == 1; });
+            }
+            bool worker = false, caller = false;
+            try {
+                pool.run(n, t, [&](size_t i0, size_t) {
+                    if (i0 > 0) throw std::runtime_error("worker");
+                });
+            } catch (const std::runtime_error& e) {
+                worker = std::string(e.what()) == "worker";
+            }
+            try {
+                pool.run(n, t, [&](size_t i0, size_t) {
+                    if (i0 == 0) throw std::runtime_error("caller");
+                });
+            } catch (const std::runtime_error& e) {
+                caller = std::string(e.what()) == "caller";
+            }
+            std::cout << once << " " << (worker || t <= 1 || n < 2) << " " << caller << "\n";
+        } else if (cmd == "parfor") {
             size_t n = 0, t = 0;
             in >> n >> t;
             std::vector<std::atomic<int>> hits(n);

@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <new>
 #include <string>
@@ -137,6 +138,11 @@ struct ics_ctx {
   uint8_t* h_hdr[kMaxSlots] = {};
   uint8_t* d_hdr[kMaxSlots] = {};
   uint32_t* d_sums[kMaxSlots] = {};  // the two-pass wrap's payload sums
+  // staging copies of pageable host batches: copy_threads ranges (the caller
+  // and copy_threads - 1 kept workers, started on first use;
+  // ICSUM_COPY_THREADS, default min(8, hardware threads))
+  size_t copy_threads = 8;
+  std::unique_ptr<icsum::detail::WorkerPool> copy_pool;
 };
 
 namespace {
@@ -452,19 +458,33 @@ bool host_pinned(const void* p) {
   return a.type == hipMemoryTypeHost;
 }
 
-// memcpy split over threads: a single core copies pageable memory into the
-// pinned slots at ~10-20 GB/s, below what PCIe Gen5 x16 moves
-void par_memcpy(void* dst, const void* src, size_t n) {
+// memcpy split over the context's copy workers: a single core copies pageable
+// memory into the pinned slots at ~10-20 GB/s, below what PCIe Gen5 x16 moves
+void par_memcpy(ics_ctx* ctx, void* dst, const void* src, size_t n) {
   constexpr size_t kMinPerThread = size_t(4) << 20;
-  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
-  const size_t t = std::min<size_t>({size_t(8), size_t(hw), std::max<size_t>(1, n / kMinPerThread)});
+  const size_t t = std::min<size_t>(ctx->copy_threads, std::max<size_t>(1, n / kMinPerThread));
   if (t <= 1) {
     std::memcpy(dst, src, n);
     return;
   }
-  icsum::detail::parallel_ranges(n, t, [=](size_t a, size_t b) {
+  if (!ctx->copy_pool) ctx->copy_pool = std::make_unique<icsum::detail::WorkerPool>(ctx->copy_threads - 1);
+  ctx->copy_pool->run(n, t, [=](size_t a, size_t b) {
     std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, b - a);
   });
+}
+
+// fn(j0, j1) over [0, m) datagrams on the copy workers (host-side stores into
+// the caller's batch at retire), serially below 16 Ki datagrams per range
+template <typename Fn>
+void host_ranges(ics_ctx* ctx, uint64_t m, Fn&& fn) {
+  constexpr uint64_t kMinPerThread = 16384;
+  const size_t t = std::min<size_t>(ctx->copy_threads, std::max<uint64_t>(1, m / kMinPerThread));
+  if (t <= 1) {
+    fn(size_t(0), size_t(m));
+    return;
+  }
+  if (!ctx->copy_pool) ctx->copy_pool = std::make_unique<icsum::detail::WorkerPool>(ctx->copy_threads - 1);
+  ctx->copy_pool->run(m, t, fn);
 }
 
 // ICS_MODE_PATCH's stores (k_ipv4_tcp, mode 2) applied on the host from a
@@ -474,11 +494,11 @@ void par_memcpy(void* dst, const void* src, size_t n) {
 // the TCP header.  Both big-endian.  `res` = the slot's results: m ip u16,
 // m tcp u16, m status bytes.
 void host_patch_fields(uint8_t* bytes, const uint64_t* offsets, uint64_t stride, uint64_t dlen, const Chunk& c,
-                       const uint8_t* res) {
+                       const uint8_t* res, uint64_t j0, uint64_t j1) {
   const uint64_t m = c.i1 - c.i0;
   const uint16_t* ip = reinterpret_cast<const uint16_t*>(res);
   const uint16_t* tcp = ip + m;
-  for (uint64_t j = 0; j < m; ++j) {
+  for (uint64_t j = j0; j < j1; ++j) {
     const uint64_t i = c.i0 + j;
     const uint64_t s = offsets ? offsets[i] : i * stride;
     const uint64_t len = offsets ? offsets[i + 1] - s : dlen;
@@ -532,20 +552,24 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
     } else if (kind == 2 && mode == 1) {  // payload-only: headers to the caller's array
       std::memcpy(reinterpret_cast<uint8_t*>(out_c) + 40 * c.i0, ctx->h_hdr[k], m * 40);
-    } else if (kind == 2) {
+    } else if (kind == 2) {  // 40 header bytes into each datagram of the caller's batch
       uint8_t* bytes = static_cast<uint8_t*>(h_bytes);
-      for (uint64_t j = 0; j < m; ++j) {
-        const uint64_t i = c.i0 + j;
-        const uint64_t s0 = h_offsets ? h_offsets[i] : i * stride;
-        const uint64_t len = h_offsets ? h_offsets[i + 1] - s0 : seg_len;
-        if (len >= 40) std::memcpy(bytes + s0, ctx->h_hdr[k] + 40 * j, 40);
-      }
+      host_ranges(ctx, m, [&](size_t j0, size_t j1) {
+        for (uint64_t j = j0; j < j1; ++j) {
+          const uint64_t i = c.i0 + j;
+          const uint64_t s0 = h_offsets ? h_offsets[i] : i * stride;
+          const uint64_t len = h_offsets ? h_offsets[i + 1] - s0 : seg_len;
+          if (len >= 40) std::memcpy(bytes + s0, ctx->h_hdr[k] + 40 * j, 40);
+        }
+      });
     } else {
       if (out_a) std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
       if (out_b) std::memcpy(out_b + c.i0, ctx->h_out[k] + m * 2, m * 2);
       if (out_c) std::memcpy(out_c + c.i0, ctx->h_out[k] + m * 4, m);
-      if (mode == ICS_MODE_PATCH)
-        host_patch_fields(static_cast<uint8_t*>(h_bytes), h_offsets, stride, seg_len, c, ctx->h_out[k]);
+      if (mode == ICS_MODE_PATCH)  // scattered 2-byte stores into the caller's batch
+        host_ranges(ctx, m, [&](size_t j0, size_t j1) {
+          host_patch_fields(static_cast<uint8_t*>(h_bytes), h_offsets, stride, seg_len, c, ctx->h_out[k], j0, j1);
+        });
     }
     busy[k] = false;
     return ICS_OK;
@@ -561,7 +585,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
     const uint64_t m = c.i1 - c.i0, nb = c.b1 - c.b0;
     uint8_t* src = static_cast<uint8_t*>(h_bytes) + c.b0;
     if (!direct) {
-      par_memcpy(ctx->h_in[slot], src, nb);
+      par_memcpy(ctx, ctx->h_in[slot], src, nb);
       src = ctx->h_in[slot];
     }
     hipStream_t st = ctx->st[slot];
@@ -692,6 +716,10 @@ int ics_create(int device, ics_ctx** out) {
   if (ctx->bin_plan > 3) ctx->bin_plan = -1;
   ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
   ctx->wrap_passes = env_u32("ICSUM_WRAP_PASSES", 0);
+  {
+    const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+    ctx->copy_threads = std::max<size_t>(1, env_u32("ICSUM_COPY_THREADS", std::min(8u, hw)));
+  }
   if (hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(ctx->d_zero);
     delete ctx;

@@ -37,7 +37,7 @@ def _selftest_lines():
     lines.append("io " + " ".join(c["wire"] for c in tw))
     lines.append("ioseq " + " ".join(c["wire"] for c in tw))
     lines.append("ioudp " + " ".join(c["wire"] for c in tw[:64]))
-    lines += ["parfor 100000 8", "parfor 7 8", "parfor 1 4", "parfor 5000 1"]
+    lines += ["parfor 100000 8", "parfor 7 8", "parfor 1 4", "parfor 5000 1", "pool 100000 8 50", "pool 5 8 20"]
     lines.append("ringstress 4 3 2000")
     lines.append("txstress 3 3000")
     return "\n".join(lines) + "\n"
@@ -62,9 +62,9 @@ def test_host_selftest_under_asan_and_tsan(host_builds):
     runs = {k: subprocess.run([exe], input=stdin, capture_output=True, text=True, timeout=600, env=env)
             for k, exe in host_builds.items()}
     assert runs["plain"].returncode == 0, runs["plain"].stderr[-2000:]
-    tail = runs["plain"].stdout.strip().splitlines()[-6:]
-    assert tail[:4] == ["1 1 1"] * 4, tail  # parfor: every index once, both exceptions carried out
-    assert tail[4] == "24000 1 1" and tail[5] == "9000 9000 1 1", tail
+    tail = runs["plain"].stdout.strip().splitlines()[-8:]
+    assert tail[:6] == ["1 1 1"] * 6, tail  # parfor / pool: every index once, both exceptions carried out
+    assert tail[6] == "24000 1 1" and tail[7] == "9000 9000 1 1", tail
     for k in ("asan", "tsan"):
         assert _clean(runs[k]), (k, runs[k].stderr[-4000:])
         assert runs[k].stdout == runs["plain"].stdout, k

@@ -71,6 +71,31 @@ def cases_for(names, engines, dev):
             for tag, e in engines.items():
                 cases[f"{nm}_{tag}"] = (lambda e, ds, inits, out16, n, L: lambda i: e.checksum_batch(
                     ds[i % R], n=n, stride=L, seg_len=L, init=inits[i % R], out=out16))(e, ds, inits, out16, n, L)
+    if "host" in names:  # PCIe-inclusive: pageable and pinned host batches, 256 Ki x 1500 B
+        n, L = 1 << 18, 1500
+        for pinned in (False, True):
+            h = torch.empty(n * L, dtype=torch.uint8, pin_memory=pinned).numpy()
+            h[:] = np.random.default_rng(3).integers(0, 256, n * L, dtype=np.uint8)
+            keep.append(h)
+            for tag, e in engines.items():
+                nm = "pinned" if pinned else "pageable"
+                cases[f"host_{nm}_{tag}"] = (lambda e, h: lambda i: e.checksum_batch_host(h, n, stride=L,
+                                                                                          seg_len=L))(e, h)
+                cases[f"hostpatch_{nm}_{tag}"] = (lambda e, h: lambda i: e.ipv4_tcp_batch_host(
+                    h, n, 2, stride=L, dgram_len=L))(e, h)
+        from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE
+
+        m = np.zeros(n, dtype=TCP_MSG_DTYPE)
+        m["flags"], m["ttl"] = 0x10, 128
+        for pinned in (False, True):
+            W = 1040
+            h = torch.empty(n * W, dtype=torch.uint8, pin_memory=pinned).numpy()
+            h[:] = 7
+            keep.append(h)
+            for tag, e in engines.items():
+                nm = "pinned" if pinned else "pageable"
+                cases[f"hostwrap_{nm}_{tag}"] = (lambda e, h: lambda i: e.tcp_wrap_batch_host(
+                    h, m, n, stride=W, dgram_len=W))(e, h)
     return cases, keep
 
 
@@ -91,6 +116,12 @@ def main():
                 for i in range(4):
                     fn(i)
                 torch.cuda.synchronize()
+            if k.startswith("host"):  # synchronous host-memory calls: wall time
+                t1 = time.perf_counter()
+                for i in range(5):
+                    fn(i)
+                res[k].append((time.perf_counter() - t1) * 1e6 / 5)
+                continue
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             for i in range(30):
