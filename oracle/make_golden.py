@@ -9,7 +9,8 @@ Builds oracle/ref (the reference's own checksum path compiled in place from
   tests/golden/tcp_wrap.json       wrap/unwrap + TCPSegment::parse (tcp_over_ip.cpp, tcp_segment.cpp)
   tests/golden/router_cases.json   Router ttl--/recompute (router.cpp:43-50)
   tests/golden/configs.json        per BASELINE config: sha256 + head of the
-                                   reference's output arrays at FULL size
+                                   reference's output arrays at FULL size; plus
+                                   6 (wrap, 1 M messages) and 7 (router step)
 
 Only needs /root/reference; run here, never on the GPU box:
     python oracle/make_golden.py [--skip-configs]
@@ -36,6 +37,13 @@ CONFIGS = {
     3: dict(name="tcp_1Mx64", n=1 << 20, stride=64, seg_len=64, inits="pseudo"),
     4: dict(name="mixed_1M_64B_64KiB", n=1 << 20, stride=0, seg_len=0, inits="pseudo", mixed=True),
     5: dict(name="jumbo_8Mx9000", n=8 << 20, stride=9000, seg_len=9000, inits="pseudo"),
+    # SURVEY §8f rows at full size (not BASELINE configs): the device wrap and
+    # the router step, through the reference's own wrap_tcp_in_ip / Router logic
+    6: dict(name="wrap_1Mx1000", n=1 << 20, payload_len=1000, payload_seed=0x10710006, field_seed=0x10710106,
+            fields="fill(field_seed, 32 i, 32): src, dst, seqno, ackno be32; sport, dport, window be16; "
+                   "flag byte (1 FIN, 2 SYN, 4 RST, 0x10 ACK present); ttl 128, id 0 (wrap_tcp_in_ip)"),
+    7: dict(name="router_64Kix1500", n=1 << 16, stride=1500, seed=0x10710002,
+            ttl="i % 4 (config 2's datagrams otherwise), then one router step"),
 }
 
 
@@ -50,7 +58,7 @@ def sha(path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--skip-configs", action="store_true")
-    ap.add_argument("--configs", default="0,2,3,4,5")
+    ap.add_argument("--configs", default="0,2,3,4,5,6,7")
     args = ap.parse_args()
     if not os.path.isdir("/root/reference"):
         sys.exit("make_golden.py needs /root/reference (run it in the build container)")
@@ -68,8 +76,21 @@ def main():
         for k in [int(x) for x in args.configs.split(",")]:
             spec = dict(CONFIGS[k])
             subprocess.check_call([GEN, "config", str(k), tmp])
-            ent = dict(spec, seed=0x10710000 + k)
-            if k == 2:
+            ent = dict(spec) if k >= 6 else dict(spec, seed=0x10710000 + k)
+            if k == 6:
+                f = os.path.join(tmp, "cfg6_hdr.bin")
+                ent["hdr_sha256"] = sha(f)
+                ent["hdr_head"] = np.fromfile(f, dtype=np.uint8)[:40 * 16].tobytes().hex()
+                for nm in ("ipck", "tcpck"):
+                    f = os.path.join(tmp, f"cfg6_{nm}.bin")
+                    ent[f"{nm}_sha256"] = sha(f)
+                    ent[f"{nm}_head"] = np.fromfile(f, dtype="<u2")[:64].tolist()
+            elif k == 7:
+                ent["out_sha256"] = sha(os.path.join(tmp, "cfg7_out.bin"))
+                fwd = np.fromfile(os.path.join(tmp, "cfg7_fwd.bin"), dtype=np.uint8)
+                ent["fwd_sha256"] = sha(os.path.join(tmp, "cfg7_fwd.bin"))
+                ent["forwarded"] = int(fwd.sum())
+            elif k == 2:
                 for nm in ("ipck", "tcpck"):
                     f = os.path.join(tmp, f"cfg2_{nm}.bin")
                     ent[f"{nm}_sha256"] = sha(f)

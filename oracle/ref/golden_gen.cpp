@@ -16,6 +16,7 @@
 //        golden_gen config K DIR     raw reference outputs of BASELINE config K
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -498,6 +499,109 @@ void config_ipv4(uint64_t n, uint64_t stride, const std::string& dir) {
   std::printf("config 2: n=%llu bytes=%llu\n", (unsigned long long)n, (unsigned long long)(n * stride));
 }
 
+// config 6 (SURVEY §8f rank 2 at MSS scale): 1 M messages, 1000-byte
+// payloads (fill(seed_p, 1000 i, 1000)), fields from fill(seed_f, 32 i, 32):
+// src, dst, seqno, ackno (be32), sport, dport, window (be16), flag byte (bit 0
+// FIN, 1 SYN, 2 RST, 4 ACK present), each through the reference's own
+// TCPOverIPv4Adapter::wrap_tcp_in_ip (tcp_over_ip.cpp:69-88); outputs: the 40
+// header bytes of every datagram and both checksums.
+void config_wrap(const std::string& dir) {
+  const uint64_t n = 1ull << 20, P = 1000, seed_p = 0x10710006ull, seed_f = 0x10710106ull;
+  std::vector<char> hdr(n * 40);
+  std::vector<uint16_t> ipc(n), tcpc(n);
+  auto ipstr = [](uint32_t a) {
+    return std::to_string(a >> 24) + "." + std::to_string((a >> 16) & 255) + "." + std::to_string((a >> 8) & 255) +
+           "." + std::to_string(a & 255);
+  };
+  unsigned nt = std::max(1u, std::thread::hardware_concurrency());
+  std::vector<std::thread> th;
+  std::atomic<bool> bad{false};
+  for (unsigned t = 0; t < nt; ++t)
+    th.emplace_back([&, t] {
+      std::string f(32, '\0'), pay(P, '\0');
+      for (uint64_t i = n * t / nt; i < n * (t + 1) / nt; ++i) {
+        fill(seed_f, 32 * i, 32, f.data());
+        fill(seed_p, P * i, P, pay.data());
+        auto u8 = [&](size_t k) { return uint8_t(f[k]); };
+        auto be16 = [&](size_t k) { return uint16_t((u8(k) << 8) | u8(k + 1)); };
+        auto be32 = [&](size_t k) { return uint32_t((uint32_t(be16(k)) << 16) | be16(k + 2)); };
+        TCPOverIPv4Adapter A;
+        A.config_mut().source = Address{ipstr(be32(0)), be16(16)};
+        A.config_mut().destination = Address{ipstr(be32(4)), be16(18)};
+        TCPMessage m;
+        m.sender.seqno = Wrap32{be32(8)};
+        m.sender.FIN = u8(22) & 1;
+        m.sender.SYN = (u8(22) >> 1) & 1;
+        m.sender.RST = (u8(22) >> 2) & 1;
+        m.sender.payload = pay;
+        if (u8(22) & 0x10) m.receiver.ackno = Wrap32{be32(12)};
+        m.receiver.window_size = be16(20);
+        const InternetDatagram dg = A.wrap_tcp_in_ip(m);
+        const std::string wire = joined(serialize(dg));
+        if (wire.size() != P + 40 || wire.compare(40, P, pay) != 0) bad = true;
+        std::memcpy(hdr.data() + 40 * i, wire.data(), 40);
+        ipc[i] = dg.header.cksum;
+        tcpc[i] = uint16_t((uint8_t(wire[36]) << 8) | uint8_t(wire[37]));
+      }
+    });
+  for (auto& x : th) x.join();
+  if (bad) {
+    std::fprintf(stderr, "config 6: a wrapped datagram is not header + payload\n");
+    std::exit(3);
+  }
+  write_bin(dir + "/cfg6_hdr.bin", hdr.data(), hdr.size());
+  write_bin(dir + "/cfg6_ipck.bin", ipc.data(), n * 2);
+  write_bin(dir + "/cfg6_tcpck.bin", tcpc.data(), n * 2);
+  std::printf("config 6: n=%llu payload bytes=%llu\n", (unsigned long long)n, (unsigned long long)(n * P));
+}
+
+// config 7: config 2's datagrams with ttl = i % 4 (so a
+// quarter are dropped at ttl 0 and a quarter at 1), each checksummed by the
+// reference, then one router step (router.cpp:43-50: parse, drop when ttl <=
+// 1, else ttl-- and compute_checksum); outputs: the whole batch after the
+// step and the forwarded flags.
+void config_router(const std::string& dir) {
+  const uint64_t n = 1ull << 16, stride = 1500, seed = 0x10710002ull;
+  std::vector<char> out(n * stride);
+  std::vector<uint8_t> fwd(n);
+  std::string raw(stride, '\0');
+  for (uint64_t i = 0; i < n; ++i) {
+    fill(seed, i * stride, stride, raw.data());
+    auto u8 = [&](size_t k) { return uint8_t(raw[k]); };
+    auto be16 = [&](size_t k) { return uint16_t((u8(k) << 8) | u8(k + 1)); };
+    auto be32 = [&](size_t k) { return uint32_t((uint32_t(be16(k)) << 16) | be16(k + 2)); };
+    TCPSegment seg;  // as config_ipv4
+    seg.udinfo.src_port = be16(20);
+    seg.udinfo.dst_port = be16(22);
+    seg.message.sender.seqno = Wrap32{be32(24)};
+    seg.message.receiver.ackno = Wrap32{be32(28)};
+    seg.message.receiver.window_size = be16(34);
+    seg.message.sender.payload = raw.substr(40);
+    IPv4Header h;
+    h.len = uint16_t(stride);
+    h.id = uint16_t(i);
+    h.ttl = uint8_t(i % 4);
+    h.src = src_of(seed, i);
+    h.dst = dst_of(seed, i);
+    seg.compute_checksum(h.pseudo_checksum());
+    h.compute_checksum();
+    std::string wire = joined(serialize(IPv4Datagram{h, serialize(seg)}));
+    IPv4Datagram dg;
+    const bool ok = parse(dg, std::vector<std::string>{wire});
+    if (ok && dg.header.ttl > 1) {
+      dg.header.ttl--;
+      dg.header.compute_checksum();
+      wire = joined(serialize(dg));
+      fwd[i] = 1;
+    }
+    if (wire.size() != stride) std::exit(3);
+    std::memcpy(out.data() + i * stride, wire.data(), stride);
+  }
+  write_bin(dir + "/cfg7_out.bin", out.data(), out.size());
+  write_bin(dir + "/cfg7_fwd.bin", fwd.data(), n);
+  std::printf("config 7: n=%llu bytes=%llu\n", (unsigned long long)n, (unsigned long long)(n * stride));
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -517,9 +621,11 @@ int main(int argc, char** argv) {
       case 3: config_bytes(3, 1ull << 20, 64, false, dir); return 0;
       case 4: config_bytes(4, 1ull << 20, 0, true, dir); return 0;
       case 5: config_bytes(5, 8ull << 20, 9000, false, dir); return 0;
+      case 6: config_wrap(dir); return 0;
+      case 7: config_router(dir); return 0;
       default: break;
     }
   }
-  std::fprintf(stderr, "usage: golden_gen kat DIR | golden_gen config {0,2,3,4,5} DIR\n");
+  std::fprintf(stderr, "usage: golden_gen kat DIR | golden_gen config {0,2,3,4,5,6,7} DIR\n");
   return 1;
 }

@@ -29,3 +29,36 @@ def pack_contiguous(segs, lead=0):
 
 def wires(name, tags=None):
     return [c for c in golden(name)["cases"] if tags is None or c.get("tag") in tags]
+
+
+# ---- configs.json "6": the full-size wrap spec (oracle/ref/golden_gen.cpp config_wrap)
+def wrap6_records(fields, dtype):
+    """n x 32 spec bytes -> ics_tcp_msg records (numpy, `dtype` =
+    engine.TCP_MSG_DTYPE): src, dst, seqno, ackno big-endian u32; ports and
+    window big-endian u16; flag byte 1 FIN, 2 SYN, 4 RST, 0x10 ACK present
+    (ackno 0 without it); ttl 128, id 0 as wrap_tcp_in_ip sets them."""
+    f = np.asarray(fields, dtype=np.uint8).reshape(-1, 32).astype(np.uint64)
+    be32 = lambda k: (f[:, k] << 24) | (f[:, k + 1] << 16) | (f[:, k + 2] << 8) | f[:, k + 3]  # noqa: E731
+    be16 = lambda k: (f[:, k] << 8) | f[:, k + 1]  # noqa: E731
+    m = np.zeros(len(f), dtype=dtype)
+    m["src"], m["dst"], m["seqno"] = be32(0), be32(4), be32(8)
+    flags = f[:, 22] & 0x17
+    m["ackno"] = np.where(flags & 0x10, be32(12), 0)
+    m["src_port"], m["dst_port"], m["window"] = be16(16), be16(18), be16(20)
+    m["flags"], m["ttl"], m["id"] = flags, 128, 0
+    return m
+
+
+def oracle_wrap_wire(orc, payload, r):
+    """serialize(wrap_tcp_in_ip(msg)) by the oracle: the header fields as
+    serialize() lays them out, both checksums by its PATCH
+    (ipv4_header.cpp:113-123, tcp_segment.cpp:109-118)."""
+    L = (40 + len(payload)) & 0xFFFF
+    b = bytearray([0x45, 0, L >> 8, L & 255, int(r["id"]) >> 8, int(r["id"]) & 255, 0x40, 0, int(r["ttl"]), 6, 0, 0])
+    b += int(r["src"]).to_bytes(4, "big") + int(r["dst"]).to_bytes(4, "big")
+    b += int(r["src_port"]).to_bytes(2, "big") + int(r["dst_port"]).to_bytes(2, "big")
+    b += int(r["seqno"]).to_bytes(4, "big") + int(r["ackno"]).to_bytes(4, "big")
+    b += bytes([0x50, int(r["flags"])]) + int(r["window"]).to_bytes(2, "big") + b"\0\0\0\0" + bytes(payload)
+    _, _, st, w = orc.ipv4_tcp(bytes(b), 2)
+    assert st & 0x03 == 0x03
+    return w

@@ -457,6 +457,22 @@ def test_config2_ipv4_full_size(engine):
     assert (st.cpu().numpy() == 0x0F).all()
 
 
+def test_config7_router_full_size(engine):
+    """Router step over config 2's datagrams with ttl = i % 4 (half dropped at
+    ttl 0 / 1) vs the reference's parse + Router step (configs.json "7")."""
+    import torch
+
+    g = golden("configs.json")["7"]
+    n, L, seed = g["n"], g["stride"], g["seed"]
+    d = _gen_bytes(engine, n * L, seed)
+    engine.ipv4_tcp_headers(d, n, L, L, seed)
+    d.view(n, L)[:, 8] = (torch.arange(n, device=d.device) % 4).to(torch.uint8)
+    engine.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)  # both checksums for the new ttl
+    st = engine.router_ttl_batch(d, n=n, stride=L, dgram_len=L).cpu().numpy()
+    assert int(st.sum()) == g["forwarded"] and _sha(st) == g["fwd_sha256"]
+    assert _sha(d.cpu().numpy()) == g["out_sha256"]
+
+
 def test_corruption_detection_full_size(engine, orc):
     # inject one random bit flip per datagram of config 2; every flip outside
     # the IPv4 reserved flag bit (which the reference does not represent,

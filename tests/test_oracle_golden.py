@@ -144,6 +144,44 @@ def test_config2_ipv4_digest(orc):
     assert (st == 0x0F).all()
 
 
+def test_config6_wrap_head(orc):
+    """The full-size wrap spec (configs.json "6", the reference's own
+    wrap_tcp_in_ip over 1 M messages): the oracle reproduces its first 16
+    headers and 64 checksum pairs."""
+    from helpers import oracle_wrap_wire, wrap6_records
+
+    from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE
+
+    g = golden("configs.json")["6"]
+    k, P = 64, g["payload_len"]
+    m = wrap6_records(orc.fill_bytes(g["field_seed"], 0, 32 * k), TCP_MSG_DTYPE)
+    pay = orc.fill_bytes(g["payload_seed"], 0, P * k)
+    wires_ = [oracle_wrap_wire(orc, pay[i * P:(i + 1) * P].tobytes(), m[i]) for i in range(k)]
+    assert all(w[40:] == pay[i * P:(i + 1) * P].tobytes() for i, w in enumerate(wires_))
+    assert b"".join(w[:40] for w in wires_[:16]).hex() == g["hdr_head"]
+    assert [int.from_bytes(w[10:12], "big") for w in wires_] == g["ipck_head"]
+    assert [int.from_bytes(w[36:38], "big") for w in wires_] == g["tcpck_head"]
+
+
+def test_config7_router_digest(orc):
+    """Config 2's datagrams with ttl = i % 4 after one router step, at full
+    size (configs.json "7", the reference's parse + Router step)."""
+    g = golden("configs.json")["7"]
+    n, stride, seed = g["n"], g["stride"], g["seed"]
+    data = orc.fill_bytes(seed, 0, n * stride)
+    for i in range(n):
+        orc.ipv4_tcp_headers(seed, i, stride, data[i * stride:])
+    data.reshape(n, stride)[:, 8] = np.arange(n) % 4
+    orc.ipv4_tcp_batch(data, n, 2, stride=stride, dgram_len=stride)  # the reference's compute_checksum pair
+    fwd = np.zeros(n, dtype=np.uint8)
+    for i in range(n):
+        st, out = orc.router_ttl(data[i * stride:(i + 1) * stride].tobytes())
+        fwd[i] = st
+        data[i * stride:(i + 1) * stride] = np.frombuffer(out, dtype=np.uint8)
+    assert int(fwd.sum()) == g["forwarded"] and _sha(fwd) == g["fwd_sha256"]
+    assert _sha(data) == g["out_sha256"]
+
+
 @pytest.mark.slow
 @pytest.mark.skipif(not os.environ.get("ICSUM_FULL_ORACLE"), reason="set ICSUM_FULL_ORACLE=1 (10 GB oracle run)")
 def test_config4_mixed_digest(orc):
