@@ -18,6 +18,7 @@
 #define ICSUM_HOST_BATCH_H
 
 #include <cstdint>
+#include <memory>
 #include <optional>
 #include <span>
 #include <string>
@@ -31,6 +32,10 @@
 #include "tcp_segment.h"
 
 namespace icsum {
+
+namespace detail {
+class WorkerPool;  // par_for.h
+}
 
 // The fields wrap_tcp_in_ip puts on the wire for `msg` from an adapter with
 // configuration `cfg` (tcp_over_ip.cpp:71-80, tcp_segment.cpp:76-106): the
@@ -84,6 +89,7 @@ class BatchEngine
     int device_ = 0;
     uint8_t* scratch_ = nullptr;
     size_t scratch_cap_ = 0;
+    std::unique_ptr<detail::WorkerPool> pool_{};  // unwrap's field parse, started on first use
 };
 
 }  // namespace icsum

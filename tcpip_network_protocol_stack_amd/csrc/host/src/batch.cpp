@@ -281,40 +281,41 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_packed(TCPOverIPv4Ada
             const std::string_view wire{reinterpret_cast<const char*>(bytes) + offsets[i],
                                         static_cast<size_t>(offsets[i + 1] - offsets[i])};
             IPv4Header& h = parsed[i].ip;
-            // only the 20 fixed header bytes are copied for the field parse
-            // (IPV4_OK implies at least 20 bytes); fields only, the GPU
-            // already compared the header checksum
-            Parser ipp{std::vector<std::string>{std::string{wire.substr(0, IPv4Header::LENGTH)}}};
-            uint8_t first = 0;
-            ipp.integer(first);
-            h.ver = first >> 4;
-            h.hlen = first & 0x0f;
-            ipp.integer(h.tos);
-            ipp.integer(h.len);
-            ipp.integer(h.id);
-            uint16_t fo = 0;
-            ipp.integer(fo);
+            // the 20 fixed header bytes, big-endian, read in place (IPV4_OK
+            // implies at least 20 bytes); fields only, the GPU already
+            // compared the header checksum
+            auto u8 = [&](size_t k) { return static_cast<uint8_t>(wire[k]); };
+            auto be16 = [&](size_t k) { return static_cast<uint16_t>((u8(k) << 8) | u8(k + 1)); };
+            h.ver = u8(0) >> 4;
+            h.hlen = u8(0) & 0x0f;
+            h.tos = u8(1);
+            h.len = be16(2);
+            h.id = be16(4);
+            const uint16_t fo = be16(6);
             h.df = (fo & 0x4000) != 0;
             h.mf = (fo & 0x2000) != 0;
             h.offset = fo & 0x1fff;
-            ipp.integer(h.ttl);
-            ipp.integer(h.proto);
-            ipp.integer(h.cksum);
-            ipp.integer(h.src);
-            ipp.integer(h.dst);
+            h.ttl = u8(8);
+            h.proto = u8(9);
+            h.cksum = be16(10);
+            h.src = (static_cast<uint32_t>(be16(12)) << 16) | be16(14);
+            h.dst = (static_cast<uint32_t>(be16(16)) << 16) | be16(18);
             // all bytes after the options (ipv4_header.cpp:50, then the
             // datagram's remaining buffer as the TCP segment); a header
-            // longer than the datagram leaves nothing, and the TCP parse fails
+            // longer than the datagram leaves nothing, and the TCP parse
+            // fails; the payload is copied once, straight from the batch
             const size_t hdr_bytes = static_cast<size_t>(h.hlen) * 4;
-            Parser tp{std::vector<std::string>{
-                std::string{hdr_bytes <= wire.size() ? wire.substr(hdr_bytes) : std::string_view{}}}};
-            detail::parse_tcp_fields(tp, parsed[i].seg);
-            parsed[i].ok = !tp.has_error();
+            parsed[i].ok = detail::parse_tcp_fields(
+                hdr_bytes <= wire.size() ? wire.substr(hdr_bytes) : std::string_view{}, parsed[i].seg);
         }
     };
     const size_t threads = std::min<size_t>({size_t(8), std::max(1u, std::thread::hardware_concurrency()),
                                              std::max<size_t>(1, n / 2048)});
-    detail::parallel_ranges(n, threads, parse_range);  // joins every worker, rethrows a worker's exception
+    if (threads > 1 && !pool_) pool_ = std::make_unique<detail::WorkerPool>(7);
+    if (threads > 1)
+        pool_->run(n, threads, parse_range);  // waits for every range, rethrows a range's exception
+    else
+        parse_range(size_t(0), n);
     std::vector<std::optional<TCPMessage>> out(n);
     for (size_t i = 0; i < n; ++i) {
         if ((st[i] & (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) !=
@@ -322,7 +323,7 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_packed(TCPOverIPv4Ada
             continue;
         if (!detail::ip_gate(adapter, parsed[i].ip)) continue;
         if (!parsed[i].ok) continue;
-        out[i] = detail::tcp_gate(adapter, parsed[i].ip, parsed[i].seg);
+        out[i] = detail::tcp_gate(adapter, parsed[i].ip, std::move(parsed[i].seg));
     }
     return out;
 }

@@ -22,20 +22,33 @@ bool ip_gate(const FdAdapterBase& adapter, const IPv4Header& h)
     return h.proto == IPv4Header::PROTO_TCP;
 }
 
-std::optional<TCPMessage> tcp_gate(FdAdapterBase& adapter, const IPv4Header& h, const TCPSegment& seg)
+namespace {
+bool tcp_gate_ok(FdAdapterBase& adapter, const IPv4Header& h, const TCPSegment& seg)
 {
     const uint16_t local_port = adapter.config().source.port();
-    if (seg.udinfo.dst_port != local_port) return std::nullopt;
+    if (seg.udinfo.dst_port != local_port) return false;
     if (adapter.listening()) {
         const TCPSenderMessage& s = seg.message.sender;
-        if (!s.SYN || s.RST) return std::nullopt;  // only a clean SYN opens the connection
+        if (!s.SYN || s.RST) return false;  // only a clean SYN opens the connection
         FdAdapterConfig& cfg = adapter.config_mut();
         cfg.source = Address{Address::from_ipv4_numeric(h.dst).ip(), local_port};
         cfg.destination = Address{Address::from_ipv4_numeric(h.src).ip(), seg.udinfo.src_port};
         adapter.set_listening(false);
     }
-    if (seg.udinfo.src_port != adapter.config().destination.port()) return std::nullopt;
+    return seg.udinfo.src_port == adapter.config().destination.port();
+}
+}  // namespace
+
+std::optional<TCPMessage> tcp_gate(FdAdapterBase& adapter, const IPv4Header& h, const TCPSegment& seg)
+{
+    if (!tcp_gate_ok(adapter, h, seg)) return std::nullopt;
     return seg.message;
+}
+
+std::optional<TCPMessage> tcp_gate(FdAdapterBase& adapter, const IPv4Header& h, TCPSegment&& seg)
+{
+    if (!tcp_gate_ok(adapter, h, seg)) return std::nullopt;
+    return std::move(seg.message);
 }
 
 void stamp_outgoing(const FdAdapterConfig& cfg, const TCPMessage& msg, IPv4Header& h, TCPSegment& seg)

@@ -5,6 +5,8 @@
 // sums that header with cksum = 0 plus the payload, seeded with the pseudo sum.
 #include "tcp_segment.h"
 
+#include <algorithm>
+
 #include "checksum.h"
 #include "wire_internal.h"
 
@@ -78,6 +80,31 @@ void parse_tcp_fields(Parser& parser, TCPSegment& seg)
         parser.remove_prefix(static_cast<size_t>(data_offset - kMinDataOffset) * 4);  // options
     }
     parser.all_remaining(seg.message.sender.payload);
+}
+bool parse_tcp_fields(std::string_view b, TCPSegment& seg)
+{
+    if (b.size() < 20) return false;
+    auto u8 = [&](size_t k) { return static_cast<uint8_t>(b[k]); };
+    auto be16 = [&](size_t k) { return static_cast<uint16_t>((u8(k) << 8) | u8(k + 1)); };
+    auto be32 = [&](size_t k) { return (static_cast<uint32_t>(be16(k)) << 16) | be16(k + 2); };
+    seg.udinfo.src_port = be16(0);
+    seg.udinfo.dst_port = be16(2);
+    seg.message.sender.seqno = Wrap32{be32(4)};
+    seg.message.receiver.ackno = Wrap32{be32(8)};
+    const uint8_t data_offset = u8(12) >> 4;
+    const uint8_t flags = u8(13);
+    if (!(flags & 0x10)) seg.message.receiver.ackno.reset();
+    seg.message.sender.RST = seg.message.receiver.RST = (flags & 0x04) != 0;
+    seg.message.sender.SYN = (flags & 0x02) != 0;
+    seg.message.sender.FIN = (flags & 0x01) != 0;
+    seg.message.receiver.window_size = be16(14);
+    seg.udinfo.cksum = be16(16);
+    if (data_offset < kMinDataOffset) return false;
+    // options past the end: the Parser's skip stops at the end without an
+    // error, and the payload is empty (parser.h remove_prefix)
+    const size_t hdr = std::min(static_cast<size_t>(data_offset) * 4, b.size());
+    seg.message.sender.payload.assign(b.data() + hdr, b.size() - hdr);
+    return true;
 }
 }  // namespace icsum::detail
 

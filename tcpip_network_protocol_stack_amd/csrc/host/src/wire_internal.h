@@ -5,6 +5,7 @@
 
 #include <cstdint>
 #include <optional>
+#include <string_view>
 
 #include "tcp_over_ip.h"
 
@@ -13,6 +14,10 @@ namespace icsum::detail {
 // tcp_segment.cpp:25-65: header fields, flags, data offset, payload (the
 // half of TCPSegment::parse after its checksum check)
 void parse_tcp_fields(Parser& parser, TCPSegment& seg);
+// the same over one contiguous buffer (the segment's bytes): false where the
+// Parser would have flagged an error (fewer than 20 bytes, data offset < 5);
+// the payload is copied once
+bool parse_tcp_fields(std::string_view bytes, TCPSegment& seg);
 uint32_t raw_of(const Wrap32& w);
 
 // tcp_over_ip.cpp:14-29 — before any TCP byte is looked at: a connected
@@ -23,6 +28,8 @@ bool ip_gate(const FdAdapterBase& adapter, const IPv4Header& h);
 // listen -> connected transition on a SYN without RST (which rewrites the
 // adapter's endpoints), then the source port
 std::optional<TCPMessage> tcp_gate(FdAdapterBase& adapter, const IPv4Header& h, const TCPSegment& seg);
+// the same, moving the message (and its payload) out of `seg` when it passes
+std::optional<TCPMessage> tcp_gate(FdAdapterBase& adapter, const IPv4Header& h, TCPSegment&& seg);
 
 // tcp_over_ip.cpp:71-80 — the ports, addresses and total length wrap sets
 // before either checksum is computed (checksum fields are left at 0)

@@ -241,6 +241,49 @@ int main()
         }
     }
 
+    // TCP data offsets 6..15 with valid checksums (options, or a header that
+    // claims more than the segment holds: the reference's Parser skips to the
+    // end without an error and the payload is empty): the batch field parse
+    // must equal the per-object one
+    {
+        std::vector<std::string> opt;
+        for (unsigned doff = 5; doff <= 15; ++doff)
+            for (size_t plen : {size_t(0), size_t(3), size_t(4), size_t(10), size_t(41), size_t(60)}) {
+                TCPMessage m;
+                m.sender.seqno = Wrap32{static_cast<uint32_t>(rng())};
+                m.sender.payload = bytes(plen);
+                m.receiver.ackno = Wrap32{static_cast<uint32_t>(rng())};
+                m.receiver.window_size = static_cast<uint16_t>(rng());
+                std::string w = joined(serialize(A.wrap_tcp_in_ip(m)));
+                w[20 + 12] = static_cast<char>(doff << 4);
+                w[20 + 16] = w[20 + 17] = 0;
+                IPv4Datagram d;
+                EXPECT(parse(d, std::vector<std::string>{w}));
+                InternetChecksum c{d.header.pseudo_checksum()};
+                c.add(std::string_view{w}.substr(20));
+                const uint16_t ck = c.value();
+                w[20 + 16] = static_cast<char>(ck >> 8);
+                w[20 + 17] = static_cast<char>(ck & 0xff);
+                opt.push_back(w);
+            }
+        std::vector<std::string_view> optv(opt.begin(), opt.end());
+        TCPOverIPv4Adapter Bg = B, Bc = B;
+        const auto got_opt = eng.unwrap_raw(Bg, optv);
+        size_t acc = 0;
+        for (size_t i = 0; i < opt.size(); ++i) {
+            IPv4Datagram d;
+            std::optional<TCPMessage> want;
+            if (parse(d, std::vector<std::string>{opt[i]})) want = Bc.unwrap_tcp_in_ip(d);
+            EXPECT(got_opt[i].has_value() == want.has_value());
+            if (want && got_opt[i]) {
+                EXPECT(got_opt[i]->sender.payload == want->sender.payload);
+                EXPECT(got_opt[i]->sender.seqno == want->sender.seqno);
+                ++acc;
+            }
+        }
+        EXPECT(acc == opt.size());  // every data offset >= 5 parses (payload empty past the end)
+    }
+
     // batched datagram I/O: the same received wires through
     // a SOCK_DGRAM socketpair into a page-locked arena, unwrapped in place
     {
