@@ -84,12 +84,14 @@ class BatchEngine
     template <typename Msgs, typename Take>
     std::vector<InternetDatagram> wrap_impl(const TCPOverIPv4Adapter& adapter, Msgs& msgs, Take take_payload);
     uint8_t* scratch(size_t bytes);  // page-locked arena reused across calls
+    template <typename Fn>
+    void ranges(size_t n, Fn&& fn);  // fn(i0, i1) over [0, n) on up to 8 of the engine's threads
 
     ics_ctx* ctx_ = nullptr;
     int device_ = 0;
     uint8_t* scratch_ = nullptr;
     size_t scratch_cap_ = 0;
-    std::unique_ptr<detail::WorkerPool> pool_{};  // unwrap's field parse, started on first use
+    std::unique_ptr<detail::WorkerPool> pool_{};  // ranges()' workers, started on first use
 };
 
 }  // namespace icsum

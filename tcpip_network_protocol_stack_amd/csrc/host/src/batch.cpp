@@ -153,26 +153,48 @@ std::vector<InternetDatagram> BatchEngine::wrap_impl(const TCPOverIPv4Adapter& a
     uint8_t* arena = scratch(std::max<uint64_t>(off[n], 1));
     std::vector<ics_tcp_msg> rec(n);
     const FdAdapterConfig& cfg = adapter.config();
-    for (size_t i = 0; i < n; ++i) {
-        const std::string& pl = msgs[i].sender.payload;
-        if (!pl.empty()) std::memcpy(arena + off[i] + 40, pl.data(), pl.size());
-        rec[i] = wrap_fields(cfg, msgs[i]);
-    }
+    // the payload copies into the arena and, after the device pass, the
+    // results' construction (allocations, payload copies or moves) are
+    // independent per message: split over the engine's workers
+    ranges(n, [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            const std::string& pl = msgs[i].sender.payload;
+            if (!pl.empty()) std::memcpy(arena + off[i] + 40, pl.data(), pl.size());
+            rec[i] = wrap_fields(cfg, msgs[i]);
+        }
+    });
     if (n) wrap_packed(arena, off.data(), rec.data(), n);
     std::vector<InternetDatagram> out(n);
-    for (size_t i = 0; i < n; ++i) {
-        IPv4Header& h = out[i].header;  // the defaults wrap_tcp_in_ip keeps (ipv4_header.h)
-        const uint8_t* w = arena + off[i];
-        h.len = static_cast<uint16_t>((w[2] << 8) | w[3]);
-        h.cksum = static_cast<uint16_t>((w[10] << 8) | w[11]);
-        h.src = rec[i].src;
-        h.dst = rec[i].dst;
-        // serialize(seg)'s pieces: the 20-byte TCP header, then the payload
-        // (Serializer::buffer, parser.h) when there is one
-        out[i].payload.emplace_back(reinterpret_cast<const char*>(w) + 20, 20);
-        if (!msgs[i].sender.payload.empty()) out[i].payload.push_back(take_payload(msgs[i]));
-    }
+    ranges(n, [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) {
+            IPv4Header& h = out[i].header;  // the defaults wrap_tcp_in_ip keeps (ipv4_header.h)
+            const uint8_t* w = arena + off[i];
+            h.len = static_cast<uint16_t>((w[2] << 8) | w[3]);
+            h.cksum = static_cast<uint16_t>((w[10] << 8) | w[11]);
+            h.src = rec[i].src;
+            h.dst = rec[i].dst;
+            // serialize(seg)'s pieces: the 20-byte TCP header, then the payload
+            // (Serializer::buffer, parser.h) when there is one
+            out[i].payload.reserve(2);
+            out[i].payload.emplace_back(reinterpret_cast<const char*>(w) + 20, 20);
+            if (!msgs[i].sender.payload.empty()) out[i].payload.push_back(take_payload(msgs[i]));
+        }
+    });
     return out;
+}
+
+template <typename Fn>
+void BatchEngine::ranges(size_t n, Fn&& fn)
+{
+    // up to 8 contiguous ranges of >= 2048 items on the engine's workers
+    const size_t threads = std::min<size_t>({size_t(8), std::max(1u, std::thread::hardware_concurrency()),
+                                             std::max<size_t>(1, n / 2048)});
+    if (threads <= 1) {
+        fn(size_t(0), n);
+        return;
+    }
+    if (!pool_) pool_ = std::make_unique<detail::WorkerPool>(7);
+    pool_->run(n, threads, fn);  // waits for every range, rethrows a range's exception
 }
 
 std::vector<InternetDatagram> BatchEngine::wrap(TCPOverIPv4Adapter& adapter, std::span<const TCPMessage> msgs)
@@ -309,13 +331,7 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_packed(TCPOverIPv4Ada
                 hdr_bytes <= wire.size() ? wire.substr(hdr_bytes) : std::string_view{}, parsed[i].seg);
         }
     };
-    const size_t threads = std::min<size_t>({size_t(8), std::max(1u, std::thread::hardware_concurrency()),
-                                             std::max<size_t>(1, n / 2048)});
-    if (threads > 1 && !pool_) pool_ = std::make_unique<detail::WorkerPool>(7);
-    if (threads > 1)
-        pool_->run(n, threads, parse_range);  // waits for every range, rethrows a range's exception
-    else
-        parse_range(size_t(0), n);
+    ranges(n, parse_range);
     std::vector<std::optional<TCPMessage>> out(n);
     for (size_t i = 0; i < n; ++i) {
         if ((st[i] & (ICS_ST_IPV4_OK | ICS_ST_TCP_CKSUM_OK | ICS_ST_TCP_HDR_OK)) !=
