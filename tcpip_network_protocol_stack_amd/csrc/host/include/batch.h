@@ -86,6 +86,8 @@ class BatchEngine
     uint8_t* scratch(size_t bytes);  // page-locked arena reused across calls
     template <typename Fn>
     void ranges(size_t n, Fn&& fn);  // fn(i0, i1) over [0, n) on up to 8 of the engine's threads
+    template <typename Len, typename Put>
+    std::vector<uint64_t> pack(size_t n, Len len, Put put);  // n items into scratch(), offsets back
 
     ics_ctx* ctx_ = nullptr;
     int device_ = 0;

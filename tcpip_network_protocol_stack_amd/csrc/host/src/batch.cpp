@@ -75,37 +75,54 @@ BatchEngine::~BatchEngine()
     ics_destroy(ctx_);
 }
 
+template <typename Len, typename Put>
+std::vector<uint64_t> BatchEngine::pack(size_t n, Len len, Put put)
+{
+    // item i's len(i) bytes at off[i] of the page-locked scratch arena, written
+    // by put(i, dst) on the engine's workers: the *_host call then DMAs the
+    // batch straight from it (no pageable staging copy)
+    std::vector<uint64_t> off(n + 1, 0);
+    for (size_t i = 0; i < n; ++i) off[i + 1] = off[i] + len(i);
+    uint8_t* base = scratch(std::max<uint64_t>(off[n], 1));
+    ranges(n, [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i) put(i, base + off[i]);
+    });
+    return off;
+}
+
 std::vector<uint16_t> BatchEngine::checksum(std::span<const std::string_view> segs, std::span<const uint32_t> init)
 {
     if (!init.empty() && init.size() != segs.size()) throw std::invalid_argument("init size != segment count");
-    Packed p;
-    for (auto s : segs) {
-        p.add(s);
-        p.end();
-    }
     std::vector<uint16_t> out(segs.size());
-    if (!segs.empty())
-        check(ics_checksum_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, init.empty() ? nullptr : init.data(),
-                                      out.data(), p.n()),
-              "ics_checksum_batch_host");
+    if (segs.empty()) return out;
+    const auto off = pack(
+        segs.size(), [&](size_t i) { return segs[i].size(); },
+        [&](size_t i, uint8_t* d) { std::memcpy(d, segs[i].data(), segs[i].size()); });
+    check(ics_checksum_batch_host(ctx_, scratch_, off.data(), 0, 0, init.empty() ? nullptr : init.data(), out.data(),
+                                  segs.size()),
+          "ics_checksum_batch_host");
     return out;
 }
 
 void BatchEngine::compute_checksums(std::span<TCPSegment> segs, std::span<const IPv4Header> hdrs)
 {
     if (hdrs.size() != segs.size()) throw std::invalid_argument("header count != segment count");
-    Packed p;
+    if (segs.empty()) return;
+    // serialize(seg)'s bytes — the 20-byte header with cksum = 0
+    // (tcp_segment.cpp:111), then the payload — written straight into the arena
     std::vector<uint32_t> init(segs.size());
-    for (size_t i = 0; i < segs.size(); ++i) {
-        segs[i].udinfo.cksum = 0;  // tcp_segment.cpp:111 — summed as zero
-        for (const auto& piece : serialize(segs[i])) p.add(piece);
-        p.end();
-        init[i] = hdrs[i].pseudo_checksum();
-    }
+    const auto off = pack(
+        segs.size(), [&](size_t i) { return 20 + segs[i].message.sender.payload.size(); },
+        [&](size_t i, uint8_t* d) {
+            segs[i].udinfo.cksum = 0;
+            detail::tcp_header_bytes(segs[i], reinterpret_cast<char*>(d));
+            const std::string& pl = segs[i].message.sender.payload;
+            if (!pl.empty()) std::memcpy(d + 20, pl.data(), pl.size());
+            init[i] = hdrs[i].pseudo_checksum();
+        });
     std::vector<uint16_t> out(segs.size());
-    if (!segs.empty())
-        check(ics_checksum_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, init.data(), out.data(), p.n()),
-              "ics_checksum_batch_host");
+    check(ics_checksum_batch_host(ctx_, scratch_, off.data(), 0, 0, init.data(), out.data(), segs.size()),
+          "ics_checksum_batch_host");
     for (size_t i = 0; i < segs.size(); ++i) segs[i].udinfo.cksum = out[i];
 }
 
@@ -127,16 +144,14 @@ void BatchEngine::compute_checksums(std::span<IPv4Header> hdrs)
 
 std::vector<uint8_t> BatchEngine::verify_raw(std::span<const std::string_view> wires)
 {
-    Packed p;
-    for (auto w : wires) {
-        p.add(w);
-        p.end();
-    }
     std::vector<uint8_t> st(wires.size());
-    if (!wires.empty())
-        check(ics_ipv4_tcp_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, p.n(), ICS_MODE_VERIFY, nullptr,
-                                      nullptr, st.data()),
-              "ics_ipv4_tcp_batch_host");
+    if (wires.empty()) return st;
+    const auto off = pack(
+        wires.size(), [&](size_t i) { return wires[i].size(); },
+        [&](size_t i, uint8_t* d) { std::memcpy(d, wires[i].data(), wires[i].size()); });
+    check(ics_ipv4_tcp_batch_host(ctx_, scratch_, off.data(), 0, 0, wires.size(), ICS_MODE_VERIFY, nullptr, nullptr,
+                                  st.data()),
+          "ics_ipv4_tcp_batch_host");
     return st;
 }
 

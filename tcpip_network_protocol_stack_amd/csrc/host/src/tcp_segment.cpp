@@ -52,6 +52,8 @@ void header_bytes(const TCPSegment& s, char* b)
 namespace icsum::detail {
 uint32_t raw_of(const Wrap32& w) { return WrapRaw{w}.raw(); }
 
+void tcp_header_bytes(const TCPSegment& seg, char* b) { header_bytes(seg, b); }
+
 void parse_tcp_fields(Parser& parser, TCPSegment& seg)
 {
     uint32_t raw32 = 0;

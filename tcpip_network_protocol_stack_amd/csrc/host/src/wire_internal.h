@@ -19,6 +19,8 @@ void parse_tcp_fields(Parser& parser, TCPSegment& seg);
 // the payload is copied once
 bool parse_tcp_fields(std::string_view bytes, TCPSegment& seg);
 uint32_t raw_of(const Wrap32& w);
+// the 20 header bytes TCPSegment::serialize emits first (tcp_segment.cpp:76-106)
+void tcp_header_bytes(const TCPSegment& seg, char* b);
 
 // tcp_over_ip.cpp:14-29 — before any TCP byte is looked at: a connected
 // adapter only takes datagrams from its peer to itself, and only TCP

@@ -307,6 +307,39 @@ int main(int argc, char** argv)
                     double(passes) * double(arena.bytes()) / sec / 1e9, ok);
         return ok == (passes + 1) * arena.size() ? 0 : 2;
     }
+    if (argc > 2 && std::string(argv[2]) == "csum") {
+        // BatchEngine::checksum over 16 Ki 1480-byte segments and
+        // compute_checksums over 16 Ki TCP segments (1460-byte payloads)
+        icsum::BatchEngine eng(0);
+        std::mt19937_64 rng(0x1074);
+        const size_t n = size_t(1) << 14;
+        std::vector<std::string> raw(n, std::string(1480, '\0'));
+        for (auto& r : raw)
+            for (auto& c : r) c = static_cast<char>(rng());
+        std::vector<std::string_view> views(raw.begin(), raw.end());
+        std::vector<TCPSegment> segs(n);
+        std::vector<IPv4Header> hdrs(n);
+        for (size_t i = 0; i < n; ++i) {
+            segs[i].message.sender.payload = raw[i].substr(0, 1460);
+            segs[i].message.sender.seqno = Wrap32{static_cast<uint32_t>(rng())};
+            hdrs[i].src = static_cast<uint32_t>(rng());
+            hdrs[i].dst = static_cast<uint32_t>(rng());
+            hdrs[i].len = 1500;
+        }
+        size_t sink = eng.checksum(views).size();
+        eng.compute_checksums(segs, hdrs);
+        auto t0 = std::chrono::steady_clock::now();
+        for (size_t p = 0; p < passes; ++p) sink += eng.checksum(views)[p % n];
+        const double s1 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        t0 = std::chrono::steady_clock::now();
+        for (size_t p = 0; p < passes; ++p) eng.compute_checksums(segs, hdrs);
+        const double s2 = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("{\"mode\": \"csum\", \"passes\": %zu, \"segments\": %zu, \"ms_per_checksum\": %.3f, "
+                    "\"ms_per_compute_checksums\": %.3f, \"GB_s_checksum\": %.3f, \"sink\": %zu}\n",
+                    passes, n, s1 * 1e3 / double(passes), s2 * 1e3 / double(passes),
+                    double(passes) * double(n) * 1480.0 / s1 / 1e9, sink);
+        return 0;
+    }
     if (argc > 2 && std::string(argv[2]) == "wrap") {
         // transmit side without a socket: BatchEngine::wrap of 16 Ki messages
         // (1460-byte payloads) per call — payloads into the DMA arena, GPU
