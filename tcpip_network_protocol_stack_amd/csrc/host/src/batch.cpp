@@ -19,18 +19,6 @@ void check(int rc, const char* what)
     if (rc != ICS_OK) throw std::runtime_error(std::string(what) + ": " + ics_last_error());
 }
 
-// contiguous wire bytes of many pieces-lists with n+1 offsets
-struct Packed
-{
-    std::string bytes{};
-    std::vector<uint64_t> off{0};
-
-    void begin() {}
-    void add(std::string_view s) { bytes.append(s); }
-    void end() { off.push_back(bytes.size()); }
-    uint64_t n() const { return off.size() - 1; }
-};
-
 }  // namespace
 
 ics_tcp_msg wrap_fields(const FdAdapterConfig& cfg, const TCPMessage& msg)
@@ -128,17 +116,20 @@ void BatchEngine::compute_checksums(std::span<TCPSegment> segs, std::span<const 
 
 void BatchEngine::compute_checksums(std::span<IPv4Header> hdrs)
 {
-    Packed p;
-    for (auto& h : hdrs) {
-        h.cksum = 0;
-        p.add(serialize(h).front());  // throws "wrong IP version" like the reference
-        p.end();
-    }
+    if (hdrs.empty()) return;
+    for (auto& h : hdrs)
+        if (h.ver != 4) throw std::runtime_error("wrong IP version");  // serialize() would, like the reference
+    const auto off = pack(
+        hdrs.size(), [](size_t) { return size_t(IPv4Header::LENGTH); },
+        [&](size_t i, uint8_t* d) {
+            hdrs[i].cksum = 0;
+            const std::string b = serialize(hdrs[i]).front();
+            std::memcpy(d, b.data(), IPv4Header::LENGTH);
+        });
     std::vector<uint16_t> ip(hdrs.size());
-    if (!hdrs.empty())
-        check(ics_ipv4_tcp_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, p.n(), ICS_MODE_COMPUTE, ip.data(),
-                                      nullptr, nullptr),
-              "ics_ipv4_tcp_batch_host");
+    check(ics_ipv4_tcp_batch_host(ctx_, scratch_, off.data(), 0, 0, hdrs.size(), ICS_MODE_COMPUTE, ip.data(), nullptr,
+                                  nullptr),
+          "ics_ipv4_tcp_batch_host");
     for (size_t i = 0; i < hdrs.size(); ++i) hdrs[i].cksum = ip[i];
 }
 
@@ -231,27 +222,48 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap(TCPOverIPv4Adapter& a
                                                            std::span<const InternetDatagram> dgrams)
 {
     // TCPSegment::parse's checksum (value() of pseudo + all payload bytes) on
-    // the GPU for the whole batch, then field parsing + filters in order
-    Packed p;
-    std::vector<uint32_t> init(dgrams.size());
-    for (size_t i = 0; i < dgrams.size(); ++i) {
-        for (const auto& piece : dgrams[i].payload) p.add(piece);
-        p.end();
-        init[i] = dgrams[i].header.pseudo_checksum();
-    }
-    std::vector<uint16_t> v(dgrams.size());
-    if (!dgrams.empty())
-        check(ics_checksum_batch_host(ctx_, p.bytes.data(), p.off.data(), 0, 0, init.data(), v.data(), p.n()),
-              "ics_checksum_batch_host");
-    std::vector<std::optional<TCPMessage>> out(dgrams.size());
-    for (size_t i = 0; i < dgrams.size(); ++i) {
+    // the GPU for the whole batch (each datagram's payload pieces written into
+    // the page-locked arena on the engine workers), then the field parse of
+    // every datagram that passed (pure: on the workers, one payload copy out
+    // of the arena) and the adapter's gates in datagram order on this thread
+    const size_t n = dgrams.size();
+    std::vector<std::optional<TCPMessage>> out(n);
+    if (n == 0) return out;
+    std::vector<uint32_t> init(n);
+    const auto off = pack(
+        n,
+        [&](size_t i) {
+            size_t b = 0;
+            for (const auto& piece : dgrams[i].payload) b += piece.size();
+            return b;
+        },
+        [&](size_t i, uint8_t* d) {
+            for (const auto& piece : dgrams[i].payload) {
+                std::memcpy(d, piece.data(), piece.size());
+                d += piece.size();
+            }
+            init[i] = dgrams[i].header.pseudo_checksum();
+        });
+    std::vector<uint16_t> v(n);
+    check(ics_checksum_batch_host(ctx_, scratch_, off.data(), 0, 0, init.data(), v.data(), n),
+          "ics_checksum_batch_host");
+    struct Parsed
+    {
+        bool ok = false;
+        TCPSegment seg{};
+    };
+    std::vector<Parsed> parsed(n);
+    ranges(n, [&](size_t i0, size_t i1) {
+        for (size_t i = i0; i < i1; ++i)
+            if (v[i] == 0)
+                parsed[i].ok = detail::parse_tcp_fields(
+                    std::string_view{reinterpret_cast<const char*>(scratch_) + off[i], off[i + 1] - off[i]},
+                    parsed[i].seg);
+    });
+    for (size_t i = 0; i < n; ++i) {
         const IPv4Header& h = dgrams[i].header;
-        if (!detail::ip_gate(adapter, h) || v[i] != 0) continue;
-        TCPSegment seg;
-        Parser parser{dgrams[i].payload};
-        detail::parse_tcp_fields(parser, seg);
-        if (parser.has_error()) continue;
-        out[i] = detail::tcp_gate(adapter, h, seg);
+        if (!detail::ip_gate(adapter, h) || v[i] != 0 || !parsed[i].ok) continue;
+        out[i] = detail::tcp_gate(adapter, h, std::move(parsed[i].seg));
     }
     return out;
 }
@@ -259,12 +271,11 @@ std::vector<std::optional<TCPMessage>> BatchEngine::unwrap(TCPOverIPv4Adapter& a
 std::vector<std::optional<TCPMessage>> BatchEngine::unwrap_raw(TCPOverIPv4Adapter& adapter,
                                                                std::span<const std::string_view> wires)
 {
-    Packed p;
-    for (auto w : wires) {
-        p.add(w);
-        p.end();
-    }
-    return unwrap_packed(adapter, reinterpret_cast<const uint8_t*>(p.bytes.data()), p.off.data(), p.n());
+    if (wires.empty()) return {};
+    const auto off = pack(
+        wires.size(), [&](size_t i) { return wires[i].size(); },
+        [&](size_t i, uint8_t* d) { std::memcpy(d, wires[i].data(), wires[i].size()); });
+    return unwrap_packed(adapter, scratch_, off.data(), wires.size());
 }
 
 std::vector<uint8_t> BatchEngine::verify_packed(const uint8_t* bytes, const uint64_t* offsets, size_t n)

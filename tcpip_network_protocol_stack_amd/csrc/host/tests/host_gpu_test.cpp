@@ -172,6 +172,13 @@ int main()
             ++accepted;
             EXPECT(got[i]->sender.payload == want->sender.payload);
             EXPECT(got[i]->sender.SYN == want->sender.SYN && got[i]->sender.FIN == want->sender.FIN);
+            if (ip_ok[i] && got2[i]) {  // unwrap(InternetDatagram) — the same message, field by field
+                EXPECT(got2[i]->sender.payload == want->sender.payload);
+                EXPECT(got2[i]->sender.seqno == want->sender.seqno && got2[i]->receiver.ackno == want->receiver.ackno);
+                EXPECT(got2[i]->sender.SYN == want->sender.SYN && got2[i]->sender.FIN == want->sender.FIN &&
+                       got2[i]->sender.RST == want->sender.RST);
+                EXPECT(got2[i]->receiver.window_size == want->receiver.window_size);
+            }
         }
     }
     EXPECT(accepted >= wires.size() / 2);
