@@ -87,6 +87,9 @@ struct ics_ctx {
   // re-plans behind its launch (stats + plan kernels), so a changed mix is
   // noticed within kPlanRefresh calls
   static constexpr uint32_t kPlanRefresh = 16;
+  // offsets batches from this many segments up (below the binning threshold)
+  // take their single launch's geometry from the cached plan
+  static constexpr uint64_t kSmallPlanMin = 16384;
   bool plan_cache = true;
   uint64_t* plan_host = nullptr;      // host view
   uint64_t* plan_host_dev = nullptr;  // the device's pointer to it
@@ -248,10 +251,56 @@ bool forced_geometry(const ics_ctx* ctx) {
 // into length bins on the device (two passes over the offsets), and every bin
 // runs with the geometry that suits its lengths; the bin lists live in
 // stream-ordered scratch, so concurrent calls on different streams are safe.
+// The plan the device reported for the last call with this offsets pointer
+// and n (ics_ctx::plan_host); any_plan = false accepts only the whole-batch
+// plans.  A miss makes this call's batch the cache key.
+bool plan_lookup(ics_ctx* ctx, const icsum::SegSpec& sp, bool any_plan, uint32_t* plan, bool* refresh) {
+  std::lock_guard<std::mutex> lock(ctx->plan_mu);
+  const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
+  const uint32_t p = uint32_t(v & 0xffu);
+  const bool whole = p == icsum::kPlanWholeBatch || p == icsum::kPlanWholeBatch16 || p == icsum::kPlanWholeBatchSmall;
+  if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && (v >> 8) == sp.n && (whole || any_plan)) {
+    *plan = p;
+    *refresh = ++ctx->plan_hits % ics_ctx::kPlanRefresh == 0;
+    return true;
+  }
+  ctx->plan_key = sp.offsets;
+  ctx->plan_key_n = sp.n;
+  ctx->plan_hits = 0;
+  return false;
+}
+
+// stats + plan kernels only (no lists) behind a launch: the plan for the next
+// call with the same offsets lands in ics_ctx::plan_host
+int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, hipStream_t st) {
+  Scratch meta(ctx, (icsum::kBinMetaBytesTotal + 255) & ~size_t(255), st);
+  ICS_HIP(meta.error());
+  ICS_HIP(icsum::launch_bin_plan(sp.offsets, sp.n, static_cast<uint32_t*>(meta.get()), lps, ctx->plan_host_dev, st));
+  return ICS_OK;
+}
+
 int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                     void* d_out, int out_kind, hipStream_t st) {
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
                       (ctx->bin == 1 || (ctx->bin < 0 && sp.n >= ctx->bin_min && !forced_geometry(ctx)));
+  const bool plannable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_cache && ctx->plan_host;
+  if (!binned && sp.offsets && plannable && !forced_geometry(ctx) && sp.n >= ics_ctx::kSmallPlanMin) {
+    // an offsets batch below the binning threshold: one launch, its geometry
+    // from the plan the device reported for this batch last time (16-lane
+    // groups for MTU-sized mixes, the small-segment body for short ones);
+    // on a miss the unknown-mix geometry, and the plan kernels run behind
+    // the launch for the next call (tools/ab_small_offsets.py)
+    uint32_t plan = 0;
+    bool refresh = false;
+    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh);
+    icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len, sp.n, 0));
+    if (hit && plan == icsum::kPlanWholeBatch16) g = {16, 8, true, 3, 1};
+    if (hit && plan == icsum::kPlanWholeBatchSmall) g = {4, 2, true, 2, 2};
+    ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
+    if (!hit || refresh)
+      if (int rc = replan(ctx, sp, 64, st)) return rc;
+    return ICS_OK;
+  }
   if (!binned) {
     // dense fixed-stride batch of short segments (config 3): the flat kernel
     if (!d_odd && ctx->dense_segs > 0 && !forced_geometry(ctx) && icsum::dense_supported(sp)) {
@@ -272,26 +321,11 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   const uint32_t lps = ctx->last_bin_lps ? ctx->last_bin_lps : (sp.n > (uint64_t(1) << 20) ? 32u : 64u);
   if (lps == 32) g_last = {32, 8, true, 3, 1};
   const uint32_t last_blocks = ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks;
-  const bool cacheable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_cache && ctx->plan_host;
+  const bool cacheable = plannable;
   if (cacheable) {
-    bool hit = false, refresh = false;
     uint32_t hit_plan = 0;
-    {
-      std::lock_guard<std::mutex> lock(ctx->plan_mu);
-      const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
-      const uint32_t plan = uint32_t(v & 0xffu);
-      if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && (v >> 8) == sp.n &&
-          (plan == icsum::kPlanWholeBatch || plan == icsum::kPlanWholeBatch16 || plan == icsum::kPlanWholeBatchSmall)) {
-        hit = true;
-        hit_plan = plan;
-        refresh = ++ctx->plan_hits % ics_ctx::kPlanRefresh == 0;
-      } else {
-        ctx->plan_key = sp.offsets;
-        ctx->plan_key_n = sp.n;
-        ctx->plan_hits = 0;
-      }
-    }
-    if (hit) {
+    bool refresh = false;
+    if (plan_lookup(ctx, sp, false, &hit_plan, &refresh)) {
       // the whole-batch plan the device chose for this batch last time, as
       // its single launch: the last bin's geometry (whole), 16-lane groups
       // (whole16) or the small-segment body (wholeS) over every segment
@@ -300,15 +334,10 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
                                                                               : g_last;
       ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_hit,
                                      hit_plan == icsum::kPlanWholeBatch ? last_blocks : ctx->max_blocks, st));
-      if (refresh) {
-        // re-plan behind it (stats + plan kernels only, no lists): a batch
-        // whose mix changed under the same pointer and size is re-binned
-        // from the next call on
-        Scratch meta(ctx, (icsum::kBinMetaBytesTotal + 255) & ~size_t(255), st);
-        ICS_HIP(meta.error());
-        ICS_HIP(icsum::launch_bin_plan(sp.offsets, sp.n, static_cast<uint32_t*>(meta.get()), lps,
-                                       ctx->plan_host_dev, st));
-      }
+      // re-plan behind it: a batch whose mix changed under the same pointer
+      // and size is re-binned from the next call on
+      if (refresh)
+        if (int rc = replan(ctx, sp, lps, st)) return rc;
       return ICS_OK;
     }
   }

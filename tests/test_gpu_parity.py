@@ -267,6 +267,40 @@ def test_auto_plan_cache_repeated_and_changed_mix(engine, orc):
         assert (_u16(engine.checksum_batch(dbuf, offsets=doff)) == want2).all(), k
 
 
+@pytest.mark.parametrize("mix", ["acks", "mtu", "bimodal", "long"])
+def test_small_offsets_batch_plan_cache(engine, orc, mix):
+    """Offsets batches below the binning threshold (16 Ki <= n < 64 Ki) take
+    their single launch's geometry from the plan cached for the same offsets
+    buffer (the plan kernels run behind the first and every 16th launch): 40
+    repeated calls, then the same buffer rewritten with another mix; every
+    output equals the oracle's."""
+    import torch
+
+    rng = np.random.default_rng(0x5A + len(mix))
+    n = 20_000
+    lens = {"bimodal": np.where(rng.random(n) < 0.5, 40, 1460) + rng.integers(0, 4, n),
+            "acks": rng.integers(40, 44, n), "mtu": rng.integers(1460, 1464, n),
+            "long": rng.integers(4096, 9000, n)}[mix]
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    lens2 = rng.integers(40, 9000, n)  # another mix, later, under the same pointer and n
+    off2 = np.zeros(n + 1, dtype=np.uint64)
+    off2[1:] = np.cumsum(lens2)
+    buf = rng.integers(0, 256, int(max(off[-1], off2[-1])) + 16, dtype=np.uint8)  # holds both mixes
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = orc.checksum_batch(buf, n, offsets=off, init=init)
+    dbuf, doff, dinit = _t(buf), _t(off), _t(init)
+    for k in range(40):
+        out = engine.checksum_batch(dbuf, offsets=doff, init=dinit)
+        if k % 9 == 0:
+            torch.cuda.synchronize()
+        assert (_u16(out) == want).all(), (mix, k)
+    doff.copy_(_t(off2))
+    want2 = orc.checksum_batch(buf, n, offsets=off2, init=init)
+    for k in range(20):
+        assert (_u16(engine.checksum_batch(dbuf, offsets=doff, init=dinit)) == want2).all(), (mix, k)
+
+
 @pytest.mark.parametrize("mix", ["bimodal", "acks", "mtu", "long"])
 def test_auto_plan_cache_every_whole_plan(engine, orc, mix):
     """Batches whose device plan is each of the whole-batch plans (whole,

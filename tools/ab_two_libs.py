@@ -71,6 +71,16 @@ def cases_for(names, engines, dev):
             for tag, e in engines.items():
                 cases[f"{nm}_{tag}"] = (lambda e, ds, inits, out16, n, L: lambda i: e.checksum_batch(
                     ds[i % R], n=n, stride=L, seg_len=L, init=inits[i % R], out=out16))(e, ds, inits, out16, n, L)
+    if "smalloff" in names:  # device offsets batches below the binning threshold
+        for n, L in ((8192, 1500), (16384, 576), (16384, 1500), (32768, 1500), (65535, 576)):
+            R = max(2, (400 << 20) // (n * L) + 1)
+            doff = torch.from_numpy(np.arange(n + 1, dtype=np.int64) * L).to(dev)
+            ds = [new.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), 9, pos0=r * n * L)
+                  for r in range(R)]
+            keep.append((doff, ds))
+            for tag, e in engines.items():
+                cases[f"off{n}x{L}_{tag}"] = (lambda e, ds, doff, R: lambda i: e.checksum_batch(
+                    ds[i % R], offsets=doff, out=o[0]))(e, ds, doff, R)
     if "host" in names:  # PCIe-inclusive: pageable and pinned host batches, 256 Ki x 1500 B
         n, L = 1 << 18, 1500
         for pinned in (False, True):
