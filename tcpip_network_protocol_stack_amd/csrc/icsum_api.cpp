@@ -90,6 +90,9 @@ struct ics_ctx {
   // offsets batches from this many segments up (below the binning threshold)
   // take their single launch's geometry from the cached plan
   static constexpr uint64_t kSmallPlanMin = 16384;
+  // ics_ipv4_tcp_batch: from this share of <= 144-byte datagrams (sixteenths,
+  // the plan word's bits 4-7) an offsets batch runs 8-lane groups
+  static constexpr uint32_t kIpv4ShortMix16 = 5;
   bool plan_cache = true;
   uint64_t* plan_host = nullptr;      // host view
   uint64_t* plan_host_dev = nullptr;  // the device's pointer to it
@@ -253,11 +256,14 @@ bool forced_geometry(const ics_ctx* ctx) {
 // stream-ordered scratch, so concurrent calls on different streams are safe.
 // The plan the device reported for the last call with this offsets pointer
 // and n (ics_ctx::plan_host); any_plan = false accepts only the whole-batch
-// plans.  A miss makes this call's batch the cache key.
-bool plan_lookup(ics_ctx* ctx, const icsum::SegSpec& sp, bool any_plan, uint32_t* plan, bool* refresh) {
+// plans; short16 (optional) receives the share of <= 144-byte segments in
+// sixteenths (k_bin_plan).  A miss makes this call's batch the cache key.
+bool plan_lookup(ics_ctx* ctx, const icsum::SegSpec& sp, bool any_plan, uint32_t* plan, bool* refresh,
+                 uint32_t* short16 = nullptr) {
   std::lock_guard<std::mutex> lock(ctx->plan_mu);
   const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
-  const uint32_t p = uint32_t(v & 0xffu);
+  const uint32_t p = uint32_t(v & 0xfu);
+  if (short16) *short16 = uint32_t(v >> 4) & 0xfu;
   const bool whole = p == icsum::kPlanWholeBatch || p == icsum::kPlanWholeBatch16 || p == icsum::kPlanWholeBatchSmall;
   if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && (v >> 8) == sp.n && (whole || any_plan)) {
     *plan = p;
@@ -850,10 +856,33 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   // most 64 KiB and mostly MTU-sized, and the 16-lane line grid is the best
   // measured geometry for both 1500- and 9000-byte datagrams (64 Ki x 1500 B:
   // 18.3 us vs 48.8 us with the 64-lane default; tools/ab_ipv4_offsets.py)
-  const icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1500 : dgram_len));
-  ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt,
-                                 static_cast<hipStream_t>(stream)));
-  return bounds_verdict(static_cast<hipStream_t>(stream), ICS_OK);
+  icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1500 : dgram_len));
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  // a receive batch of mostly short datagrams (pure ACKs: 40 bytes) leaves
+  // most of a 16-lane group idle: from 16 Ki datagrams up the geometry
+  // follows the plan the device reported for the same offsets buffer last
+  // time (4-lane groups when it was the small-segment plan, 8-lane groups
+  // from 5/16 of <= 144-byte datagrams, 16 x 4 below that), the plan
+  // kernels running behind the first and every 16th launch (DESIGN.md §4,
+  // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
+  bool plan_after = false;
+  if (d_offsets && ctx->plan_cache && ctx->plan_host && !forced_geometry(ctx) && n >= ics_ctx::kSmallPlanMin &&
+      n <= 0xFFFFFFFFull) {
+    uint32_t plan = 0, short16 = 0;
+    bool refresh = false;
+    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &short16);
+    if (hit && plan == icsum::kPlanWholeBatchSmall)
+      g = ipv4_geometry({4, 2, true, 2, 1});
+    else if (hit && short16 >= ics_ctx::kIpv4ShortMix16)
+      g = ipv4_geometry({8, 8, true, 3, 1});  // ACK + MTU mixes: half the idle lanes on the ACKs
+    else if (hit)
+      g = ipv4_geometry({16, 4, true, 3, 1});  // MTU + a few ACKs: shorter unroll, 1-4 % (1 M datagrams)
+    plan_after = !hit || refresh;
+  }
+  ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt, st));
+  if (plan_after)
+    if (int rc = replan(ctx, sp, 64, st)) return rc;
+  return bounds_verdict(st, ICS_OK);
 }
 
 namespace {

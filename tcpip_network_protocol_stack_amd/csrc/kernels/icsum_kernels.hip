@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint64_t waves = n * last_lps / 64;  // the last bin's launch
-    uint64_t total = 0, t_split = 26000 + waves * 53 / 1000, t16 = (waves - n / 4) * 53 / 1000,
+    uint64_t total = 0, short_n = 0, t_split = 26000 + waves * 53 / 1000, t16 = (waves - n / 4) * 53 / 1000,
              t_small = (waves - n / 32) * 53 / 1000;
 #pragma unroll
     for (int k = 0; k < kBins; ++k) {
@@ -180,6 +180,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
         v += wb[q][k];
       }
       meta[kBinMetaCount + k] = c;
+      if (k == 0) short_n = c;
       total += v;
       const uint64_t tb = v / (k == kBins - 1 ? 6400 : 5000), tn = c / 10;
       t_split += tb > tn ? tb : tn;
@@ -199,9 +200,11 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       if (t_small < best) plan = kPlanWholeSmall;
     }
     meta[kBinMetaPlan] = plan;
-    // the host's plan cache (icsum_api.cpp): batch size and plan, one 8-byte
-    // store to page-locked host memory
-    if (plan_out) *plan_out = (n << 8) | plan;
+    // the host's plan cache (icsum_api.cpp): batch size, the share of bin-0
+    // (<= 144-byte) segments in sixteenths (bits 4-7) and the plan (bits
+    // 0-3), one 8-byte store to page-locked host memory
+    const uint64_t short16 = n ? short_n * 16 / n : 0;
+    if (plan_out) *plan_out = (n << 8) | ((short16 < 15 ? short16 : 15) << 4) | plan;
   }
 }
 

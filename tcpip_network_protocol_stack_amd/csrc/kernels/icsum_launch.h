@@ -62,7 +62,8 @@ constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks
 // batch in 16-lane groups, 3 whole batch through the small-segment body (tests); last_lps: lanes per segment of the last
 // bin's launch (its wave count enters the plan's cost model)
 // plan_out (nullable, device-visible page-locked host memory): the plan
-// kernel stores (n << 8) | plan there for the host's plan cache
+// kernel stores (n << 8) | (share of <= 144-byte segments in sixteenths << 4)
+// | plan there for the host's plan cache
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
                                uint32_t last_lps, uint64_t* plan_out, hipStream_t st);
 // k_bin_plan's whole-batch plans (the split plan is 1)

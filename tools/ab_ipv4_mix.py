@@ -72,7 +72,8 @@ def batch(eng, n, ack_frac, seed):
 def main():
     eng = Engine(0)
     forced = {f"{l}x{u}m{m}": engine_with(l, u, m) for l, u, m in ((4, 2, 2), (8, 2, 2), (8, 8, 3), (16, 4, 3))}
-    for ack_frac in (0.5, 0.0):
+    fracs = [float(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else (0.5, 0.0)
+    for ack_frac in fracs:
         n = 1 << 20
         d, doff, nbytes = batch(eng, n, ack_frac, 7)
         ip = torch.empty(n, dtype=torch.int16, device="cuda")

@@ -51,9 +51,10 @@ def cases_for(names, engines, dev):
         keep.append(bufs)
         for tag, e in engines.items():
             for mode, mn in ((0, "compute"), (1, "verify")):
-                cases[f"cfg2_{mn}_{tag}"] = (lambda e, mode: lambda i: e.ipv4_tcp_batch(
+                # every value bound now: later blocks rebind n / L / R
+                cases[f"cfg2_{mn}_{tag}"] = (lambda e, mode, bufs=bufs, n=n, L=L, R=R: lambda i: e.ipv4_tcp_batch(
                     bufs[i % R], mode, n=n, stride=L, dgram_len=L, ip_ck=o[0], tcp_ck=o[1], status=o[2]))(e, mode)
-    for nm, af in (("ipv4_off", 0.0), ("ipv4_mix", 0.5)):
+    for nm, af in (("ipv4_off", 0.0), ("ipv4_mix", 0.5), ("ipv4_acks", 1.0)):
         if nm in names:
             d, doff, _ = batch(new, 1 << 20, af, 7)
             keep.append((d, doff))
@@ -69,7 +70,7 @@ def cases_for(names, engines, dev):
             out16 = torch.empty(n, dtype=torch.int16, device=dev)
             keep.append((ds, inits, out16))
             for tag, e in engines.items():
-                cases[f"{nm}_{tag}"] = (lambda e, ds, inits, out16, n, L: lambda i: e.checksum_batch(
+                cases[f"{nm}_{tag}"] = (lambda e, ds, inits, out16, n, L, R=R: lambda i: e.checksum_batch(
                     ds[i % R], n=n, stride=L, seg_len=L, init=inits[i % R], out=out16))(e, ds, inits, out16, n, L)
     if "smalloff" in names:  # device offsets batches below the binning threshold
         for n, L in ((8192, 1500), (16384, 576), (16384, 1500), (32768, 1500), (65535, 576)):
@@ -89,9 +90,9 @@ def cases_for(names, engines, dev):
             keep.append(h)
             for tag, e in engines.items():
                 nm = "pinned" if pinned else "pageable"
-                cases[f"host_{nm}_{tag}"] = (lambda e, h: lambda i: e.checksum_batch_host(h, n, stride=L,
-                                                                                          seg_len=L))(e, h)
-                cases[f"hostpatch_{nm}_{tag}"] = (lambda e, h: lambda i: e.ipv4_tcp_batch_host(
+                cases[f"host_{nm}_{tag}"] = (lambda e, h, n=n, L=L: lambda i: e.checksum_batch_host(
+                    h, n, stride=L, seg_len=L))(e, h)
+                cases[f"hostpatch_{nm}_{tag}"] = (lambda e, h, n=n, L=L: lambda i: e.ipv4_tcp_batch_host(
                     h, n, 2, stride=L, dgram_len=L))(e, h)
         from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE
 
@@ -104,7 +105,7 @@ def cases_for(names, engines, dev):
             keep.append(h)
             for tag, e in engines.items():
                 nm = "pinned" if pinned else "pageable"
-                cases[f"hostwrap_{nm}_{tag}"] = (lambda e, h: lambda i: e.tcp_wrap_batch_host(
+                cases[f"hostwrap_{nm}_{tag}"] = (lambda e, h, n=n, W=W: lambda i: e.tcp_wrap_batch_host(
                     h, m, n, stride=W, dgram_len=W))(e, h)
     return cases, keep
 
