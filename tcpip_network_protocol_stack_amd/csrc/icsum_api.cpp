@@ -93,6 +93,8 @@ struct ics_ctx {
   // ics_ipv4_tcp_batch: from this share of <= 144-byte datagrams (sixteenths,
   // the plan word's bits 4-7) an offsets batch runs 8-lane groups
   static constexpr uint32_t kIpv4ShortMix16 = 5;
+  // the plain checksum's 8-lane threshold (short_mix)
+  static constexpr uint32_t kShortMix16 = 7;
   bool plan_cache = true;
   uint64_t* plan_host = nullptr;      // host view
   uint64_t* plan_host_dev = nullptr;  // the device's pointer to it
@@ -256,16 +258,21 @@ bool forced_geometry(const ics_ctx* ctx) {
 // stream-ordered scratch, so concurrent calls on different streams are safe.
 // The plan the device reported for the last call with this offsets pointer
 // and n (ics_ctx::plan_host); any_plan = false accepts only the whole-batch
-// plans; short16 (optional) receives the share of <= 144-byte segments in
-// sixteenths (k_bin_plan).  A miss makes this call's batch the cache key.
+// plans.  The mix (optional) receives the shares k_bin_plan reported, in
+// sixteenths: segments of <= 144 bytes, and bytes in segments over 1920
+// bytes.  A miss makes this call's batch the cache key.
+struct PlanMix {
+  uint32_t short16 = 0, long16 = 0;
+};
 bool plan_lookup(ics_ctx* ctx, const icsum::SegSpec& sp, bool any_plan, uint32_t* plan, bool* refresh,
-                 uint32_t* short16 = nullptr) {
+                 PlanMix* mix = nullptr) {
   std::lock_guard<std::mutex> lock(ctx->plan_mu);
   const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
   const uint32_t p = uint32_t(v & 0xfu);
-  if (short16) *short16 = uint32_t(v >> 4) & 0xfu;
+  if (mix) *mix = {uint32_t(v >> 4) & 0xfu, uint32_t(v >> 40) & 0xfu};
   const bool whole = p == icsum::kPlanWholeBatch || p == icsum::kPlanWholeBatch16 || p == icsum::kPlanWholeBatchSmall;
-  if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && (v >> 8) == sp.n && (whole || any_plan)) {
+  const bool same_n = (v >> 44) == 0 && ((v >> 8) & 0xFFFFFFFFull) == sp.n;  // ~0: nothing reported yet
+  if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && same_n && (whole || any_plan)) {
     *plan = p;
     *refresh = ++ctx->plan_hits % ics_ctx::kPlanRefresh == 0;
     return true;
@@ -285,6 +292,13 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, hipStream_t st)
   return ICS_OK;
 }
 
+// a batch mostly of short segments with (almost) no bytes in long ones: from
+// 7/16 <= 144-byte segments and under 1/16 of the bytes in segments over 1920
+// bytes, 8-lane groups beat both the binned launches and 16-lane groups
+// (1 M datagrams, 50 % / 75 % 40-byte ACKs + 1500 B: 139.5 / 107.4 us vs
+// 146.0 / 125.6 us AUTO; profiles/r2_csum_mix_sweep.jsonl)
+bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
+
 int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                     void* d_out, int out_kind, hipStream_t st) {
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
@@ -297,10 +311,12 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     // on a miss the unknown-mix geometry, and the plan kernels run behind
     // the launch for the next call (tools/ab_small_offsets.py)
     uint32_t plan = 0;
+    PlanMix mix;
     bool refresh = false;
-    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh);
+    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &mix);
     icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len, sp.n, 0));
     if (hit && plan == icsum::kPlanWholeBatch16) g = {16, 8, true, 3, 1};
+    if (hit && plan != icsum::kPlanWholeBatchSmall && short_mix(mix)) g = {8, 8, true, 3, 1};
     if (hit && plan == icsum::kPlanWholeBatchSmall) g = {4, 2, true, 2, 2};
     ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
     if (!hit || refresh)
@@ -330,16 +346,22 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   const bool cacheable = plannable;
   if (cacheable) {
     uint32_t hit_plan = 0;
+    PlanMix mix;
     bool refresh = false;
-    if (plan_lookup(ctx, sp, false, &hit_plan, &refresh)) {
+    const bool hit = plan_lookup(ctx, sp, true, &hit_plan, &refresh, &mix);
+    const bool mix8 = hit && hit_plan != icsum::kPlanWholeBatchSmall && short_mix(mix);
+    if (hit && (hit_plan != icsum::kPlanSplitBins || mix8)) {
       // the whole-batch plan the device chose for this batch last time, as
       // its single launch: the last bin's geometry (whole), 16-lane groups
-      // (whole16) or the small-segment body (wholeS) over every segment
-      const icsum::Geometry g_hit = hit_plan == icsum::kPlanWholeBatch16      ? icsum::Geometry{16, 8, true, 3, 1}
+      // (whole16) or the small-segment body (wholeS) over every segment; a
+      // short-heavy mix with no long segments (received traffic: ACKs + MTU
+      // data) runs 8-lane groups whatever the plan (tools/ab_ipv4_mix.py)
+      const icsum::Geometry g_hit = mix8                                        ? icsum::Geometry{8, 8, true, 3, 1}
+                                    : hit_plan == icsum::kPlanWholeBatch16      ? icsum::Geometry{16, 8, true, 3, 1}
                                     : hit_plan == icsum::kPlanWholeBatchSmall ? icsum::Geometry{4, 2, true, 2, 2}
                                                                               : g_last;
       ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_hit,
-                                     hit_plan == icsum::kPlanWholeBatch ? last_blocks : ctx->max_blocks, st));
+                                     hit_plan == icsum::kPlanWholeBatch && !mix8 ? last_blocks : ctx->max_blocks, st));
       // re-plan behind it: a batch whose mix changed under the same pointer
       // and size is re-binned from the next call on
       if (refresh)
@@ -868,12 +890,13 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   bool plan_after = false;
   if (d_offsets && ctx->plan_cache && ctx->plan_host && !forced_geometry(ctx) && n >= ics_ctx::kSmallPlanMin &&
       n <= 0xFFFFFFFFull) {
-    uint32_t plan = 0, short16 = 0;
+    uint32_t plan = 0;
+    PlanMix mix;
     bool refresh = false;
-    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &short16);
+    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &mix);
     if (hit && plan == icsum::kPlanWholeBatchSmall)
       g = ipv4_geometry({4, 2, true, 2, 1});
-    else if (hit && short16 >= ics_ctx::kIpv4ShortMix16)
+    else if (hit && mix.short16 >= ics_ctx::kIpv4ShortMix16 && mix.long16 == 0)
       g = ipv4_geometry({8, 8, true, 3, 1});  // ACK + MTU mixes: half the idle lanes on the ACKs
     else if (hit)
       g = ipv4_geometry({16, 4, true, 3, 1});  // MTU + a few ACKs: shorter unroll, 1-4 % (1 M datagrams)

@@ -129,7 +129,7 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total)
 // 1429 / 1622 / 1682, 2 M bimodal 40+1460 B 525 / 473 / 364, 2 M x 4-6 KiB
 // 1515 / 1589 / 1593, 1 M x 1460 B 520 / 429 / 296, 1 M x 40 B 451 / 168 / 205.
 constexpr uint32_t kPlanWhole = 0, kPlanSplit = 1, kPlanWhole16 = 2, kPlanWholeSmall = 3;
-static_assert(kPlanWhole == kPlanWholeBatch && kPlanWhole16 == kPlanWholeBatch16 &&
+static_assert(kPlanWhole == kPlanWholeBatch && kPlanSplit == kPlanSplitBins && kPlanWhole16 == kPlanWholeBatch16 &&
               kPlanWholeSmall == kPlanWholeBatchSmall, "plan ids shared with the host's plan cache");
 
 __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta, const uint32_t* __restrict__ cnt_part,
@@ -168,7 +168,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint64_t waves = n * last_lps / 64;  // the last bin's launch
-    uint64_t total = 0, short_n = 0, t_split = 26000 + waves * 53 / 1000, t16 = (waves - n / 4) * 53 / 1000,
+    uint64_t total = 0, short_n = 0, long_bytes = 0, t_split = 26000 + waves * 53 / 1000, t16 = (waves - n / 4) * 53 / 1000,
              t_small = (waves - n / 32) * 53 / 1000;
 #pragma unroll
     for (int k = 0; k < kBins; ++k) {
@@ -181,6 +181,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       }
       meta[kBinMetaCount + k] = c;
       if (k == 0) short_n = c;
+      if (k >= 3) long_bytes += v;  // segments > 1920 bytes
       total += v;
       const uint64_t tb = v / (k == kBins - 1 ? 6400 : 5000), tn = c / 10;
       t_split += tb > tn ? tb : tn;
@@ -200,11 +201,14 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       if (t_small < best) plan = kPlanWholeSmall;
     }
     meta[kBinMetaPlan] = plan;
-    // the host's plan cache (icsum_api.cpp): batch size, the share of bin-0
-    // (<= 144-byte) segments in sixteenths (bits 4-7) and the plan (bits
-    // 0-3), one 8-byte store to page-locked host memory
-    const uint64_t short16 = n ? short_n * 16 / n : 0;
-    if (plan_out) *plan_out = (n << 8) | ((short16 < 15 ? short16 : 15) << 4) | plan;
+    // the host's plan cache (icsum_api.cpp), one 8-byte store to page-locked
+    // host memory: the plan (bits 0-3), the share of bin-0 (<= 144-byte)
+    // segments in sixteenths (bits 4-7), the batch size (bits 8-39) and the
+    // share of bytes in segments over 1920 bytes in sixteenths (bits 40-43)
+    const uint64_t short16 = n ? short_n * 16 / n : 0, long16 = total ? long_bytes * 16 / total : 0;
+    if (plan_out)
+      *plan_out = plan | ((short16 < 15 ? short16 : 15) << 4) | ((n & 0xFFFFFFFFull) << 8) |
+                  ((long16 < 15 ? long16 : 15) << 40);
   }
 }
 

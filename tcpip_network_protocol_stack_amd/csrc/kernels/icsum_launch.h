@@ -62,12 +62,13 @@ constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks
 // batch in 16-lane groups, 3 whole batch through the small-segment body (tests); last_lps: lanes per segment of the last
 // bin's launch (its wave count enters the plan's cost model)
 // plan_out (nullable, device-visible page-locked host memory): the plan
-// kernel stores (n << 8) | (share of <= 144-byte segments in sixteenths << 4)
-// | plan there for the host's plan cache
+// kernel stores the plan, n and two mix shares there for the host's plan
+// cache (k_bin_plan: plan bits 0-3, <= 144-byte segments in sixteenths 4-7,
+// n 8-39, bytes in segments over 1920 bytes in sixteenths 40-43)
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
                                uint32_t last_lps, uint64_t* plan_out, hipStream_t st);
-// k_bin_plan's whole-batch plans (the split plan is 1)
-constexpr uint32_t kPlanWholeBatch = 0, kPlanWholeBatch16 = 2, kPlanWholeBatchSmall = 3;
+// k_bin_plan's plans: the whole-batch ones and the split plan
+constexpr uint32_t kPlanWholeBatch = 0, kPlanSplitBins = 1, kPlanWholeBatch16 = 2, kPlanWholeBatchSmall = 3;
 // the stats + plan passes alone (no bin lists): a re-plan for the plan cache
 hipError_t launch_bin_plan(const uint64_t* offsets, uint64_t n, uint32_t* meta, uint32_t last_lps,
                            uint64_t* plan_out, hipStream_t st);

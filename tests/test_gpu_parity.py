@@ -267,7 +267,18 @@ def test_auto_plan_cache_repeated_and_changed_mix(engine, orc):
         assert (_u16(engine.checksum_batch(dbuf, offsets=doff)) == want2).all(), k
 
 
-@pytest.mark.parametrize("mix", ["acks", "mtu", "bimodal", "long"])
+def _mix_lengths(rng, n, mix):
+    """Segment lengths of the plan-cache tests' mixes: pure ACKs, MTU data,
+    half and three quarters 40-byte ACKs among MTU segments (the 8-lane
+    short-mix geometry), ACKs among jumbo segments (long bytes: not 8-lane)
+    and long segments."""
+    ack = lambda p, big: np.where(rng.random(n) < p, 40, big) + rng.integers(0, 4, n)  # noqa: E731
+    return {"bimodal": lambda: ack(0.5, 1460), "ackheavy": lambda: ack(0.75, 1460),
+            "ackjumbo": lambda: ack(0.75, 9000), "acks": lambda: rng.integers(40, 44, n),
+            "mtu": lambda: rng.integers(1460, 1464, n), "long": lambda: rng.integers(4096, 9000, n)}[mix]()
+
+
+@pytest.mark.parametrize("mix", ["acks", "mtu", "bimodal", "ackheavy", "ackjumbo", "long"])
 def test_small_offsets_batch_plan_cache(engine, orc, mix):
     """Offsets batches below the binning threshold (16 Ki <= n < 64 Ki) take
     their single launch's geometry from the plan cached for the same offsets
@@ -278,9 +289,7 @@ def test_small_offsets_batch_plan_cache(engine, orc, mix):
 
     rng = np.random.default_rng(0x5A + len(mix))
     n = 20_000
-    lens = {"bimodal": np.where(rng.random(n) < 0.5, 40, 1460) + rng.integers(0, 4, n),
-            "acks": rng.integers(40, 44, n), "mtu": rng.integers(1460, 1464, n),
-            "long": rng.integers(4096, 9000, n)}[mix]
+    lens = _mix_lengths(rng, n, mix)
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum(lens)
     lens2 = rng.integers(40, 9000, n)  # another mix, later, under the same pointer and n
@@ -301,26 +310,36 @@ def test_small_offsets_batch_plan_cache(engine, orc, mix):
         assert (_u16(engine.checksum_batch(dbuf, offsets=doff, init=dinit)) == want2).all(), (mix, k)
 
 
-@pytest.mark.parametrize("mix", ["bimodal", "acks", "mtu", "long"])
+@pytest.mark.parametrize("mix", ["bimodal", "ackheavy", "ackjumbo", "acks", "mtu", "long"])
 def test_auto_plan_cache_every_whole_plan(engine, orc, mix):
     """Batches whose device plan is each of the whole-batch plans (whole,
-    whole16, small body) and the split plan, called 40 times back to back:
-    cached calls run the plan's single launch; every output equals the oracle's."""
+    whole16, small body), the split plan and the 8-lane short mix, called 40
+    times back to back: cached calls run the plan's single launch; then the
+    same offsets buffer rewritten with the bimodal (or, for it, the long) mix
+    and called 20 times more; every output equals the oracle's."""
+    import torch
+
     rng = np.random.default_rng(len(mix))
     n = 300_000
-    lens = {"bimodal": np.where(rng.random(n) < 0.5, 40, 1460) + rng.integers(0, 4, n),
-            "acks": rng.integers(40, 44, n), "mtu": rng.integers(1460, 1464, n),
-            "long": rng.integers(4096, 9000, n)}[mix]
+    lens = _mix_lengths(rng, n, mix)
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum(lens)
     off += 5
-    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    off2 = np.zeros(n + 1, dtype=np.uint64)
+    off2[1:] = np.cumsum(_mix_lengths(rng, n, "long" if mix == "bimodal" else "bimodal"))
+    buf = rng.integers(0, 256, int(max(off[-1], off2[-1])) + 16, dtype=np.uint8)  # holds both mixes
     init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
     want = orc.checksum_batch(buf, n, offsets=off, init=init)
     dbuf, doff, dinit = _t(buf), _t(off), _t(init)
     outs = [engine.checksum_batch(dbuf, offsets=doff, init=dinit) for _ in range(40)]
     for k, o in enumerate(outs):
         assert (_u16(o) == want).all(), k
+    torch.cuda.synchronize()
+    doff.copy_(_t(off2))
+    want2 = orc.checksum_batch(buf, n, offsets=off2, init=init)
+    outs = [engine.checksum_batch(dbuf, offsets=doff, init=dinit) for _ in range(20)]
+    for k, o in enumerate(outs):
+        assert (_u16(o) == want2).all(), (mix, k)
 
 
 @pytest.mark.parametrize("stride,seg_len", [(1500, 1500), (1501, 1497), (64, 64), (9000, 9000),
@@ -668,6 +687,48 @@ def test_host_path_ipv4_patch_fixed_stride(engine, orc, pinned):
     w = orc.ipv4_tcp_batch(hb, n, 2, stride=L, dgram_len=L)
     assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all()
     assert (h == hb).all()
+
+
+@pytest.mark.parametrize("mix", ["acks", "mtu", "bimodal", "ackheavy", "ackjumbo", "long"])
+def test_ipv4_offsets_plan_cache(engine, orc, mix):
+    """Raw-datagram offsets batches of >= 16 Ki datagrams take their geometry
+    from the plan cached for the offsets buffer (4-lane groups for ACK
+    batches, 8-lane groups for ACK-heavy MTU mixes, 16 x 4 otherwise; the plan
+    kernels run behind the first and every 16th call): 20 calls in COMPUTE and
+    VERIFY, the same buffer rewritten with another mix, then PATCH; every
+    output and the patched bytes equal the oracle's."""
+    import torch
+
+    rng = np.random.default_rng(0x1B + len(mix))
+    n = 20_000
+    offs = []
+    for m in (mix, "mtu" if mix != "mtu" else "acks"):
+        lens = _mix_lengths(rng, n, m).astype(np.uint64)
+        o = np.zeros(n + 1, dtype=np.uint64)
+        o[1:] = np.cumsum(lens)
+        offs.append(o + 3)  # unaligned starts
+    buf = rng.integers(0, 256, int(max(o[-1] for o in offs)) + 16, dtype=np.uint8)  # holds both mixes
+    for o in offs:  # IPv4/TCP headers that parse: ver 4, hlen 5, len, proto 6, TCP data offset 5
+        s, ln = o[:-1].astype(np.int64), np.diff(o)
+        buf[s], buf[s + 2], buf[s + 3] = 0x45, (ln >> 8).astype(np.uint8), (ln & 255).astype(np.uint8)
+        buf[s + 6], buf[s + 8], buf[s + 9], buf[s + 32] = 0x40, 64, 6, 0x50
+    dbuf = _t(buf)
+    doff = _t(offs[0])
+    for k, off in enumerate(offs):
+        if k:
+            torch.cuda.synchronize()
+            doff.copy_(_t(off))
+        for mode in (0, 1):
+            want = orc.ipv4_tcp_batch(buf.copy(), n, mode, offsets=off)
+            for call in range(20):
+                ip, tcp, st = engine.ipv4_tcp_batch(dbuf, mode, offsets=doff)
+                assert (_u16(ip) == want[0]).all(), (mix, k, mode, call)
+                assert (_u16(tcp) == want[1]).all(), (mix, k, mode, call)
+                assert (st.cpu().numpy() == want[2]).all(), (mix, k, mode, call)
+    hb = buf.copy()
+    orc.ipv4_tcp_batch(hb, n, 2, offsets=offs[1])
+    engine.ipv4_tcp_batch(dbuf, 2, offsets=doff)
+    assert (dbuf.cpu().numpy() == hb).all(), mix
 
 
 @pytest.mark.parametrize("lead", [0, 1, 2, 3])

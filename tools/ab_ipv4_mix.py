@@ -3,7 +3,8 @@
 received-traffic mix — raw datagrams back to back (offsets), half of them
 40-byte pure ACKs and half 1500-byte data segments — at the default geometry
 (16-lane groups for offsets batches) and at forced ones, beside the plain
-checksum of the same bytes (binned AUTO) and the all-MTU batch."""
+checksum of the same bytes (binned AUTO, and single launches at the forced
+geometries) and the all-MTU batch.  Argument: comma-separated ACK shares."""
 import json
 import os
 import sys
@@ -71,7 +72,7 @@ def batch(eng, n, ack_frac, seed):
 
 def main():
     eng = Engine(0)
-    forced = {f"{l}x{u}m{m}": engine_with(l, u, m) for l, u, m in ((4, 2, 2), (8, 2, 2), (8, 8, 3), (16, 4, 3))}
+    forced = {f"{l}x{u}m{m}": engine_with(l, u, m) for l, u, m in ((4, 2, 2), (8, 2, 2), (8, 4, 3), (8, 8, 3), (16, 4, 3), (16, 8, 3), (32, 8, 3))}
     fracs = [float(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else (0.5, 0.0)
     for ack_frac in fracs:
         n = 1 << 20
@@ -87,6 +88,7 @@ def main():
         for k, e in forced.items():
             rows[f"verify_{k}"] = (lambda e: lambda: e.ipv4_tcp_batch(d, 1, n=n, offsets=doff, ip_ck=ip, tcp_ck=tcp,
                                                                      status=st))(e)
+            rows[f"plain_{k}"] = (lambda e: lambda: e.checksum_batch(d, offsets=doff, out=out))(e)
         for k, fn in rows.items():
             t = timed(fn)
             print(json.dumps({"ack_frac": ack_frac, "n": n, "bytes": nbytes, "case": k, "us": round(t * 1e6, 2),
