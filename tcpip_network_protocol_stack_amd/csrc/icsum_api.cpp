@@ -55,6 +55,35 @@ uint32_t env_u32(const char* name, uint32_t dflt) {
 
 }  // namespace
 
+namespace icsum::detail {
+// Device scratch kept across calls (hipMallocAsync + hipFreeAsync per call
+// cost ≈5 us between the kernels).  A Scratch lease holds `mu` while the
+// call enqueues its kernels, then records `ev` on its stream; a call on
+// another stream first makes its stream wait for that event, and growing the
+// buffer waits for it on the host.  It grows to the largest call's need and
+// lives until ics_destroy; `zeroed` areas are cleared (stream-ordered) when
+// they grow.
+struct ScratchArea {
+  explicit ScratchArea(bool zero = false) : zeroed(zero) {}
+  std::mutex mu;
+  void* buf = nullptr;
+  size_t cap = 0;
+  hipEvent_t ev = nullptr;
+  hipStream_t owner = nullptr;
+  bool used = false;
+  bool zeroed = false;
+  void release() {
+    if (buf) {
+      if (used) (void)hipEventSynchronize(ev);
+      (void)hipFree(buf);
+      buf = nullptr;
+    }
+    if (ev) (void)hipEventDestroy(ev);
+    ev = nullptr;
+  }
+};
+}  // namespace icsum::detail
+
 // One engine context per GPU.  Staging for the host-memory path is created
 // on first use and guarded by `mu`.
 struct ics_ctx {
@@ -102,20 +131,18 @@ struct ics_ctx {
   const uint64_t* plan_key = nullptr;
   uint64_t plan_key_n = 0;
   uint32_t plan_hits = 0;
-  // Device scratch of the binned dispatch and the two-pass wrap, kept across
-  // calls (hipMallocAsync + hipFreeAsync per call cost ≈5 us between the
-  // kernels).  A Scratch lease holds scratch_mu while the call enqueues its
-  // kernels, then records scratch_ev on its stream; a call on another stream
-  // first makes its stream wait for that event, and growing the buffer waits
-  // for it on the host.  It grows to the largest call's need (a binned batch
-  // of n segments: 80 n bytes + 16 KiB; a two-pass wrap: 4 n) and lives until
-  // ics_destroy.
-  std::mutex scratch_mu;
-  void* scratch = nullptr;
-  size_t scratch_cap = 0;
-  hipEvent_t scratch_ev = nullptr;
-  hipStream_t scratch_owner = nullptr;
-  bool scratch_used = false;
+  // device scratch of the binned dispatch and the two-pass wrap (a binned
+  // batch of n segments: 80 n bytes + 16 KiB; a two-pass wrap: 4 n)
+  icsum::detail::ScratchArea scratch;
+  // the flat dispatch's per-wave slots (k_checksum_flat: nwaves u32 sums,
+  // left zero by k_flat_finish, + nwaves u32 claims): its own area, zeroed
+  // when it grows, since the sums must start at zero
+  icsum::detail::ScratchArea flat{true};
+  // flat dispatch (ICSUM_FLAT): -1 auto, 0 off, 1 every offsets batch;
+  // flat_waves (ICSUM_FLAT_WAVES): waves of k_checksum_flat (each streams an
+  // equal share of the batch's 8 KiB tiles)
+  int flat_mode = 0;
+  uint32_t flat_waves = 16384;
   std::mutex mu;
   // host path: nslots slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each
   // (ICSUM_HOST_SLOT_MB), each with pinned in/out staging, device buffers and a stream
@@ -169,38 +196,40 @@ bool wrap_two_pass(const ics_ctx* ctx, bool headers_apart, uint64_t n) {
 // Scratch for the kernels one call enqueues on `st` (see ics_ctx::scratch).
 class Scratch {
  public:
-  Scratch(ics_ctx* ctx, size_t bytes, hipStream_t st) : ctx_(ctx), lock_(ctx->scratch_mu), st_(st) {
-    if (ctx->scratch_used && ctx->scratch_owner != st) err_ = hipStreamWaitEvent(st, ctx->scratch_ev, 0);
-    if (err_ == hipSuccess && bytes > ctx->scratch_cap) {
-      if (ctx->scratch) {
-        if (ctx->scratch_used) err_ = hipEventSynchronize(ctx->scratch_ev);
-        if (err_ == hipSuccess) err_ = hipFree(ctx->scratch);
-        ctx->scratch = nullptr;
-        ctx->scratch_cap = 0;
+  Scratch(icsum::detail::ScratchArea& a, size_t bytes, hipStream_t st) : a_(a), lock_(a.mu), st_(st) {
+    if (a.used && a.owner != st) err_ = hipStreamWaitEvent(st, a.ev, 0);
+    if (err_ == hipSuccess && bytes > a.cap) {
+      if (a.buf) {
+        if (a.used) err_ = hipEventSynchronize(a.ev);
+        if (err_ == hipSuccess) err_ = hipFree(a.buf);
+        a.buf = nullptr;
+        a.cap = 0;
       }
       const size_t cap = (bytes + (size_t(2) << 20) - 1) & ~((size_t(2) << 20) - 1);
-      if (err_ == hipSuccess) err_ = hipMalloc(&ctx->scratch, cap);
-      if (err_ == hipSuccess) ctx->scratch_cap = cap;
-      else ctx->scratch = nullptr;
+      if (err_ == hipSuccess) err_ = hipMalloc(&a.buf, cap);
+      if (err_ == hipSuccess && a.zeroed) err_ = hipMemsetAsync(a.buf, 0, cap, st);
+      if (err_ == hipSuccess) a.cap = cap;
+      else a.buf = nullptr;
     }
   }
+  Scratch(ics_ctx* ctx, size_t bytes, hipStream_t st) : Scratch(ctx->scratch, bytes, st) {}
   ~Scratch() {
     if (err_ != hipSuccess) return;
-    if (hipEventRecord(ctx_->scratch_ev, st_) == hipSuccess) {
-      ctx_->scratch_owner = st_;
-      ctx_->scratch_used = true;
+    if (hipEventRecord(a_.ev, st_) == hipSuccess) {
+      a_.owner = st_;
+      a_.used = true;
     } else {  // cannot track this call's use: the next one waits for the device
       (void)hipDeviceSynchronize();
-      ctx_->scratch_used = false;
+      a_.used = false;
     }
   }
   Scratch(const Scratch&) = delete;
   Scratch& operator=(const Scratch&) = delete;
   hipError_t error() const { return err_; }
-  void* get() const { return ctx_->scratch; }
+  void* get() const { return a_.buf; }
 
  private:
-  ics_ctx* ctx_;
+  icsum::detail::ScratchArea& a_;
   std::lock_guard<std::mutex> lock_;
   hipStream_t st_;
   hipError_t err_ = hipSuccess;
@@ -299,8 +328,22 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, hipStream_t st)
 // 146.0 / 125.6 us AUTO; profiles/r2_csum_mix_sweep.jsonl)
 bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
 
+// the flat dispatch (k_checksum_flat + k_flat_finish): one stream over the
+// batch's bytes, the cuts deciding where the sums go
+int checksum_flat(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
+                  void* d_out, int out_kind, hipStream_t st) {
+  const uint32_t nw = ctx->flat_waves;
+  Scratch ws(ctx->flat, size_t(nw) * 8, st);
+  ICS_HIP(ws.error());
+  uint32_t* accw = static_cast<uint32_t*>(ws.get());
+  ICS_HIP(icsum::launch_checksum_flat(sp, d_init, d_odd, d_out, out_kind, accw, accw + nw, nw, st));
+  return ICS_OK;
+}
+
 int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                     void* d_out, int out_kind, hipStream_t st) {
+  if (sp.offsets && ctx->flat_mode == 1 && sp.n < 0xFFFFFFFFull)
+    return checksum_flat(ctx, sp, d_init, d_odd, d_out, out_kind, st);
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
                       (ctx->bin == 1 || (ctx->bin < 0 && sp.n >= ctx->bin_min && !forced_geometry(ctx)));
   const bool plannable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_cache && ctx->plan_host;
@@ -777,7 +820,9 @@ int ics_create(int device, ics_ctx** out) {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     ctx->copy_threads = std::max<size_t>(1, env_u32("ICSUM_COPY_THREADS", std::min(8u, hw)));
   }
-  if (hipEventCreateWithFlags(&ctx->scratch_ev, hipEventDisableTiming) != hipSuccess) {
+  if (hipEventCreateWithFlags(&ctx->scratch.ev, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->flat.ev, hipEventDisableTiming) != hipSuccess) {
+    ctx->scratch.release();
     (void)hipFree(ctx->d_zero);
     delete ctx;
     return fail(ICS_ERR_HIP, "event creation failed");
@@ -799,6 +844,8 @@ int ics_create(int device, ics_ctx** out) {
     (void)hipGetLastError();
   }
   ctx->bin_debug = std::getenv("ICSUM_BIN_DEBUG") != nullptr;
+  if (std::getenv("ICSUM_FLAT")) ctx->flat_mode = int(env_u32("ICSUM_FLAT", 0)) == 1 ? 1 : 0;
+  ctx->flat_waves = std::max<uint32_t>(1, env_u32("ICSUM_FLAT_WAVES", ctx->flat_waves));
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
   ctx->blocking_sync = env_u32("ICSUM_HOST_BLOCKING_SYNC", 0) != 0;
@@ -813,11 +860,8 @@ int ics_destroy(ics_ctx* ctx) {
     free_staging(ctx);
     if (ctx->d_zero) (void)hipFree(ctx->d_zero);
     if (ctx->plan_host) (void)hipHostFree(ctx->plan_host);
-    if (ctx->scratch) {
-      if (ctx->scratch_used) (void)hipEventSynchronize(ctx->scratch_ev);
-      (void)hipFree(ctx->scratch);
-    }
-    if (ctx->scratch_ev) (void)hipEventDestroy(ctx->scratch_ev);
+    ctx->scratch.release();
+    ctx->flat.release();
   }
   delete ctx;
   return ICS_OK;

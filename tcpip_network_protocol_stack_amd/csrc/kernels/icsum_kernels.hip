@@ -598,6 +598,267 @@ __global__ void k_fold(const uint32_t* __restrict__ sum, uint16_t* __restrict__ 
   ICS_GRID_STRIDE(i, n) out[i] = fold_value(sum[i]);
 }
 
+// ------------------------------------------------- flat offsets batches ---
+// A packed offsets batch is ONE byte stream [offsets[0], offsets[n]) cut at
+// the offsets (segment i = [offsets[i], offsets[i+1])).  k_checksum_flat reads
+// it as such, whatever the length mix: wave w streams an equal share of
+// 8 KiB tiles (chunk u*64 + lane of a tile is lane `lane`'s slot u, so every
+// load instruction of the wave reads 1 KiB contiguous), and the cuts only
+// decide where the sums go:
+//   * a tile without a cut adds its bytes to the open segment (lane-local
+//     even/odd sums, no cross-lane work);
+//   * a tile with cuts takes the exclusive prefix of its chunks' even/odd
+//     sums (DPP wave scans, kept in LDS); the cut at x, in chunk k at byte r,
+//     has prefix P(x) = pfx[k] + the even/odd sums of chunk k's first r bytes,
+//     and segment j's piece of the tile is P(end_j) - P(start_j);
+//   * a segment that starts and ends inside the wave's share is written
+//     directly (init + sum, folded); the pieces of a segment that crosses a
+//     share boundary are added (u32 atomics: the sum is mod 2^32, so any order
+//     is exact) into the slot of the wave whose share holds its start, and
+//     k_flat_finish folds them.
+// Every segment costs a few instructions at its cut instead of a lane group:
+// the rate no longer depends on the lengths (bimodal 40 B / 1460 B batches,
+// BASELINE config 4's 64 B - 64 KiB mix).  The byte roles come from absolute
+// addresses as everywhere (icsum_device.h), so a piece's even/odd sums are
+// combined with its segment's own swap.
+constexpr uint32_t kFlatNone = 0xFFFFFFFFu;
+constexpr int kFlatSlots = 8;  // 16-byte chunks per lane per tile: 8 KiB tiles
+
+// inclusive scan over the 64 lanes (row_shr 1/2/4/8 inside each row, then
+// row_bcast15 / row_bcast31 across rows)
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, true);   // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, true);   // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, true);   // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true);   // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
+__device__ __forceinline__ uint32_t wave_total(uint32_t x) {
+  return __builtin_amdgcn_readlane(group_sum<64>(x), 63);
+}
+
+__device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
+  return uint64_t(__builtin_amdgcn_readlane(uint32_t(x), l)) |
+         (uint64_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), l)) << 32);
+}
+
+// number of leading lanes (from lane 0) whose predicate holds
+__device__ __forceinline__ uint32_t leading_lanes(bool p) {
+  const uint64_t m = __ballot(p);
+  return ~m ? uint32_t(__builtin_ctzll(~m)) : 64u;
+}
+
+// the segment open at byte position pos > offsets[0]: the first j < n with
+// offsets[j + 1] > pos (offsets[n] > pos), by 64-way probing (one dependent
+// load per factor of 64; every probe index is clamped into [lo, hi])
+__device__ __forceinline__ uint64_t flat_find(const uint64_t* __restrict__ off, uint64_t n, uint64_t pos,
+                                              uint32_t lane) {
+  uint64_t lo = 0, hi = n - 1;  // the answer lies in [lo, hi]
+  while (hi - lo >= 64) {
+    const uint64_t step = ((hi - lo) >> 6) + 1;
+    const uint64_t p = lo + uint64_t(lane) * step;
+    const uint64_t pc = p < hi ? p : hi;
+    const uint64_t m = __ballot(off[pc + 1] > pos);
+    if (m == 0) {
+      lo += 63 * step + 1;  // every probe is <= hi here and below the answer
+      continue;
+    }
+    const uint32_t f = uint32_t(__builtin_ctzll(m));
+    if (f == 0) return lo;
+    const uint64_t pf = lo + uint64_t(f) * step;
+    hi = pf < hi ? pf : hi;
+    lo += uint64_t(f - 1) * step + 1;
+  }
+  const uint64_t p = lo + lane, pc = p < hi ? p : hi;
+  const uint64_t m = __ballot(off[pc + 1] > pos);
+  return m ? lo + uint64_t(__builtin_ctzll(m)) : hi;
+}
+
+// the wave whose share holds byte position s (shares of rt tiles from r0)
+__device__ __forceinline__ uint32_t flat_owner(uint64_t s, uint64_t r0, uint64_t rt, uint32_t nwaves) {
+  constexpr uint64_t kTile = 16ull * 64 * kFlatSlots;
+  const uint64_t w = s > r0 ? (s - r0) / kTile / rt : 0;
+  return uint32_t(w < nwaves - 1 ? w : nwaves - 1);
+}
+
+template <bool NT, int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum_flat(const uint8_t* __restrict__ bytes,
+                                                          const uint64_t* __restrict__ offsets, uint64_t n,
+                                                          const uint32_t* __restrict__ init, uint32_t init_step,
+                                                          const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                                          void* __restrict__ out, uint32_t* __restrict__ accw,
+                                                          uint32_t* __restrict__ tailw, uint32_t nwaves) {
+  constexpr uint32_t kChunks = 64 * kFlatSlots;
+  constexpr uint64_t kTile = 16ull * kChunks;
+  __shared__ uint32_t pfx[kBlock / 64][2][kChunks];  // per wave: exclusive prefix of the even / odd sums
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t w = blockIdx.x * (kBlock / 64) + wv;
+  if (w >= nwaves) return;
+  const uint64_t off0 = offsets[0], offn = offsets[n];
+  const uint64_t r0 = off0 & ~uint64_t(15);
+  const uint64_t total = offn > r0 ? offn - r0 : 0;  // 0: every segment empty
+  const uint64_t ntiles = total ? (total + kTile - 1) / kTile : 1;
+  const uint64_t rt = (ntiles + nwaves - 1) / nwaves;  // tiles per wave
+  const uint64_t t0 = uint64_t(w) * rt, t1 = t0 + rt < ntiles ? t0 + rt : ntiles;
+  if (t0 >= t1) {
+    if (lane == 0) tailw[w] = kFlatNone;
+    return;
+  }
+  const uint64_t wbeg = r0 + t0 * kTile, wend = r0 + t1 * kTile;
+  const uint64_t lastc = offn > r0 ? (offn - 1) & ~uint64_t(15) : r0;  // last chunk holding a byte
+  [[maybe_unused]] const uint8_t* env_lo = bytes + r0;
+  [[maybe_unused]] const uint8_t* env_hi = bytes + lastc + 16;
+  // the open segment: its index, start, whether its start lies in this share,
+  // and (lane-local) the even/odd sums of its bytes in earlier tiles
+  uint64_t cur = w == 0 ? 0 : flat_find(offsets, n, wbeg, lane);
+  uint64_t cur_start = offsets[cur];
+  bool started = w == 0 || cur_start >= wbeg;
+  uint32_t accE = 0, accO = 0;
+  for (uint64_t t = t0; t < t1; ++t) {
+    const uint64_t T = r0 + t * kTile, tend = T + kTile;
+    u32x4 v[kFlatSlots];
+#pragma unroll
+    for (int u = 0; u < kFlatSlots; ++u) {
+      const uint64_t a = T + (uint64_t(u) * 64 + lane) * 16;
+      const uint64_t q = a < lastc ? a : lastc;
+      ICS_CHECK16(bytes + q, env_lo, env_hi);
+      v[u] = total ? load16<NT>(reinterpret_cast<const u32x4*>(bytes + q)) : u32x4{0u, 0u, 0u, 0u};
+    }
+    // cut candidates: lane i holds offsets[cur + 1 + i], the end of segment cur + i
+    uint64_t ci = cur + 1 + lane;
+    uint64_t x = offsets[ci <= n ? ci : n];
+    uint32_t m = leading_lanes(ci <= n && x <= tend);
+    uint32_t e[kFlatSlots], o[kFlatSlots];
+#pragma unroll
+    for (int u = 0; u < kFlatSlots; ++u) {
+      const uint64_t a = T + (uint64_t(u) * 64 + lane) * 16;
+      if (a < off0 || a + 16 > offn) {  // the batch's first and last chunks, and past its end
+        const uint32_t lo = a < off0 ? uint32_t(off0 - a) : 0u;
+        const uint32_t hi = a >= offn ? 0u : (offn - a >= 16 ? 16u : uint32_t(offn - a));
+        v[u] = v[u] & byte_range_mask(lo, hi);
+      }
+      e[u] = 0;
+      o[u] = 0;
+      acc_chunk(v[u], e[u], o[u]);
+    }
+    if (m == 0) {  // the open segment runs through the tile
+#pragma unroll
+      for (int u = 0; u < kFlatSlots; ++u) {
+        accE += e[u];
+        accO += o[u];
+      }
+      continue;
+    }
+    // the open segment's bytes in earlier tiles, over the wave
+    uint32_t carryE = wave_total(accE), carryO = wave_total(accO);
+    accE = accO = 0;
+    // exclusive prefix of the tile's chunks (chunk u*64 + lane)
+    uint32_t totE = 0, totO = 0;
+#pragma unroll
+    for (int u = 0; u < kFlatSlots; ++u) {
+      const uint32_t ie = wave_scan_incl(e[u]), io = wave_scan_incl(o[u]);
+      pfx[wv][0][u * 64 + lane] = totE + ie - e[u];
+      pfx[wv][1][u * 64 + lane] = totO + io - o[u];
+      totE += __builtin_amdgcn_readlane(ie, 63);
+      totO += __builtin_amdgcn_readlane(io, 63);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t popE = 0, popO = 0;  // P at the open segment's start in this tile
+    for (;;) {
+      // P(x) at this lane's cut (x clamped into the tile: malformed offsets
+      // give wrong sums, never a read outside the batch)
+      const uint64_t xc = x < T ? T : (x > tend ? tend : x);
+      const uint32_t rel = uint32_t(xc - T), k = rel >> 4, r = rel & 15u;
+      uint32_t pE = totE, pO = totO;
+      if (lane < m && k < kChunks) {
+        pE = pfx[wv][0][k];
+        pO = pfx[wv][1][k];
+        if (r != 0 && total) {
+          const uint64_t a0 = T + uint64_t(k) * 16, a = a0 < lastc ? a0 : lastc;
+          ICS_CHECK16(bytes + a, env_lo, env_hi);
+          const u32x4 c = *reinterpret_cast<const u32x4*>(bytes + a);
+          const uint32_t lo = a < off0 ? uint32_t(off0 - a) : 0u;
+          acc_chunk(c & byte_range_mask(lo, r), pE, pO);
+        }
+      }
+      // the previous cut (lane 0: the open segment's start)
+      uint32_t qE = uint32_t(__shfl_up(int(pE), 1, 64)), qO = uint32_t(__shfl_up(int(pO), 1, 64));
+      uint64_t xs = uint64_t(__shfl_up((long long)xc, 1, 64));
+      if (lane == 0) {
+        qE = popE - carryE;
+        qO = popO - carryO;
+        xs = cur_start;
+      }
+      if (lane < m) {
+        const uint64_t j = cur + lane;  // < n: its end cut exists
+        const uint32_t sw = (uint32_t(xs) ^ uint32_t(odd[j * odd_step])) & 1u;
+        const uint32_t c = combine_roles(pE - qE, pO - qO, sw);
+        if (lane == 0 && !started) {
+          atomicAdd(&accw[flat_owner(xs, r0, rt, nwaves)], c);
+        } else {
+          const uint32_t s = init[j * init_step] + c;
+          if (OUT == 0)
+            static_cast<uint16_t*>(out)[j] = fold_value(s);
+          else
+            static_cast<uint32_t*>(out)[j] = s;
+        }
+      }
+      // the segment the last cut opens
+      popE = __builtin_amdgcn_readlane(pE, m - 1);
+      popO = __builtin_amdgcn_readlane(pO, m - 1);
+      cur_start = readlane64(xc, m - 1);
+      cur += m;
+      started = true;
+      carryE = carryO = 0;
+      if (m < 64) break;
+      ci = cur + 1 + lane;  // more cuts in this tile: the next 64 candidates
+      x = offsets[ci <= n ? ci : n];
+      m = leading_lanes(ci <= n && x <= tend);
+      if (m == 0) break;
+    }
+    if (lane == 0) {  // the open segment's bytes after its start in this tile
+      accE = totE - popE;
+      accO = totO - popO;
+    }
+  }
+  // the open segment continues past this share: add its piece to the slot of
+  // the wave that holds its start; that wave claims it when the start is here
+  const uint32_t ae = wave_total(accE), ao = wave_total(accO);
+  if (lane == 0) {
+    uint32_t claim = kFlatNone;
+    if (cur < n && cur_start < wend) {
+      const uint32_t sw = (uint32_t(cur_start) ^ uint32_t(odd[cur * odd_step])) & 1u;
+      atomicAdd(&accw[flat_owner(cur_start, r0, rt, nwaves)], combine_roles(ae, ao, sw));
+      if (started) claim = uint32_t(cur);
+    }
+    tailw[w] = claim;
+  }
+}
+
+// the segments that crossed a share boundary: init + their pieces' sum; the
+// slots are left zero for the next batch
+template <int OUT>
+__global__ void k_flat_finish(uint32_t* __restrict__ accw, const uint32_t* __restrict__ tailw,
+                              const uint32_t* __restrict__ init, uint32_t init_step, void* __restrict__ out,
+                              uint32_t nwaves) {
+  ICS_GRID_STRIDE(w, nwaves) {
+    const uint32_t s = accw[w], j = tailw[w];
+    accw[w] = 0;
+    if (j != kFlatNone) {
+      const uint32_t v = init[uint64_t(j) * init_step] + s;
+      if (OUT == 0)
+        static_cast<uint16_t*>(out)[j] = fold_value(v);
+      else
+        static_cast<uint32_t*>(out)[j] = v;
+    }
+  }
+}
+
 // ---------------------------------------------- IPv4 header fields ------
 // The first 20 wire bytes of a datagram as 5 little-endian dwords relative to
 // its (possibly unaligned) start: 6 aligned dword loads + alignbyte.
@@ -1470,6 +1731,29 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_checksum_flat(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
+                                int out_kind, uint32_t* accw, uint32_t* tailw, uint32_t nwaves, hipStream_t st) {
+  if (!sp.offsets || sp.n == 0 || sp.n >= 0xFFFFFFFFull || nwaves == 0 || nwaves > (1u << 24))
+    return hipErrorInvalidValue;
+  const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
+  const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
+  const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
+  const dim3 grid((nwaves + kBlock / 64 - 1) / (kBlock / 64));
+  const dim3 fgrid((nwaves + kBlock - 1) / kBlock < 1024 ? (nwaves + kBlock - 1) / kBlock : 1024);
+  if (out_kind == 0) {
+    hipLaunchKernelGGL((k_checksum_flat<true, 0>), grid, dim3(kBlock), 0, st, sp.bytes, sp.offsets, sp.n, ip, is,
+                       op, os, out, accw, tailw, nwaves);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL(k_flat_finish<0>, fgrid, dim3(kBlock), 0, st, accw, tailw, ip, is, out, nwaves);
+  } else {
+    hipLaunchKernelGGL((k_checksum_flat<true, 1>), grid, dim3(kBlock), 0, st, sp.bytes, sp.offsets, sp.n, ip, is,
+                       op, os, out, accw, tailw, nwaves);
+    if (hipError_t e = hipGetLastError()) return e;
+    hipLaunchKernelGGL(k_flat_finish<1>, fgrid, dim3(kBlock), 0, st, accw, tailw, ip, is, out, nwaves);
+  }
+  return hipGetLastError();
 }
 
 bool dense_supported(const SegSpec& sp) {

@@ -83,6 +83,12 @@ SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, i
 // out_kind 0: u16 value(), 1: u32 raw sum
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st);
+// Flat dispatch of a packed offsets batch (n < 2^32 - 1): k_checksum_flat
+// (nwaves waves, each an equal share of the batch's 8 KiB tiles) then
+// k_flat_finish.  accw: nwaves u32 that are zero on entry (and left zero),
+// tailw: nwaves u32 of scratch
+hipError_t launch_checksum_flat(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
+                                int out_kind, uint32_t* accw, uint32_t* tailw, uint32_t nwaves, hipStream_t st);
 // Dense fixed-stride batches (stride == seg_len in {32, 64, 128}, 16-byte
 // aligned bytes, no parity array): k_checksum_dense, SEGS segments per lane
 // group in flight (segs in {1, 2, 4, 8}; not every (seg_len, segs) pair exists)

@@ -1,0 +1,146 @@
+"""GPU parity of the flat dispatch of packed offsets batches
+(k_checksum_flat + k_flat_finish, forced with ICSUM_FLAT=1): one byte stream
+cut at the offsets, against the golden KATs and the oracle.
+
+Wave counts from 1 (one share: every segment finishes inside it) to a few
+dozen (segments crossing share boundaries, finished through the per-wave
+slots) and the default (more waves than tiles on small batches: empty
+shares).  Bar: bit-exact."""
+import numpy as np
+import pytest
+
+from helpers import kat_cases, pack_contiguous
+from test_gpu_parity import _engine_with, _t, _u16, _u32
+
+pytestmark = pytest.mark.gpu
+
+FLAT_ENVS = [{"ICSUM_FLAT": "1"},
+             {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "1"},
+             {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "7"},
+             {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "97"}]
+
+
+@pytest.fixture(scope="module", params=FLAT_ENVS, ids=lambda e: "-".join(f"{k[6:]}{v}" for k, v in e.items()))
+def flat_engine(request):
+    yield from _engine_with(request.param)
+
+
+def _check(eng, orc, buf, off, rng, tag=""):
+    n = off.size - 1
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    out = eng.checksum_batch(_t(buf), offsets=_t(off), init=_t(init))
+    assert (_u16(out) == orc.checksum_batch(buf, n, offsets=off, init=init)).all(), tag
+    out0 = eng.checksum_batch(_t(buf), offsets=_t(off))  # init NULL = 0
+    assert (_u16(out0) == orc.checksum_batch(buf, n, offsets=off)).all(), tag
+    odd = rng.integers(0, 2, n).astype(np.uint8)
+    sums = eng.sum_batch(_t(buf), offsets=_t(off), init=_t(init), odd=_t(odd))
+    assert (_u32(sums) == orc.sum_batch(buf, n, offsets=off, init=init, odd=odd)).all(), tag
+
+
+def test_flat_kats(flat_engine):
+    # every KAT (lengths 0-257, inits, whole segments, the 131076-byte 0xFF
+    # wrap) at four alignments of the first byte
+    cases = kat_cases({"rfc1071", "len", "init", "whole", "fill"})
+    segs = [b"".join(p) for _, p, _, _ in cases]
+    init = np.array([c[0] for c in cases], dtype=np.uint32)
+    for lead in (0, 1, 6, 15):
+        buf, off = pack_contiguous(segs, lead)
+        out = flat_engine.checksum_batch(_t(buf), offsets=_t(off), init=_t(init))
+        assert _u16(out).tolist() == [c[2] for c in cases], f"lead={lead}"
+
+
+def test_flat_split_pieces_chain(flat_engine):
+    # add(vector<string>) with parity carried across pieces (checksum.h:44-59)
+    cases = kat_cases({"split"})
+    maxp = max(len(p) for _, p, _, _ in cases)
+    sums = np.array([c[0] for c in cases], dtype=np.uint32)
+    odd = np.zeros(len(cases), dtype=np.uint8)
+    for k in range(maxp):
+        segs = [p[k] if k < len(p) else b"" for _, p, _, _ in cases]
+        buf, off = pack_contiguous(segs, 1)
+        sums = _u32(flat_engine.sum_batch(_t(buf), offsets=_t(off), init=_t(sums), odd=_t(odd))).copy()
+        odd ^= np.array([len(x) & 1 for x in segs], dtype=np.uint8)
+    assert _u16(flat_engine.fold_batch(_t(sums))).tolist() == [c[2] for c in cases]
+
+
+def test_flat_mixed(flat_engine, orc):
+    # lengths over every bin, zero-length segments, a few long ones
+    rng = np.random.default_rng(0xF1A7)
+    n = 6000
+    edges = [0, 1, 15, 16, 17, 143, 144, 145, 1919, 1920, 4096, 8191, 8192, 8193]
+    lens = rng.choice([40, 64, 100, 576, 1500, 3000, 9000, 40000], n) + rng.integers(-7, 8, n)
+    lens[: len(edges)] = edges
+    lens[len(edges)::101] = 0
+    segs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
+    for lead in (0, 5, 15):
+        buf, off = pack_contiguous(segs, lead)
+        _check(flat_engine, orc, buf, off, rng, f"lead={lead}")
+
+
+def test_flat_tiny_segments(flat_engine, orc):
+    # 0-20 byte segments: several cuts inside one 16-byte chunk, more than 64
+    # cuts per tile (the cut loop's further rounds)
+    rng = np.random.default_rng(0x7111)
+    n = 40_000
+    lens = rng.integers(0, 21, n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    off += 3
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    _check(flat_engine, orc, buf, off, rng)
+
+
+def test_flat_long_segments(flat_engine, orc):
+    # segments far longer than a share (3 MiB, 1 MiB + 1) between short ones:
+    # their pieces come from many waves
+    rng = np.random.default_rng(0x10E6)
+    lens = rng.integers(0, 3000, 400)
+    lens[50] = 3 << 20
+    lens[51] = (1 << 20) + 1
+    lens[399] = 700_001
+    off = np.zeros(lens.size + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    off += 9
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    _check(flat_engine, orc, buf, off, rng)
+
+
+@pytest.mark.parametrize("lens", [[0] * 100, [0], [1], [15], [16], [17], [100_000], [0, 0, 5, 0, 0],
+                                  [8192] * 3, [8191, 1, 8192, 0]])
+def test_flat_edge_batches(flat_engine, orc, lens):
+    # all-empty batches (every output = the folded init), single segments,
+    # segments that end exactly on tile boundaries
+    rng = np.random.default_rng(len(lens) * 7 + sum(lens))
+    for lead in (0, 11):
+        off = np.zeros(len(lens) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        off += lead
+        buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+        _check(flat_engine, orc, buf, off, rng, f"lead={lead}")
+
+
+def test_flat_bimodal_large(flat_engine, orc):
+    # ACK-sized + MSS-sized segments interleaved (a TCP receive mix)
+    rng = np.random.default_rng(0xACC)
+    n = 150_000
+    lens = np.where(rng.random(n) < 0.5, 40, 1460) + rng.integers(0, 4, n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    off += 1
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    out = flat_engine.checksum_batch(_t(buf), offsets=_t(off))
+    assert (_u16(out) == orc.checksum_batch(buf, n, offsets=off)).all()
+
+
+def test_flat_repeated_calls_leave_slots_clean(flat_engine, orc):
+    # the per-wave sums are left zero by k_flat_finish: the same batch twice
+    # and a different batch after it give the reference values every time
+    rng = np.random.default_rng(0x5107)
+    for rep in range(3):
+        lens = rng.integers(0, 20000, 300)
+        off = np.zeros(lens.size + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+        for _ in range(2):
+            out = flat_engine.checksum_batch(_t(buf), offsets=_t(off))
+            assert (_u16(out) == orc.checksum_batch(buf, lens.size, offsets=off)).all(), rep
