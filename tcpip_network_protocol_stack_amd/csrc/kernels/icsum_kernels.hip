@@ -641,8 +641,9 @@ __device__ __forceinline__ uint32_t wave_total(uint32_t x) {
 }
 
 __device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
-  return uint64_t(__builtin_amdgcn_readlane(uint32_t(x), l)) |
-         (uint64_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), l)) << 32);
+  // (the builtin returns int: through uint32_t, or a low word >= 2^31 would sign-extend)
+  return uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x), l))) |
+         (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), l))) << 32);
 }
 
 // number of leading lanes (from lane 0) whose predicate holds
@@ -717,44 +718,141 @@ __global__ __launch_bounds__(kBlock) void k_checksum_flat(const uint8_t* __restr
   uint64_t cur_start = offsets[cur];
   bool started = w == 0 || cur_start >= wbeg;
   uint32_t accE = 0, accO = 0;
+  // per segment that completes: its sum to `out` (init added) or, for the
+  // open segment whose start lies in an earlier share, its last piece to the
+  // slot of that share's wave
+  auto finish = [&](uint64_t j, uint64_t start, uint32_t pe, uint32_t po, bool here) {
+    const uint32_t c = combine_roles(pe, po, (uint32_t(start) ^ uint32_t(odd[j * odd_step])) & 1u);
+    if (!here) {
+      atomicAdd(&accw[flat_owner(start, r0, rt, nwaves)], c);
+    } else {
+      const uint32_t sv = init[j * init_step] + c;
+      if (OUT == 0)
+        static_cast<uint16_t*>(out)[j] = fold_value(sv);
+      else
+        static_cast<uint32_t*>(out)[j] = sv;
+    }
+  };
+  const u32x4* __restrict__ lanep = reinterpret_cast<const u32x4*>(bytes) + lane;
   for (uint64_t t = t0; t < t1; ++t) {
     const uint64_t T = r0 + t * kTile, tend = T + kTile;
+    // the batch's first and last tiles (bytes outside [offsets[0],
+    // offsets[n]) are masked, chunks past the end not read): a uniform branch
+    const bool edge = T < off0 || tend > offn;
     u32x4 v[kFlatSlots];
+    if (!edge) {
+      const u32x4* __restrict__ p = lanep + (T >> 4);
 #pragma unroll
-    for (int u = 0; u < kFlatSlots; ++u) {
-      const uint64_t a = T + (uint64_t(u) * 64 + lane) * 16;
-      const uint64_t q = a < lastc ? a : lastc;
-      ICS_CHECK16(bytes + q, env_lo, env_hi);
-      v[u] = total ? load16<NT>(reinterpret_cast<const u32x4*>(bytes + q)) : u32x4{0u, 0u, 0u, 0u};
+      for (int u = 0; u < kFlatSlots; ++u) {
+        ICS_CHECK16(p + u * 64, env_lo, env_hi);
+        v[u] = load16<NT>(p + u * 64);
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < kFlatSlots; ++u) {
+        const uint64_t a = T + (uint64_t(u) * 64 + lane) * 16;
+        const uint64_t q = a < lastc ? a : lastc;
+        ICS_CHECK16(bytes + q, env_lo, env_hi);
+        v[u] = total ? load16<NT>(reinterpret_cast<const u32x4*>(bytes + q)) : u32x4{0u, 0u, 0u, 0u};
+      }
     }
     // cut candidates: lane i holds offsets[cur + 1 + i], the end of segment cur + i
-    uint64_t ci = cur + 1 + lane;
+    const uint64_t ci = cur + 1 + lane;
     uint64_t x = offsets[ci <= n ? ci : n];
     uint32_t m = leading_lanes(ci <= n && x <= tend);
-    uint32_t e[kFlatSlots], o[kFlatSlots];
+    if (edge) {
 #pragma unroll
-    for (int u = 0; u < kFlatSlots; ++u) {
-      const uint64_t a = T + (uint64_t(u) * 64 + lane) * 16;
-      if (a < off0 || a + 16 > offn) {  // the batch's first and last chunks, and past its end
+      for (int u = 0; u < kFlatSlots; ++u) {
+        const uint64_t a = T + (uint64_t(u) * 64 + lane) * 16;
         const uint32_t lo = a < off0 ? uint32_t(off0 - a) : 0u;
         const uint32_t hi = a >= offn ? 0u : (offn - a >= 16 ? 16u : uint32_t(offn - a));
         v[u] = v[u] & byte_range_mask(lo, hi);
       }
+    }
+    if (m == 0) {  // the open segment runs through the tile
+#pragma unroll
+      for (int u = 0; u < kFlatSlots; ++u) acc_chunk(v[u], accE, accO);
+      continue;
+    }
+    // one or two cuts (long segments): the first bytes of each cut's chunk,
+    // summed in its owner lane now, so that the chunks can be dropped
+    uint32_t hE[2] = {0u, 0u}, hO[2] = {0u, 0u};
+    if (m <= 2) {
+#pragma unroll
+      for (uint32_t i = 0; i < 2; ++i) {
+        if (i < m) {
+          const uint64_t xi = readlane64(x, i);
+          const uint64_t xc = xi < T ? T : (xi > tend ? tend : xi);
+          const uint32_t rel = uint32_t(xc - T), k = rel >> 4, r = rel & 15u;
+          if (k < kChunks && r != 0) {
+            const uint32_t uk = k >> 6;
+            u32x4 cv = v[0];
+#pragma unroll
+            for (int u = 1; u < kFlatSlots; ++u)
+              if (uint32_t(u) == uk) cv = v[u];
+            const uint64_t a = T + uint64_t(k) * 16;
+            const uint32_t lo = a < off0 ? uint32_t(off0 - a) : 0u;
+            if (lane == (k & 63u)) acc_chunk(cv & byte_range_mask(lo, r), hE[i], hO[i]);
+          }
+        }
+      }
+    }
+    uint32_t e[kFlatSlots], o[kFlatSlots];
+#pragma unroll
+    for (int u = 0; u < kFlatSlots; ++u) {
       e[u] = 0;
       o[u] = 0;
       acc_chunk(v[u], e[u], o[u]);
     }
-    if (m == 0) {  // the open segment runs through the tile
-#pragma unroll
-      for (int u = 0; u < kFlatSlots; ++u) {
-        accE += e[u];
-        accO += o[u];
-      }
-      continue;
-    }
     // the open segment's bytes in earlier tiles, over the wave
     uint32_t carryE = wave_total(accE), carryO = wave_total(accO);
     accE = accO = 0;
+    if (m <= 2) {
+      // one or two cuts (long segments): P(x) by one masked wave sum per cut
+      // (chunks before x's chunk, plus x's chunk's first bytes in its owner
+      // lane) instead of the tile's prefix scans
+      uint32_t se = 0, so = 0;
+#pragma unroll
+      for (int u = 0; u < kFlatSlots; ++u) {
+        se += e[u];
+        so += o[u];
+      }
+      const uint32_t totE = wave_total(se), totO = wave_total(so);
+      uint32_t prevE = 0, prevO = 0;
+      for (uint32_t i = 0; i < m; ++i) {
+        const uint64_t xi = readlane64(x, i);
+        const uint64_t xc = xi < T ? T : (xi > tend ? tend : xi);
+        const uint32_t rel = uint32_t(xc - T), k = rel >> 4, r = rel & 15u;
+        uint32_t pE = totE, pO = totO;
+        if (k < kChunks) {
+          uint32_t ce = i == 0 ? hE[0] : hE[1], co = i == 0 ? hO[0] : hO[1];
+          (void)r;
+#pragma unroll
+          for (int u = 0; u < kFlatSlots; ++u) {
+            const bool before = uint32_t(u) * 64 + lane < k;
+            ce += before ? e[u] : 0u;
+            co += before ? o[u] : 0u;
+          }
+          pE = wave_total(ce);
+          pO = wave_total(co);
+        }
+        if (lane == 0) {
+          const uint64_t j = cur + i;  // < n: its end cut exists
+          finish(j, cur_start, pE - prevE + carryE, pO - prevO + carryO, i != 0 || started);
+        }
+        prevE = pE;
+        prevO = pO;
+        carryE = carryO = 0;
+        cur_start = xc;
+      }
+      cur += m;
+      started = true;
+      if (lane == 0) {  // the open segment's bytes after its start in this tile
+        accE = totE - prevE;
+        accO = totO - prevO;
+      }
+      continue;
+    }
     // exclusive prefix of the tile's chunks (chunk u*64 + lane)
     uint32_t totE = 0, totO = 0;
 #pragma unroll
@@ -794,20 +892,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_flat(const uint8_t* __restr
         qO = popO - carryO;
         xs = cur_start;
       }
-      if (lane < m) {
-        const uint64_t j = cur + lane;  // < n: its end cut exists
-        const uint32_t sw = (uint32_t(xs) ^ uint32_t(odd[j * odd_step])) & 1u;
-        const uint32_t c = combine_roles(pE - qE, pO - qO, sw);
-        if (lane == 0 && !started) {
-          atomicAdd(&accw[flat_owner(xs, r0, rt, nwaves)], c);
-        } else {
-          const uint32_t s = init[j * init_step] + c;
-          if (OUT == 0)
-            static_cast<uint16_t*>(out)[j] = fold_value(s);
-          else
-            static_cast<uint32_t*>(out)[j] = s;
-        }
-      }
+      if (lane < m) finish(cur + lane, xs, pE - qE, pO - qO, lane != 0 || started);  // cur + lane < n
       // the segment the last cut opens
       popE = __builtin_amdgcn_readlane(pE, m - 1);
       popO = __builtin_amdgcn_readlane(pO, m - 1);
@@ -816,9 +901,9 @@ __global__ __launch_bounds__(kBlock) void k_checksum_flat(const uint8_t* __restr
       started = true;
       carryE = carryO = 0;
       if (m < 64) break;
-      ci = cur + 1 + lane;  // more cuts in this tile: the next 64 candidates
-      x = offsets[ci <= n ? ci : n];
-      m = leading_lanes(ci <= n && x <= tend);
+      const uint64_t cn = cur + 1 + lane;  // more cuts in this tile: the next 64 candidates
+      x = offsets[cn <= n ? cn : n];
+      m = leading_lanes(cn <= n && x <= tend);
       if (m == 0) break;
     }
     if (lane == 0) {  // the open segment's bytes after its start in this tile
