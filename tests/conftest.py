@@ -41,3 +41,41 @@ def engine():
     yield eng
     torch.cuda.synchronize()
     eng.close()
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _sentinel_outputs():
+    """GPU runs: every output array the Engine allocates starts as a 0x5A byte
+    pattern, so an output no kernel writes cannot pass on an earlier call's
+    results left in a block the caching allocator hands out again."""
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        yield
+        return
+    if not torch.cuda.is_available():
+        yield
+        return
+    import tcpip_network_protocol_stack_amd.engine as em
+
+    real = em.torch
+
+    class _Torch:
+        def __getattr__(self, name):
+            return getattr(real, name)
+
+        @staticmethod
+        def empty(*args, **kw):
+            t = real.empty(*args, **kw)
+            if t.is_cuda and t.numel():
+                if t.dtype.is_floating_point:
+                    t.fill_(float("nan"))
+                else:
+                    t.fill_(int.from_bytes(b"\x5a" * t.element_size(), "little", signed=t.dtype != real.uint8))
+            return t
+
+    em.torch = _Torch()
+    try:
+        yield
+    finally:
+        em.torch = real
