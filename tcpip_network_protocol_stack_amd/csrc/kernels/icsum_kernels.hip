@@ -658,7 +658,9 @@ __device__ __forceinline__ uint32_t leading_lanes(bool p) {
 __device__ __forceinline__ uint64_t flat_find(const uint64_t* __restrict__ off, uint64_t n, uint64_t pos,
                                               uint32_t lane) {
   uint64_t lo = 0, hi = n - 1;  // the answer lies in [lo, hi]
-  while (hi - lo >= 64) {
+  // (bounded: 11 rounds cover 2^64 for monotone offsets; malformed ones end
+  // here too, with some index in [0, n - 1])
+  for (int round = 0; round < 11 && lo <= hi && hi - lo >= 64; ++round) {
     const uint64_t step = ((hi - lo) >> 6) + 1;
     const uint64_t p = lo + uint64_t(lane) * step;
     const uint64_t pc = p < hi ? p : hi;
@@ -673,9 +675,11 @@ __device__ __forceinline__ uint64_t flat_find(const uint64_t* __restrict__ off, 
     hi = pf < hi ? pf : hi;
     lo += uint64_t(f - 1) * step + 1;
   }
+  if (lo > hi) lo = hi;
   const uint64_t p = lo + lane, pc = p < hi ? p : hi;
   const uint64_t m = __ballot(off[pc + 1] > pos);
-  return m ? lo + uint64_t(__builtin_ctzll(m)) : hi;
+  const uint64_t r = m ? lo + uint64_t(__builtin_ctzll(m)) : hi;
+  return r < n ? r : n - 1;
 }
 
 // the wave whose share holds byte position s (shares of rt tiles from r0)

@@ -178,3 +178,19 @@ def test_flat_config4_full_size(flat_engine):
     torch.cuda.empty_cache()
     assert out[:64].tolist() == g["out_head"]
     assert hashlib.sha256(out.tobytes()).hexdigest() == g["out_sha256"]
+
+
+def test_flat_malformed_offsets_terminate(flat_engine, orc):
+    # non-monotone offsets (a contract violation: results are undefined) must
+    # still end the call in bounded time without a fault, and leave the
+    # per-wave slots clean for the next, valid batch
+    rng = np.random.default_rng(0xBAD0)
+    n = 5000
+    off = rng.integers(0, 1 << 22, n + 1).astype(np.uint64)
+    off[-1] = 1 << 22
+    buf = rng.integers(0, 256, (1 << 22) + 16, dtype=np.uint8)
+    flat_engine.checksum_batch(_t(buf), offsets=_t(off))
+    off2 = np.sort(off)
+    off2[0] = 0
+    out = flat_engine.checksum_batch(_t(buf), offsets=_t(off2))
+    assert (_u16(out) == orc.checksum_batch(buf, n, offsets=off2)).all()
