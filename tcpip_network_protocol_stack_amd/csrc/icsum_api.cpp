@@ -265,6 +265,7 @@ icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
 // one-segment kernel of the same lane shape
 icsum::Geometry ipv4_geometry(icsum::Geometry g) {
   g.segs = 1;
+  if (g.mode == icsum::kModeTiny) g = {4, 1, true, 2, 1};  // the tiny kernel is checksum-only
   if (!icsum::geometry_supported(g)) g.mode = 0;
   if (!icsum::geometry_supported(g)) g = {64, 8, true, 1, 1};
   return g;
@@ -291,16 +292,16 @@ bool forced_geometry(const ics_ctx* ctx) {
 // sixteenths: segments of <= 144 bytes, and bytes in segments over 1920
 // bytes.  A miss makes this call's batch the cache key.
 struct PlanMix {
-  uint32_t short16 = 0, long16 = 0;
+  uint32_t short16 = 0, long16 = 0, avg = 0;  // avg: mean segment length, bytes (capped at 4095)
 };
 bool plan_lookup(ics_ctx* ctx, const icsum::SegSpec& sp, bool any_plan, uint32_t* plan, bool* refresh,
                  PlanMix* mix = nullptr) {
   std::lock_guard<std::mutex> lock(ctx->plan_mu);
   const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
   const uint32_t p = uint32_t(v & 0xfu);
-  if (mix) *mix = {uint32_t(v >> 4) & 0xfu, uint32_t(v >> 40) & 0xfu};
+  if (mix) *mix = {uint32_t(v >> 4) & 0xfu, uint32_t(v >> 40) & 0xfu, uint32_t(v >> 44) & 0xfffu};
   const bool whole = p == icsum::kPlanWholeBatch || p == icsum::kPlanWholeBatch16 || p == icsum::kPlanWholeBatchSmall;
-  const bool same_n = (v >> 44) == 0 && ((v >> 8) & 0xFFFFFFFFull) == sp.n;  // ~0: nothing reported yet
+  const bool same_n = (v >> 56) == 0 && ((v >> 8) & 0xFFFFFFFFull) == sp.n;  // ~0: nothing reported yet
   if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && same_n && (whole || any_plan)) {
     *plan = p;
     *refresh = ++ctx->plan_hits % ics_ctx::kPlanRefresh == 0;
@@ -327,6 +328,13 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, hipStream_t st)
 // (1 M datagrams, 50 % / 75 % 40-byte ACKs + 1500 B: 139.5 / 107.4 us vs
 // 146.0 / 125.6 us AUTO; profiles/r2_csum_mix_sweep.jsonl)
 bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
+
+// the small-segment plan's single launch: one lane per segment for ACK-sized
+// means (icsum::kTinyMaxAvg), else 4-lane groups with 2 segments in flight
+icsum::Geometry small_plan_geometry(const PlanMix& m) {
+  return m.avg <= icsum::kTinyMaxAvg ? icsum::Geometry{1, 4, false, icsum::kModeTiny, 1}
+                                     : icsum::Geometry{4, 2, true, 2, 2};
+}
 
 // the flat dispatch (k_checksum_flat + k_flat_finish): one stream over the
 // batch's bytes, the cuts deciding where the sums go
@@ -360,7 +368,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len, sp.n, 0));
     if (hit && plan == icsum::kPlanWholeBatch16) g = {16, 8, true, 3, 1};
     if (hit && plan != icsum::kPlanWholeBatchSmall && short_mix(mix)) g = {8, 8, true, 3, 1};
-    if (hit && plan == icsum::kPlanWholeBatchSmall) g = {4, 2, true, 2, 2};
+    if (hit && plan == icsum::kPlanWholeBatchSmall) g = small_plan_geometry(mix);
     ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
     if (!hit || refresh)
       if (int rc = replan(ctx, sp, 64, st)) return rc;
@@ -401,7 +409,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
       // data) runs 8-lane groups whatever the plan (tools/ab_ipv4_mix.py)
       const icsum::Geometry g_hit = mix8                                        ? icsum::Geometry{8, 8, true, 3, 1}
                                     : hit_plan == icsum::kPlanWholeBatch16      ? icsum::Geometry{16, 8, true, 3, 1}
-                                    : hit_plan == icsum::kPlanWholeBatchSmall ? icsum::Geometry{4, 2, true, 2, 2}
+                                    : hit_plan == icsum::kPlanWholeBatchSmall ? small_plan_geometry(mix)
                                                                               : g_last;
       ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_hit,
                                      hit_plan == icsum::kPlanWholeBatch && !mix8 ? last_blocks : ctx->max_blocks, st));

@@ -201,14 +201,17 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       if (t_small < best) plan = kPlanWholeSmall;
     }
     meta[kBinMetaPlan] = plan;
+    const uint64_t avg = n ? total / n : 0;
+    meta[kBinMetaAvgLen] = uint32_t(avg < 0xFFFFFFFFull ? avg : 0xFFFFFFFFull);
     // the host's plan cache (icsum_api.cpp), one 8-byte store to page-locked
     // host memory: the plan (bits 0-3), the share of bin-0 (<= 144-byte)
-    // segments in sixteenths (bits 4-7), the batch size (bits 8-39) and the
+    // segments in sixteenths (bits 4-7), the batch size (bits 8-39), the
     // share of bytes in segments over 1920 bytes in sixteenths (bits 40-43)
+    // and the mean segment length in bytes, capped at 4095 (bits 44-55)
     const uint64_t short16 = n ? short_n * 16 / n : 0, long16 = total ? long_bytes * 16 / total : 0;
     if (plan_out)
       *plan_out = plan | ((short16 < 15 ? short16 : 15) << 4) | ((n & 0xFFFFFFFFull) << 8) |
-                  ((long16 < 15 ? long16 : 15) << 40);
+                  ((long16 < 15 ? long16 : 15) << 40) | ((avg < 4095 ? avg : 4095) << 44);
   }
 }
 
@@ -377,6 +380,13 @@ __device__ __forceinline__ void checksum_small_body(const uint8_t* __restrict__ 
                                                     const u32x4* __restrict__ zero16, void* __restrict__ out,
                                                     uint64_t n, uint32_t blk, uint32_t nblk);  // below
 
+template <int OUT>
+__device__ __forceinline__ void checksum_tiny_body(const uint8_t* __restrict__ bytes, const SegSrc& src,
+                                                   const uint32_t* __restrict__ init, uint32_t init_step,
+                                                   const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                                   const u32x4* __restrict__ zero16, void* __restrict__ out,
+                                                   uint64_t n, uint32_t blk, uint32_t nblk);  // below
+
 template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
 __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes, SegSrc src,
                                                      const uint32_t* __restrict__ init,
@@ -399,8 +409,20 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
       checksum_body<16, 8, true, 3, OUT>(bytes, whole, init, init_step, odd, odd_step, out, n, blk, nblk16);
       return;
     }
-    // ... under kPlanWholeSmall: the small-segment body (4 lanes, 2 segments
-    // per group in flight) in the first n/128 (logical) blocks
+    // ... under kPlanWholeSmall: ACK-sized segments (mean <= kTinyMaxAvg
+    // bytes) one per lane in the first n/256 (logical) blocks, otherwise the
+    // small-segment body (4 lanes, 2 segments per group in flight) in the
+    // first n/128
+    if (src.list && src.bin == kBins - 1 && src.meta[kBinMetaPlan] == kPlanWholeSmall &&
+        src.meta[kBinMetaAvgLen] <= kTinyMaxAvg) {
+      const uint64_t need = (n + kBlock - 1) / kBlock;
+      const uint32_t nblks = uint32_t(need < gridDim.x ? need : gridDim.x);
+      if (blk >= nblks) return;
+      SegSrc whole = src;
+      whole.list = nullptr;
+      checksum_tiny_body<OUT>(bytes, whole, init, init_step, odd, odd_step, zero16, out, n, blk, nblks);
+      return;
+    }
     if (src.list && src.bin == kBins - 1 && src.meta[kBinMetaPlan] == kPlanWholeSmall) {
       constexpr uint32_t kPerBlock = (kBlock / 4) * 2;
       const uint64_t need = (n + kPerBlock - 1) / kPerBlock;
@@ -511,6 +533,73 @@ __global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __rest
                                                            void* __restrict__ out, uint64_t n) {
   checksum_small_body<LPS, UNROLL, SEGS, OUT>(bytes, src, init, init_step, odd, odd_step, zero16, out, n,
                                               blockIdx.x, gridDim.x);
+}
+
+// Tiny segments (ACK-sized TCP segments, <= 4 chunks): ONE lane per segment.
+// The wave's offsets load is one coalesced 512-byte read, each lane then
+// issues its segment's (up to) four 16-byte loads at once — neighbouring
+// lanes' segments share lines, so the loads keep the default cache policy
+// and a line a neighbour also reads comes from L2 — and masks them to the
+// segment.  A longer segment finishes its remaining chunks in a loop (rare
+// in this kernel's range: the plans send it batches of short segments).
+// Absent per-segment arrays: zero16 + step 0.
+template <int OUT>
+__device__ __forceinline__ void checksum_tiny_body(const uint8_t* __restrict__ bytes, const SegSrc& src,
+                                                   const uint32_t* __restrict__ init, uint32_t init_step,
+                                                   const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                                   const u32x4* __restrict__ zero16, void* __restrict__ out,
+                                                   uint64_t n, uint32_t blk, uint32_t nblk) {
+  constexpr int kSlots = 4;
+  const Work w = resolve(src, n);
+  for (uint64_t g0 = uint64_t(blk) * kBlock; g0 < w.items; g0 += uint64_t(nblk) * kBlock) {
+    const uint64_t gi = g0 + threadIdx.x;
+    uint64_t seg, s, e;
+    src_locate(src, w, gi, n, seg, s, e);
+    const uint64_t a0 = s & ~uint64_t(15);
+    const uint64_t span = e > s ? e - a0 : 0;
+    const uint32_t nch = uint32_t((span + 15) >> 4);
+    const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(bytes + a0);
+    u32x4 v[kSlots];
+#pragma unroll
+    for (int u = 0; u < kSlots; ++u) {
+      // unconditional load from a valid address (empty segment -> zero16)
+      const u32x4* q = nch ? p + (uint32_t(u) < nch ? uint32_t(u) : nch - 1) : zero16;
+      if (nch) ICS_CHECK16(q, bytes + a0, bytes + a0 + (uint64_t(nch) << 4));
+      v[u] = *q;
+    }
+    const uint32_t i0 = init[seg * init_step];
+    const uint32_t swap = (uint32_t(s) ^ uint32_t(odd[seg * odd_step])) & 1u;
+    uint32_t ev = 0, od = 0;
+#pragma unroll
+    for (int u = 0; u < kSlots; ++u) {
+      const uint64_t at = uint64_t(u) << 4;
+      const uint32_t lo = u == 0 ? uint32_t(s) & 15u : 0u;
+      const uint32_t hi = at >= span ? 0u : (span - at >= 16 ? 16u : uint32_t(span - at));
+      acc_chunk(v[u] & byte_range_mask(lo, hi), ev, od);
+    }
+    for (uint32_t c = kSlots; c < nch; ++c) {  // longer segments
+      const uint64_t at = uint64_t(c) << 4;
+      const uint32_t hi = span - at >= 16 ? 16u : uint32_t(span - at);
+      ICS_CHECK16(p + c, bytes + a0, bytes + a0 + (uint64_t(nch) << 4));
+      acc_chunk(p[c] & byte_range_mask(0u, hi), ev, od);
+    }
+    if (gi < w.items) {
+      const uint32_t sum = i0 + combine_roles(ev, od, swap);
+      if (OUT == 0)
+        static_cast<uint16_t*>(out)[seg] = fold_value(sum);
+      else
+        static_cast<uint32_t*>(out)[seg] = sum;
+    }
+  }
+}
+
+template <int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum_tiny(const uint8_t* __restrict__ bytes, SegSrc src,
+                                                          const uint32_t* __restrict__ init, uint32_t init_step,
+                                                          const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                                          const u32x4* __restrict__ zero16, void* __restrict__ out,
+                                                          uint64_t n) {
+  checksum_tiny_body<OUT>(bytes, src, init, init_step, odd, odd_step, zero16, out, n, blockIdx.x, gridDim.x);
 }
 
 // Dense fixed-stride batches of short segments (stride == seg_len == 16*LPS,
@@ -1712,6 +1801,22 @@ hipError_t launch_checksum_small_t(const SegSpec& sp, const uint32_t* init, cons
   return hipGetLastError();
 }
 
+hipError_t launch_checksum_tiny_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
+                                  int out_kind, uint32_t max_blocks, hipStream_t st) {
+  const uint32_t blocks = blocks_for(sp.n, kBlock, max_blocks);
+  const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
+  const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
+  const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
+  const u32x4* z = static_cast<const u32x4*>(sp.zero16);
+  if (out_kind == 0)
+    hipLaunchKernelGGL(k_checksum_tiny<0>, dim3(blocks), dim3(kBlock), 0, st, sp.bytes, src_of(sp), ip, is, op, os,
+                       z, out, sp.n);
+  else
+    hipLaunchKernelGGL(k_checksum_tiny<1>, dim3(blocks), dim3(kBlock), 0, st, sp.bytes, src_of(sp), ip, is, op, os,
+                       z, out, sp.n);
+  return hipGetLastError();
+}
+
 template <int LPS, int SEGS>
 hipError_t launch_dense_t(const SegSpec& sp, const uint32_t* init, void* out, int out_kind, hipStream_t st) {
   const uint64_t segs_per_block = uint64_t(kBlock / LPS) * SEGS;
@@ -1775,6 +1880,7 @@ hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_ou
 // (16,4), 1460/1500 B (16,8).
 Geometry pick_geometry(uint64_t avg_len) {
   const uint64_t m = (avg_len + 15) / 16;  // 16-byte chunks of the payload
+  if (avg_len <= kTinyMaxAvg) return {1, 4, false, kModeTiny, 1};  // one lane per segment (ACK-sized)
   if (m <= 5) return {4, 1, true, 2, 2};   // small-segment kernel, 2 segments per group in flight
   if (m <= 9) return {4, 2, true, 2, 2};
   if (m <= 17) return {8, 2, true, 2, 2};
@@ -1806,6 +1912,7 @@ Geometry pick_geometry(uint64_t avg_len) {
 
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st) {
+  if (g.mode == kModeTiny) return launch_checksum_tiny_t(sp, init, odd, out, out_kind, max_blocks, st);
   if (g.segs > 1) {
 #define ICS_SMALL(L, U, K)                                                            \
   if (g.lps == L && g.unroll == U && g.segs == K)                                     \
@@ -1995,6 +2102,7 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
 }
 
 bool geometry_supported(Geometry g) {
+  if (g.mode == kModeTiny) return g.lps == 1 && g.segs == 1;
   if (g.segs > 1) {
 #define ICS_SMALL(L, U, K) \
   if (g.lps == L && g.unroll == U && g.segs == K) return true;

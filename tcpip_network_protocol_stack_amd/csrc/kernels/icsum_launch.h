@@ -17,6 +17,14 @@ struct Geometry {
   int segs = 1;  // > 1: small-segment kernel, SEGS segments per lane group in flight
 };
 
+// Geometry::mode of the tiny-segment kernel (k_checksum_tiny: one lane per
+// segment, up to four 16-byte loads in flight; {1, 4, false, kModeTiny, 1})
+constexpr int kModeTiny = 4;
+// batches of at most this mean segment length run one lane per segment:
+// 1 M x 40-43 B offsets 21.9 -> 11.4 us, fixed 40 / 52 B 15.8 -> 13.2 us;
+// 64-144 B segments are faster 4 lanes each (tools/ab_tiny.py)
+constexpr uint32_t kTinyMaxAvg = 56;
+
 // Pick a geometry from the (average) segment length in bytes.
 Geometry pick_geometry(uint64_t avg_len);
 bool geometry_supported(Geometry g);
@@ -53,7 +61,9 @@ constexpr int kBins = 5;
 constexpr int kBinMetaCount = 0;
 constexpr int kBinMetaCursor = 20;  // scatter pass: entries placed per bin
 constexpr int kBinMetaPlan = 28;    // 0: whole batch, 1: split into bins, 2: whole batch in 16-lane groups,
-                                    // 3: whole batch through the small-segment body
+                                    // 3: whole batch through the small-segment body (or, for a mean
+                                    // segment length <= kTinyMaxAvg, the tiny-segment body)
+constexpr int kBinMetaAvgLen = 29;  // mean segment length in bytes (plan kernel)
 constexpr int kBinMetaWords = 32;
 constexpr uint32_t kBinStatBlocks = 256;  // stats pass partials follow meta (<= 256: one per plan thread)
 // bytes of meta + the stats pass's partials (the lists follow, 16-byte aligned)

@@ -22,7 +22,8 @@ GEOMETRIES = [(1, 4, 0), (1, 8, 0), (2, 4, 0), (4, 1, 0), (4, 2, 0), (8, 2, 0), 
               (64, 8, 0), (8, 4, 1), (16, 4, 1), (16, 6, 1), (16, 8, 1), (32, 3, 1), (32, 4, 1),
               (64, 4, 1), (64, 8, 1), (1, 4, 2), (1, 8, 2), (2, 4, 2), (4, 1, 2), (4, 2, 2), (8, 1, 2),
               (8, 2, 2), (16, 2, 2), (16, 8, 3), (32, 4, 3), (64, 8, 3), (16, 4, 3), (32, 8, 3),
-              (16, 6, 3), (32, 3, 3), (8, 8, 3), (16, 5, 3)]
+              (16, 6, 3), (32, 3, 3), (8, 8, 3), (16, 5, 3),
+              (1, 4, 4)]  # MODE 4: k_checksum_tiny, one lane per segment
 # small-segment kernel (k_checksum_small): (LPS, UNROLL, MODE unused, SEGS) — ICS_SMALL_GEOMETRIES
 SMALL_GEOMETRIES = [(4, 1, 0, 2), (4, 1, 0, 4), (4, 1, 0, 8), (4, 2, 0, 2), (4, 2, 0, 4), (8, 1, 0, 4),
                     (8, 2, 0, 2), (8, 2, 0, 4), (16, 2, 0, 2)]
@@ -214,6 +215,28 @@ def test_binned_bimodal_large(bin_engine, orc):
     buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
     out = bin_engine.checksum_batch(_t(buf), offsets=_t(off))
     assert (_u16(out) == orc.checksum_batch(buf, n, offsets=off)).all()
+
+
+def test_binned_ack_batch(bin_engine, orc):
+    # ACK-sized segments (0-60 B, mean ~30 B): under the small-segment plan
+    # the device runs one lane per segment (k_checksum_tiny's body inside the
+    # last bin's launch), and on the second call the plan cache's single
+    # launch does the same from the host; every dispatch gives the reference
+    rng = np.random.default_rng(0xAC0)
+    n = 70_000
+    lens = rng.integers(0, 61, n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    off += 5
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    want = orc.checksum_batch(buf, n, offsets=off, init=init)
+    d, doff, dinit = _t(buf), _t(off), _t(init)
+    for call in range(3):
+        assert (_u16(bin_engine.checksum_batch(d, offsets=doff, init=dinit)) == want).all(), call
+    odd = rng.integers(0, 2, n).astype(np.uint8)
+    sums = bin_engine.sum_batch(d, offsets=doff, init=dinit, odd=_t(odd))
+    assert (_u32(sums) == orc.sum_batch(buf, n, offsets=off, init=init, odd=odd)).all()
 
 
 def test_set_binning_modes(engine, orc):
