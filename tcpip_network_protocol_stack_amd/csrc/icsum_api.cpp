@@ -930,7 +930,12 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   // most 64 KiB and mostly MTU-sized, and the 16-lane line grid is the best
   // measured geometry for both 1500- and 9000-byte datagrams (64 Ki x 1500 B:
   // 18.3 us vs 48.8 us with the 64-lane default; tools/ab_ipv4_offsets.py)
-  icsum::Geometry g = ipv4_geometry(geometry_for(ctx, d_offsets ? 1500 : dgram_len));
+  // ACK-sized datagrams (a fixed length <= kTinyMaxAvg, or a cached plan
+  // whose mean is) run one lane per datagram with default-policy loads
+  // (neighbours share lines): 1 M x 40 B VERIFY 30.3 -> 10.6 us (tools/ab_ipv4_mix.py, AB_LANE1)
+  const icsum::Geometry lane1{1, 4, false, 0, 1};
+  const icsum::Geometry base = geometry_for(ctx, d_offsets ? 1500 : dgram_len);
+  icsum::Geometry g = base.mode == icsum::kModeTiny ? lane1 : ipv4_geometry(base);
   hipStream_t st = static_cast<hipStream_t>(stream);
   // a receive batch of mostly short datagrams (pure ACKs: 40 bytes) leaves
   // most of a 16-lane group idle: from 16 Ki datagrams up the geometry
@@ -946,7 +951,9 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
     PlanMix mix;
     bool refresh = false;
     const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &mix);
-    if (hit && plan == icsum::kPlanWholeBatchSmall)
+    if (hit && plan == icsum::kPlanWholeBatchSmall && mix.avg <= icsum::kTinyMaxAvg)
+      g = lane1;
+    else if (hit && plan == icsum::kPlanWholeBatchSmall)
       g = ipv4_geometry({4, 2, true, 2, 1});
     else if (hit && mix.short16 >= ics_ctx::kIpv4ShortMix16 && mix.long16 == 0)
       g = ipv4_geometry({8, 8, true, 3, 1});  // ACK + MTU mixes: half the idle lanes on the ACKs

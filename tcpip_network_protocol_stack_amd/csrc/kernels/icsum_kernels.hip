@@ -1904,7 +1904,7 @@ Geometry pick_geometry(uint64_t avg_len) {
   X(1, 4, true, 2) X(1, 8, true, 2) X(2, 4, true, 2) X(4, 1, true, 2) X(4, 2, true, 2)     \
   X(8, 1, true, 2) X(8, 2, true, 2) X(16, 2, true, 2) X(16, 8, false, 1) X(64, 8, false, 1)    \
   X(16, 8, true, 3) X(32, 4, true, 3) X(64, 8, true, 3) X(16, 4, true, 3) X(32, 8, true, 3)   \
-  X(16, 6, true, 3) X(32, 3, true, 3) X(8, 8, true, 3) X(16, 5, true, 3)
+  X(16, 6, true, 3) X(32, 3, true, 3) X(8, 8, true, 3) X(16, 5, true, 3) X(1, 4, false, 0)
 
 // small-segment kernel instantiations (LPS, UNROLL, SEGS); Geometry::segs > 1
 #define ICS_SMALL_GEOMETRIES(X) \
