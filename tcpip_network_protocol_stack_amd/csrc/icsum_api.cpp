@@ -142,6 +142,10 @@ struct ics_ctx {
   // flat_waves (ICSUM_FLAT_WAVES): waves of k_checksum_flat (each streams an
   // equal share of the batch's 8 KiB tiles)
   int flat_mode = 0;
+  // ICSUM_TWOCLASS: 0 = short-heavy mixes (short_mix) run the two-class
+  // launch with 16-lane long groups; 1 = they run 8-lane groups (the earlier
+  // choice, A/B); 8 / 16 = every offsets batch through the two-class launch
+  int twoclass = 0;
   uint32_t flat_waves = 16384;
   std::mutex mu;
   // host path: nslots slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each
@@ -329,6 +333,19 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, hipStream_t st)
 // 146.0 / 125.6 us AUTO; profiles/r2_csum_mix_sweep.jsonl)
 bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
 
+// a short-heavy mix's single launch: the two-class launch (ACK-sized segments
+// one per lane, the rest 16 lanes each; 2 M x 40 / 1460 B 280.4 -> 255.8 us,
+// tools/ab_lastbin.py --var ICSUM_TWOCLASS), or 8-lane groups (ICSUM_TWOCLASS=1)
+hipError_t launch_mix(const ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
+                      void* d_out, int out_kind, hipStream_t st) {
+  if (ctx->twoclass != 1) {
+    const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, 16, st);
+    if (e != hipErrorInvalidValue) return e;
+  }
+  return icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, icsum::Geometry{8, 8, true, 3, 1},
+                                ctx->max_blocks, st);
+}
+
 // the small-segment plan's single launch: one lane per segment for ACK-sized
 // means (icsum::kTinyMaxAvg), else 4-lane groups with 2 segments in flight
 icsum::Geometry small_plan_geometry(const PlanMix& m) {
@@ -352,6 +369,10 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
                     void* d_out, int out_kind, hipStream_t st) {
   if (sp.offsets && ctx->flat_mode == 1 && sp.n < 0xFFFFFFFFull)
     return checksum_flat(ctx, sp, d_init, d_odd, d_out, out_kind, st);
+  if (sp.offsets && (ctx->twoclass == 8 || ctx->twoclass == 16)) {
+    ICS_HIP(icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, ctx->twoclass, st));
+    return ICS_OK;
+  }
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
                       (ctx->bin == 1 || (ctx->bin < 0 && sp.n >= ctx->bin_min && !forced_geometry(ctx)));
   const bool plannable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_cache && ctx->plan_host;
@@ -367,9 +388,11 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &mix);
     icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len, sp.n, 0));
     if (hit && plan == icsum::kPlanWholeBatch16) g = {16, 8, true, 3, 1};
-    if (hit && plan != icsum::kPlanWholeBatchSmall && short_mix(mix)) g = {8, 8, true, 3, 1};
     if (hit && plan == icsum::kPlanWholeBatchSmall) g = small_plan_geometry(mix);
-    ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
+    if (hit && plan != icsum::kPlanWholeBatchSmall && short_mix(mix))
+      ICS_HIP(launch_mix(ctx, sp, d_init, d_odd, d_out, out_kind, st));
+    else
+      ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
     if (!hit || refresh)
       if (int rc = replan(ctx, sp, 64, st)) return rc;
     return ICS_OK;
@@ -406,13 +429,15 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
       // its single launch: the last bin's geometry (whole), 16-lane groups
       // (whole16) or the small-segment body (wholeS) over every segment; a
       // short-heavy mix with no long segments (received traffic: ACKs + MTU
-      // data) runs 8-lane groups whatever the plan (tools/ab_ipv4_mix.py)
-      const icsum::Geometry g_hit = mix8                                        ? icsum::Geometry{8, 8, true, 3, 1}
-                                    : hit_plan == icsum::kPlanWholeBatch16      ? icsum::Geometry{16, 8, true, 3, 1}
+      // data) runs the two-class launch whatever the plan (launch_mix)
+      const icsum::Geometry g_hit = hit_plan == icsum::kPlanWholeBatch16      ? icsum::Geometry{16, 8, true, 3, 1}
                                     : hit_plan == icsum::kPlanWholeBatchSmall ? small_plan_geometry(mix)
                                                                               : g_last;
-      ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_hit,
-                                     hit_plan == icsum::kPlanWholeBatch && !mix8 ? last_blocks : ctx->max_blocks, st));
+      if (mix8)
+        ICS_HIP(launch_mix(ctx, sp, d_init, d_odd, d_out, out_kind, st));
+      else
+        ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_hit,
+                                       hit_plan == icsum::kPlanWholeBatch ? last_blocks : ctx->max_blocks, st));
       // re-plan behind it: a batch whose mix changed under the same pointer
       // and size is re-binned from the next call on
       if (refresh)
@@ -854,6 +879,7 @@ int ics_create(int device, ics_ctx** out) {
   ctx->bin_debug = std::getenv("ICSUM_BIN_DEBUG") != nullptr;
   if (std::getenv("ICSUM_FLAT")) ctx->flat_mode = int(env_u32("ICSUM_FLAT", 0)) == 1 ? 1 : 0;
   ctx->flat_waves = std::max<uint32_t>(1, env_u32("ICSUM_FLAT_WAVES", ctx->flat_waves));
+  ctx->twoclass = int(env_u32("ICSUM_TWOCLASS", 0));
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
   ctx->blocking_sync = env_u32("ICSUM_HOST_BLOCKING_SYNC", 0) != 0;

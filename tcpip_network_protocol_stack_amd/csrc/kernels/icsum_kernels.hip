@@ -602,6 +602,88 @@ __global__ __launch_bounds__(kBlock) void k_checksum_tiny(const uint8_t* __restr
   checksum_tiny_body<OUT>(bytes, src, init, init_step, odd, odd_step, zero16, out, n, blockIdx.x, gridDim.x);
 }
 
+// Two-class launch for receive mixes (ACKs among MTU segments), no binning
+// pass: wave w reads the bounds of segments [64 w, 64 w + 64), finishes the
+// short ones (<= 4 chunks) one per lane as k_checksum_tiny does, then its
+// long ones LONG_LPS lanes each (the line grid, unroll 8), 64 / LONG_LPS at a
+// time from a per-wave LDS list.
+template <int LONG_LPS, int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __restrict__ bytes, SegSrc src,
+                                                              const uint32_t* __restrict__ init, uint32_t init_step,
+                                                              const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                                              const u32x4* __restrict__ zero16,
+                                                              void* __restrict__ out, uint64_t n) {
+  __shared__ uint64_t lst[kBlock / 64][64][2];  // per wave: the long segments' {start, end}
+  __shared__ uint32_t lseg[kBlock / 64][64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const Work w{n, nullptr};
+  const uint64_t gi = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * 64 + lane;
+  uint64_t seg, s, e;
+  src_locate(src, w, gi, n, seg, s, e);
+  const bool valid = gi < n;
+  const uint64_t a0 = s & ~uint64_t(15);
+  const uint64_t span = e > s ? e - a0 : 0;
+  const uint32_t nch = uint32_t((span + 15) >> 4);
+  const bool is_short = nch <= 4;
+  // short segments: one lane each (long lanes load the zero block)
+  const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(bytes + a0);
+  u32x4 v[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const u32x4* q = nch && is_short ? p + (uint32_t(u) < nch ? uint32_t(u) : nch - 1) : zero16;
+    v[u] = *q;
+  }
+  // the long ones go to the wave's list, in lane order
+  const uint64_t lmask = __ballot(valid && !is_short);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(lmask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(lmask), 0u));
+  if (valid && !is_short) {
+    lst[wv][rank][0] = s;
+    lst[wv][rank][1] = e;
+    lseg[wv][rank] = uint32_t(seg);
+  }
+  if (valid && is_short) {
+    uint32_t ev = 0, od = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const uint64_t at = uint64_t(u) << 4;
+      const uint32_t lo = u == 0 ? uint32_t(s) & 15u : 0u;
+      const uint32_t hi = at >= span ? 0u : (span - at >= 16 ? 16u : uint32_t(span - at));
+      acc_chunk(v[u] & byte_range_mask(lo, hi), ev, od);
+    }
+    const uint32_t sw = (uint32_t(s) ^ uint32_t(odd[seg * odd_step])) & 1u;
+    const uint32_t sum = init[seg * init_step] + combine_roles(ev, od, sw);
+    if (OUT == 0)
+      static_cast<uint16_t*>(out)[seg] = fold_value(sum);
+    else
+      static_cast<uint32_t*>(out)[seg] = sum;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  constexpr uint32_t kGroups = 64 / LONG_LPS;
+  const uint32_t nlong = uint32_t(__builtin_popcountll(lmask));
+  const uint32_t g = lane / LONG_LPS, gl = lane & (LONG_LPS - 1);
+  for (uint32_t r0 = 0; r0 < nlong; r0 += kGroups) {  // uniform
+    const uint32_t k = r0 + g;
+    const bool mine = k < nlong;
+    const uint32_t kc = mine ? k : 0u;
+    const uint64_t ls = mine ? lst[wv][kc][0] : 0, le = mine ? lst[wv][kc][1] : 0;
+    const uint64_t lsg = lseg[wv][kc];
+    const uint32_t i0 = init[lsg * init_step];
+    const uint32_t sw = (uint32_t(ls) ^ uint32_t(odd[lsg * odd_step])) & 1u;
+    uint32_t ev = 0, od = 0;
+    range_sums_line_primed<LONG_LPS, 8, true>(bytes, ls, le, gl, ev, od);
+    const uint32_t tot = group_sum<LONG_LPS>(combine_roles(ev, od, sw));
+    if (mine && gl == LONG_LPS - 1) {
+      const uint32_t sum = i0 + tot;
+      if (OUT == 0)
+        static_cast<uint16_t*>(out)[lsg] = fold_value(sum);
+      else
+        static_cast<uint32_t*>(out)[lsg] = sum;
+    }
+  }
+}
+
 // Dense fixed-stride batches of short segments (stride == seg_len == 16*LPS,
 // 16-byte aligned base — config 3's 1 M x 64 B TCP segments): the batch is one
 // flat array of 16-byte chunks, every chunk belongs whole to one segment, so
@@ -1801,6 +1883,24 @@ hipError_t launch_checksum_small_t(const SegSpec& sp, const uint32_t* init, cons
   return hipGetLastError();
 }
 
+template <int LONG_LPS>
+hipError_t launch_twoclass_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
+                             hipStream_t st) {
+  const uint64_t blocks = (sp.n + kBlock - 1) / kBlock;
+  if (blocks == 0 || blocks > (uint64_t(1) << 24)) return hipErrorInvalidValue;
+  const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
+  const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
+  const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
+  const u32x4* z = static_cast<const u32x4*>(sp.zero16);
+  if (out_kind == 0)
+    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
+                       src_of(sp), ip, is, op, os, z, out, sp.n);
+  else
+    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
+                       src_of(sp), ip, is, op, os, z, out, sp.n);
+  return hipGetLastError();
+}
+
 hipError_t launch_checksum_tiny_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                                   int out_kind, uint32_t max_blocks, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock, max_blocks);
@@ -1950,6 +2050,14 @@ hipError_t launch_checksum_flat(const SegSpec& sp, const uint32_t* init, const u
     hipLaunchKernelGGL(k_flat_finish<1>, fgrid, dim3(kBlock), 0, st, accw, tailw, ip, is, out, nwaves);
   }
   return hipGetLastError();
+}
+
+hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
+                                    int out_kind, int long_lps, hipStream_t st) {
+  if (sp.list) return hipErrorInvalidValue;
+  if (long_lps == 8) return launch_twoclass_t<8>(sp, init, odd, out, out_kind, st);
+  if (long_lps == 16) return launch_twoclass_t<16>(sp, init, odd, out, out_kind, st);
+  return hipErrorInvalidValue;
 }
 
 bool dense_supported(const SegSpec& sp) {

@@ -1,6 +1,7 @@
-"""GPU parity of the flat dispatch of packed offsets batches
-(k_checksum_flat + k_flat_finish, forced with ICSUM_FLAT=1): one byte stream
-cut at the offsets, against the golden KATs and the oracle.
+"""GPU parity of the alternative dispatches of packed offsets batches — the
+flat dispatch (k_checksum_flat + k_flat_finish, forced with ICSUM_FLAT=1: one
+byte stream cut at the offsets) and the two-class launch (ICSUM_TWOCLASS) —
+against the golden KATs and the oracle.
 
 Wave counts from 1 (one share: every segment finishes inside it) to a few
 dozen (segments crossing share boundaries, finished through the per-wave
@@ -17,7 +18,12 @@ pytestmark = pytest.mark.gpu
 FLAT_ENVS = [{"ICSUM_FLAT": "1"},
              {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "1"},
              {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "7"},
-             {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "97"}]
+             {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "97"},
+             # the two-class launch (k_checksum_twoclass: short segments one per
+             # lane, long ones 16 / 8 lanes each) forced on every offsets batch;
+             # AUTO uses it for short-heavy mixes
+             {"ICSUM_TWOCLASS": "16"},
+             {"ICSUM_TWOCLASS": "8"}]
 
 
 @pytest.fixture(scope="module", params=FLAT_ENVS, ids=lambda e: "-".join(f"{k[6:]}{v}" for k, v in e.items()))
