@@ -122,6 +122,8 @@ struct ics_ctx {
   // ics_ipv4_tcp_batch: from this share of <= 144-byte datagrams (sixteenths,
   // the plan word's bits 4-7) an offsets batch runs 8-lane groups
   static constexpr uint32_t kIpv4ShortMix16 = 5;
+  // ... and from this share up the two-class launch (k_ipv4_twoclass)
+  static constexpr uint32_t kIpv4TwoClass16 = 8;
   // the plain checksum's 8-lane threshold (short_mix)
   static constexpr uint32_t kShortMix16 = 7;
   bool plan_cache = true;
@@ -970,7 +972,7 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   // from 5/16 of <= 144-byte datagrams, 16 x 4 below that), the plan
   // kernels running behind the first and every 16th launch (DESIGN.md §4,
   // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
-  bool plan_after = false;
+  bool plan_after = false, two = false;
   if (d_offsets && ctx->plan_cache && ctx->plan_host && !forced_geometry(ctx) && n >= ics_ctx::kSmallPlanMin &&
       n <= 0xFFFFFFFFull) {
     uint32_t plan = 0;
@@ -985,9 +987,19 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
       g = ipv4_geometry({8, 8, true, 3, 1});  // ACK + MTU mixes: half the idle lanes on the ACKs
     else if (hit)
       g = ipv4_geometry({16, 4, true, 3, 1});  // MTU + a few ACKs: shorter unroll, 1-4 % (1 M datagrams)
+    // from half ACKs up: the two-class launch (ICSUM_TWOCLASS=1: the 8-lane
+    // groups above; 1 M datagrams VERIFY 3/4 ACKs 128.8 -> 86.0 us, 1/2
+    // 158.7 -> 154.7, but 5/16 204 us: tools/ab_ipv4_mix.py)
+    two = hit && plan != icsum::kPlanWholeBatchSmall && mix.short16 >= ics_ctx::kIpv4TwoClass16 &&
+          mix.long16 == 0 && ctx->twoclass != 1;
     plan_after = !hit || refresh;
   }
-  ICS_HIP(icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt, st));
+  if (d_offsets && (ctx->twoclass == 8 || ctx->twoclass == 16)) two = true;  // forced (A/B, tests)
+  hipError_t le = hipErrorInvalidValue;
+  if (two) le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, ctx->patch_wt, st);
+  if (le == hipErrorInvalidValue)
+    le = icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt, st);
+  ICS_HIP(le);
   if (plan_after)
     if (int rc = replan(ctx, sp, 64, st)) return rc;
   return bounds_verdict(st, ICS_OK);

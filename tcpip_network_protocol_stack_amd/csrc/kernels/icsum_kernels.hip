@@ -1294,6 +1294,90 @@ __device__ __forceinline__ uint32_t ipv4_pseudo(const Hdr& h) {
 }
 
 // --------------------------------------------- fused IPv4 + TCP ----------
+// One datagram [s, e) per group of LPS lanes (every lane of the wave calls it:
+// group sums and the wave-uniform re-sum below); `valid` false: an idle group.
+template <int LPS, int UNROLL, bool NT, int MODE>
+__device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, uint64_t e, uint64_t seg, bool valid,
+                                          uint32_t lane, int mode, uint16_t* __restrict__ ip_ck,
+                                          uint16_t* __restrict__ tcp_ck, uint8_t* __restrict__ status, int patch_wt,
+                                          const uint8_t* __restrict__ zpad, const uint32_t* zlast) {
+  const bool hdr = e - s >= 20;
+  // Speculate the usual header length (hlen = 5): the IPv4 header dwords,
+  // the TCP fields the verdict needs (data offset, checksum) and the TCP
+  // byte stream are all requested before any of them returns; every lane
+  // loads the header (same addresses per group, one request per wave
+  // instruction), from the 32-byte zero pad when the datagram is too short.
+  // A datagram with options (rare) redoes its stream below.
+  uint64_t t0 = hdr ? s + 20 : e;  // TCP part: [t0, e)
+  const uint32_t* last = hdr ? last_dword(dg + e) : zlast;
+  Hdr h;
+  uint32_t tf0 = 0, tf1 = 0;  // TCP bytes 12..15 and 16..19 (little-endian)
+  const bool tcpf = hdr && e - t0 >= 18;
+  GroupHdr gh{};
+  if constexpr (LPS >= 16) {
+    gh = group_hdr_load<LPS>(hdr ? dg + s : zpad, last, tcpf ? dg + t0 : zpad, tcpf ? last : zlast);
+  } else {
+    h = load_hdr(hdr ? dg + s : zpad, last);
+    load_tcp_fields(tcpf ? dg + t0 : zpad, tcpf ? last : zlast, tf0, tf1);
+  }
+  uint32_t ev = 0, od = 0;
+  seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
+  if constexpr (LPS >= 16) group_hdr_take<LPS>(gh, h, tf0, tf1);
+  bool redo = false;
+  if (hdr) {
+    uint64_t off = 4u * (h.byte(0) & 0x0fu);  // options skipped (ipv4_header.cpp:50)
+    if (off < 20) off = 20;
+    if (off > e - s) off = e - s;
+    redo = s + off != t0;
+    t0 = s + off;
+    if (redo) {
+      tf0 = tf1 = 0;
+      if (e - t0 >= 18) load_tcp_fields(dg + t0, last, tf0, tf1);
+    }
+  }
+  if (__any(redo)) {  // wave-uniform; groups without options re-sum the same bytes
+    ev = od = 0;
+    seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
+  }
+  const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(t0) & 1u));
+  if (valid && lane == LPS - 1) {
+    uint16_t ipc = 0, tcv = 0;
+    uint8_t st = 0;
+    if (hdr) {
+      const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu;
+      const bool hdr_ok = ver == 4 && hlen >= 5;  // ipv4_header.cpp:32-41
+      ipc = fold_value(ipv4_header_sum(h));
+      const uint32_t pseudo = ipv4_pseudo(h);
+      const uint64_t rem = e - t0;
+      if (h.byte(9) == 6) st |= 0x08;  // proto TCP
+      if (rem >= 20 && ((tf0 & 0xffu) >> 4) >= 5) st |= 0x04;  // tcp_segment.cpp:25-65
+      if (mode == 1) {
+        tcv = fold_value(pseudo + tot);  // tcp_segment.cpp:11-18
+        if (hdr_ok && ipc == h.be16(10)) st |= 0x01;  // ipv4_header.cpp:53-58
+        if (tcv == 0) st |= 0x02;
+      } else {
+        // tcp_segment.cpp:143: the checksum field counts as 0
+        uint32_t sum = pseudo + tot;
+        if (rem > 16) sum -= (rem >= 18 ? tf1 & 0xffu : uint32_t(dg[t0 + 16])) << 8;
+        if (rem > 17) sum -= (tf1 >> 8) & 0xffu;
+        tcv = fold_value(sum);
+        if (hdr_ok) st |= 0x01;
+        if (rem >= 18) st |= 0x02;
+        if (mode == 2 && patch_wt) {
+          store_be16<true>(dg + s + 10, ipc);
+          if (rem >= 18) store_be16<true>(dg + t0 + 16, tcv);
+        } else if (mode == 2) {
+          store_be16(dg + s + 10, ipc);
+          if (rem >= 18) store_be16(dg + t0 + 16, tcv);
+        }
+      }
+    }
+    if (ip_ck) ip_ck[seg] = ipc;
+    if (tcp_ck) tcp_ck[seg] = tcv;
+    if (status) status[seg] = st;
+  }
+}
+
 template <int LPS, int UNROLL, bool NT, int MODE>
 __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      const uint64_t* __restrict__ offsets,
@@ -1314,81 +1398,49 @@ __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_ipv4_tcp(uint8_t* __restric
     uint64_t s, e;
     seg_bounds(offsets, stride, dlen, valid ? seg : n - 1, s, e);
     if (!valid) e = s;
-    const bool hdr = e - s >= 20;
-    // Speculate the usual header length (hlen = 5): the IPv4 header dwords,
-    // the TCP fields the verdict needs (data offset, checksum) and the TCP
-    // byte stream are all requested before any of them returns; every lane
-    // loads the header (same addresses per group, one request per wave
-    // instruction), from the 32-byte zero pad when the datagram is too short.
-    // A datagram with options (rare) redoes its stream below.
-    uint64_t t0 = hdr ? s + 20 : e;  // TCP part: [t0, e)
-    const uint32_t* last = hdr ? last_dword(dg + e) : zlast;
-    Hdr h;
-    uint32_t tf0 = 0, tf1 = 0;  // TCP bytes 12..15 and 16..19 (little-endian)
-    const bool tcpf = hdr && e - t0 >= 18;
-    GroupHdr gh{};
-    if constexpr (LPS >= 16) {
-      gh = group_hdr_load<LPS>(hdr ? dg + s : zpad, last, tcpf ? dg + t0 : zpad, tcpf ? last : zlast);
-    } else {
-      h = load_hdr(hdr ? dg + s : zpad, last);
-      load_tcp_fields(tcpf ? dg + t0 : zpad, tcpf ? last : zlast, tf0, tf1);
-    }
-    uint32_t ev = 0, od = 0;
-    seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
-    if constexpr (LPS >= 16) group_hdr_take<LPS>(gh, h, tf0, tf1);
-    bool redo = false;
-    if (hdr) {
-      uint64_t off = 4u * (h.byte(0) & 0x0fu);  // options skipped (ipv4_header.cpp:50)
-      if (off < 20) off = 20;
-      if (off > e - s) off = e - s;
-      redo = s + off != t0;
-      t0 = s + off;
-      if (redo) {
-        tf0 = tf1 = 0;
-        if (e - t0 >= 18) load_tcp_fields(dg + t0, last, tf0, tf1);
-      }
-    }
-    if (__any(redo)) {  // wave-uniform; groups without options re-sum the same bytes
-      ev = od = 0;
-      seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
-    }
-    const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(t0) & 1u));
-    if (valid && lane == LPS - 1) {
-      uint16_t ipc = 0, tcv = 0;
-      uint8_t st = 0;
-      if (hdr) {
-        const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu;
-        const bool hdr_ok = ver == 4 && hlen >= 5;  // ipv4_header.cpp:32-41
-        ipc = fold_value(ipv4_header_sum(h));
-        const uint32_t pseudo = ipv4_pseudo(h);
-        const uint64_t rem = e - t0;
-        if (h.byte(9) == 6) st |= 0x08;  // proto TCP
-        if (rem >= 20 && ((tf0 & 0xffu) >> 4) >= 5) st |= 0x04;  // tcp_segment.cpp:25-65
-        if (mode == 1) {
-          tcv = fold_value(pseudo + tot);  // tcp_segment.cpp:11-18
-          if (hdr_ok && ipc == h.be16(10)) st |= 0x01;  // ipv4_header.cpp:53-58
-          if (tcv == 0) st |= 0x02;
-        } else {
-          // tcp_segment.cpp:143: the checksum field counts as 0
-          uint32_t sum = pseudo + tot;
-          if (rem > 16) sum -= (rem >= 18 ? tf1 & 0xffu : uint32_t(dg[t0 + 16])) << 8;
-          if (rem > 17) sum -= (tf1 >> 8) & 0xffu;
-          tcv = fold_value(sum);
-          if (hdr_ok) st |= 0x01;
-          if (rem >= 18) st |= 0x02;
-          if (mode == 2 && patch_wt) {
-            store_be16<true>(dg + s + 10, ipc);
-            if (rem >= 18) store_be16<true>(dg + t0 + 16, tcv);
-          } else if (mode == 2) {
-            store_be16(dg + s + 10, ipc);
-            if (rem >= 18) store_be16(dg + t0 + 16, tcv);
-          }
-        }
-      }
-      if (ip_ck) ip_ck[seg] = ipc;
-      if (tcp_ck) tcp_ck[seg] = tcv;
-      if (status) status[seg] = st;
-    }
+    ipv4_item<LPS, UNROLL, NT, MODE>(dg, s, e, seg, valid, lane, mode, ip_ck, tcp_ck, status, patch_wt, zpad, zlast);
+  }
+}
+
+// Two-class launch for receive mixes (ACKs among MTU datagrams): wave w
+// takes datagrams [64 w, 64 w + 64); those of <= 64 bytes one per lane, the
+// rest 16 lanes each from a per-wave LDS list, four at a time.
+__global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
+                                                          uint64_t stride, uint64_t dlen, uint64_t n, int mode,
+                                                          uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
+                                                          uint8_t* __restrict__ status, int patch_wt,
+                                                          const uint8_t* __restrict__ zpad) {
+  __shared__ uint64_t lst[kBlock / 64][64][2];
+  __shared__ uint32_t lseg[kBlock / 64][64];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
+  const uint64_t seg = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * 64 + lane;
+  const bool valid = seg < n;
+  uint64_t s, e;
+  seg_bounds(offsets, stride, dlen, valid ? seg : n - 1, s, e);
+  if (!valid) e = s;
+  const bool is_short = e - s <= 64;
+  const uint64_t lmask = __ballot(valid && !is_short);
+  const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(lmask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(lmask), 0u));
+  if (valid && !is_short) {
+    lst[wv][rank][0] = s;
+    lst[wv][rank][1] = e;
+    lseg[wv][rank] = uint32_t(seg);
+  }
+  // short datagrams: one lane each (the long lanes run an empty item)
+  ipv4_item<1, 4, false, 0>(dg, s, is_short ? e : s, seg, valid && is_short, 0u, mode, ip_ck, tcp_ck, status,
+                            patch_wt, zpad, zlast);
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  const uint32_t nlong = uint32_t(__builtin_popcountll(lmask));
+  const uint32_t g = lane >> 4, gl = lane & 15u;
+  for (uint32_t r0 = 0; r0 < nlong; r0 += 4) {  // uniform
+    const uint32_t k = r0 + g;
+    const bool mine = k < nlong;
+    const uint32_t kc = mine ? k : 0u;
+    const uint64_t ls = lst[wv][kc][0], le = mine ? lst[wv][kc][1] : ls;
+    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[wv][kc], mine, gl, mode, ip_ck, tcp_ck, status, patch_wt, zpad, zlast);
   }
 }
 
@@ -2188,6 +2240,16 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
+}
+
+hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
+                                bool patch_wt, hipStream_t st) {
+  const uint64_t blocks = (sp.n + kBlock - 1) / kBlock;
+  if (sp.list || blocks == 0 || blocks > (uint64_t(1) << 24)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_ipv4_twoclass, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes),
+                     sp.offsets, sp.stride, sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, int(patch_wt),
+                     static_cast<const uint8_t*>(sp.zero16));
+  return hipGetLastError();
 }
 
 hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,

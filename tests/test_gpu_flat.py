@@ -200,3 +200,44 @@ def test_flat_malformed_offsets_terminate(flat_engine, orc):
     off2[0] = 0
     out = flat_engine.checksum_batch(_t(buf), offsets=_t(off2))
     assert (_u16(out) == orc.checksum_batch(buf, n, offsets=off2)).all()
+
+
+@pytest.fixture(scope="module", params=["16", "1"], ids=lambda v: f"TWOCLASS{v}")
+def two_engine(request):
+    yield from _engine_with({"ICSUM_TWOCLASS": request.param})
+
+
+@pytest.mark.parametrize("mix", ["bimodal", "ackheavy", "tricky"])
+def test_ipv4_twoclass_vs_oracle(two_engine, orc, mix):
+    """Raw IPv4/TCP datagram batches through the two-class fused launch
+    (k_ipv4_twoclass: <= 64-byte datagrams one per lane, the rest 16 lanes
+    each; forced with ICSUM_TWOCLASS=16, the 8-lane launch with =1): COMPUTE,
+    VERIFY and PATCH against the oracle, patched bytes included.  "tricky"
+    adds short (< 20 B), 64/65-byte edge, option-carrying and corrupted
+    datagrams."""
+    rng = np.random.default_rng(0x1F0 + len(mix))
+    n = 20_000
+    ack = lambda p: np.where(rng.random(n) < p, 40, 1460) + rng.integers(0, 4, n)  # noqa: E731
+    lens = {"bimodal": lambda: ack(0.5), "ackheavy": lambda: ack(0.75),
+            "tricky": lambda: rng.choice([0, 7, 19, 20, 39, 40, 41, 63, 64, 65, 100, 1460, 1500], n)}[mix]()
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    off += 3
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    s, ln = off[:-1].astype(np.int64), np.diff(off).astype(np.int64)
+    ok = ln >= 40
+    s, ln = s[ok], ln[ok]
+    buf[s], buf[s + 2], buf[s + 3] = 0x45, (ln >> 8).astype(np.uint8), (ln & 255).astype(np.uint8)
+    buf[s + 6], buf[s + 8], buf[s + 9], buf[s + 32] = 0x40, 64, 6, 0x50
+    if mix == "tricky":
+        buf[s[::7]] = 0x46  # options (hlen 6)
+        buf[s[::11] + 25] ^= 0x10  # corrupted TCP bytes
+    for mode in (0, 1, 2):
+        hb = buf.copy()
+        want = orc.ipv4_tcp_batch(hb, n, mode, offsets=off)
+        d = _t(buf)
+        ip, tcp, st = two_engine.ipv4_tcp_batch(d, mode, offsets=_t(off))
+        assert (_u16(ip) == want[0]).all(), (mix, mode)
+        assert (_u16(tcp) == want[1]).all(), (mix, mode)
+        assert (st.cpu().numpy() == want[2]).all(), (mix, mode)
+        assert (d.cpu().numpy() == hb).all(), (mix, mode)  # PATCH wrote what the oracle wrote
