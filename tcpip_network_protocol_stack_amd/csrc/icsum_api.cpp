@@ -336,12 +336,18 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, hipStream_t st)
 bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
 
 // a short-heavy mix's single launch: the two-class launch (ACK-sized segments
-// one per lane, the rest 16 lanes each; 2 M x 40 / 1460 B 280.4 -> 255.8 us,
-// tools/ab_lastbin.py --var ICSUM_TWOCLASS), or 8-lane groups (ICSUM_TWOCLASS=1)
+// one per lane, the rest 16 lanes each), 32 segments per wave from 3/4 short
+// segments up and 16 below (fewer long segments per wave: shorter-lived
+// waves), or 8-lane groups (ICSUM_TWOCLASS=1).  2 M x 40 / 1460 B: 8-lane
+// 279.5, 64 / 32 / 16 per wave 255.7 / 234.9 / 231.1 us; raw-datagram mixes
+// (tools/ab_ipv4_mix.py plain rows, 64 / 32 / 16): 7/8 ACKs 43.5 / 42.2 /
+// 54.5, 3/4 74.8 / 68.5 / 74.5, 1/2 132.4 / 122.5 / 119.0, 7/16 145.0 /
+// 139.3 / 131.9 us (profiles/r2_twoclass_spw*.jsonl)
 hipError_t launch_mix(const ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
-                      void* d_out, int out_kind, hipStream_t st) {
+                      void* d_out, int out_kind, const PlanMix& mix, hipStream_t st) {
   if (ctx->twoclass != 1) {
-    const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, 16, st);
+    const int spw = mix.short16 >= 12 ? 32 : 16;
+    const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, 16 | (spw << 8), st);
     if (e != hipErrorInvalidValue) return e;
   }
   return icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, icsum::Geometry{8, 8, true, 3, 1},
@@ -371,7 +377,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
                     void* d_out, int out_kind, hipStream_t st) {
   if (sp.offsets && ctx->flat_mode == 1 && sp.n < 0xFFFFFFFFull)
     return checksum_flat(ctx, sp, d_init, d_odd, d_out, out_kind, st);
-  if (sp.offsets && (ctx->twoclass == 8 || ctx->twoclass == 16)) {
+  if (sp.offsets && ((ctx->twoclass & 0xff) == 8 || (ctx->twoclass & 0xff) == 16)) {
     ICS_HIP(icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, ctx->twoclass, st));
     return ICS_OK;
   }
@@ -392,7 +398,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     if (hit && plan == icsum::kPlanWholeBatch16) g = {16, 8, true, 3, 1};
     if (hit && plan == icsum::kPlanWholeBatchSmall) g = small_plan_geometry(mix);
     if (hit && plan != icsum::kPlanWholeBatchSmall && short_mix(mix))
-      ICS_HIP(launch_mix(ctx, sp, d_init, d_odd, d_out, out_kind, st));
+      ICS_HIP(launch_mix(ctx, sp, d_init, d_odd, d_out, out_kind, mix, st));
     else
       ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
     if (!hit || refresh)
@@ -436,7 +442,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
                                     : hit_plan == icsum::kPlanWholeBatchSmall ? small_plan_geometry(mix)
                                                                               : g_last;
       if (mix8)
-        ICS_HIP(launch_mix(ctx, sp, d_init, d_odd, d_out, out_kind, st));
+        ICS_HIP(launch_mix(ctx, sp, d_init, d_odd, d_out, out_kind, mix, st));
       else
         ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_hit,
                                        hit_plan == icsum::kPlanWholeBatch ? last_blocks : ctx->max_blocks, st));
@@ -994,7 +1000,7 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
           mix.long16 == 0 && ctx->twoclass != 1;
     plan_after = !hit || refresh;
   }
-  if (d_offsets && (ctx->twoclass == 8 || ctx->twoclass == 16)) two = true;  // forced (A/B, tests)
+  if (d_offsets && ((ctx->twoclass & 0xff) == 8 || (ctx->twoclass & 0xff) == 16)) two = true;  // forced (A/B, tests)
   hipError_t le = hipErrorInvalidValue;
   if (two) le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, ctx->patch_wt, st);
   if (le == hipErrorInvalidValue)

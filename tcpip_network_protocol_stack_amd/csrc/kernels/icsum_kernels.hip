@@ -607,7 +607,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_tiny(const uint8_t* __restr
 // short ones (<= 4 chunks) one per lane as k_checksum_tiny does, then its
 // long ones LONG_LPS lanes each (the line grid, unroll 8), 64 / LONG_LPS at a
 // time from a per-wave LDS list.
-template <int LONG_LPS, int OUT>
+template <int LONG_LPS, int SPW, int OUT>
 __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __restrict__ bytes, SegSrc src,
                                                               const uint32_t* __restrict__ init, uint32_t init_step,
                                                               const uint8_t* __restrict__ odd, uint32_t odd_step,
@@ -617,10 +617,12 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
   __shared__ uint32_t lseg[kBlock / 64][64];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const Work w{n, nullptr};
-  const uint64_t gi = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * 64 + lane;
+  // SPW segments per wave (lanes >= SPW idle in the short phase): fewer
+  // long segments per wave, so shorter-lived waves when long ones abound
+  const uint64_t gi = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
   uint64_t seg, s, e;
   src_locate(src, w, gi, n, seg, s, e);
-  const bool valid = gi < n;
+  const bool valid = gi < n && lane < SPW;
   const uint64_t a0 = s & ~uint64_t(15);
   const uint64_t span = e > s ? e - a0 : 0;
   const uint32_t nch = uint32_t((span + 15) >> 4);
@@ -1935,21 +1937,22 @@ hipError_t launch_checksum_small_t(const SegSpec& sp, const uint32_t* init, cons
   return hipGetLastError();
 }
 
-template <int LONG_LPS>
+template <int LONG_LPS, int SPW>
 hipError_t launch_twoclass_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
                              hipStream_t st) {
-  const uint64_t blocks = (sp.n + kBlock - 1) / kBlock;
+  const uint64_t per_block = uint64_t(kBlock / 64) * SPW;
+  const uint64_t blocks = (sp.n + per_block - 1) / per_block;
   if (blocks == 0 || blocks > (uint64_t(1) << 24)) return hipErrorInvalidValue;
   const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
   const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
   const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
   const u32x4* z = static_cast<const u32x4*>(sp.zero16);
   if (out_kind == 0)
-    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, z, out, sp.n);
+    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, SPW, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st,
+                       sp.bytes, src_of(sp), ip, is, op, os, z, out, sp.n);
   else
-    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, z, out, sp.n);
+    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, SPW, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st,
+                       sp.bytes, src_of(sp), ip, is, op, os, z, out, sp.n);
   return hipGetLastError();
 }
 
@@ -2107,8 +2110,12 @@ hipError_t launch_checksum_flat(const SegSpec& sp, const uint32_t* init, const u
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                                     int out_kind, int long_lps, hipStream_t st) {
   if (sp.list) return hipErrorInvalidValue;
-  if (long_lps == 8) return launch_twoclass_t<8>(sp, init, odd, out, out_kind, st);
-  if (long_lps == 16) return launch_twoclass_t<16>(sp, init, odd, out, out_kind, st);
+  const int spw = long_lps >> 8;  // bits 8+: segments per wave (0 = 64)
+  long_lps &= 0xff;
+  if (long_lps == 8 && (spw == 0 || spw == 64)) return launch_twoclass_t<8, 64>(sp, init, odd, out, out_kind, st);
+  if (long_lps == 16 && (spw == 0 || spw == 64)) return launch_twoclass_t<16, 64>(sp, init, odd, out, out_kind, st);
+  if (long_lps == 16 && spw == 32) return launch_twoclass_t<16, 32>(sp, init, odd, out, out_kind, st);
+  if (long_lps == 16 && spw == 16) return launch_twoclass_t<16, 16>(sp, init, odd, out, out_kind, st);
   return hipErrorInvalidValue;
 }
 

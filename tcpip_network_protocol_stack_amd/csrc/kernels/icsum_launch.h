@@ -100,7 +100,9 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
 hipError_t launch_checksum_flat(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                                 int out_kind, uint32_t* accw, uint32_t* tailw, uint32_t nwaves, hipStream_t st);
 // Two-class launch (k_checksum_twoclass): short segments (<= 4 chunks) one
-// per lane, long ones long_lps (8 or 16) lanes each, one wave per 64 segments
+// per lane, long ones long_lps (8 or 16) lanes each, one wave per 64
+// segments; long_lps | (spw << 8) selects 32 or 16 segments per wave (16-lane
+// long groups only)
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                                     int out_kind, int long_lps, hipStream_t st);
 // Dense fixed-stride batches (stride == seg_len in {32, 64, 128}, 16-byte

@@ -23,7 +23,9 @@ FLAT_ENVS = [{"ICSUM_FLAT": "1"},
              # lane, long ones 16 / 8 lanes each) forced on every offsets batch;
              # AUTO uses it for short-heavy mixes
              {"ICSUM_TWOCLASS": "16"},
-             {"ICSUM_TWOCLASS": "8"}]
+             {"ICSUM_TWOCLASS": "8"},
+             {"ICSUM_TWOCLASS": str(16 | 32 << 8)},  # 32 segments per wave
+             {"ICSUM_TWOCLASS": str(16 | 16 << 8)}]  # 16 segments per wave
 
 
 @pytest.fixture(scope="module", params=FLAT_ENVS, ids=lambda e: "-".join(f"{k[6:]}{v}" for k, v in e.items()))
