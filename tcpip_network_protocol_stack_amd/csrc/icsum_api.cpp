@@ -122,8 +122,9 @@ struct ics_ctx {
   // ics_ipv4_tcp_batch: from this share of <= 144-byte datagrams (sixteenths,
   // the plan word's bits 4-7) an offsets batch runs 8-lane groups
   static constexpr uint32_t kIpv4ShortMix16 = 5;
-  // ... and from this share up the two-class launch (k_ipv4_twoclass)
-  static constexpr uint32_t kIpv4TwoClass16 = 8;
+  // ... and from this share up the two-class launch (k_ipv4_twoclass, 32
+  // datagrams per wave), which beats the 8-lane groups from 5/16 ACKs up
+  static constexpr uint32_t kIpv4TwoClass16 = 5;
   // the plain checksum's 8-lane threshold (short_mix)
   static constexpr uint32_t kShortMix16 = 7;
   bool plan_cache = true;
@@ -148,6 +149,7 @@ struct ics_ctx {
   // launch with 16-lane long groups; 1 = they run 8-lane groups (the earlier
   // choice, A/B); 8 / 16 = every offsets batch through the two-class launch
   int twoclass = 0;
+  int v4_spw = 32;  // ICSUM_V4_SPW (A/B): datagrams per wave of k_ipv4_twoclass
   uint32_t flat_waves = 16384;
   std::mutex mu;
   // host path: nslots slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each
@@ -888,6 +890,7 @@ int ics_create(int device, ics_ctx** out) {
   if (std::getenv("ICSUM_FLAT")) ctx->flat_mode = int(env_u32("ICSUM_FLAT", 0)) == 1 ? 1 : 0;
   ctx->flat_waves = std::max<uint32_t>(1, env_u32("ICSUM_FLAT_WAVES", ctx->flat_waves));
   ctx->twoclass = int(env_u32("ICSUM_TWOCLASS", 0));
+  ctx->v4_spw = int(env_u32("ICSUM_V4_SPW", 32));
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
   ctx->blocking_sync = env_u32("ICSUM_HOST_BLOCKING_SYNC", 0) != 0;
@@ -979,6 +982,7 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   // kernels running behind the first and every 16th launch (DESIGN.md §4,
   // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
   bool plan_after = false, two = false;
+  int two_spw = ctx->v4_spw;
   if (d_offsets && ctx->plan_cache && ctx->plan_host && !forced_geometry(ctx) && n >= ics_ctx::kSmallPlanMin &&
       n <= 0xFFFFFFFFull) {
     uint32_t plan = 0;
@@ -993,16 +997,21 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
       g = ipv4_geometry({8, 8, true, 3, 1});  // ACK + MTU mixes: half the idle lanes on the ACKs
     else if (hit)
       g = ipv4_geometry({16, 4, true, 3, 1});  // MTU + a few ACKs: shorter unroll, 1-4 % (1 M datagrams)
-    // from half ACKs up: the two-class launch (ICSUM_TWOCLASS=1: the 8-lane
-    // groups above; 1 M datagrams VERIFY 3/4 ACKs 128.8 -> 86.0 us, 1/2
-    // 158.7 -> 154.7, but 5/16 204 us: tools/ab_ipv4_mix.py)
+    // the two-class launch, 32 datagrams per wave (ICSUM_TWOCLASS=1: the
+    // 8-lane groups above).  1 M datagrams VERIFY, 8-lane vs two-class at
+    // 64 / 32 / 16 per wave (tools/ab_ipv4_mix.py): 3/4 ACKs 127.3 vs 85.3 /
+    // 83.7 / 98.9 us, 1/2 157.9 vs 154.0 / 139.8 / 149.7, 7/16 166.0 vs 169.7
+    // / 153.8 / 164.3, 5/16 183.1 vs 201.0 / 181.1 / 185.5
     two = hit && plan != icsum::kPlanWholeBatchSmall && mix.short16 >= ics_ctx::kIpv4TwoClass16 &&
           mix.long16 == 0 && ctx->twoclass != 1;
     plan_after = !hit || refresh;
   }
-  if (d_offsets && ((ctx->twoclass & 0xff) == 8 || (ctx->twoclass & 0xff) == 16)) two = true;  // forced (A/B, tests)
+  if (d_offsets && ((ctx->twoclass & 0xff) == 8 || (ctx->twoclass & 0xff) == 16)) {  // forced (A/B, tests)
+    two = true;
+    if (ctx->twoclass >> 8) two_spw = ctx->twoclass >> 8;
+  }
   hipError_t le = hipErrorInvalidValue;
-  if (two) le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, ctx->patch_wt, st);
+  if (two) le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, ctx->patch_wt, two_spw, st);
   if (le == hipErrorInvalidValue)
     le = icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt, st);
   ICS_HIP(le);

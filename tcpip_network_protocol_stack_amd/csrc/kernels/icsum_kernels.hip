@@ -1407,6 +1407,7 @@ __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_ipv4_tcp(uint8_t* __restric
 // Two-class launch for receive mixes (ACKs among MTU datagrams): wave w
 // takes datagrams [64 w, 64 w + 64); those of <= 64 bytes one per lane, the
 // rest 16 lanes each from a per-wave LDS list, four at a time.
+template <int SPW>
 __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
                                                           uint64_t stride, uint64_t dlen, uint64_t n, int mode,
                                                           uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
@@ -1416,10 +1417,11 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
   __shared__ uint32_t lseg[kBlock / 64][64];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
-  const uint64_t seg = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * 64 + lane;
-  const bool valid = seg < n;
+  // SPW datagrams per wave (lanes >= SPW idle in the short phase)
+  const uint64_t seg = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
+  const bool valid = seg < n && lane < SPW;
   uint64_t s, e;
-  seg_bounds(offsets, stride, dlen, valid ? seg : n - 1, s, e);
+  seg_bounds(offsets, stride, dlen, seg < n ? seg : n - 1, s, e);
   if (!valid) e = s;
   const bool is_short = e - s <= 64;
   const uint64_t lmask = __ballot(valid && !is_short);
@@ -2250,12 +2252,19 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 }
 
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                bool patch_wt, hipStream_t st) {
-  const uint64_t blocks = (sp.n + kBlock - 1) / kBlock;
+                                bool patch_wt, int spw, hipStream_t st) {
+  if (spw != 16 && spw != 32 && spw != 64) return hipErrorInvalidValue;
+  const uint64_t per_block = uint64_t(kBlock / 64) * uint64_t(spw);
+  const uint64_t blocks = (sp.n + per_block - 1) / per_block;
   if (sp.list || blocks == 0 || blocks > (uint64_t(1) << 24)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_ipv4_twoclass, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes),
-                     sp.offsets, sp.stride, sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, int(patch_wt),
-                     static_cast<const uint8_t*>(sp.zero16));
+#define ICS_V4TWO(W)                                                                                               \
+  hipLaunchKernelGGL(k_ipv4_twoclass<W>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes), \
+                     sp.offsets, sp.stride, sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, int(patch_wt),          \
+                     static_cast<const uint8_t*>(sp.zero16))
+  if (spw == 16) ICS_V4TWO(16);
+  else if (spw == 32) ICS_V4TWO(32);
+  else ICS_V4TWO(64);
+#undef ICS_V4TWO
   return hipGetLastError();
 }
 

@@ -119,9 +119,10 @@ hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, bool patch_wt, hipStream_t st);
 // fused IPv4 + TCP for receive mixes: datagrams of <= 64 bytes one per lane,
-// the rest 16 lanes each (k_ipv4_twoclass, one wave per 64 datagrams)
+// the rest 16 lanes each (k_ipv4_twoclass, one wave per spw = 16, 32 or 64
+// datagrams)
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                bool patch_wt, hipStream_t st);
+                                bool patch_wt, int spw, hipStream_t st);
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg

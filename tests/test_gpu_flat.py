@@ -204,9 +204,10 @@ def test_flat_malformed_offsets_terminate(flat_engine, orc):
     assert (_u16(out) == orc.checksum_batch(buf, n, offsets=off2)).all()
 
 
-@pytest.fixture(scope="module", params=["16", "1"], ids=lambda v: f"TWOCLASS{v}")
+@pytest.fixture(scope="module", params=[("16", "32"), ("16", "16"), ("16", "64"), ("1", "32")],
+                ids=lambda v: f"TWOCLASS{v[0]}-SPW{v[1]}")
 def two_engine(request):
-    yield from _engine_with({"ICSUM_TWOCLASS": request.param})
+    yield from _engine_with({"ICSUM_TWOCLASS": request.param[0], "ICSUM_V4_SPW": request.param[1]})
 
 
 @pytest.mark.parametrize("mix", ["bimodal", "ackheavy", "tricky"])
