@@ -125,8 +125,11 @@ struct ics_ctx {
   // ... and from this share up the two-class launch (k_ipv4_twoclass, 32
   // datagrams per wave), which beats the 8-lane groups from 5/16 ACKs up
   static constexpr uint32_t kIpv4TwoClass16 = 5;
-  // the plain checksum's 8-lane threshold (short_mix)
-  static constexpr uint32_t kShortMix16 = 7;
+  // the plain checksum's short-mix threshold (short_mix: the two-class
+  // launch); raw-datagram ACK shares, AUTO vs two-class at 16 per wave
+  // (tools/ab_ipv4_mix.py plain rows): 3/8 156.1 vs 144.1 us, 5/16 163.6 vs
+  // 157.8, 1/4 169.6 vs 169.0, 3/16 178.3 vs 181.4
+  static constexpr uint32_t kShortMix16 = 5;
   bool plan_cache = true;
   uint64_t* plan_host = nullptr;      // host view
   uint64_t* plan_host_dev = nullptr;  // the device's pointer to it
@@ -330,11 +333,12 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, hipStream_t st)
   return ICS_OK;
 }
 
-// a batch mostly of short segments with (almost) no bytes in long ones: from
-// 7/16 <= 144-byte segments and under 1/16 of the bytes in segments over 1920
-// bytes, 8-lane groups beat both the binned launches and 16-lane groups
-// (1 M datagrams, 50 % / 75 % 40-byte ACKs + 1500 B: 139.5 / 107.4 us vs
-// 146.0 / 125.6 us AUTO; profiles/r2_csum_mix_sweep.jsonl)
+// a batch of many short segments with (almost) no bytes in long ones: from
+// kShortMix16 sixteenths of <= 144-byte segments and under 1/16 of the bytes
+// in segments over 1920 bytes, one launch beats the binned launches and
+// 16-lane groups — first 8-lane groups (1 M datagrams, 50 % / 75 % 40-byte
+// ACKs + 1500 B: 139.5 / 107.4 us vs 146.0 / 125.6 us AUTO;
+// profiles/r2_csum_mix_sweep.jsonl), now the two-class launch (launch_mix)
 bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
 
 // a short-heavy mix's single launch: the two-class launch (ACK-sized segments
