@@ -633,6 +633,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const u32x4* q = nch && is_short ? p + (uint32_t(u) < nch ? uint32_t(u) : nch - 1) : zero16;
+    if (nch && is_short) ICS_CHECK16(q, bytes + a0, bytes + a0 + (uint64_t(nch) << 4));
     v[u] = *q;
   }
   // the long ones go to the wave's list, in lane order

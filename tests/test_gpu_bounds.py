@@ -126,3 +126,57 @@ def test_non_monotone_offsets_are_reported(dbg, engine):
             _u(engine.checksum_batch(d, offsets=good), np.uint16)).all()
     with pytest.raises(IcsumError, match="bounds check"):
         dbg.ipv4_tcp_batch(d, 1, offsets=do)
+
+
+@pytest.mark.parametrize("env", [{"ICSUM_LPS": "1", "ICSUM_UNROLL": "4", "ICSUM_MODE": "4"},
+                                 {"ICSUM_TWOCLASS": str(16 | 16 << 8), "ICSUM_V4_SPW": "16"},
+                                 {"ICSUM_TWOCLASS": "16", "ICSUM_V4_SPW": "64"},
+                                 {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "37"}],
+                         ids=["tiny", "twoclass16", "twoclass64", "flat"])
+def test_round2_dispatches_clean_and_identical(engine, env):
+    # the round-2 kernels (one lane per segment, the two-class launches, the
+    # flat dispatch) under the bounds-checked build: clean, and equal to the
+    # release library's default dispatch, on ACK/MTU mixes of segments and of
+    # raw IPv4 datagrams
+    import os
+
+    import torch
+
+    from tcpip_network_protocol_stack_amd.engine import Engine
+
+    os.environ.update(env)
+    try:
+        dbg = Engine(0, debug=True)
+    finally:
+        for k in env:
+            del os.environ[k]
+    try:
+        rng = np.random.default_rng(0x2B)
+        n = 30_000
+        lens = np.where(rng.random(n) < 0.6, 40, 1460) + rng.integers(0, 4, n)
+        lens[::17] = rng.integers(0, 70, lens[::17].size)
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        off += 5
+        buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+        s, ln = off[:-1].astype(np.int64), np.diff(off).astype(np.int64)
+        ok = ln >= 40
+        buf[s[ok]], buf[s[ok] + 9], buf[s[ok] + 32] = 0x45, 6, 0x50
+        buf[s[ok] + 2], buf[s[ok] + 3] = (ln[ok] >> 8).astype(np.uint8), (ln[ok] & 255).astype(np.uint8)
+        d, do = _t(buf), _t(off)
+        odd = _t(rng.integers(0, 2, n).astype(np.uint8))
+        for _ in range(2):  # miss, then a plan-cache hit
+            assert (_u(dbg.checksum_batch(d, offsets=do), np.uint16) ==
+                    _u(engine.checksum_batch(d, offsets=do), np.uint16)).all()
+            assert (_u(dbg.sum_batch(d, offsets=do, odd=odd), np.uint32) ==
+                    _u(engine.sum_batch(d, offsets=do, odd=odd), np.uint32)).all()
+        for mode in (0, 1, 2):
+            d1, d2 = _t(buf), _t(buf)
+            r1 = dbg.ipv4_tcp_batch(d1, mode, offsets=do)
+            r2 = engine.ipv4_tcp_batch(d2, mode, offsets=do)
+            for x, y in zip(r1, r2):
+                assert (x.cpu().numpy() == y.cpu().numpy()).all(), mode
+            assert (d1.cpu().numpy() == d2.cpu().numpy()).all(), mode
+        torch.cuda.synchronize()
+    finally:
+        dbg.close()
