@@ -1,0 +1,68 @@
+#!/usr/bin/env python3
+"""Dev tool: the device wrap (ics_tcp_wrap_batch, in place) of pure-ACK and
+short messages — 1 M datagrams of 40-56 bytes, packed offsets — at the
+default geometry (16-lane groups) and one lane per datagram (forced
+ICSUM_LPS=1 ICSUM_UNROLL=4 ICSUM_MODE=0 ICSUM_NT=0); outputs compared."""
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE, Engine  # noqa: E402
+
+
+def engine(env):
+    os.environ.update(env)
+    try:
+        return Engine(0)
+    finally:
+        for k in env:
+            del os.environ[k]
+
+
+def main():
+    engs = {"default": engine({}), "lane1": engine({"ICSUM_LPS": "1", "ICSUM_UNROLL": "4", "ICSUM_MODE": "0",
+                                                    "ICSUM_NT": "0"})}
+    rng = np.random.default_rng(0x3A)
+    n = 1 << 20
+    for name, lens in (("acks_40B", np.full(n, 40)), ("short_40_56B", rng.integers(40, 57, n))):
+        off = np.zeros(n + 1, dtype=np.int64)
+        off[1:] = np.cumsum(lens)
+        m = np.zeros(n, dtype=TCP_MSG_DTYPE)
+        m["seqno"] = np.arange(n, dtype=np.uint32)
+        m["ttl"], m["flags"], m["window"] = 64, 0x10, 1000
+        dm = torch.from_numpy(m.view(np.uint8).copy()).cuda()
+        doff = torch.from_numpy(off).cuda()
+        base = torch.from_numpy(rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)).cuda()
+        outs = {}
+        for k, e in engs.items():
+            d = base.clone()
+            e.tcp_wrap_batch(d, dm, n=n, offsets=doff)
+            outs[k] = d
+        torch.cuda.synchronize()
+        assert torch.equal(outs["default"], outs["lane1"]), name
+        st = torch.cuda.current_stream()
+        times = {k: [] for k in engs}
+        for _ in range(5):
+            for k, e in engs.items():
+                d = outs[k]
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+                for _ in range(20):
+                    e.tcp_wrap_batch(d, dm, n=n, offsets=doff)
+                b.record(st)
+                torch.cuda.synchronize()
+                times[k].append(a.elapsed_time(b) * 1e3 / 20)
+        for k, ts in times.items():
+            print(json.dumps({"workload": name, "n": n, "bytes": int(off[-1]), "variant": k,
+                              "med_us": round(statistics.median(ts), 2)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
