@@ -8,7 +8,14 @@ workload is the north-star configuration: 1 M x 1500 B segments (1.57 GB, far
 larger than the 256 MiB Infinity Cache, so every step streams from HBM).
 At N>1 (torchrun, one process per GPU) every rank owns its own 1 M-segment
 shard of one global spec stream — weak scaling, no data-path collective; the
-only collectives are the timing barrier and the max-over-ranks reduction.
+only collectives are the timing barrier and the max-over-ranks reduction, both
+over gloo on the host (the device is synchronised before each, so nothing on
+the path needs RCCL — north_star: "no RCCL collective").
+
+The same line carries `config5`: BASELINE config 5 (8 M x 9000 B, 75.5 GB)
+sharded over the N GPUs — strong scaling, its own timed region after the NS
+one — so a 1/2/4/8 run measures both the north-star weak-scaling value and the
+config-5 curve.
 
 `--gpus N` without an outer launcher starts the N ranks itself (one process
 per GPU via torch.distributed.run on 127.0.0.1; this parent never touches the
@@ -64,6 +71,9 @@ def parse():
                     help="CPU-baseline threads (0 = every CPU this process may run on)")
     ap.add_argument("--launch-check", action="store_true",
                     help="ranks report their rank/world wiring over gloo and exit (no GPU use)")
+    ap.add_argument("--no-config5", action="store_true",
+                    help="skip the BASELINE config-5 strong-scaling sub-measurement")
+    ap.add_argument("--config5-steps", type=int, default=0, help="timed steps of config 5 (0 = --steps)")
     return ap.parse_args()
 
 
@@ -241,24 +251,60 @@ def main():
 
     import torch
 
+    from tcpip_network_protocol_stack_amd import shard
     from tcpip_network_protocol_stack_amd.engine import Engine
 
-    # one process per GPU; ICSUM_DIST_BACKEND=gloo rehearses N ranks on fewer
-    # GPUs (ranks then share a card: local % device_count)
-    backend = os.environ.get("ICSUM_DIST_BACKEND", "nccl")
-    local = local % max(1, torch.cuda.device_count()) if backend != "nccl" else local
+    # one process per GPU (ranks share a card when there are fewer GPUs than
+    # ranks: the one-card rehearsal of an N-rank run)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    dist = None
     if world > 1:
         import torch.distributed as dist
 
-        if backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group(backend)
-    from tcpip_network_protocol_stack_amd import shard
-
+        # host-side group for the timing barrier and the max over ranks only:
+        # every rank synchronises its device before either, so a host
+        # collective brackets exactly the same work an RCCL one would
+        dist.init_process_group("gloo")
     eng = Engine(local)
+    stream = torch.cuda.current_stream(dev)
+
+    def timed(step, steps):
+        """barrier + synchronize on both sides of `steps` back-to-back steps;
+        returns (max-over-ranks wall seconds, this rank's HIP-event seconds per
+        step on the launch stream)"""
+        ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        ev0.record(stream)
+        for _ in range(steps):
+            step()
+        ev1.record(stream)
+        torch.cuda.synchronize(dev)
+        # this rank's time stops when its own steps have drained; the closing
+        # barrier keeps the ranks bracketed, and the MAX makes the slowest
+        # rank's time the job's (a barrier's own latency is not a step's work)
+        elapsed = time.perf_counter() - t0
+        if dist:
+            dist.barrier()
+        return shard.max_over_ranks(elapsed, dist), ev0.elapsed_time(ev1) / 1e3 / steps
+
+    def settle(step):
+        for _ in range(args.warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        # settle the chip's power management: a load step from idle leaves the
+        # first ~10-50 ms of launches 5-25 % off steady state (measured, DESIGN.md
+        # §Measurement); keep warming (untimed) until >= --settle-ms of kernels ran
+        t_settle = time.perf_counter()
+        while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
+            for _ in range(8):
+                step()
+            torch.cuda.synchronize(dev)
+
     # rank r owns a contiguous range of global segments of ONE spec stream
     n_total = n_cfg * world if scaling == "weak" else n_cfg
     sh = shard.fixed_stride_shard(n_total, seg, seg, rank, world)
@@ -267,22 +313,11 @@ def main():
     eng.fill_bytes(data, seed, pos0=sh.byte0)
     init = eng.pseudo_inits(n, seed, seg_len=seg, index0=sh.index0)
     out = torch.empty(n, dtype=torch.int16, device=dev)
-    stream = torch.cuda.current_stream(dev)
 
     def step():
         eng.checksum_batch(data, n=n, stride=seg, seg_len=seg, init=init, out=out, stream=stream)
 
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize(dev)
-    # settle the chip's power management: a load step from idle leaves the
-    # first ~10-50 ms of launches 5-25 % off steady state (measured, DESIGN.md
-    # §Measurement); keep warming (untimed) until >= --settle-ms of kernels ran
-    t_settle = time.perf_counter()
-    while (time.perf_counter() - t_settle) * 1e3 < args.settle_ms:
-        for _ in range(8):
-            step()
-        torch.cuda.synchronize(dev)
+    settle(step)
     if args.pmc_child:
         for _ in range(args.steps):
             step()
@@ -292,26 +327,7 @@ def main():
     # kernel time: HIP events on the stream the kernel runs on, bracketing the
     # K back-to-back launches of the timed region (per-launch event pairs
     # would insert markers between dispatches and measure their gaps too)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
-    t0 = time.perf_counter()
-    ev0.record(stream)
-    for _ in range(args.steps):
-        step()
-    ev1.record(stream)
-    torch.cuda.synchronize(dev)
-    # this rank's time stops when its own K steps have drained; the closing
-    # barrier keeps the ranks bracketed, and the MAX below makes the slowest
-    # rank's time the job's (a barrier's own latency is not a step's work)
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        dist.barrier()
-    elapsed = shard.max_over_ranks(elapsed, dist if world > 1 else None,
-                                   dev if backend == "nccl" else torch.device("cpu"))
-    kern_s = ev0.elapsed_time(ev1) / 1e3 / args.steps  # average launch duration (this rank)
-
+    elapsed, kern_s = timed(step, args.steps)
     bytes_step = n * seg  # algorithmic bytes per rank per step (each byte read once)
     value = n_total * seg * args.steps / elapsed / 2**30  # all ranks' bytes / max-over-ranks time
     achieved = bytes_step / kern_s / 1e9  # GB/s, decimal like the 8 TB/s peak
@@ -319,6 +335,33 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(data, init, out, seg, args.cpu_seconds, args.cpu_threads)
+    del data, init, out
+
+    # BASELINE config 5: 8 M x 9000 B sharded over the N GPUs (strong scaling)
+    config5 = None
+    if not args.no_config5 and args.workload != "jumbo_8Mx9000":
+        n5, seg5, seed5, _ = WORKLOADS["jumbo_8Mx9000"]
+        sh5 = shard.fixed_stride_shard(n5, seg5, seg5, rank, world)
+        torch.cuda.empty_cache()
+        d5 = torch.empty(sh5.nbytes, dtype=torch.uint8, device=dev)
+        eng.fill_bytes(d5, seed5, pos0=sh5.byte0)
+        i5 = eng.pseudo_inits(sh5.n, seed5, seg_len=seg5, index0=sh5.index0)
+        o5 = torch.empty(sh5.n, dtype=torch.int16, device=dev)
+
+        def step5():
+            eng.checksum_batch(d5, n=sh5.n, stride=seg5, seg_len=seg5, init=i5, out=o5, stream=stream)
+
+        settle(step5)
+        k5 = args.config5_steps or args.steps
+        el5, kern5 = timed(step5, k5)
+        config5 = {"workload": "jumbo_8Mx9000", "scaling": "strong", "segments_total": n5,
+                   "segments_per_gpu": sh5.n, "segment_bytes": seg5, "steps": k5,
+                   "ms_per_step": round(el5 / k5 * 1e3, 4),
+                   "value": round(n5 * seg5 * k5 / el5 / 2**30, 2), "unit": "GiB/s",
+                   "kernel_ms": round(kern5 * 1e3, 4),
+                   "roofline_frac": round(sh5.n * seg5 / kern5 / 1e9 / HBM_PEAK_GBS, 4)}
+        del d5, i5, o5
+        torch.cuda.empty_cache()
 
     if rank == 0:
         line = {
@@ -337,17 +380,19 @@ def main():
             "config": {"workload": args.workload, "segments_total": n_total, "segments_per_gpu": n,
                        "segment_bytes": seg,
                        "bytes_per_step_per_gpu": bytes_step, "inits": "IPv4 pseudo-header sums",
-                       "entry": "ics_checksum_batch", "parallelism": f"shard{world}"},
+                       "entry": "ics_checksum_batch", "parallelism": f"shard{world}",
+                       "ranks_per_gpu": -(-world // max(1, torch.cuda.device_count()))},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),
                          "kernel_ms": round(kern_s * 1e3, 4),
                          "traffic_source": traffic_src},
             "cpu_baseline": cpu,
+            "config5": config5,
         }
         print(json.dumps(line), flush=True)
     eng.close()
-    if world > 1:
+    if dist:
         dist.destroy_process_group()
 
 

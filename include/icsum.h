@@ -235,6 +235,34 @@ int ics_memcpy_htod(ics_ctx* ctx, void* d_dst, const void* h_src, size_t bytes, 
 int ics_memcpy_dtoh(ics_ctx* ctx, void* h_dst, const void* d_src, size_t bytes, void* stream);
 int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 
+/* ---- diagnostics (not a reference interface) ----------------------------- */
+/* Which launch the last batch call on this context issued, and the plan
+ * cache's counters since ics_create: a caller can check that its steady-state
+ * batches hit the cached plan (and tests check which kernel ran).  Racy
+ * snapshots when several threads share the context. */
+#define ICS_K_CHECKSUM 1         /* k_checksum: one lane group per segment */
+#define ICS_K_SMALL 2            /* k_checksum_small: several short segments per lane group */
+#define ICS_K_TINY 3             /* k_checksum_tiny: one lane per segment */
+#define ICS_K_DENSE 4            /* k_checksum_dense: fixed stride == length in {32, 64, 128} */
+#define ICS_K_TWOCLASS 5         /* k_checksum_twoclass: short segments one per lane, long ones 16 lanes */
+#define ICS_K_BINNED 6           /* the length-binning passes + bin launches */
+#define ICS_K_IPV4 7             /* k_ipv4_tcp */
+#define ICS_K_IPV4_TWOCLASS 8    /* k_ipv4_twoclass */
+#define ICS_K_WRAP 9             /* k_tcp_wrap, one pass */
+#define ICS_K_WRAP_2PASS 10      /* k_tcp_wrap (payload sums) + k_tcp_hdr */
+#define ICS_K_ROUTER 11          /* k_router_ttl */
+#define ICS_K_BATCHV 12          /* several batches in one launch (ics_*_batchv) */
+typedef struct ics_dispatch_info_t {
+  uint64_t plan_hits;      /* lookups that found this batch's landed plan */
+  uint64_t plan_misses;    /* lookups that did not (first call, plan still in flight) */
+  uint64_t plan_requests;  /* plan kernels queued behind launches */
+  int32_t last_kernel;     /* ICS_K_* of the last call's main launch (0: none yet) */
+  int32_t last_lps;        /* its lanes per segment (two-class: long-segment lanes) */
+  int32_t last_unroll;     /* its loads in flight per lane (two-class: segments per wave) */
+  int32_t last_plan;       /* the cached plan it followed (k_bin_plan ids 0-3), -1 none */
+} ics_dispatch_info_t;
+int ics_dispatch_info(const ics_ctx* ctx, ics_dispatch_info_t* info);
+
 #ifdef __cplusplus
 }
 #endif

@@ -32,6 +32,19 @@ class TcpMsg(ctypes.Structure):
 
 assert ctypes.sizeof(TcpMsg) == 28
 
+
+class DispatchInfo(ctypes.Structure):
+    """struct ics_dispatch_info_t (include/icsum.h): the last call's launch and
+    the plan cache's counters."""
+    _fields_ = [("plan_hits", ctypes.c_uint64), ("plan_misses", ctypes.c_uint64),
+                ("plan_requests", ctypes.c_uint64), ("last_kernel", ctypes.c_int32),
+                ("last_lps", ctypes.c_int32), ("last_unroll", ctypes.c_int32), ("last_plan", ctypes.c_int32)]
+
+
+# ICS_K_* kernel ids of ics_dispatch_info_t.last_kernel
+KERNELS = {1: "checksum", 2: "small", 3: "tiny", 4: "dense", 5: "twoclass", 6: "binned", 7: "ipv4",
+           8: "ipv4_twoclass", 9: "wrap", 10: "wrap_2pass", 11: "router", 12: "batchv"}
+
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
 _int = ctypes.c_int
@@ -65,6 +78,7 @@ SIGNATURES = {
     "ics_memcpy_htod": (_int, [_p, _p, _p, ctypes.c_size_t, _p]),
     "ics_memcpy_dtoh": (_int, [_p, _p, _p, ctypes.c_size_t, _p]),
     "ics_stream_synchronize": (_int, [_p, _p]),
+    "ics_dispatch_info": (_int, [_p, ctypes.POINTER(DispatchInfo)]),
     "icsw_fill_bytes": (_int, [_p, _p, _u64, _u64, _u64, _p]),
     "icsw_pseudo_inits": (_int, [_p, _p, _p, _u64, _u64, _u64, _u64, _p]),
     "icsw_ipv4_tcp_headers": (_int, [_p, _p, _u64, _u64, _u64, _u64, _u64, _p]),

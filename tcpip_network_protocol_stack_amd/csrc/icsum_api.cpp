@@ -7,6 +7,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -89,33 +90,48 @@ struct ScratchArea {
 struct ics_ctx {
   int device = 0;
   void* d_zero = nullptr;  // 64 zero bytes (icsum::SegSpec::zero16; the IPv4 kernel's header pad)
-  uint32_t max_blocks = 0;  // 0 = one lane group per segment (no grid-stride cap)
-  int force_lps = 0, force_unroll = 0, force_nt = -1, force_mode = -1, force_segs = 0;
+  // ---- test hooks (ICSUM_FORCE, read once at ics_create; parity tests only):
+  // force one kernel shape or dispatch decision so every instantiation can be
+  // pinned against the oracle.  None selects anything faster than the default.
+  int force_lps = 0, force_unroll = 0, force_mode = -1, force_segs = 0;
   // length binning of offsets batches: -1 auto (n >= bin_min), 0 off, 1 always
   int bin = -1;
-  uint64_t bin_min = 0;
-  uint32_t bin_blocks = 0;  // grid of each bin's launch (its size is only known on the device)
+  uint64_t bin_min = uint64_t(1) << 16;
+  uint32_t bin_blocks = 2048;    // grid of the bins 0-3 launch (their sizes are only known on the device)
   uint32_t last_bin_blocks = 0;  // grid cap of the last bin's launch (0: one lane group per segment)
   uint32_t last_bin_lps = 0;     // lanes per segment of the last bin's launch (0: auto, see checksum_device)
-  int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off); 4 measured best
-  int bin_plan = -1;        // -1: decided on the device per batch; forced (tests): 0 whole, 1 split, 2 whole16, 3 wholeS
-  bool patch_wt = false;    // ICS_MODE_PATCH field stores write-through (sc1); measured slower
-  // ICSUM_WRAP_PASSES: 0 = two passes (payload sums, then a header launch)
-  // when the headers go to an array of their own and the batch has at least
+  int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off)
+  int bin_plan = -1;  // -1: decided on the device per batch; forced: 0 whole, 1 split, 2 whole16, 3 wholeS
+  int twoclass = 0;   // 0: auto; 16 / 32: every offsets batch through the two-class launch (that many per wave)
+  // device wrap: 0 = two passes (payload sums, then a header launch) when
+  // the headers go to an array of their own and the batch has at least
   // kWrapTwoPassMin datagrams, otherwise one pass (headers stored inside the
   // payload stream) — each the faster there (tools/ab_wrap_twopass.py,
-  // DESIGN.md §6); 1 / 2 = always one / two (A/B)
+  // DESIGN.md §6); 1 / 2 = always one / two (tests)
   static constexpr uint64_t kWrapTwoPassMin = uint64_t(1) << 18;
   uint32_t wrap_passes = 0;
-  bool bin_debug = false;   // ICSUM_BIN_DEBUG: dump the binning pass's meta words after each binned call (dev)
-  // plan cache of the AUTO dispatch (ICSUM_PLAN_CACHE, default on): the plan
-  // kernel reports (n << 8) | plan into page-locked host memory; a batch with
-  // the same offsets pointer and n as the last binned one whose plan came back
-  // as one of the whole-batch plans skips the binning passes (their 4
-  // dispatches, ~25 us) and runs as that plan's single launch; every kPlanRefresh-th such call
-  // re-plans behind its launch (stats + plan kernels), so a changed mix is
-  // noticed within kPlanRefresh calls
+  // ---- plan cache of the AUTO dispatch: the plan kernel (k_bin_plan)
+  // reports its plan word into one of kPlanSlots page-locked host words, each
+  // keyed by (offsets pointer, n) and stamped with the slot's generation, so
+  // a word is only trusted for the batch whose miss asked for it.  A batch
+  // whose key holds a whole-batch plan skips the binning passes (their 4
+  // dispatches, ~25 us) and runs that plan's single launch; every
+  // kPlanRefresh-th hit re-plans behind its launch, so a changed mix is
+  // noticed within kPlanRefresh calls.  Several slots: a stack alternates its
+  // transmit buffer (wrap) with its receive buffer (verify / unwrap), and
+  // neither may evict the other's plan (LRU over the slots).
   static constexpr uint32_t kPlanRefresh = 16;
+  static constexpr int kPlanSlots = 4;
+  struct PlanSlot {
+    const uint64_t* key = nullptr;
+    uint64_t n = 0;
+    uint32_t gen = 0;   // 1..254, in bits 56-63 of the slot's word
+    uint32_t hits = 0;  // lookups since the slot was keyed
+    uint64_t used = 0;  // LRU clock
+  };
+  PlanSlot plan_slot[kPlanSlots];
+  uint64_t plan_clock = 0;
+  uint32_t plan_gen = 0;
   // offsets batches from this many segments up (below the binning threshold)
   // take their single launch's geometry from the cached plan
   static constexpr uint64_t kSmallPlanMin = 16384;
@@ -130,30 +146,15 @@ struct ics_ctx {
   // (tools/ab_ipv4_mix.py plain rows): 3/8 156.1 vs 144.1 us, 5/16 163.6 vs
   // 157.8, 1/4 169.6 vs 169.0, 3/16 178.3 vs 181.4
   static constexpr uint32_t kShortMix16 = 5;
-  bool plan_cache = true;
-  uint64_t* plan_host = nullptr;      // host view
-  uint64_t* plan_host_dev = nullptr;  // the device's pointer to it
+  uint64_t* plan_host = nullptr;      // host view of the kPlanSlots words
+  uint64_t* plan_host_dev = nullptr;  // the device's pointer to them
   std::mutex plan_mu;
-  const uint64_t* plan_key = nullptr;
-  uint64_t plan_key_n = 0;
-  uint32_t plan_hits = 0;
+  // diagnostics (ics_dispatch_info)
+  std::atomic<uint64_t> n_hits{0}, n_misses{0}, n_replans{0};
+  std::atomic<int32_t> last_kernel{0}, last_lps{0}, last_unroll{0}, last_plan{-1};
   // device scratch of the binned dispatch and the two-pass wrap (a binned
   // batch of n segments: 80 n bytes + 16 KiB; a two-pass wrap: 4 n)
   icsum::detail::ScratchArea scratch;
-  // the flat dispatch's per-wave slots (k_checksum_flat: nwaves u32 sums,
-  // left zero by k_flat_finish, + nwaves u32 claims): its own area, zeroed
-  // when it grows, since the sums must start at zero
-  icsum::detail::ScratchArea flat{true};
-  // flat dispatch (ICSUM_FLAT): -1 auto, 0 off, 1 every offsets batch;
-  // flat_waves (ICSUM_FLAT_WAVES): waves of k_checksum_flat (each streams an
-  // equal share of the batch's 8 KiB tiles)
-  int flat_mode = 0;
-  // ICSUM_TWOCLASS: 0 = short-heavy mixes (short_mix) run the two-class
-  // launch with 16-lane long groups; 1 = they run 8-lane groups (the earlier
-  // choice, A/B); 8 / 16 = every offsets batch through the two-class launch
-  int twoclass = 0;
-  int v4_spw = 32;  // ICSUM_V4_SPW (A/B): datagrams per wave of k_ipv4_twoclass
-  uint32_t flat_waves = 16384;
   std::mutex mu;
   // host path: nslots slots (2..kMaxSlots, ICSUM_HOST_SLOTS) of slot_bytes each
   // (ICSUM_HOST_SLOT_MB), each with pinned in/out staging, device buffers and a stream
@@ -162,9 +163,6 @@ struct ics_ctx {
   int nslots = 3;  // 3 x 32 MiB: pageable 49.2 -> 51.4 GB/s over 2 x 64 MiB, pinned equal (tools/ab_host.py)
   size_t slot_bytes = size_t(32) << 20;
   bool staged = false;
-  // ICSUM_HOST_BLOCKING_SYNC: the host path's waits sleep (interrupt) instead
-  // of polling, for many host threads driving engines at once
-  bool blocking_sync = false;
   hipStream_t st[kMaxSlots] = {};
   hipEvent_t ev[kMaxSlots] = {};
   uint8_t* h_in[kMaxSlots] = {};
@@ -265,7 +263,6 @@ int bounds_verdict(hipStream_t st, int rc) {
 icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
   icsum::Geometry g = icsum::pick_geometry(avg_len);
   if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll, g.nt, g.mode, 1};
-  if (ctx->force_nt >= 0) g.nt = ctx->force_nt != 0;
   if (ctx->force_mode >= 0) g.mode = ctx->force_mode;
   if (ctx->force_segs > 0) g.segs = ctx->force_segs;
   if (!icsum::geometry_supported(g)) g = icsum::pick_geometry(avg_len);
@@ -277,59 +274,100 @@ icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
 icsum::Geometry ipv4_geometry(icsum::Geometry g) {
   g.segs = 1;
   if (g.mode == icsum::kModeTiny) g = {4, 1, true, 2, 1};  // the tiny kernel is checksum-only
-  if (!icsum::geometry_supported(g)) g.mode = 0;
-  if (!icsum::geometry_supported(g)) g = {64, 8, true, 1, 1};
+  if (!icsum::geometry_supported(g)) g = {16, 8, true, 3, 1};
   return g;
 }
 
 // average segment length for the geometry choice without reading d_offsets
-uint64_t avg_len_hint(const uint64_t* offsets, uint64_t seg_len, uint64_t n, uint64_t total_hint) {
-  if (!offsets) return seg_len;
-  return total_hint && n ? total_hint / n : 65536;  // unknown mix: the long-segment geometry
+uint64_t avg_len_hint(const uint64_t* offsets, uint64_t seg_len) {
+  return offsets ? 65536 : seg_len;  // unknown mix: the long-segment geometry
 }
 
 bool forced_geometry(const ics_ctx* ctx) {
-  return ctx->force_lps || ctx->force_unroll || ctx->force_nt >= 0 || ctx->force_mode >= 0 ||
-         ctx->force_segs;
+  return ctx->force_lps || ctx->force_unroll || ctx->force_mode >= 0 || ctx->force_segs;
+}
+
+// diagnostics: the last call's main launch (ics_dispatch_info)
+void note(ics_ctx* ctx, int kernel, icsum::Geometry g = {0, 0, true, 0, 1}, int plan = -1) {
+  ctx->last_kernel.store(kernel, std::memory_order_relaxed);
+  ctx->last_lps.store(g.lps, std::memory_order_relaxed);
+  ctx->last_unroll.store(g.unroll, std::memory_order_relaxed);
+  ctx->last_plan.store(plan, std::memory_order_relaxed);
+}
+
+int kernel_of(icsum::Geometry g) {
+  return g.mode == icsum::kModeTiny ? ICS_K_TINY : g.segs > 1 ? ICS_K_SMALL : ICS_K_CHECKSUM;
 }
 
 // a1-a4 on device buffers.  An offsets batch of unknown length mix is split
 // into length bins on the device (two passes over the offsets), and every bin
 // runs with the geometry that suits its lengths; the bin lists live in
 // stream-ordered scratch, so concurrent calls on different streams are safe.
-// The plan the device reported for the last call with this offsets pointer
-// and n (ics_ctx::plan_host); any_plan = false accepts only the whole-batch
-// plans.  The mix (optional) receives the shares k_bin_plan reported, in
+//
+// The plan cache (ics_ctx::plan_slot): a lookup finds the slot keyed by this
+// batch's (offsets pointer, n) and trusts its word only when the word carries
+// the slot's generation — i.e. it was written by a plan kernel this key's
+// miss (or refresh) queued, and has landed.  any_plan = false accepts only
+// the whole-batch plans.  The mix receives the shares k_bin_plan reported, in
 // sixteenths: segments of <= 144 bytes, and bytes in segments over 1920
-// bytes.  A miss makes this call's batch the cache key.
+// bytes.  A miss (re)keys the least recently used slot; *want_plan asks the
+// caller to queue the plan kernels (into *plan_dst, with *plan_gen) behind its
+// launch: on a miss, on every kPlanRefresh-th hit, and every kPlanRefresh-th
+// lookup of a key whose plan has not landed yet.
 struct PlanMix {
   uint32_t short16 = 0, long16 = 0, avg = 0;  // avg: mean segment length, bytes (capped at 4095)
 };
-bool plan_lookup(ics_ctx* ctx, const icsum::SegSpec& sp, bool any_plan, uint32_t* plan, bool* refresh,
+struct PlanReq {
+  bool want = false;
+  uint64_t* dst = nullptr;  // device view of the slot's word
+  uint32_t gen = 0;
+};
+bool plan_lookup(ics_ctx* ctx, const icsum::SegSpec& sp, bool any_plan, uint32_t* plan, PlanReq* req,
                  PlanMix* mix = nullptr) {
+  *req = {};
+  if (!ctx->plan_host) return false;
   std::lock_guard<std::mutex> lock(ctx->plan_mu);
-  const uint64_t v = __atomic_load_n(ctx->plan_host, __ATOMIC_ACQUIRE);
-  const uint32_t p = uint32_t(v & 0xfu);
-  if (mix) *mix = {uint32_t(v >> 4) & 0xfu, uint32_t(v >> 40) & 0xfu, uint32_t(v >> 44) & 0xfffu};
-  const bool whole = p == icsum::kPlanWholeBatch || p == icsum::kPlanWholeBatch16 || p == icsum::kPlanWholeBatchSmall;
-  const bool same_n = (v >> 56) == 0 && ((v >> 8) & 0xFFFFFFFFull) == sp.n;  // ~0: nothing reported yet
-  if (ctx->plan_key == sp.offsets && ctx->plan_key_n == sp.n && same_n && (whole || any_plan)) {
-    *plan = p;
-    *refresh = ++ctx->plan_hits % ics_ctx::kPlanRefresh == 0;
-    return true;
+  int k = -1, lru = 0;
+  for (int i = 0; i < ics_ctx::kPlanSlots; ++i) {
+    const ics_ctx::PlanSlot& ps = ctx->plan_slot[i];
+    if (ps.key == sp.offsets && ps.n == sp.n && ps.gen) k = i;
+    if (ps.used < ctx->plan_slot[lru].used) lru = i;
   }
-  ctx->plan_key = sp.offsets;
-  ctx->plan_key_n = sp.n;
-  ctx->plan_hits = 0;
+  if (k >= 0) {
+    ics_ctx::PlanSlot& ps = ctx->plan_slot[k];
+    ps.used = ++ctx->plan_clock;
+    const uint64_t v = __atomic_load_n(ctx->plan_host + k, __ATOMIC_ACQUIRE);
+    const uint32_t p = uint32_t(v & 0xfu);
+    const bool landed = (v >> 56) == ps.gen && ((v >> 8) & 0xFFFFFFFFull) == (sp.n & 0xFFFFFFFFull);
+    const bool whole = p == icsum::kPlanWholeBatch || p == icsum::kPlanWholeBatch16 || p == icsum::kPlanWholeBatchSmall;
+    const bool again = ++ps.hits % ics_ctx::kPlanRefresh == 0;
+    *req = {again, ctx->plan_host_dev + k, ps.gen};
+    if (landed && (whole || any_plan)) {
+      if (mix) *mix = {uint32_t(v >> 4) & 0xfu, uint32_t(v >> 40) & 0xfu, uint32_t(v >> 44) & 0xfffu};
+      *plan = p;
+      ctx->n_hits.fetch_add(1, std::memory_order_relaxed);
+      return true;
+    }
+    ctx->n_misses.fetch_add(1, std::memory_order_relaxed);
+    return false;
+  }
+  ics_ctx::PlanSlot& ps = ctx->plan_slot[lru];
+  ctx->plan_gen = ctx->plan_gen % 254 + 1;  // 1..254: never the 0xFF of an unwritten word
+  ps = {sp.offsets, sp.n, ctx->plan_gen, 0, ++ctx->plan_clock};
+  __atomic_store_n(ctx->plan_host + lru, ~uint64_t(0), __ATOMIC_RELEASE);
+  *req = {true, ctx->plan_host_dev + lru, ps.gen};
+  ctx->n_misses.fetch_add(1, std::memory_order_relaxed);
   return false;
 }
 
 // stats + plan kernels only (no lists) behind a launch: the plan for the next
-// call with the same offsets lands in ics_ctx::plan_host
-int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, hipStream_t st) {
+// call with the same offsets lands in the slot plan_lookup named
+int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, const PlanReq& req, hipStream_t st) {
+  if (!req.want) return ICS_OK;
   Scratch meta(ctx, (icsum::kBinMetaBytesTotal + 255) & ~size_t(255), st);
   ICS_HIP(meta.error());
-  ICS_HIP(icsum::launch_bin_plan(sp.offsets, sp.n, static_cast<uint32_t*>(meta.get()), lps, ctx->plan_host_dev, st));
+  ICS_HIP(icsum::launch_bin_plan(sp.offsets, sp.n, static_cast<uint32_t*>(meta.get()), lps, req.dst, req.gen, st));
+  ctx->n_replans.fetch_add(1, std::memory_order_relaxed);
   return ICS_OK;
 }
 
@@ -344,20 +382,22 @@ bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m
 // a short-heavy mix's single launch: the two-class launch (ACK-sized segments
 // one per lane, the rest 16 lanes each), 32 segments per wave from 3/4 short
 // segments up and 16 below (fewer long segments per wave: shorter-lived
-// waves), or 8-lane groups (ICSUM_TWOCLASS=1).  2 M x 40 / 1460 B: 8-lane
-// 279.5, 64 / 32 / 16 per wave 255.7 / 234.9 / 231.1 us; raw-datagram mixes
-// (tools/ab_ipv4_mix.py plain rows, 64 / 32 / 16): 7/8 ACKs 43.5 / 42.2 /
-// 54.5, 3/4 74.8 / 68.5 / 74.5, 1/2 132.4 / 122.5 / 119.0, 7/16 145.0 /
-// 139.3 / 131.9 us (profiles/r2_twoclass_spw*.jsonl)
-hipError_t launch_mix(const ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
+// waves).  2 M x 40 / 1460 B: 8-lane groups 279.5, two-class 64 / 32 / 16 per
+// wave 255.7 / 234.9 / 231.1 us; raw-datagram mixes (tools/ab_ipv4_mix.py
+// plain rows, 64 / 32 / 16): 7/8 ACKs 43.5 / 42.2 / 54.5, 3/4 74.8 / 68.5 /
+// 74.5, 1/2 132.4 / 122.5 / 119.0, 7/16 145.0 / 139.3 / 131.9 us
+// (profiles/r2_twoclass_spw*.jsonl).  Batches past the two-class grid's
+// limit run 8-lane groups.
+hipError_t launch_mix(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                       void* d_out, int out_kind, const PlanMix& mix, hipStream_t st) {
-  if (ctx->twoclass != 1) {
-    const int spw = mix.short16 >= 12 ? 32 : 16;
-    const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, 16 | (spw << 8), st);
-    if (e != hipErrorInvalidValue) return e;
+  const int spw = mix.short16 >= 12 ? 32 : 16;
+  const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, spw, st);
+  if (e != hipErrorInvalidValue) {
+    note(ctx, ICS_K_TWOCLASS, {16, spw, true, 3, 1});
+    return e;
   }
-  return icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, icsum::Geometry{8, 8, true, 3, 1},
-                                ctx->max_blocks, st);
+  note(ctx, ICS_K_CHECKSUM, {8, 8, true, 3, 1});
+  return icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, icsum::Geometry{8, 8, true, 3, 1}, 0, st);
 }
 
 // the small-segment plan's single launch: one lane per segment for ACK-sized
@@ -367,29 +407,16 @@ icsum::Geometry small_plan_geometry(const PlanMix& m) {
                                      : icsum::Geometry{4, 2, true, 2, 2};
 }
 
-// the flat dispatch (k_checksum_flat + k_flat_finish): one stream over the
-// batch's bytes, the cuts deciding where the sums go
-int checksum_flat(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
-                  void* d_out, int out_kind, hipStream_t st) {
-  const uint32_t nw = ctx->flat_waves;
-  Scratch ws(ctx->flat, size_t(nw) * 8, st);
-  ICS_HIP(ws.error());
-  uint32_t* accw = static_cast<uint32_t*>(ws.get());
-  ICS_HIP(icsum::launch_checksum_flat(sp, d_init, d_odd, d_out, out_kind, accw, accw + nw, nw, st));
-  return ICS_OK;
-}
-
 int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                     void* d_out, int out_kind, hipStream_t st) {
-  if (sp.offsets && ctx->flat_mode == 1 && sp.n < 0xFFFFFFFFull)
-    return checksum_flat(ctx, sp, d_init, d_odd, d_out, out_kind, st);
-  if (sp.offsets && ((ctx->twoclass & 0xff) == 8 || (ctx->twoclass & 0xff) == 16)) {
+  if (sp.offsets && ctx->twoclass) {  // test hook: the two-class launch on every offsets batch
     ICS_HIP(icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, ctx->twoclass, st));
+    note(ctx, ICS_K_TWOCLASS, {16, ctx->twoclass, true, 3, 1});
     return ICS_OK;
   }
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
                       (ctx->bin == 1 || (ctx->bin < 0 && sp.n >= ctx->bin_min && !forced_geometry(ctx)));
-  const bool plannable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_cache && ctx->plan_host;
+  const bool plannable = ctx->bin < 0 && ctx->bin_plan < 0 && ctx->plan_host && sp.n <= 0xFFFFFFFFull;
   if (!binned && sp.offsets && plannable && !forced_geometry(ctx) && sp.n >= ics_ctx::kSmallPlanMin) {
     // an offsets batch below the binning threshold: one launch, its geometry
     // from the plan the device reported for this batch last time (16-lane
@@ -398,30 +425,32 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     // the launch for the next call (tools/ab_small_offsets.py)
     uint32_t plan = 0;
     PlanMix mix;
-    bool refresh = false;
-    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &mix);
-    icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len, sp.n, 0));
+    PlanReq req;
+    const bool hit = plan_lookup(ctx, sp, true, &plan, &req, &mix);
+    icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len));
     if (hit && plan == icsum::kPlanWholeBatch16) g = {16, 8, true, 3, 1};
     if (hit && plan == icsum::kPlanWholeBatchSmall) g = small_plan_geometry(mix);
-    if (hit && plan != icsum::kPlanWholeBatchSmall && short_mix(mix))
+    if (hit && plan != icsum::kPlanWholeBatchSmall && short_mix(mix)) {
       ICS_HIP(launch_mix(ctx, sp, d_init, d_odd, d_out, out_kind, mix, st));
-    else
-      ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
-    if (!hit || refresh)
-      if (int rc = replan(ctx, sp, 64, st)) return rc;
-    return ICS_OK;
+    } else {
+      ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, 0, st));
+      note(ctx, kernel_of(g), g, hit ? int(plan) : -1);
+    }
+    return replan(ctx, sp, 64, req, st);
   }
   if (!binned) {
-    // dense fixed-stride batch of short segments (config 3): the flat kernel
+    // dense fixed-stride batch of short segments (config 3): the flat-array kernel
     if (!d_odd && ctx->dense_segs > 0 && !forced_geometry(ctx) && icsum::dense_supported(sp)) {
       const hipError_t e = icsum::launch_checksum_dense(sp, d_init, d_out, out_kind, ctx->dense_segs, st);
       if (e != hipErrorInvalidValue) {
         ICS_HIP(e);
+        note(ctx, ICS_K_DENSE, {int(sp.seg_len / 16), ctx->dense_segs, true, 0, 1});
         return ICS_OK;
       }
     }
-    const icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len, sp.n, 0));
-    ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, ctx->max_blocks, st));
+    const icsum::Geometry g = geometry_for(ctx, avg_len_hint(sp.offsets, sp.seg_len));
+    ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g, 0, st));
+    note(ctx, kernel_of(g), g);
     return ICS_OK;
   }
   // the whole-batch plan's launch geometry: one lane group per segment of the
@@ -430,13 +459,11 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   icsum::Geometry g_last = icsum::bin_geometry(icsum::kBins - 1);
   const uint32_t lps = ctx->last_bin_lps ? ctx->last_bin_lps : (sp.n > (uint64_t(1) << 20) ? 32u : 64u);
   if (lps == 32) g_last = {32, 8, true, 3, 1};
-  const uint32_t last_blocks = ctx->max_blocks ? ctx->max_blocks : ctx->last_bin_blocks;
-  const bool cacheable = plannable;
-  if (cacheable) {
+  PlanReq req;
+  if (plannable) {
     uint32_t hit_plan = 0;
     PlanMix mix;
-    bool refresh = false;
-    const bool hit = plan_lookup(ctx, sp, true, &hit_plan, &refresh, &mix);
+    const bool hit = plan_lookup(ctx, sp, true, &hit_plan, &req, &mix);
     const bool mix8 = hit && hit_plan != icsum::kPlanWholeBatchSmall && short_mix(mix);
     if (hit && (hit_plan != icsum::kPlanSplitBins || mix8)) {
       // the whole-batch plan the device chose for this batch last time, as
@@ -447,16 +474,16 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
       const icsum::Geometry g_hit = hit_plan == icsum::kPlanWholeBatch16      ? icsum::Geometry{16, 8, true, 3, 1}
                                     : hit_plan == icsum::kPlanWholeBatchSmall ? small_plan_geometry(mix)
                                                                               : g_last;
-      if (mix8)
+      if (mix8) {
         ICS_HIP(launch_mix(ctx, sp, d_init, d_odd, d_out, out_kind, mix, st));
-      else
+      } else {
         ICS_HIP(icsum::launch_checksum(sp, d_init, d_odd, d_out, out_kind, g_hit,
-                                       hit_plan == icsum::kPlanWholeBatch ? last_blocks : ctx->max_blocks, st));
+                                       hit_plan == icsum::kPlanWholeBatch ? ctx->last_bin_blocks : 0, st));
+        note(ctx, kernel_of(g_hit), g_hit, int(hit_plan));
+      }
       // re-plan behind it: a batch whose mix changed under the same pointer
       // and size is re-binned from the next call on
-      if (refresh)
-        if (int rc = replan(ctx, sp, lps, st)) return rc;
-      return ICS_OK;
+      return replan(ctx, sp, lps, req, st);
     }
   }
   const size_t meta_bytes = (icsum::kBinMetaBytesTotal + 255) & ~size_t(255);
@@ -464,28 +491,22 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   ICS_HIP(ws.error());
   uint32_t* meta = static_cast<uint32_t*>(ws.get());
   void* list = static_cast<uint8_t*>(ws.get()) + meta_bytes;
-  // the last bin's launch dispatches one lane group per segment of the whole
-  // batch (whatever the plan)
+  // the binning passes; the plan kernel also reports into the plan cache's
+  // slot when this call's lookup asked for a plan
   hipError_t e = icsum::launch_bin_segments(sp.offsets, sp.n, list, meta, ctx->bin_plan, lps,
-                                            cacheable ? ctx->plan_host_dev : nullptr, st);
+                                            req.want ? req.dst : nullptr, req.gen, st);
   // bins 0..3: one launch, a capped grid striding over each bin; the last
   // bin: one lane group per segment of the batch (it takes the whole batch
   // under the whole-batch plans)
   if (e == hipSuccess)
     e = icsum::launch_checksum_bins(icsum::bin_spec(sp, list, meta, 0), d_init, d_odd, d_out, out_kind,
-                                    ctx->max_blocks ? ctx->max_blocks : ctx->bin_blocks, st);
+                                    ctx->bin_blocks, st);
   if (e == hipSuccess)
     e = icsum::launch_checksum(icsum::bin_spec(sp, list, meta, icsum::kBins - 1), d_init, d_odd, d_out, out_kind,
-                               g_last, last_blocks, st);
-  if (e == hipSuccess && ctx->bin_debug) {  // dev: dump the binning pass's meta words
-    uint32_t h[icsum::kBinMetaWords];
-    if (hipMemcpyAsync(h, meta, sizeof h, hipMemcpyDeviceToHost, st) == hipSuccess && hipStreamSynchronize(st) == hipSuccess) {
-      std::fprintf(stderr, "icsum bin meta:");
-      for (int k = 0; k < icsum::kBinMetaWords; ++k) std::fprintf(stderr, " %u", h[k]);
-      std::fprintf(stderr, "\n");
-    }
-  }
+                               g_last, ctx->last_bin_blocks, st);
   ICS_HIP(e);
+  if (req.want) ctx->n_replans.fetch_add(1, std::memory_order_relaxed);
+  note(ctx, ICS_K_BINNED, g_last, ctx->bin_plan);
   return ICS_OK;
 }
 
@@ -493,8 +514,7 @@ int ensure_staging(ics_ctx* ctx) {
   if (ctx->staged) return ICS_OK;
   for (int k = 0; k < ctx->nslots; ++k) {
     ICS_HIP(hipStreamCreateWithFlags(&ctx->st[k], hipStreamNonBlocking));
-    ICS_HIP(hipEventCreateWithFlags(&ctx->ev[k], hipEventDisableTiming |
-                                                     (ctx->blocking_sync ? hipEventBlockingSync : 0)));
+    ICS_HIP(hipEventCreateWithFlags(&ctx->ev[k], hipEventDisableTiming));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_in[k]), ctx->slot_bytes, 0));
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_in[k]), ctx->slot_bytes));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_off[k]), (ics_ctx::kSlotSegs + 1) * 8, 0));
@@ -748,7 +768,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       ICS_HIP(hipMemcpyAsync(ctx->d_init[slot], odd, parts, hipMemcpyHostToDevice, st));
       const icsum::SegSpec sp{ctx->d_in[slot], ctx->d_off[slot], 0, 0, parts, ctx->d_zero};
       ICS_HIP(icsum::launch_checksum(sp, nullptr, reinterpret_cast<const uint8_t*>(ctx->d_init[slot]),
-                                     ctx->d_out[slot], 1, geometry_for(ctx, kSubPiece), ctx->max_blocks, st));
+                                     ctx->d_out[slot], 1, geometry_for(ctx, kSubPiece), 0, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], parts * 4, hipMemcpyDeviceToHost, st));
       ICS_HIP(hipEventRecord(ctx->ev[slot], st));
       pending[slot] = c;
@@ -777,7 +797,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(ctx->d_msg[slot]),
                                      reinterpret_cast<uint32_t*>(ctx->d_hdr[slot]), nullptr, nullptr, mode == 1,
                                      wrap_two_pass(ctx, true, m) ? ctx->d_sums[slot] : nullptr, ipv4_geometry(g),
-                                     ctx->max_blocks, st));
+                                     0, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_hdr[slot], ctx->d_hdr[slot], m * 40, hipMemcpyDeviceToHost, st));
     } else if (kind == 0) {
       const uint32_t* d_init = nullptr;
@@ -786,7 +806,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
         ICS_HIP(hipMemcpyAsync(ctx->d_init[slot], ctx->h_init[slot], m * 4, hipMemcpyHostToDevice, st));
         d_init = ctx->d_init[slot];
       }
-      ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, ctx->d_out[slot], 0, g, ctx->max_blocks, st));
+      ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, ctx->d_out[slot], 0, g, 0, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 2, hipMemcpyDeviceToHost, st));
     } else {
       uint16_t* a = reinterpret_cast<uint16_t*>(ctx->d_out[slot]);
@@ -797,7 +817,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       // fields are written into the caller's bytes on the host at retire,
       // instead of copying every patched byte back over PCIe
       const int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;
-      ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, ipv4_geometry(g), ctx->max_blocks, ctx->patch_wt, st));
+      ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, ipv4_geometry(g), 0, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 5, hipMemcpyDeviceToHost, st));
     }
     ICS_HIP(hipEventRecord(ctx->ev[slot], st));
@@ -809,6 +829,44 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   for (int k = 0; k < ctx->nslots; ++k)  // oldest first
     if (int rc = retire((slot + k) % ctx->nslots)) return rc;
   return bounds_verdict(ctx->st[0], ICS_OK);
+}
+
+// ICSUM_FORCE (test hook): "key=value,key=value" forcing
+// one kernel shape or dispatch decision so parity tests reach every
+// instantiation.  An unknown key fails ics_create (a mistyped hook must not
+// silently test the default path).
+int apply_force(ics_ctx* ctx, const char* spec) {
+  if (!spec || !*spec) return ICS_OK;
+  std::string all(spec);
+  size_t pos = 0;
+  while (pos <= all.size()) {
+    const size_t end = std::min(all.find(',', pos), all.size());
+    const std::string item = all.substr(pos, end - pos);
+    pos = end + 1;
+    if (item.empty()) continue;
+    const size_t eq = item.find('=');
+    if (eq == std::string::npos) return fail(ICS_ERR_INVALID, "ICSUM_FORCE: '%s' is not key=value", item.c_str());
+    const std::string k = item.substr(0, eq);
+    char* tail = nullptr;
+    const long long v = std::strtoll(item.c_str() + eq + 1, &tail, 0);
+    if (!tail || *tail) return fail(ICS_ERR_INVALID, "ICSUM_FORCE: bad value in '%s'", item.c_str());
+    if (k == "lps") ctx->force_lps = int(v);
+    else if (k == "unroll") ctx->force_unroll = int(v);
+    else if (k == "mode") ctx->force_mode = int(v);
+    else if (k == "segs") ctx->force_segs = int(v);
+    else if (k == "bin") ctx->bin = int(v);
+    else if (k == "bin_min") ctx->bin_min = uint64_t(v);
+    else if (k == "bin_plan") ctx->bin_plan = v >= 0 && v <= 3 ? int(v) : -1;
+    else if (k == "bin_blocks") ctx->bin_blocks = uint32_t(std::max<long long>(v, 1));
+    else if (k == "last_bin_lps") ctx->last_bin_lps = uint32_t(v);
+    else if (k == "last_bin_blocks") ctx->last_bin_blocks = uint32_t(v);
+    else if (k == "dense_segs") ctx->dense_segs = int(v);
+    else if (k == "twoclass" && (v == 0 || v == 16 || v == 32)) ctx->twoclass = int(v);
+    else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
+    else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
+    else return fail(ICS_ERR_INVALID, "ICSUM_FORCE: unknown or out-of-range '%s'", item.c_str());
+  }
+  return ICS_OK;
 }
 
 }  // namespace
@@ -843,43 +901,28 @@ int ics_create(int device, ics_ctx** out) {
   ics_ctx* ctx = new (std::nothrow) ics_ctx();
   if (!ctx) return fail(ICS_ERR_NOMEM, "context allocation failed");
   ctx->device = device;
+  if (int rc = apply_force(ctx, std::getenv("ICSUM_FORCE"))) {
+    delete ctx;
+    return rc;
+  }
   if (hipMalloc(&ctx->d_zero, 64) != hipSuccess || hipMemset(ctx->d_zero, 0, 64) != hipSuccess) {
     delete ctx;
     return fail(ICS_ERR_NOMEM, "device allocation failed");
   }
-  ctx->max_blocks = env_u32("ICSUM_MAX_BLOCKS", 0);
-  ctx->force_lps = int(env_u32("ICSUM_LPS", 0));
-  ctx->force_unroll = int(env_u32("ICSUM_UNROLL", 0));
-  ctx->force_nt = std::getenv("ICSUM_NT") ? int(env_u32("ICSUM_NT", 1)) : -1;
-  ctx->force_mode = std::getenv("ICSUM_MODE") ? int(env_u32("ICSUM_MODE", 0)) : -1;
-  ctx->force_segs = int(env_u32("ICSUM_SEGS", 0));
-  ctx->bin = std::getenv("ICSUM_BIN") ? int(env_u32("ICSUM_BIN", 1)) : -1;
-  ctx->bin_min = env_u32("ICSUM_BIN_MIN", 1u << 16);
-  ctx->bin_blocks = env_u32("ICSUM_BIN_BLOCKS", 2048);
-  ctx->last_bin_blocks = env_u32("ICSUM_LAST_BIN_BLOCKS", 0);
-  ctx->last_bin_lps = env_u32("ICSUM_LAST_BIN_LPS", 0);
-  if (std::getenv("ICSUM_DENSE_SEGS")) ctx->dense_segs = int(env_u32("ICSUM_DENSE_SEGS", 4));
-  ctx->bin_plan = std::getenv("ICSUM_BIN_PLAN") ? int(env_u32("ICSUM_BIN_PLAN", 1)) : -1;
-  if (ctx->bin_plan > 3) ctx->bin_plan = -1;
-  ctx->patch_wt = env_u32("ICSUM_PATCH_WT", 0) != 0;
-  ctx->wrap_passes = env_u32("ICSUM_WRAP_PASSES", 0);
   {
     const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
     ctx->copy_threads = std::max<size_t>(1, env_u32("ICSUM_COPY_THREADS", std::min(8u, hw)));
   }
-  if (hipEventCreateWithFlags(&ctx->scratch.ev, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&ctx->flat.ev, hipEventDisableTiming) != hipSuccess) {
-    ctx->scratch.release();
+  if (hipEventCreateWithFlags(&ctx->scratch.ev, hipEventDisableTiming) != hipSuccess) {
     (void)hipFree(ctx->d_zero);
     delete ctx;
     return fail(ICS_ERR_HIP, "event creation failed");
   }
-  ctx->plan_cache = env_u32("ICSUM_PLAN_CACHE", 1) != 0;
-  if (ctx->plan_cache) {  // coherent: the plan kernel's store reaches host memory without a flush
+  {  // the plan cache's words; coherent: the plan kernel's store reaches host memory without a flush
     void* p = nullptr;
-    if (hipHostMalloc(&p, 64, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess) {
+    if (hipHostMalloc(&p, 8 * ics_ctx::kPlanSlots, hipHostMallocCoherent | hipHostMallocMapped) == hipSuccess) {
       ctx->plan_host = static_cast<uint64_t*>(p);
-      *ctx->plan_host = ~uint64_t(0);
+      for (int k = 0; k < ics_ctx::kPlanSlots; ++k) ctx->plan_host[k] = ~uint64_t(0);
       void* dp = nullptr;
       if (hipHostGetDevicePointer(&dp, p, 0) == hipSuccess) {
         ctx->plan_host_dev = static_cast<uint64_t*>(dp);
@@ -890,15 +933,8 @@ int ics_create(int device, ics_ctx** out) {
     }
     (void)hipGetLastError();
   }
-  ctx->bin_debug = std::getenv("ICSUM_BIN_DEBUG") != nullptr;
-  if (std::getenv("ICSUM_FLAT")) ctx->flat_mode = int(env_u32("ICSUM_FLAT", 0)) == 1 ? 1 : 0;
-  ctx->flat_waves = std::max<uint32_t>(1, env_u32("ICSUM_FLAT_WAVES", ctx->flat_waves));
-  ctx->twoclass = int(env_u32("ICSUM_TWOCLASS", 0));
-  ctx->v4_spw = int(env_u32("ICSUM_V4_SPW", 32));
   ctx->nslots = int(std::min<uint32_t>(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOTS", 3), 2), ics_ctx::kMaxSlots));
   ctx->slot_bytes = size_t(std::max<uint32_t>(env_u32("ICSUM_HOST_SLOT_MB", 32), 1)) << 20;
-  ctx->blocking_sync = env_u32("ICSUM_HOST_BLOCKING_SYNC", 0) != 0;
-  if (std::getenv("ICSUM_XCD_REMAP")) icsum::set_xcd_remap(env_u32("ICSUM_XCD_REMAP", 0));
   *out = ctx;
   return ICS_OK;
 }
@@ -910,9 +946,20 @@ int ics_destroy(ics_ctx* ctx) {
     if (ctx->d_zero) (void)hipFree(ctx->d_zero);
     if (ctx->plan_host) (void)hipHostFree(ctx->plan_host);
     ctx->scratch.release();
-    ctx->flat.release();
   }
   delete ctx;
+  return ICS_OK;
+}
+
+int ics_dispatch_info(const ics_ctx* ctx, ics_dispatch_info_t* info) {
+  if (!ctx || !info) return fail(ICS_ERR_INVALID, "null argument");
+  info->plan_hits = ctx->n_hits.load(std::memory_order_relaxed);
+  info->plan_misses = ctx->n_misses.load(std::memory_order_relaxed);
+  info->plan_requests = ctx->n_replans.load(std::memory_order_relaxed);
+  info->last_kernel = ctx->last_kernel.load(std::memory_order_relaxed);
+  info->last_lps = ctx->last_lps.load(std::memory_order_relaxed);
+  info->last_unroll = ctx->last_unroll.load(std::memory_order_relaxed);
+  info->last_plan = ctx->last_plan.load(std::memory_order_relaxed);
   return ICS_OK;
 }
 
@@ -985,83 +1032,88 @@ int ics_ipv4_tcp_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   // from 5/16 of <= 144-byte datagrams, 16 x 4 below that), the plan
   // kernels running behind the first and every 16th launch (DESIGN.md §4,
   // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
-  bool plan_after = false, two = false;
-  int two_spw = ctx->v4_spw;
-  if (d_offsets && ctx->plan_cache && ctx->plan_host && !forced_geometry(ctx) && n >= ics_ctx::kSmallPlanMin &&
-      n <= 0xFFFFFFFFull) {
+  bool two = false;
+  PlanReq req;
+  int plan_used = -1;
+  if (d_offsets && !forced_geometry(ctx) && !ctx->twoclass && n >= ics_ctx::kSmallPlanMin && n <= 0xFFFFFFFFull) {
     uint32_t plan = 0;
     PlanMix mix;
-    bool refresh = false;
-    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &mix);
+    const bool hit = plan_lookup(ctx, sp, true, &plan, &req, &mix);
     if (hit && plan == icsum::kPlanWholeBatchSmall && mix.avg <= icsum::kTinyMaxAvg)
       g = lane1;
     else if (hit && plan == icsum::kPlanWholeBatchSmall)
       g = ipv4_geometry({4, 2, true, 2, 1});
     else if (hit && mix.short16 >= ics_ctx::kIpv4ShortMix16 && mix.long16 == 0)
-      g = ipv4_geometry({8, 8, true, 3, 1});  // ACK + MTU mixes: half the idle lanes on the ACKs
+      g = ipv4_geometry({8, 8, true, 3, 1});  // ACK + MTU mixes past the two-class grid's limit
     else if (hit)
       g = ipv4_geometry({16, 4, true, 3, 1});  // MTU + a few ACKs: shorter unroll, 1-4 % (1 M datagrams)
-    // the two-class launch, 32 datagrams per wave (ICSUM_TWOCLASS=1: the
-    // 8-lane groups above).  1 M datagrams VERIFY, 8-lane vs two-class at
-    // 64 / 32 / 16 per wave (tools/ab_ipv4_mix.py): 3/4 ACKs 127.3 vs 85.3 /
-    // 83.7 / 98.9 us, 1/2 157.9 vs 154.0 / 139.8 / 149.7, 7/16 166.0 vs 169.7
-    // / 153.8 / 164.3, 5/16 183.1 vs 201.0 / 181.1 / 185.5
-    two = hit && plan != icsum::kPlanWholeBatchSmall && mix.short16 >= ics_ctx::kIpv4TwoClass16 &&
-          mix.long16 == 0 && ctx->twoclass != 1;
-    plan_after = !hit || refresh;
+    // the two-class launch, 32 datagrams per wave.  1 M datagrams VERIFY,
+    // 8-lane groups vs two-class at 64 / 32 / 16 per wave (tools/ab_ipv4_mix.py):
+    // 3/4 ACKs 127.3 vs 85.3 / 83.7 / 98.9 us, 1/2 157.9 vs 154.0 / 139.8 /
+    // 149.7, 7/16 166.0 vs 169.7 / 153.8 / 164.3, 5/16 183.1 vs 201.0 / 181.1 / 185.5
+    two = hit && plan != icsum::kPlanWholeBatchSmall && mix.short16 >= ics_ctx::kIpv4TwoClass16 && mix.long16 == 0;
+    plan_used = hit ? int(plan) : -1;
   }
-  if (d_offsets && ((ctx->twoclass & 0xff) == 8 || (ctx->twoclass & 0xff) == 16)) {  // forced (A/B, tests)
-    two = true;
-    if (ctx->twoclass >> 8) two_spw = ctx->twoclass >> 8;
-  }
+  if (d_offsets && ctx->twoclass) two = true;  // test hook
   hipError_t le = hipErrorInvalidValue;
-  if (two) le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, ctx->patch_wt, two_spw, st);
-  if (le == hipErrorInvalidValue)
-    le = icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, ctx->max_blocks, ctx->patch_wt, st);
+  if (two) {
+    le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, st);
+    if (le != hipErrorInvalidValue) note(ctx, ICS_K_IPV4_TWOCLASS, {16, 32, true, 3, 1}, plan_used);
+  }
+  if (le == hipErrorInvalidValue) {
+    le = icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, 0, st);
+    note(ctx, ICS_K_IPV4, g, plan_used);
+  }
   ICS_HIP(le);
-  if (plan_after)
-    if (int rc = replan(ctx, sp, 64, st)) return rc;
+  if (int rc = replan(ctx, sp, 64, req, st)) return rc;
   return bounds_verdict(st, ICS_OK);
 }
+
+}  // extern "C"
 
 namespace {
 // The device wrap: two passes (payload sums into n words of scratch, then the
 // header launch) or one (ics_ctx::wrap_passes)
 hipError_t device_wrap(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* msgs, uint32_t* hdr_out,
-                       uint16_t* ip_ck, uint16_t* tcp_ck, bool payload_only, icsum::Geometry g, hipStream_t st) {
+                       uint16_t* ip_ck, uint16_t* tcp_ck, bool payload_only, icsum::Geometry g, int plan,
+                       hipStream_t st) {
   const icsum::TcpMsg* m = reinterpret_cast<const icsum::TcpMsg*>(msgs);
-  if (!wrap_two_pass(ctx, hdr_out != nullptr, sp.n))
-    return icsum::launch_tcp_wrap(sp, m, hdr_out, ip_ck, tcp_ck, payload_only, nullptr, g, ctx->max_blocks, st);
+  if (!wrap_two_pass(ctx, hdr_out != nullptr, sp.n)) {
+    note(ctx, ICS_K_WRAP, g, plan);
+    return icsum::launch_tcp_wrap(sp, m, hdr_out, ip_ck, tcp_ck, payload_only, nullptr, g, 0, st);
+  }
   Scratch sums(ctx, sp.n * 4, st);
   if (sums.error() != hipSuccess) return sums.error();
+  note(ctx, ICS_K_WRAP_2PASS, g, plan);
   return icsum::launch_tcp_wrap(sp, m, hdr_out, ip_ck, tcp_ck, payload_only, static_cast<uint32_t*>(sums.get()), g,
-                                ctx->max_blocks, st);
+                                0, st);
 }
-}  // namespace
 
-namespace {
 // The device wrap's geometry: one lane per datagram for ACK-sized batches (a
 // fixed length, or a cached small plan with a mean <= kTinyMaxAvg: 1 M pure
 // ACKs in place 78.3 -> 36.6 us, 40-56 B 119.0 -> 47.4 us,
 // tools/ab_wrap_ack.py), else the fused kernel's geometry for the length
-// hint; plan_after: run the plan kernels behind the launch
-icsum::Geometry wrap_geometry(ics_ctx* ctx, const icsum::SegSpec& sp, uint64_t hint, bool* plan_after) {
+// hint.  The plan kernels run behind the launch as plan_lookup asks (the
+// wrap's transmit buffer keeps its own cache slot: a stack's receive-side
+// verify in between does not evict it).
+icsum::Geometry wrap_geometry(ics_ctx* ctx, const icsum::SegSpec& sp, uint64_t hint, PlanReq* req, int* plan_used) {
   const icsum::Geometry lane1{1, 4, false, 0, 1};
   const icsum::Geometry base = geometry_for(ctx, sp.offsets ? hint : sp.seg_len);
   icsum::Geometry g = base.mode == icsum::kModeTiny ? lane1 : ipv4_geometry(base);
-  *plan_after = false;
-  if (sp.offsets && ctx->plan_cache && ctx->plan_host && !forced_geometry(ctx) && sp.n >= ics_ctx::kSmallPlanMin &&
-      sp.n <= 0xFFFFFFFFull) {
+  *req = {};
+  *plan_used = -1;
+  if (sp.offsets && !forced_geometry(ctx) && sp.n >= ics_ctx::kSmallPlanMin && sp.n <= 0xFFFFFFFFull) {
     uint32_t plan = 0;
     PlanMix mix;
-    bool refresh = false;
-    const bool hit = plan_lookup(ctx, sp, true, &plan, &refresh, &mix);
+    const bool hit = plan_lookup(ctx, sp, true, &plan, req, &mix);
     if (hit && plan == icsum::kPlanWholeBatchSmall && mix.avg <= icsum::kTinyMaxAvg) g = lane1;
-    *plan_after = !hit || refresh;
+    if (hit) *plan_used = int(plan);
   }
   return g;
 }
 }  // namespace
+
+extern "C" {
 
 int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,
                        uint64_t dgram_len, uint64_t n, const ics_tcp_msg* d_msgs, uint16_t* d_ip_ck,
@@ -1073,12 +1125,12 @@ int ics_tcp_wrap_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets, 
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
   // the stack's segments are <= 1000 B of payload (TCPConfig::MAX_PAYLOAD_SIZE): the
   // 16-lane line grid of MTU-sized datagrams unless a fixed length says otherwise
-  bool plan_after = false;
-  const icsum::Geometry g = wrap_geometry(ctx, sp, 1040, &plan_after);
+  PlanReq req;
+  int plan = -1;
+  const icsum::Geometry g = wrap_geometry(ctx, sp, 1040, &req, &plan);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  ICS_HIP(device_wrap(ctx, sp, d_msgs, nullptr, d_ip_ck, d_tcp_ck, false, g, st));
-  if (plan_after)
-    if (int rc = replan(ctx, sp, 64, st)) return rc;
+  ICS_HIP(device_wrap(ctx, sp, d_msgs, nullptr, d_ip_ck, d_tcp_ck, false, g, plan, st));
+  if (int rc = replan(ctx, sp, 64, req, st)) return rc;
   return bounds_verdict(st, ICS_OK);
 }
 
@@ -1091,12 +1143,12 @@ int ics_tcp_wrap_headers(ics_ctx* ctx, const void* d_payloads, const uint64_t* d
   if (reinterpret_cast<uintptr_t>(d_msgs) & 3u) return fail(ICS_ERR_INVALID, "message records not 4-byte aligned");
   if (reinterpret_cast<uintptr_t>(d_hdrs) & 3u) return fail(ICS_ERR_INVALID, "header array not 4-byte aligned");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_payloads), d_offsets, stride, payload_len, n, ctx->d_zero};
-  bool plan_after = false;
-  const icsum::Geometry g = wrap_geometry(ctx, sp, 1000, &plan_after);
+  PlanReq req;
+  int plan = -1;
+  const icsum::Geometry g = wrap_geometry(ctx, sp, 1000, &req, &plan);
   hipStream_t st = static_cast<hipStream_t>(stream);
-  ICS_HIP(device_wrap(ctx, sp, d_msgs, static_cast<uint32_t*>(d_hdrs), d_ip_ck, d_tcp_ck, true, g, st));
-  if (plan_after)
-    if (int rc = replan(ctx, sp, 64, st)) return rc;
+  ICS_HIP(device_wrap(ctx, sp, d_msgs, static_cast<uint32_t*>(d_hdrs), d_ip_ck, d_tcp_ck, true, g, plan, st));
+  if (int rc = replan(ctx, sp, 64, req, st)) return rc;
   return bounds_verdict(st, ICS_OK);
 }
 
@@ -1125,6 +1177,7 @@ int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets
   if (!d_dgrams || !d_status) return fail(ICS_ERR_INVALID, "null device buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
   ICS_HIP(icsum::launch_router_ttl(sp, d_status, static_cast<hipStream_t>(stream)));
+  note(ctx, ICS_K_ROUTER);
   return bounds_verdict(static_cast<hipStream_t>(stream), ICS_OK);
 }
 

@@ -164,52 +164,6 @@ __device__ __forceinline__ void range_sums(const uint8_t* __restrict__ base, uin
   }
 }
 
-// Same sums with the chunk grid anchored on the 128-byte cache line that
-// holds s: slot u of a group covers chunks [u*LPS, (u+1)*LPS) from that line,
-// i.e. whole lines, so with LPS >= 8 no line is touched by two load
-// instructions of the wave (non-temporal streams would otherwise re-fetch the
-// shared lines).  Every slot is a plain unmasked load; the lanes that happen
-// to hold the head chunk (index cs) or the tail chunk keep a copy, masked
-// once at the end.  Chunks before cs in the head line are loaded (same line)
-// and discarded.
-template <int LPS, int UNROLL, bool NT>
-__device__ __forceinline__ void range_sums_line(const uint8_t* __restrict__ base, uint64_t s,
-                                                uint64_t e, uint32_t lane, uint32_t& ev,
-                                                uint32_t& od) {
-  const uint64_t a0 = s & ~uint64_t(127);
-  const uint64_t span = e > s ? e - a0 : 0;
-  const uint32_t nch = uint32_t((span + 15) >> 4);
-  const uint32_t cs = uint32_t(s - a0) >> 4;   // head chunk (0..7)
-  const uint32_t lastc = nch ? nch - 1 : 0u;   // tail chunk
-  const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(base + a0);
-  [[maybe_unused]] const uint8_t* env_lo = base + a0;
-  [[maybe_unused]] const uint8_t* env_hi = base + ((e + 15) & ~uint64_t(15));
-  u32x4 hd = {0u, 0u, 0u, 0u}, td = {0u, 0u, 0u, 0u};
-  for (uint32_t c = lane; c < nch; c += uint32_t(LPS * UNROLL)) {
-    u32x4 v[UNROLL];
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const uint32_t cc = c + uint32_t(u * LPS);
-      ICS_CHECK16(p + (cc < lastc ? cc : lastc), env_lo, env_hi);
-      v[u] = load16<NT>(p + (cc < lastc ? cc : lastc));
-    }
-#pragma unroll
-    for (int u = 0; u < UNROLL; ++u) {
-      const uint32_t cc = c + uint32_t(u * LPS);
-      const uint32_t keep = (cc > cs && cc < lastc) ? ~0u : 0u;
-      acc_chunk(v[u] & keep, ev, od);
-      if (cc == cs) hd = v[u];
-      if (cc == lastc && lastc != cs) td = v[u];
-    }
-  }
-  if (nch) {
-    const uint32_t tail = uint32_t(span - (uint64_t(lastc) << 4));  // valid bytes of the tail chunk
-    const uint32_t lo0 = uint32_t(s) & 15u;
-    acc_chunk(hd & byte_range_mask(lo0, lastc == cs ? tail : 16u), ev, od);
-    acc_chunk(td & byte_range_mask(0u, tail), ev, od);
-  }
-}
-
 // Line-anchored grid with the two boundary chunks loaded FIRST, with the
 // default (cache-allocating) policy, by lanes 0 (head) and 1 (tail) of the
 // group; the slot loop then streams only the interior chunks non-temporally
@@ -299,14 +253,16 @@ __device__ __forceinline__ void range_sums_masked(const uint8_t* __restrict__ ba
 }
 
 // Chunk-grid modes (Geometry::mode): 0 = 16-byte grid, interior unmasked +
-// boundary instruction; 1 = 128-byte-line grid; 2 = 16-byte grid, all masked;
-// 3 = 128-byte-line grid with default-policy boundary loads issued first.
+// boundary instruction (the fused kernel's one-lane shape); 2 = 16-byte grid,
+// all masked (4- and 8-lane shapes); 3 = 128-byte-line grid, slot u of a group
+// covering chunks [u*LPS, (u+1)*LPS) from the line that holds the start, with
+// default-policy boundary loads issued first (every longer segment).  Mode 1
+// (the line grid without the primed boundary loads) was superseded by 3.
 template <int LPS, int UNROLL, bool NT, int MODE>
 __device__ __forceinline__ void seg_sums(const uint8_t* __restrict__ base, uint64_t s, uint64_t e,
                                          uint32_t lane, uint32_t& ev, uint32_t& od) {
-  if (MODE == 1)
-    range_sums_line<LPS, UNROLL, NT>(base, s, e, lane, ev, od);
-  else if (MODE == 3)
+  static_assert(MODE == 0 || MODE == 2 || MODE == 3, "chunk-grid mode");
+  if (MODE == 3)
     range_sums_line_primed<LPS, UNROLL, NT>(base, s, e, lane, ev, od);
   else if (MODE == 2)
     range_sums_masked<LPS, UNROLL, NT>(base, s, e, lane, ev, od);

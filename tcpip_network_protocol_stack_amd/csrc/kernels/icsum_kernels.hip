@@ -28,12 +28,6 @@ __device__ BoundsState g_icsum_bounds;
 namespace {
 
 constexpr int kBlock = 256;
-// ICSUM_OCC8 builds (A/B): hold the fused kernels to 8 waves per SIMD (<= 64 VGPRs)
-#ifdef ICSUM_OCC8
-#define ICS_OCC8 __attribute__((amdgpu_waves_per_eu(ICSUM_OCC8, 8)))
-#else
-#define ICS_OCC8
-#endif
 
 __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets, uint64_t stride,
                                            uint64_t seg_len, uint64_t i, uint64_t& s,
@@ -110,31 +104,40 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total)
 //   kPlanSplit  every bin runs from its list with its own geometry
 //   kPlanWhole16 the last bin's launch takes every segment with 16-lane
 //               groups in its first n/16 blocks (the rest exit at once)
-// Cost model in ns, measured on MI355X (tools/ab_bins.py, tools/ab_lastbin.py);
-// the last bin's launch dispatches n * last_lps / 64 waves under every plan,
-// ≈0.053 ns each when they find no work:
-//   whole:   max(bytes / 7100 GB/s, n * 0.45 ns)   (64 lanes per segment)
-//   split:   sum over bins of max(bytes_b / rate_b, n_b * 0.1 ns) + 26 us
-//            + the empty last-bin waves, with rate 5000 GB/s for bins 0-3 and
-//            6400 GB/s for the last (its segments no longer contiguous)
-//   whole16: sum over bins of max(bytes_b / r16_b, n_b * 0.16 ns) + the
-//            waves past n/4, r16 = 7000 GB/s up to 1920-byte segments, 6500 up
-//            to 4 KiB, 5000 above (16 lanes loop over long segments)
-//   wholeS:  the small-segment body (4 lanes, 2 segments per group in flight)
-//            over every segment: bin 0 max(bytes / 5000, n_b * 0.02 ns), any
-//            longer segment max(bytes / 800, n_b * 0.5 ns) (4 lanes loop), +
-//            the waves past n/32 — for batches of ACK-sized segments
+//   kPlanWholeSmall the last bin's launch takes every segment through the
+//               small-segment body (or one lane per segment for ACK-sized means)
+// The choice is the cheapest plan under kPlanCost (below): every estimate is
+// in ns, a sum over the bins of max(bytes / rate, segments * per-segment
+// cost) plus the dispatch of the last bin's idle waves.
 // Measured under each forced plan (tools/ab_lastbin.py --var ICSUM_BIN_PLAN,
 // profiles/r1_ab_plans.jsonl), µs whole / split / whole16: config 4
 // 1429 / 1622 / 1682, 2 M bimodal 40+1460 B 525 / 473 / 364, 2 M x 4-6 KiB
 // 1515 / 1589 / 1593, 1 M x 1460 B 520 / 429 / 296, 1 M x 40 B 451 / 168 / 205.
+struct PlanCostTable {
+  // rates in GB/s (= bytes per ns), per-segment costs in ns x 100; sources in profiles/
+  uint32_t whole_rate;            // whole: 64-lane groups over a long mix; config 4 whole 1429 us = 7.2 TB/s (r1_ab_plans)
+  uint32_t whole_seg_c;           // whole: ns x 100 per segment floor; 1 M x 40 B whole 451 us (r1_ab_plans)
+  uint32_t split_fixed_ns;        // split: the scatter pass and the bins 0-3 launch, 26 us fixed (tools/ab_bins.py, r1_ab_bins)
+  uint32_t empty_wave_ps;         // every plan: an idle wave of the last bin's launch, 0.053 ns (tools/probe/dispatch_probe.hip)
+  uint32_t split_rate_bins;       // split: bins 0-3 from their lists, 5.0 TB/s (r1_ab_bins)
+  uint32_t split_rate_last;       // split: last bin, segments no longer contiguous, 6.4 TB/s (r1_ab_bins)
+  uint32_t split_seg_c;           // split: ns x 100 per listed segment (r1_ab_bins: 1 M x 40 B split 168 us)
+  uint32_t w16_rate[kBins];       // whole16 per bin: 7.0 TB/s to 1920 B, 6.5 to 4 KiB, 5.0 above (16 lanes loop; r1_ab_plans)
+  uint32_t w16_seg_c;             // whole16: ns x 100 per segment (1 M x 1460 B whole16 296 us)
+  uint32_t small_rate[kBins];     // wholeS per bin: 5.0 TB/s for bin 0, 0.8 for longer (4 lanes loop; r1_ab_plans small)
+  uint32_t small_seg_c[kBins];    // wholeS: ns x 100 per segment, 0.02 bin 0 / 0.5 longer (1 M x 40-43 B small 140 us)
+};
+constexpr PlanCostTable kPlanCost = {7100, 45, 26000, 53, 5000, 6400, 10,
+                                     {7000, 7000, 7000, 6500, 5000}, 16,
+                                     {5000, 800, 800, 800, 800}, {2, 50, 50, 50, 50}};
 constexpr uint32_t kPlanWhole = 0, kPlanSplit = 1, kPlanWhole16 = 2, kPlanWholeSmall = 3;
 static_assert(kPlanWhole == kPlanWholeBatch && kPlanSplit == kPlanSplitBins && kPlanWhole16 == kPlanWholeBatch16 &&
               kPlanWholeSmall == kPlanWholeBatchSmall, "plan ids shared with the host's plan cache");
 
 __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta, const uint32_t* __restrict__ cnt_part,
                                                      const uint64_t* __restrict__ by_part, uint32_t parts, uint64_t n,
-                                                     int force, uint32_t last_lps, uint64_t* __restrict__ plan_out) {
+                                                     int force, uint32_t last_lps, uint64_t* __restrict__ plan_out,
+                                                     uint32_t gen) {
   // totals per bin from the stats pass's per-block partials (parts <= kBlock:
   // one partial per thread, all loads in flight together)
   __shared__ uint32_t wc[kBlock / 64][kBins];
@@ -168,8 +171,11 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
   __syncthreads();
   if (threadIdx.x == 0) {
     const uint64_t waves = n * last_lps / 64;  // the last bin's launch
-    uint64_t total = 0, short_n = 0, long_bytes = 0, t_split = 26000 + waves * 53 / 1000, t16 = (waves - n / 4) * 53 / 1000,
-             t_small = (waves - n / 32) * 53 / 1000;
+    const PlanCostTable& C = kPlanCost;
+    uint64_t total = 0, short_n = 0, long_bytes = 0;
+    uint64_t t_split = C.split_fixed_ns + waves * C.empty_wave_ps / 1000;
+    uint64_t t16 = (waves - n / 4) * C.empty_wave_ps / 1000;        // whole16 uses the first n/16 blocks
+    uint64_t t_small = (waves - n / 32) * C.empty_wave_ps / 1000;   // wholeS the first n/128
 #pragma unroll
     for (int k = 0; k < kBins; ++k) {
       uint32_t c = 0;
@@ -183,14 +189,14 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
       if (k == 0) short_n = c;
       if (k >= 3) long_bytes += v;  // segments > 1920 bytes
       total += v;
-      const uint64_t tb = v / (k == kBins - 1 ? 6400 : 5000), tn = c / 10;
+      const uint64_t tb = v / (k == kBins - 1 ? C.split_rate_last : C.split_rate_bins), tn = uint64_t(c) * C.split_seg_c / 100;
       t_split += tb > tn ? tb : tn;
-      const uint64_t sb = v / (k < kBins - 2 ? 7000 : (k == kBins - 2 ? 6500 : 5000)), sn = uint64_t(c) * 16 / 100;
+      const uint64_t sb = v / C.w16_rate[k], sn = uint64_t(c) * C.w16_seg_c / 100;
       t16 += sb > sn ? sb : sn;
-      const uint64_t mb = v / (k == 0 ? 5000 : 800), mn = uint64_t(c) * (k == 0 ? 2 : 50) / 100;
+      const uint64_t mb = v / C.small_rate[k], mn = uint64_t(c) * C.small_seg_c[k] / 100;
       t_small += mb > mn ? mb : mn;
     }
-    const uint64_t tb = total / 7100, tn = n * 45 / 100, t_whole = tb > tn ? tb : tn;
+    const uint64_t tb = total / C.whole_rate, tn = n * C.whole_seg_c / 100, t_whole = tb > tn ? tb : tn;
     uint32_t plan = kPlanWhole;
     if (force >= 0) {
       plan = uint32_t(force);
@@ -207,11 +213,13 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
     // host memory: the plan (bits 0-3), the share of bin-0 (<= 144-byte)
     // segments in sixteenths (bits 4-7), the batch size (bits 8-39), the
     // share of bytes in segments over 1920 bytes in sixteenths (bits 40-43)
-    // and the mean segment length in bytes, capped at 4095 (bits 44-55)
+    // the mean segment length in bytes, capped at 4095 (bits 44-55), and the
+    // generation of the cache slot that asked for it (bits 56-63)
     const uint64_t short16 = n ? short_n * 16 / n : 0, long16 = total ? long_bytes * 16 / total : 0;
     if (plan_out)
       *plan_out = plan | ((short16 < 15 ? short16 : 15) << 4) | ((n & 0xFFFFFFFFull) << 8) |
-                  ((long16 < 15 ? long16 : 15) << 40) | ((avg < 4095 ? avg : 4095) << 44);
+                  ((long16 < 15 ? long16 : 15) << 40) | ((avg < 4095 ? avg : 4095) << 44) |
+                  (uint64_t(gen & 0xffu) << 56);
   }
 }
 
@@ -772,356 +780,6 @@ __global__ void k_fold(const uint32_t* __restrict__ sum, uint16_t* __restrict__ 
   ICS_GRID_STRIDE(i, n) out[i] = fold_value(sum[i]);
 }
 
-// ------------------------------------------------- flat offsets batches ---
-// A packed offsets batch is ONE byte stream [offsets[0], offsets[n]) cut at
-// the offsets (segment i = [offsets[i], offsets[i+1])).  k_checksum_flat reads
-// it as such, whatever the length mix: wave w streams an equal share of
-// 8 KiB tiles (chunk u*64 + lane of a tile is lane `lane`'s slot u, so every
-// load instruction of the wave reads 1 KiB contiguous), and the cuts only
-// decide where the sums go:
-//   * a tile without a cut adds its bytes to the open segment (lane-local
-//     even/odd sums, no cross-lane work);
-//   * a tile with cuts takes the exclusive prefix of its chunks' even/odd
-//     sums (DPP wave scans, kept in LDS); the cut at x, in chunk k at byte r,
-//     has prefix P(x) = pfx[k] + the even/odd sums of chunk k's first r bytes,
-//     and segment j's piece of the tile is P(end_j) - P(start_j);
-//   * a segment that starts and ends inside the wave's share is written
-//     directly (init + sum, folded); the pieces of a segment that crosses a
-//     share boundary are added (u32 atomics: the sum is mod 2^32, so any order
-//     is exact) into the slot of the wave whose share holds its start, and
-//     k_flat_finish folds them.
-// Every segment costs a few instructions at its cut instead of a lane group:
-// the rate no longer depends on the lengths (bimodal 40 B / 1460 B batches,
-// BASELINE config 4's 64 B - 64 KiB mix).  The byte roles come from absolute
-// addresses as everywhere (icsum_device.h), so a piece's even/odd sums are
-// combined with its segment's own swap.
-constexpr uint32_t kFlatNone = 0xFFFFFFFFu;
-constexpr int kFlatSlots = 8;  // 16-byte chunks per lane per tile: 8 KiB tiles
-
-// inclusive scan over the 64 lanes (row_shr 1/2/4/8 inside each row, then
-// row_bcast15 / row_bcast31 across rows)
-__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, true);   // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, true);   // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, true);   // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, true);   // row_shr:8
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
-  return x;
-}
-
-__device__ __forceinline__ uint32_t wave_total(uint32_t x) {
-  return __builtin_amdgcn_readlane(group_sum<64>(x), 63);
-}
-
-__device__ __forceinline__ uint64_t readlane64(uint64_t x, uint32_t l) {
-  // (the builtin returns int: through uint32_t, or a low word >= 2^31 would sign-extend)
-  return uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x), l))) |
-         (uint64_t(uint32_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), l))) << 32);
-}
-
-// number of leading lanes (from lane 0) whose predicate holds
-__device__ __forceinline__ uint32_t leading_lanes(bool p) {
-  const uint64_t m = __ballot(p);
-  return ~m ? uint32_t(__builtin_ctzll(~m)) : 64u;
-}
-
-// the segment open at byte position pos > offsets[0]: the first j < n with
-// offsets[j + 1] > pos (offsets[n] > pos), by 64-way probing (one dependent
-// load per factor of 64; every probe index is clamped into [lo, hi])
-__device__ __forceinline__ uint64_t flat_find(const uint64_t* __restrict__ off, uint64_t n, uint64_t pos,
-                                              uint32_t lane) {
-  uint64_t lo = 0, hi = n - 1;  // the answer lies in [lo, hi]
-  // (bounded: 11 rounds cover 2^64 for monotone offsets; malformed ones end
-  // here too, with some index in [0, n - 1])
-  for (int round = 0; round < 11 && lo <= hi && hi - lo >= 64; ++round) {
-    const uint64_t step = ((hi - lo) >> 6) + 1;
-    const uint64_t p = lo + uint64_t(lane) * step;
-    const uint64_t pc = p < hi ? p : hi;
-    const uint64_t m = __ballot(off[pc + 1] > pos);
-    if (m == 0) {
-      lo += 63 * step + 1;  // every probe is <= hi here and below the answer
-      continue;
-    }
-    const uint32_t f = uint32_t(__builtin_ctzll(m));
-    if (f == 0) return lo;
-    const uint64_t pf = lo + uint64_t(f) * step;
-    hi = pf < hi ? pf : hi;
-    lo += uint64_t(f - 1) * step + 1;
-  }
-  if (lo > hi) lo = hi;
-  const uint64_t p = lo + lane, pc = p < hi ? p : hi;
-  const uint64_t m = __ballot(off[pc + 1] > pos);
-  const uint64_t r = m ? lo + uint64_t(__builtin_ctzll(m)) : hi;
-  return r < n ? r : n - 1;
-}
-
-// the wave whose share holds byte position s (shares of rt tiles from r0)
-__device__ __forceinline__ uint32_t flat_owner(uint64_t s, uint64_t r0, uint64_t rt, uint32_t nwaves) {
-  constexpr uint64_t kTile = 16ull * 64 * kFlatSlots;
-  const uint64_t w = s > r0 ? (s - r0) / kTile / rt : 0;
-  return uint32_t(w < nwaves - 1 ? w : nwaves - 1);
-}
-
-template <bool NT, int OUT>
-__global__ __launch_bounds__(kBlock) void k_checksum_flat(const uint8_t* __restrict__ bytes,
-                                                          const uint64_t* __restrict__ offsets, uint64_t n,
-                                                          const uint32_t* __restrict__ init, uint32_t init_step,
-                                                          const uint8_t* __restrict__ odd, uint32_t odd_step,
-                                                          void* __restrict__ out, uint32_t* __restrict__ accw,
-                                                          uint32_t* __restrict__ tailw, uint32_t nwaves) {
-  constexpr uint32_t kChunks = 64 * kFlatSlots;
-  constexpr uint64_t kTile = 16ull * kChunks;
-  __shared__ uint32_t pfx[kBlock / 64][2][kChunks];  // per wave: exclusive prefix of the even / odd sums
-  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
-  const uint32_t w = blockIdx.x * (kBlock / 64) + wv;
-  if (w >= nwaves) return;
-  const uint64_t off0 = offsets[0], offn = offsets[n];
-  const uint64_t r0 = off0 & ~uint64_t(15);
-  const uint64_t total = offn > r0 ? offn - r0 : 0;  // 0: every segment empty
-  const uint64_t ntiles = total ? (total + kTile - 1) / kTile : 1;
-  const uint64_t rt = (ntiles + nwaves - 1) / nwaves;  // tiles per wave
-  const uint64_t t0 = uint64_t(w) * rt, t1 = t0 + rt < ntiles ? t0 + rt : ntiles;
-  if (t0 >= t1) {
-    if (lane == 0) tailw[w] = kFlatNone;
-    return;
-  }
-  const uint64_t wbeg = r0 + t0 * kTile, wend = r0 + t1 * kTile;
-  const uint64_t lastc = offn > r0 ? (offn - 1) & ~uint64_t(15) : r0;  // last chunk holding a byte
-  [[maybe_unused]] const uint8_t* env_lo = bytes + r0;
-  [[maybe_unused]] const uint8_t* env_hi = bytes + lastc + 16;
-  // the open segment: its index, start, whether its start lies in this share,
-  // and (lane-local) the even/odd sums of its bytes in earlier tiles
-  uint64_t cur = w == 0 ? 0 : flat_find(offsets, n, wbeg, lane);
-  uint64_t cur_start = offsets[cur];
-  bool started = w == 0 || cur_start >= wbeg;
-  uint32_t accE = 0, accO = 0;
-  // per segment that completes: its sum to `out` (init added) or, for the
-  // open segment whose start lies in an earlier share, its last piece to the
-  // slot of that share's wave
-  auto finish = [&](uint64_t j, uint64_t start, uint32_t pe, uint32_t po, bool here) {
-    const uint32_t c = combine_roles(pe, po, (uint32_t(start) ^ uint32_t(odd[j * odd_step])) & 1u);
-    if (!here) {
-      atomicAdd(&accw[flat_owner(start, r0, rt, nwaves)], c);
-    } else {
-      const uint32_t sv = init[j * init_step] + c;
-      if (OUT == 0)
-        static_cast<uint16_t*>(out)[j] = fold_value(sv);
-      else
-        static_cast<uint32_t*>(out)[j] = sv;
-    }
-  };
-  const u32x4* __restrict__ lanep = reinterpret_cast<const u32x4*>(bytes) + lane;
-  for (uint64_t t = t0; t < t1; ++t) {
-    const uint64_t T = r0 + t * kTile, tend = T + kTile;
-    // the batch's first and last tiles (bytes outside [offsets[0],
-    // offsets[n]) are masked, chunks past the end not read): a uniform branch
-    const bool edge = T < off0 || tend > offn;
-    u32x4 v[kFlatSlots];
-    if (!edge) {
-      const u32x4* __restrict__ p = lanep + (T >> 4);
-#pragma unroll
-      for (int u = 0; u < kFlatSlots; ++u) {
-        ICS_CHECK16(p + u * 64, env_lo, env_hi);
-        v[u] = load16<NT>(p + u * 64);
-      }
-    } else {
-#pragma unroll
-      for (int u = 0; u < kFlatSlots; ++u) {
-        const uint64_t a = T + (uint64_t(u) * 64 + lane) * 16;
-        const uint64_t q = a < lastc ? a : lastc;
-        ICS_CHECK16(bytes + q, env_lo, env_hi);
-        v[u] = total ? load16<NT>(reinterpret_cast<const u32x4*>(bytes + q)) : u32x4{0u, 0u, 0u, 0u};
-      }
-    }
-    // cut candidates: lane i holds offsets[cur + 1 + i], the end of segment cur + i
-    const uint64_t ci = cur + 1 + lane;
-    uint64_t x = offsets[ci <= n ? ci : n];
-    uint32_t m = leading_lanes(ci <= n && x <= tend);
-    if (edge) {
-#pragma unroll
-      for (int u = 0; u < kFlatSlots; ++u) {
-        const uint64_t a = T + (uint64_t(u) * 64 + lane) * 16;
-        const uint32_t lo = a < off0 ? uint32_t(off0 - a) : 0u;
-        const uint32_t hi = a >= offn ? 0u : (offn - a >= 16 ? 16u : uint32_t(offn - a));
-        v[u] = v[u] & byte_range_mask(lo, hi);
-      }
-    }
-    if (m == 0) {  // the open segment runs through the tile
-#pragma unroll
-      for (int u = 0; u < kFlatSlots; ++u) acc_chunk(v[u], accE, accO);
-      continue;
-    }
-    // one or two cuts (long segments): the first bytes of each cut's chunk,
-    // summed in its owner lane now, so that the chunks can be dropped
-    uint32_t hE[2] = {0u, 0u}, hO[2] = {0u, 0u};
-    if (m <= 2) {
-#pragma unroll
-      for (uint32_t i = 0; i < 2; ++i) {
-        if (i < m) {
-          const uint64_t xi = readlane64(x, i);
-          const uint64_t xc = xi < T ? T : (xi > tend ? tend : xi);
-          const uint32_t rel = uint32_t(xc - T), k = rel >> 4, r = rel & 15u;
-          if (k < kChunks && r != 0) {
-            const uint32_t uk = k >> 6;
-            u32x4 cv = v[0];
-#pragma unroll
-            for (int u = 1; u < kFlatSlots; ++u)
-              if (uint32_t(u) == uk) cv = v[u];
-            const uint64_t a = T + uint64_t(k) * 16;
-            const uint32_t lo = a < off0 ? uint32_t(off0 - a) : 0u;
-            if (lane == (k & 63u)) acc_chunk(cv & byte_range_mask(lo, r), hE[i], hO[i]);
-          }
-        }
-      }
-    }
-    uint32_t e[kFlatSlots], o[kFlatSlots];
-#pragma unroll
-    for (int u = 0; u < kFlatSlots; ++u) {
-      e[u] = 0;
-      o[u] = 0;
-      acc_chunk(v[u], e[u], o[u]);
-    }
-    // the open segment's bytes in earlier tiles, over the wave
-    uint32_t carryE = wave_total(accE), carryO = wave_total(accO);
-    accE = accO = 0;
-    if (m <= 2) {
-      // one or two cuts (long segments): P(x) by one masked wave sum per cut
-      // (chunks before x's chunk, plus x's chunk's first bytes in its owner
-      // lane) instead of the tile's prefix scans
-      uint32_t se = 0, so = 0;
-#pragma unroll
-      for (int u = 0; u < kFlatSlots; ++u) {
-        se += e[u];
-        so += o[u];
-      }
-      const uint32_t totE = wave_total(se), totO = wave_total(so);
-      uint32_t prevE = 0, prevO = 0;
-      for (uint32_t i = 0; i < m; ++i) {
-        const uint64_t xi = readlane64(x, i);
-        const uint64_t xc = xi < T ? T : (xi > tend ? tend : xi);
-        const uint32_t rel = uint32_t(xc - T), k = rel >> 4, r = rel & 15u;
-        uint32_t pE = totE, pO = totO;
-        if (k < kChunks) {
-          uint32_t ce = i == 0 ? hE[0] : hE[1], co = i == 0 ? hO[0] : hO[1];
-          (void)r;
-#pragma unroll
-          for (int u = 0; u < kFlatSlots; ++u) {
-            const bool before = uint32_t(u) * 64 + lane < k;
-            ce += before ? e[u] : 0u;
-            co += before ? o[u] : 0u;
-          }
-          pE = wave_total(ce);
-          pO = wave_total(co);
-        }
-        if (lane == 0) {
-          const uint64_t j = cur + i;  // < n: its end cut exists
-          finish(j, cur_start, pE - prevE + carryE, pO - prevO + carryO, i != 0 || started);
-        }
-        prevE = pE;
-        prevO = pO;
-        carryE = carryO = 0;
-        cur_start = xc;
-      }
-      cur += m;
-      started = true;
-      if (lane == 0) {  // the open segment's bytes after its start in this tile
-        accE = totE - prevE;
-        accO = totO - prevO;
-      }
-      continue;
-    }
-    // exclusive prefix of the tile's chunks (chunk u*64 + lane)
-    uint32_t totE = 0, totO = 0;
-#pragma unroll
-    for (int u = 0; u < kFlatSlots; ++u) {
-      const uint32_t ie = wave_scan_incl(e[u]), io = wave_scan_incl(o[u]);
-      pfx[wv][0][u * 64 + lane] = totE + ie - e[u];
-      pfx[wv][1][u * 64 + lane] = totO + io - o[u];
-      totE += __builtin_amdgcn_readlane(ie, 63);
-      totO += __builtin_amdgcn_readlane(io, 63);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    uint32_t popE = 0, popO = 0;  // P at the open segment's start in this tile
-    for (;;) {
-      // P(x) at this lane's cut (x clamped into the tile: malformed offsets
-      // give wrong sums, never a read outside the batch)
-      const uint64_t xc = x < T ? T : (x > tend ? tend : x);
-      const uint32_t rel = uint32_t(xc - T), k = rel >> 4, r = rel & 15u;
-      uint32_t pE = totE, pO = totO;
-      if (lane < m && k < kChunks) {
-        pE = pfx[wv][0][k];
-        pO = pfx[wv][1][k];
-        if (r != 0 && total) {
-          const uint64_t a0 = T + uint64_t(k) * 16, a = a0 < lastc ? a0 : lastc;
-          ICS_CHECK16(bytes + a, env_lo, env_hi);
-          const u32x4 c = *reinterpret_cast<const u32x4*>(bytes + a);
-          const uint32_t lo = a < off0 ? uint32_t(off0 - a) : 0u;
-          acc_chunk(c & byte_range_mask(lo, r), pE, pO);
-        }
-      }
-      // the previous cut (lane 0: the open segment's start)
-      uint32_t qE = uint32_t(__shfl_up(int(pE), 1, 64)), qO = uint32_t(__shfl_up(int(pO), 1, 64));
-      uint64_t xs = uint64_t(__shfl_up((long long)xc, 1, 64));
-      if (lane == 0) {
-        qE = popE - carryE;
-        qO = popO - carryO;
-        xs = cur_start;
-      }
-      if (lane < m) finish(cur + lane, xs, pE - qE, pO - qO, lane != 0 || started);  // cur + lane < n
-      // the segment the last cut opens
-      popE = __builtin_amdgcn_readlane(pE, m - 1);
-      popO = __builtin_amdgcn_readlane(pO, m - 1);
-      cur_start = readlane64(xc, m - 1);
-      cur += m;
-      started = true;
-      carryE = carryO = 0;
-      if (m < 64) break;
-      const uint64_t cn = cur + 1 + lane;  // more cuts in this tile: the next 64 candidates
-      x = offsets[cn <= n ? cn : n];
-      m = leading_lanes(cn <= n && x <= tend);
-      if (m == 0) break;
-    }
-    if (lane == 0) {  // the open segment's bytes after its start in this tile
-      accE = totE - popE;
-      accO = totO - popO;
-    }
-  }
-  // the open segment continues past this share: add its piece to the slot of
-  // the wave that holds its start; that wave claims it when the start is here
-  const uint32_t ae = wave_total(accE), ao = wave_total(accO);
-  if (lane == 0) {
-    uint32_t claim = kFlatNone;
-    if (cur < n && cur_start < wend) {
-      const uint32_t sw = (uint32_t(cur_start) ^ uint32_t(odd[cur * odd_step])) & 1u;
-      atomicAdd(&accw[flat_owner(cur_start, r0, rt, nwaves)], combine_roles(ae, ao, sw));
-      if (started) claim = uint32_t(cur);
-    }
-    tailw[w] = claim;
-  }
-}
-
-// the segments that crossed a share boundary: init + their pieces' sum; the
-// slots are left zero for the next batch
-template <int OUT>
-__global__ void k_flat_finish(uint32_t* __restrict__ accw, const uint32_t* __restrict__ tailw,
-                              const uint32_t* __restrict__ init, uint32_t init_step, void* __restrict__ out,
-                              uint32_t nwaves) {
-  ICS_GRID_STRIDE(w, nwaves) {
-    const uint32_t s = accw[w], j = tailw[w];
-    accw[w] = 0;
-    if (j != kFlatNone) {
-      const uint32_t v = init[uint64_t(j) * init_step] + s;
-      if (OUT == 0)
-        static_cast<uint16_t*>(out)[j] = fold_value(v);
-      else
-        static_cast<uint32_t*>(out)[j] = v;
-    }
-  }
-}
-
 // ---------------------------------------------- IPv4 header fields ------
 // The first 20 wire bytes of a datagram as 5 little-endian dwords relative to
 // its (possibly unaligned) start: 6 aligned dword loads + alignbyte.
@@ -1161,33 +819,16 @@ __device__ __forceinline__ Hdr load_hdr(const uint8_t* p, const uint32_t* last) 
   return h;
 }
 
-// big-endian 16-bit field store: one short store when 2-byte aligned.
-// WT: write-through (sc1; a relaxed agent-scope atomic store is a plain
-// global_store_short/byte with sc1 on gfx950).  A patched field is the only
-// written part of its 128-byte line; a default-policy store leaves that line
-// dirty in the XCD's L2 until the end-of-kernel release writes every such
-// line back (MI355X_MICROARCH.md, boundary row: + dirty bytes / 6 TB/s),
-// after the stream.  Written through, the bytes leave during the stream.
-template <bool WT>
-__device__ __forceinline__ void store_byte(uint8_t* p, uint32_t v) {
-  if (WT)
-    __hip_atomic_store(p, uint8_t(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  else
-    *p = uint8_t(v);
-}
-
-template <bool WT = false>
+// big-endian 16-bit field store: one short store when 2-byte aligned.  The
+// default write-back policy: write-through (sc1), non-temporal and wider
+// (16-byte, 64-byte, whole-line) stores of the same fields all measured the
+// same or slower (PATCH).
 __device__ __forceinline__ void store_be16(uint8_t* p, uint32_t v) {
   if ((reinterpret_cast<uintptr_t>(p) & 1u) == 0) {
-    uint16_t* q = reinterpret_cast<uint16_t*>(p);
-    const uint16_t w = uint16_t(((v & 0xffu) << 8) | ((v >> 8) & 0xffu));
-    if (WT)
-      __hip_atomic_store(q, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else
-      *q = w;
+    *reinterpret_cast<uint16_t*>(p) = uint16_t(((v & 0xffu) << 8) | ((v >> 8) & 0xffu));
   } else {
-    store_byte<WT>(p, v >> 8);
-    store_byte<WT>(p + 1, v);
+    p[0] = uint8_t(v >> 8);
+    p[1] = uint8_t(v);
   }
 }
 
@@ -1302,7 +943,7 @@ __device__ __forceinline__ uint32_t ipv4_pseudo(const Hdr& h) {
 template <int LPS, int UNROLL, bool NT, int MODE>
 __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, uint64_t e, uint64_t seg, bool valid,
                                           uint32_t lane, int mode, uint16_t* __restrict__ ip_ck,
-                                          uint16_t* __restrict__ tcp_ck, uint8_t* __restrict__ status, int patch_wt,
+                                          uint16_t* __restrict__ tcp_ck, uint8_t* __restrict__ status,
                                           const uint8_t* __restrict__ zpad, const uint32_t* zlast) {
   const bool hdr = e - s >= 20;
   // Speculate the usual header length (hlen = 5): the IPv4 header dwords,
@@ -1366,10 +1007,7 @@ __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, 
         tcv = fold_value(sum);
         if (hdr_ok) st |= 0x01;
         if (rem >= 18) st |= 0x02;
-        if (mode == 2 && patch_wt) {
-          store_be16<true>(dg + s + 10, ipc);
-          if (rem >= 18) store_be16<true>(dg + t0 + 16, tcv);
-        } else if (mode == 2) {
+        if (mode == 2) {
           store_be16(dg + s + 10, ipc);
           if (rem >= 18) store_be16(dg + t0 + 16, tcv);
         }
@@ -1382,13 +1020,13 @@ __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, 
 }
 
 template <int LPS, int UNROLL, bool NT, int MODE>
-__global__ __launch_bounds__(kBlock) ICS_OCC8 void k_ipv4_tcp(uint8_t* __restrict__ dg,
+__global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
                                                      int mode, uint16_t* __restrict__ ip_ck,
                                                      uint16_t* __restrict__ tcp_ck,
                                                      uint8_t* __restrict__ status, uint32_t remap,
-                                                     int patch_wt, const uint8_t* __restrict__ zpad) {
+                                                     const uint8_t* __restrict__ zpad) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
@@ -1401,7 +1039,7 @@ __global__ __launch_bounds__(kBlock) ICS_OCC8 void k_ipv4_tcp(uint8_t* __restric
     uint64_t s, e;
     seg_bounds(offsets, stride, dlen, valid ? seg : n - 1, s, e);
     if (!valid) e = s;
-    ipv4_item<LPS, UNROLL, NT, MODE>(dg, s, e, seg, valid, lane, mode, ip_ck, tcp_ck, status, patch_wt, zpad, zlast);
+    ipv4_item<LPS, UNROLL, NT, MODE>(dg, s, e, seg, valid, lane, mode, ip_ck, tcp_ck, status, zpad, zlast);
   }
 }
 
@@ -1412,7 +1050,7 @@ template <int SPW>
 __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
                                                           uint64_t stride, uint64_t dlen, uint64_t n, int mode,
                                                           uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
-                                                          uint8_t* __restrict__ status, int patch_wt,
+                                                          uint8_t* __restrict__ status,
                                                           const uint8_t* __restrict__ zpad) {
   __shared__ uint64_t lst[kBlock / 64][64][2];
   __shared__ uint32_t lseg[kBlock / 64][64];
@@ -1434,7 +1072,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
   }
   // short datagrams: one lane each (the long lanes run an empty item)
   ipv4_item<1, 4, false, 0>(dg, s, is_short ? e : s, seg, valid && is_short, 0u, mode, ip_ck, tcp_ck, status,
-                            patch_wt, zpad, zlast);
+                            zpad, zlast);
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -1445,7 +1083,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
     const bool mine = k < nlong;
     const uint32_t kc = mine ? k : 0u;
     const uint64_t ls = lst[wv][kc][0], le = mine ? lst[wv][kc][1] : ls;
-    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[wv][kc], mine, gl, mode, ip_ck, tcp_ck, status, patch_wt, zpad, zlast);
+    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[wv][kc], mine, gl, mode, ip_ck, tcp_ck, status, zpad, zlast);
   }
 }
 
@@ -1463,7 +1101,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
 // hdr_out[40 i ..] instead of in place (the host-memory path copies only them
 // back).  Datagrams shorter than 40 bytes are left as they are.
 template <int LPS, int UNROLL, bool NT, int MODE, bool SUMS>
-__global__ __launch_bounds__(kBlock) ICS_OCC8 void k_tcp_wrap(uint8_t* __restrict__ dg,
+__global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
                                                      const uint64_t* __restrict__ offsets,
                                                      uint64_t stride, uint64_t dlen, uint64_t n,
                                                      const TcpMsg* __restrict__ msgs,
@@ -1993,11 +1631,11 @@ hipError_t launch_dense_t(const SegSpec& sp, const uint32_t* init, void* out, in
 
 template <int LPS, int UNROLL, bool NT, int MODE>
 hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
-                         uint8_t* status, uint32_t max_blocks, bool patch_wt, hipStream_t st) {
+                         uint8_t* status, uint32_t max_blocks, hipStream_t st) {
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
   hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, mode,
-                     ip_ck, tcp_ck, status, g_xcd_remap, int(patch_wt), static_cast<const uint8_t*>(sp.zero16));
+                     ip_ck, tcp_ck, status, g_xcd_remap, static_cast<const uint8_t*>(sp.zero16));
   return hipGetLastError();
 }
 
@@ -2051,22 +1689,18 @@ Geometry pick_geometry(uint64_t avg_len) {
   return {64, 8, true, 3, 1};
 }
 
-// every instantiated (LPS, UNROLL, NT) triple
-#define ICS_GEOMETRIES(X)                                                                 \
-  X(1, 4, true, 0) X(1, 8, true, 0) X(2, 4, true, 0) X(4, 1, true, 0) X(4, 2, true, 0)    \
-  X(8, 2, true, 0) X(8, 4, true, 0) X(16, 4, true, 0) X(16, 6, true, 0) X(16, 8, true, 0) \
-  X(32, 3, true, 0) X(32, 4, true, 0) X(64, 2, true, 0) X(64, 3, true, 0)                 \
-  X(64, 4, true, 0) X(64, 8, true, 0) X(16, 6, false, 0) X(64, 2, false, 0)               \
-  X(8, 4, true, 1) X(16, 4, true, 1) X(16, 6, true, 1) X(16, 8, true, 1) X(32, 3, true, 1) \
-  X(32, 4, true, 1) X(64, 4, true, 1) X(64, 8, true, 1) X(16, 6, false, 1)                 \
-  X(1, 4, true, 2) X(1, 8, true, 2) X(2, 4, true, 2) X(4, 1, true, 2) X(4, 2, true, 2)     \
-  X(8, 1, true, 2) X(8, 2, true, 2) X(16, 2, true, 2) X(16, 8, false, 1) X(64, 8, false, 1)    \
-  X(16, 8, true, 3) X(32, 4, true, 3) X(64, 8, true, 3) X(16, 4, true, 3) X(32, 8, true, 3)   \
-  X(16, 6, true, 3) X(32, 3, true, 3) X(8, 8, true, 3) X(16, 5, true, 3) X(1, 4, false, 0)
+// every instantiated (LPS, UNROLL, NT, MODE) of k_checksum, k_ipv4_tcp and
+// k_tcp_wrap: exactly the shapes the dispatch can reach — pick_geometry's line
+// grids, the last bin's 32/64-lane launch, the fused kernel's 4/8-lane shapes of
+// short datagrams (ipv4_geometry), its one-lane shape for ACK-sized datagrams
+// (mode 0, default-policy loads) and the 8-lane groups of ACK + MTU mixes
+#define ICS_GEOMETRIES(X)                                                                     \
+  X(1, 4, false, 0) X(4, 1, true, 2) X(4, 2, true, 2) X(8, 2, true, 2) X(8, 8, true, 3)      \
+  X(16, 4, true, 3) X(16, 5, true, 3) X(16, 6, true, 3) X(16, 8, true, 3) X(32, 8, true, 3) \
+  X(64, 8, true, 3)
 
 // small-segment kernel instantiations (LPS, UNROLL, SEGS); Geometry::segs > 1
-#define ICS_SMALL_GEOMETRIES(X) \
-  X(4, 1, 2) X(4, 1, 4) X(4, 1, 8) X(4, 2, 2) X(4, 2, 4) X(8, 1, 4) X(8, 2, 2) X(8, 2, 4) X(16, 2, 2)
+#define ICS_SMALL_GEOMETRIES(X) X(4, 1, 2) X(4, 2, 2) X(8, 2, 2)
 
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st) {
@@ -2087,38 +1721,11 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
   return hipErrorInvalidValue;
 }
 
-hipError_t launch_checksum_flat(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
-                                int out_kind, uint32_t* accw, uint32_t* tailw, uint32_t nwaves, hipStream_t st) {
-  if (!sp.offsets || sp.n == 0 || sp.n >= 0xFFFFFFFFull || nwaves == 0 || nwaves > (1u << 24))
-    return hipErrorInvalidValue;
-  const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
-  const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
-  const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
-  const dim3 grid((nwaves + kBlock / 64 - 1) / (kBlock / 64));
-  const dim3 fgrid((nwaves + kBlock - 1) / kBlock < 1024 ? (nwaves + kBlock - 1) / kBlock : 1024);
-  if (out_kind == 0) {
-    hipLaunchKernelGGL((k_checksum_flat<true, 0>), grid, dim3(kBlock), 0, st, sp.bytes, sp.offsets, sp.n, ip, is,
-                       op, os, out, accw, tailw, nwaves);
-    if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL(k_flat_finish<0>, fgrid, dim3(kBlock), 0, st, accw, tailw, ip, is, out, nwaves);
-  } else {
-    hipLaunchKernelGGL((k_checksum_flat<true, 1>), grid, dim3(kBlock), 0, st, sp.bytes, sp.offsets, sp.n, ip, is,
-                       op, os, out, accw, tailw, nwaves);
-    if (hipError_t e = hipGetLastError()) return e;
-    hipLaunchKernelGGL(k_flat_finish<1>, fgrid, dim3(kBlock), 0, st, accw, tailw, ip, is, out, nwaves);
-  }
-  return hipGetLastError();
-}
-
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
-                                    int out_kind, int long_lps, hipStream_t st) {
+                                    int out_kind, int spw, hipStream_t st) {
   if (sp.list) return hipErrorInvalidValue;
-  const int spw = long_lps >> 8;  // bits 8+: segments per wave (0 = 64)
-  long_lps &= 0xff;
-  if (long_lps == 8 && (spw == 0 || spw == 64)) return launch_twoclass_t<8, 64>(sp, init, odd, out, out_kind, st);
-  if (long_lps == 16 && (spw == 0 || spw == 64)) return launch_twoclass_t<16, 64>(sp, init, odd, out, out_kind, st);
-  if (long_lps == 16 && spw == 32) return launch_twoclass_t<16, 32>(sp, init, odd, out, out_kind, st);
-  if (long_lps == 16 && spw == 16) return launch_twoclass_t<16, 16>(sp, init, odd, out, out_kind, st);
+  if (spw == 32) return launch_twoclass_t<16, 32>(sp, init, odd, out, out_kind, st);
+  if (spw == 16) return launch_twoclass_t<16, 16>(sp, init, odd, out, out_kind, st);
   return hipErrorInvalidValue;
 }
 
@@ -2142,7 +1749,7 @@ hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* 
 }
 
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
-                               uint32_t last_lps, uint64_t* plan_out, hipStream_t st) {
+                               uint32_t last_lps, uint64_t* plan_out, uint32_t gen, hipStream_t st) {
   if (!offsets || n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   uint32_t* cnt_part = meta + kBinMetaWords;
   uint64_t* by_part = reinterpret_cast<uint64_t*>(cnt_part + kBins * kBinStatBlocks);
@@ -2151,7 +1758,7 @@ hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, 
   hipLaunchKernelGGL(k_bin_stats, dim3(parts), dim3(kBlock), 0, st, offsets, n, cnt_part, by_part);
   if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(kBlock), 0, st, meta, cnt_part, by_part, parts, n, force_plan,
-                     last_lps, plan_out);
+                     last_lps, plan_out, gen);
   if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL(k_bin_scatter, dim3(uint32_t(tiles < 2048 ? tiles : 2048)), dim3(kBlock), 0, st,
                      offsets, n, meta, static_cast<u32x4*>(list));
@@ -2159,7 +1766,7 @@ hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, 
 }
 
 hipError_t launch_bin_plan(const uint64_t* offsets, uint64_t n, uint32_t* meta, uint32_t last_lps,
-                           uint64_t* plan_out, hipStream_t st) {
+                           uint64_t* plan_out, uint32_t gen, hipStream_t st) {
   if (!offsets || n == 0 || n > 0xFFFFFFFFull) return hipErrorInvalidValue;
   uint32_t* cnt_part = meta + kBinMetaWords;
   uint64_t* by_part = reinterpret_cast<uint64_t*>(cnt_part + kBins * kBinStatBlocks);
@@ -2168,7 +1775,7 @@ hipError_t launch_bin_plan(const uint64_t* offsets, uint64_t n, uint32_t* meta, 
   hipLaunchKernelGGL(k_bin_stats, dim3(parts), dim3(kBlock), 0, st, offsets, n, cnt_part, by_part);
   if (hipError_t e = hipGetLastError()) return e;
   hipLaunchKernelGGL(k_bin_plan, dim3(1), dim3(kBlock), 0, st, meta, cnt_part, by_part, parts, n, -1, last_lps,
-                     plan_out);
+                     plan_out, gen);
   return hipGetLastError();
 }
 
@@ -2243,29 +1850,24 @@ SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, i
 }
 
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
-                           uint8_t* status, Geometry g, uint32_t max_blocks, bool patch_wt, hipStream_t st) {
+                           uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st) {
 #define ICS_CASE(L, U, T, A)                                      \
   if (g.lps == L && g.unroll == U && g.nt == T && g.mode == A)                \
-    return launch_ipv4_t<L, U, T, A>(sp, mode, ip_ck, tcp_ck, status, max_blocks, patch_wt, st);
+    return launch_ipv4_t<L, U, T, A>(sp, mode, ip_ck, tcp_ck, status, max_blocks, st);
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return hipErrorInvalidValue;
 }
 
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                bool patch_wt, int spw, hipStream_t st) {
-  if (spw != 16 && spw != 32 && spw != 64) return hipErrorInvalidValue;
-  const uint64_t per_block = uint64_t(kBlock / 64) * uint64_t(spw);
+                                hipStream_t st) {
+  constexpr uint64_t kSpw = 32;  // datagrams per wave (measured best over 16 / 32 / 64)
+  const uint64_t per_block = uint64_t(kBlock / 64) * kSpw;
   const uint64_t blocks = (sp.n + per_block - 1) / per_block;
   if (sp.list || blocks == 0 || blocks > (uint64_t(1) << 24)) return hipErrorInvalidValue;
-#define ICS_V4TWO(W)                                                                                               \
-  hipLaunchKernelGGL(k_ipv4_twoclass<W>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes), \
-                     sp.offsets, sp.stride, sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, int(patch_wt),          \
-                     static_cast<const uint8_t*>(sp.zero16))
-  if (spw == 16) ICS_V4TWO(16);
-  else if (spw == 32) ICS_V4TWO(32);
-  else ICS_V4TWO(64);
-#undef ICS_V4TWO
+  hipLaunchKernelGGL(k_ipv4_twoclass<kSpw>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes),
+                     sp.offsets, sp.stride, sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status,
+                     static_cast<const uint8_t*>(sp.zero16));
   return hipGetLastError();
 }
 

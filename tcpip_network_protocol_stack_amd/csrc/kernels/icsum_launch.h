@@ -13,7 +13,7 @@ struct Geometry {
   int lps;
   int unroll;
   bool nt;   // non-temporal loads
-  int mode;  // chunk grid: 0 16-byte + boundary slot, 1 128-byte line, 2 16-byte all masked
+  int mode;  // chunk grid: 0 16-byte + boundary slot, 2 16-byte all masked, 3 128-byte line, primed boundaries
   int segs = 1;  // > 1: small-segment kernel, SEGS segments per lane group in flight
 };
 
@@ -72,16 +72,18 @@ constexpr size_t kBinMetaBytesTotal = kBinMetaWords * 4 + kBins * kBinStatBlocks
 // batch in 16-lane groups, 3 whole batch through the small-segment body (tests); last_lps: lanes per segment of the last
 // bin's launch (its wave count enters the plan's cost model)
 // plan_out (nullable, device-visible page-locked host memory): the plan
-// kernel stores the plan, n and two mix shares there for the host's plan
-// cache (k_bin_plan: plan bits 0-3, <= 144-byte segments in sixteenths 4-7,
-// n 8-39, bytes in segments over 1920 bytes in sixteenths 40-43)
+// kernel stores its plan word there for the host's plan cache (k_bin_plan:
+// plan bits 0-3, <= 144-byte segments in sixteenths 4-7, n 8-39, bytes in
+// segments over 1920 bytes in sixteenths 40-43, mean length 44-55, `gen`
+// 56-63: the cache slot's generation, so the host trusts only the word its
+// own request produced)
 hipError_t launch_bin_segments(const uint64_t* offsets, uint64_t n, void* list, uint32_t* meta, int force_plan,
-                               uint32_t last_lps, uint64_t* plan_out, hipStream_t st);
+                               uint32_t last_lps, uint64_t* plan_out, uint32_t gen, hipStream_t st);
 // k_bin_plan's plans: the whole-batch ones and the split plan
 constexpr uint32_t kPlanWholeBatch = 0, kPlanSplitBins = 1, kPlanWholeBatch16 = 2, kPlanWholeBatchSmall = 3;
 // the stats + plan passes alone (no bin lists): a re-plan for the plan cache
 hipError_t launch_bin_plan(const uint64_t* offsets, uint64_t n, uint32_t* meta, uint32_t last_lps,
-                           uint64_t* plan_out, hipStream_t st);
+                           uint64_t* plan_out, uint32_t gen, hipStream_t st);
 Geometry bin_geometry(int bin);
 // bins 0..kBins-2 in one launch (sp = bin_spec(whole, list, meta, 0)),
 // blocks_per_bin blocks striding over each bin
@@ -93,18 +95,10 @@ SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, i
 // out_kind 0: u16 value(), 1: u32 raw sum
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st);
-// Flat dispatch of a packed offsets batch (n < 2^32 - 1): k_checksum_flat
-// (nwaves waves, each an equal share of the batch's 8 KiB tiles) then
-// k_flat_finish.  accw: nwaves u32 that are zero on entry (and left zero),
-// tailw: nwaves u32 of scratch
-hipError_t launch_checksum_flat(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
-                                int out_kind, uint32_t* accw, uint32_t* tailw, uint32_t nwaves, hipStream_t st);
 // Two-class launch (k_checksum_twoclass): short segments (<= 4 chunks) one
-// per lane, long ones long_lps (8 or 16) lanes each, one wave per 64
-// segments; long_lps | (spw << 8) selects 32 or 16 segments per wave (16-lane
-// long groups only)
+// per lane, long ones 16 lanes each; spw (16 or 32) segments per wave
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
-                                    int out_kind, int long_lps, hipStream_t st);
+                                    int out_kind, int spw, hipStream_t st);
 // Dense fixed-stride batches (stride == seg_len in {32, 64, 128}, 16-byte
 // aligned bytes, no parity array): k_checksum_dense, SEGS segments per lane
 // group in flight (segs in {1, 2, 4, 8}; not every (seg_len, segs) pair exists)
@@ -115,14 +109,12 @@ hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
 void set_xcd_remap(uint32_t run_log2);  // log2 XCD run length (default 10 = 1024 blocks), 0: hardware order
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
-// patch_wt: PATCH-mode field stores write-through (sc1) instead of write-back
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
-                           uint8_t* status, Geometry g, uint32_t max_blocks, bool patch_wt, hipStream_t st);
+                           uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
 // fused IPv4 + TCP for receive mixes: datagrams of <= 64 bytes one per lane,
-// the rest 16 lanes each (k_ipv4_twoclass, one wave per spw = 16, 32 or 64
-// datagrams)
+// the rest 16 lanes each (k_ipv4_twoclass, one wave per 32 datagrams)
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                bool patch_wt, int spw, hipStream_t st);
+                                hipStream_t st);
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg

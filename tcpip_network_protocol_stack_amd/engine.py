@@ -59,6 +59,15 @@ class Engine:
         (ics_set_binning)."""
         self._check(self.lib.ics_set_binning(self.ctx, int(mode)))
 
+    def dispatch_info(self):
+        """ics_dispatch_info: {'plan_hits', 'plan_misses', 'plan_requests',
+        'kernel' (name of the last call's main launch), 'lps', 'unroll', 'plan'}."""
+        d = _lib.DispatchInfo()
+        self._check(self.lib.ics_dispatch_info(self.ctx, ctypes.byref(d)))
+        return {"plan_hits": d.plan_hits, "plan_misses": d.plan_misses, "plan_requests": d.plan_requests,
+                "kernel": _lib.KERNELS.get(d.last_kernel), "lps": d.last_lps, "unroll": d.last_unroll,
+                "plan": d.last_plan}
+
     def close(self):
         if self.ctx:
             self.lib.ics_destroy(self.ctx)

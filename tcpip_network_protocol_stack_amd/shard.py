@@ -3,8 +3,8 @@
 Segments are independent and no segment spans GPUs, so the batch splits into
 contiguous index ranges, one per rank (one process per GPU), with no data-path
 collective: every GPU reads only its own HBM shard and writes its own outputs.
-The only cross-rank traffic is timing (barrier + max) and, optionally, the
-gather of the u16 outputs.  Fixed-stride batches split by segment count;
+The only cross-rank traffic is timing (barrier + max, over gloo on the host)
+and, in the tests, the gather of the u16 outputs.  Fixed-stride batches split by segment count;
 mixed-length batches split by bytes (cut at the prefix sums of the lengths) so
 every GPU streams about the same number of bytes.
 """
@@ -52,12 +52,14 @@ def offsets_shard(offsets, rank, world):
     return Shard(rank, i0, i1 - i0, b0, int(offsets[i1]) - b0)
 
 
-def max_over_ranks(value, dist=None, device=None):
-    """MAX of a float over all ranks (the timing reduction bench.py reports)."""
+def max_over_ranks(value, dist=None):
+    """MAX of a float over all ranks (the timing reduction bench.py reports),
+    over the process group's own backend on a host tensor (bench.py's group
+    is gloo: timing needs no device collective)."""
     if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
         return float(value)
     import torch
 
-    t = torch.tensor([float(value)], dtype=torch.float64, device=device)
+    t = torch.tensor([float(value)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

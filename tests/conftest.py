@@ -29,6 +29,33 @@ def orc():
     return oracle
 
 
+def engine_with(force=None, debug=False):
+    """Generator: an Engine created with the ICSUM_FORCE test hook set to
+    `force` ({key: value}: lps, unroll, mode, segs, bin, bin_min, bin_plan,
+    bin_blocks, last_bin_lps, last_bin_blocks, dense_segs, twoclass,
+    wrap_passes, xcd_remap — INTEGRATION.md §6), read once at ics_create."""
+    import torch
+
+    from tcpip_network_protocol_stack_amd.engine import Engine
+
+    old = os.environ.pop("ICSUM_FORCE", None)
+    if force:
+        os.environ["ICSUM_FORCE"] = ",".join(f"{k}={v}" for k, v in force.items())
+    try:
+        eng = Engine(0, debug=debug)
+    finally:
+        os.environ.pop("ICSUM_FORCE", None)
+        if old is not None:
+            os.environ["ICSUM_FORCE"] = old
+    yield eng
+    torch.cuda.synchronize()
+    eng.close()
+
+
+def force_id(force):
+    return "-".join(f"{k}{v}" for k, v in force.items()) or "auto"
+
+
 @pytest.fixture(scope="session")
 def engine():
     import torch

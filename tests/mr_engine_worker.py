@@ -1,8 +1,15 @@
 """Worker of tests/test_gpu_multirank.py (one process per rank; not a test
-module).  Rank r of WORLD_SIZE joins a gloo group, runs ITS contiguous shard
-of BASELINE config 0 (1 M x 1500 B, pseudo-header inits) through the engine
-(libicsum.so) on the GPU, and rank 0 gathers the u16 outputs in rank order
-and prints their SHA-256."""
+module).  Rank r of WORLD_SIZE joins a gloo group, runs ITS shard of a
+BASELINE configuration through the engine (libicsum.so) on the GPU, and rank
+0 gathers the u16 outputs in rank order and prints their SHA-256.
+
+ICSUM_MR_CONFIG selects the configuration (tests/golden/configs.json):
+  "0": 1 M x 1500 B, contiguous shards (shard.fixed_stride_shard)
+  "5": 8 M x 9000 B (75.5 GB), contiguous shards
+  "4": 1 M mixed 64 B-64 KiB packed offsets, byte-balanced shards
+       (shard.offsets_shard: cut at the prefix sums of the lengths)
+Every config uses pseudo-header inits; every rank's bytes are generated on
+its own GPU from the spec stream at its shard's global offset."""
 import hashlib
 import json
 import os
@@ -18,28 +25,43 @@ def main():
     import torch.distributed as dist
 
     from tcpip_network_protocol_stack_amd import shard
-    from tcpip_network_protocol_stack_amd.engine import Engine
+    from tcpip_network_protocol_stack_amd.engine import Engine, mixed_offsets
 
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        g = json.load(f)[os.environ.get("ICSUM_MR_CONFIG", "0")]
     dist.init_process_group("gloo")
-    dev = torch.cuda.device_count()
-    eng = Engine(rank % dev)  # ranks share the card on a one-GPU box
-    n, L, seed = 1 << 20, 1500, 0x10710000
-    sh = shard.fixed_stride_shard(n, L, L, rank, world)
-    d = torch.device("cuda", rank % dev)
-    data = torch.empty(sh.nbytes, dtype=torch.uint8, device=d)
-    eng.fill_bytes(data, seed, pos0=sh.byte0)
-    init = eng.pseudo_inits(sh.n, seed, seg_len=L, index0=sh.index0)
-    out = eng.checksum_batch(data, n=sh.n, stride=L, seg_len=L, init=init)
+    ndev = torch.cuda.device_count()
+    d = torch.device("cuda", rank % ndev)  # ranks share the card on a one-GPU box
+    eng = Engine(rank % ndev)
+    n, seed = g["n"], g["seed"]
+    if "stride" in g:
+        L = g["seg_len"]
+        sh = shard.fixed_stride_shard(n, g["stride"], L, rank, world)
+        data = torch.empty(sh.nbytes, dtype=torch.uint8, device=d)
+        eng.fill_bytes(data, seed, pos0=sh.byte0)
+        init = eng.pseudo_inits(sh.n, seed, seg_len=L, index0=sh.index0)
+        out = eng.checksum_batch(data, n=sh.n, stride=g["stride"], seg_len=L, init=init)
+    else:
+        off = mixed_offsets(n, seed)
+        sh = shard.offsets_shard(off, rank, world)
+        sub = (off[sh.index0:sh.index0 + sh.n + 1] - np.uint64(sh.byte0)).view(np.int64)
+        doff = torch.from_numpy(sub.copy()).to(d)
+        data = torch.empty(sh.nbytes, dtype=torch.uint8, device=d)
+        eng.fill_bytes(data, seed, pos0=sh.byte0)
+        init = eng.pseudo_inits(sh.n, seed, offsets=doff, index0=sh.index0)
+        out = eng.checksum_batch(data, offsets=doff, init=init)
     torch.cuda.synchronize(d)
     mine = out.cpu().numpy().view(np.uint16).tobytes()
+    del data, init, out
+    torch.cuda.empty_cache()
     parts = [None] * world
-    dist.all_gather_object(parts, (sh.index0, sh.n, mine))
+    dist.all_gather_object(parts, (sh.index0, sh.n, sh.nbytes, mine))
     if rank == 0:
         parts.sort()
-        whole = b"".join(p[2] for p in parts)
+        whole = b"".join(p[3] for p in parts)
         print(json.dumps({"sha256": hashlib.sha256(whole).hexdigest(), "n": sum(p[1] for p in parts),
-                          "shards": [[p[0], p[1]] for p in parts]}), flush=True)
+                          "shards": [[p[0], p[1], p[2]] for p in parts]}), flush=True)
     eng.close()
     dist.destroy_process_group()
 

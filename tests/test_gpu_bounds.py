@@ -128,28 +128,19 @@ def test_non_monotone_offsets_are_reported(dbg, engine):
         dbg.ipv4_tcp_batch(d, 1, offsets=do)
 
 
-@pytest.mark.parametrize("env", [{"ICSUM_LPS": "1", "ICSUM_UNROLL": "4", "ICSUM_MODE": "4"},
-                                 {"ICSUM_TWOCLASS": str(16 | 16 << 8), "ICSUM_V4_SPW": "16"},
-                                 {"ICSUM_TWOCLASS": "16", "ICSUM_V4_SPW": "64"},
-                                 {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "37"}],
-                         ids=["tiny", "twoclass16", "twoclass64", "flat"])
-def test_round2_dispatches_clean_and_identical(engine, env):
-    # the round-2 kernels (one lane per segment, the two-class launches, the
-    # flat dispatch) under the bounds-checked build: clean, and equal to the
-    # release library's default dispatch, on ACK/MTU mixes of segments and of
-    # raw IPv4 datagrams
-    import os
-
+@pytest.mark.parametrize("force", [{"lps": 1, "unroll": 4, "mode": 4}, {"twoclass": 16}, {"twoclass": 32}],
+                         ids=["tiny", "twoclass16", "twoclass32"])
+def test_round2_dispatches_clean_and_identical(engine, force):
+    # the round-2 kernels (one lane per segment, the two-class launches)
+    # under the bounds-checked build: clean, and equal to the release
+    # library's default dispatch, on ACK/MTU mixes of segments and of raw
+    # IPv4 datagrams
     import torch
 
-    from tcpip_network_protocol_stack_amd.engine import Engine
+    from conftest import engine_with
 
-    os.environ.update(env)
-    try:
-        dbg = Engine(0, debug=True)
-    finally:
-        for k in env:
-            del os.environ[k]
+    gen = engine_with(force, debug=True)
+    dbg = next(gen)
     try:
         rng = np.random.default_rng(0x2B)
         n = 30_000

@@ -1,8 +1,15 @@
 """GPU: the N > 1 path through the ENGINE (not the oracle stand-in of
-tests/test_multirank.py): two processes on one card (gloo), each
-checksumming its shard.fixed_stride_shard of BASELINE config 0 through
-libicsum.so; the rank-ordered concatenation of their outputs must equal the
-reference's SHA-256 digest of the whole batch (tests/golden/configs.json["0"])."""
+tests/test_multirank.py): W processes on one card (gloo), each checksumming
+its shard of a BASELINE configuration through libicsum.so; the rank-ordered
+concatenation of their outputs must equal the reference's SHA-256 digest of
+the whole batch (tests/golden/configs.json).
+
+  config 0 (1 M x 1500 B) in 2 and 3 contiguous shards;
+  config 5 (8 M x 9000 B, 75.5 GB) in 8 contiguous shards of ~9.4 GB — the
+    8-way split BASELINE names, eight engine processes on one card;
+  config 4 (1 M mixed 64 B-64 KiB) in 2 and 3 byte-balanced shards of its
+    packed offsets (cut by the prefix sum of L_i), each rank's
+    byte count within one segment of an equal share."""
 import json
 import os
 import socket
@@ -22,28 +29,38 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3])
-def test_engine_shards_concatenate_to_reference_digest(world):
-    g = golden("configs.json")["0"]
+def _run(config, world, timeout):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world),
-                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), ICSUM_MR_CONFIG=config)
         procs.append(subprocess.Popen([sys.executable, WORKER], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.PIPE, text=True))
     outs = []
-    for p in procs:
-        try:
-            o, e = p.communicate(timeout=100)
-        except subprocess.TimeoutExpired:
-            for q in procs:
-                q.kill()
-            raise
-        outs.append((p.returncode, o, e))
+    try:
+        for p in procs:
+            o, e = p.communicate(timeout=timeout)
+            outs.append((p.returncode, o, e))
+    except subprocess.TimeoutExpired:
+        for q in procs:
+            q.kill()
+        raise
     assert all(rc == 0 for rc, _, _ in outs), [e[-1500:] for _, _, e in outs]
-    line = json.loads([l for l in outs[0][1].splitlines() if l.startswith("{")][-1])
+    return json.loads([l for l in outs[0][1].splitlines() if l.startswith("{")][-1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("config,world", [("0", 2), ("0", 3), ("5", 8), ("4", 2), ("4", 3)])
+def test_engine_shards_concatenate_to_reference_digest(config, world):
+    g = golden("configs.json")[config]
+    line = _run(config, world, timeout=110)
     assert line["n"] == g["n"]
-    assert line["shards"][0][0] == 0 and sum(s[1] for s in line["shards"]) == g["n"]
+    shards = line["shards"]
+    assert len(shards) == world and shards[0][0] == 0
+    assert all(a[0] + a[1] == b[0] for a, b in zip(shards, shards[1:]))  # contiguous, in order
     assert line["sha256"] == g["out_sha256"]
+    if config == "4":
+        nb = [s[2] for s in shards]
+        ideal = sum(nb) / world
+        assert all(abs(b - ideal) < 65536 for b in nb), nb  # each within one segment (< 64 KiB) of an equal share

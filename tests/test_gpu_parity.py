@@ -9,24 +9,19 @@ import os
 import numpy as np
 import pytest
 
-from conftest import golden
+from conftest import engine_with, force_id, golden
 from helpers import kat_cases, pack_contiguous, wires
 
 pytestmark = pytest.mark.gpu
 
-# every instantiated (LPS, UNROLL, MODE) with NT loads — keep in sync with
-# ICS_GEOMETRIES in icsum_kernels.hip (MODE 0: 16-byte grid + boundary slot,
-# 1: 128-byte-line grid, 2: 16-byte grid fully masked)
-GEOMETRIES = [(1, 4, 0), (1, 8, 0), (2, 4, 0), (4, 1, 0), (4, 2, 0), (8, 2, 0), (8, 4, 0), (16, 4, 0),
-              (16, 6, 0), (16, 8, 0), (32, 3, 0), (32, 4, 0), (64, 2, 0), (64, 3, 0), (64, 4, 0),
-              (64, 8, 0), (8, 4, 1), (16, 4, 1), (16, 6, 1), (16, 8, 1), (32, 3, 1), (32, 4, 1),
-              (64, 4, 1), (64, 8, 1), (1, 4, 2), (1, 8, 2), (2, 4, 2), (4, 1, 2), (4, 2, 2), (8, 1, 2),
-              (8, 2, 2), (16, 2, 2), (16, 8, 3), (32, 4, 3), (64, 8, 3), (16, 4, 3), (32, 8, 3),
-              (16, 6, 3), (32, 3, 3), (8, 8, 3), (16, 5, 3),
-              (1, 4, 4)]  # MODE 4: k_checksum_tiny, one lane per segment
+# every instantiated (LPS, UNROLL, MODE) of k_checksum the dispatch can reach —
+# keep in sync with ICS_GEOMETRIES in icsum_kernels.hip (MODE 2: 16-byte grid
+# fully masked, 3: 128-byte-line grid with primed boundary loads) — plus MODE
+# 4, k_checksum_tiny (one lane per segment)
+GEOMETRIES = [(4, 1, 2), (4, 2, 2), (8, 2, 2), (8, 8, 3), (16, 4, 3), (16, 5, 3), (16, 6, 3), (16, 8, 3),
+              (32, 8, 3), (64, 8, 3), (1, 4, 4)]
 # small-segment kernel (k_checksum_small): (LPS, UNROLL, MODE unused, SEGS) — ICS_SMALL_GEOMETRIES
-SMALL_GEOMETRIES = [(4, 1, 0, 2), (4, 1, 0, 4), (4, 1, 0, 8), (4, 2, 0, 2), (4, 2, 0, 4), (8, 1, 0, 4),
-                    (8, 2, 0, 2), (8, 2, 0, 4), (16, 2, 0, 2)]
+SMALL_GEOMETRIES = [(4, 1, 0, 2), (4, 2, 0, 2), (8, 2, 0, 2)]
 
 
 _SIGNED = {np.dtype(np.uint16): np.int16, np.dtype(np.uint32): np.int32, np.dtype(np.uint64): np.int64}
@@ -59,49 +54,50 @@ def _sha(a):
 @pytest.fixture(scope="module", params=GEOMETRIES + SMALL_GEOMETRIES,
                 ids=lambda g: f"lps{g[0]}x{g[1]}m{g[2]}" + (f"s{g[3]}" if len(g) > 3 else ""))
 def geo_engine(request):
-    """An engine per lane-group geometry (forced through ICSUM_LPS/UNROLL/MODE/SEGS)."""
-    env = dict(zip(("ICSUM_LPS", "ICSUM_UNROLL", "ICSUM_MODE", "ICSUM_SEGS"), map(str, request.param)))
-    yield from _engine_with(env)
-
-
-def _engine_with(env):
-    """An Engine created with the ICSUM_* tuning variables `env` set (the
-    context reads them once, at creation)."""
-    import torch
-
-    from tcpip_network_protocol_stack_amd.engine import Engine
-
-    os.environ.update(env)
-    try:
-        eng = Engine(0)
-    finally:
-        for k in env:
-            del os.environ[k]
+    """An engine per lane-group geometry (forced through the ICSUM_FORCE hook)."""
+    force = dict(zip(("lps", "unroll", "mode", "segs"), request.param))
+    if len(request.param) == 3:
+        del force["segs"]
+    gen = _engine_with(force)
+    eng = next(gen)
+    eng.forced = request.param
     yield eng
-    torch.cuda.synchronize()
-    eng.close()
+    next(gen, None)
 
 
-# length binning of offsets batches: forced split into bins (PLAN1) or whole
-# batch through the last bin's launch (PLAN0), the on-device plan, tiny grids
-# (many ticketed runs per block), and ICSUM_BIN=0 (single-geometry dispatch)
-BIN_ENVS = [{"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "1"},
-            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "1", "ICSUM_BIN_BLOCKS": "3"},
-            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "0", "ICSUM_BIN_BLOCKS": "5"},
+def _assert_forced(eng):
+    """the forced geometry is the one that ran (an uninstantiated shape would
+    silently fall back to the default and test nothing new)"""
+    info = eng.dispatch_info()
+    lps, unroll, mode = eng.forced[:3]
+    kernel = "tiny" if mode == 4 else ("small" if len(eng.forced) > 3 else "checksum")
+    assert (info["kernel"], info["lps"], info["unroll"]) == (kernel, lps, unroll), (info, eng.forced)
+
+
+def _engine_with(force):
+    yield from engine_with(force)
+
+
+# length binning of offsets batches: forced split into bins (plan 1) or whole
+# batch through the last bin's launch (plan 0), the on-device plan, tiny grids
+# (many ticketed runs per block), and bin=0 (single-geometry dispatch)
+BIN_ENVS = [{"bin": 1, "bin_plan": 1},
+            {"bin": 1, "bin_plan": 1, "bin_blocks": 3},
+            {"bin": 1, "bin_plan": 0, "bin_blocks": 5},
             # the 32-lane last-bin launch (auto above 1 M segments) under both plans
-            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "0", "ICSUM_LAST_BIN_LPS": "32"},
-            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "1", "ICSUM_LAST_BIN_LPS": "32"},
+            {"bin": 1, "bin_plan": 0, "last_bin_lps": 32},
+            {"bin": 1, "bin_plan": 1, "last_bin_lps": 32},
             # the whole batch in 16-lane groups from the last bin's launch
-            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "2"},
-            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "2", "ICSUM_LAST_BIN_LPS": "32", "ICSUM_LAST_BIN_BLOCKS": "7"},
+            {"bin": 1, "bin_plan": 2},
+            {"bin": 1, "bin_plan": 2, "last_bin_lps": 32, "last_bin_blocks": 7},
             # ... or through the small-segment body
-            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "3"},
-            {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "3", "ICSUM_LAST_BIN_LPS": "32", "ICSUM_LAST_BIN_BLOCKS": "5"},
-            {"ICSUM_BIN": "1"},
-            {"ICSUM_BIN": "0"}]
+            {"bin": 1, "bin_plan": 3},
+            {"bin": 1, "bin_plan": 3, "last_bin_lps": 32, "last_bin_blocks": 5},
+            {"bin": 1},
+            {"bin": 0}]
 
 
-@pytest.fixture(scope="module", params=BIN_ENVS, ids=lambda e: "-".join(f"{k[6:]}{v}" for k, v in e.items()))
+@pytest.fixture(scope="module", params=BIN_ENVS, ids=force_id)
 def bin_engine(request):
     yield from _engine_with(request.param)
 
@@ -116,6 +112,7 @@ def test_kat_all_geometries(geo_engine):
         init = np.array([c[0] for c in cases], dtype=np.uint32)
         out = geo_engine.checksum_batch(_t(buf), offsets=_t(off), init=_t(init))
         assert _u16(out).tolist() == want, f"lead={lead}"
+        _assert_forced(geo_engine)
 
 
 def test_kat_fill_and_wrap(engine):
@@ -836,7 +833,7 @@ def test_xcd_block_order_is_a_permutation(run, orc):
     restored afterwards."""
     import torch
 
-    gen = _engine_with({"ICSUM_XCD_REMAP": str(run)})
+    gen = _engine_with({"xcd_remap": run})
     eng = next(gen)
     try:
         rng = np.random.default_rng(run + 7)
@@ -859,7 +856,7 @@ def test_xcd_block_order_is_a_permutation(run, orc):
     finally:
         torch.cuda.synchronize()
         eng.close()
-        next(_engine_with({"ICSUM_XCD_REMAP": "10"})).close()  # restore the default order
+        next(_engine_with({"xcd_remap": 10})).close()  # restore the default order
 
 
 @pytest.mark.parametrize("segs", [1, 2, 4, 8])
@@ -868,7 +865,7 @@ def test_dense_fixed_stride_kernel(segs, orc):
     parity array) at every SEGS: u16 values and raw u32 sums, with and without
     inits, on batch sizes that leave partial waves and blocks; unsupported
     (seg_len, segs) pairs fall back to the general kernels and must agree too."""
-    gen = _engine_with({"ICSUM_DENSE_SEGS": str(segs)})
+    gen = _engine_with({"dense_segs": segs})
     eng = next(gen)
     try:
         rng = np.random.default_rng(100 + segs)

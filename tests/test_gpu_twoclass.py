@@ -1,36 +1,25 @@
-"""GPU parity of the alternative dispatches of packed offsets batches — the
-flat dispatch (k_checksum_flat + k_flat_finish, forced with ICSUM_FLAT=1: one
-byte stream cut at the offsets) and the two-class launch (ICSUM_TWOCLASS) —
-against the golden KATs and the oracle.
-
-Wave counts from 1 (one share: every segment finishes inside it) to a few
-dozen (segments crossing share boundaries, finished through the per-wave
-slots) and the default (more waves than tiles on small batches: empty
-shares).  Bar: bit-exact."""
+"""GPU parity of the two-class launches of packed offsets batches
+(k_checksum_twoclass and k_ipv4_twoclass: short segments one per lane, long
+ones 16 lanes each from a per-wave LDS list), forced on every offsets batch
+with the `twoclass` test hook at both wave loads AUTO uses (16 and 32
+segments per wave), against the golden KATs and the oracle.  AUTO reaches
+them through a cached plan of a short-heavy mix; the last test checks that
+path.  Bar: bit-exact."""
 import numpy as np
 import pytest
 
 from helpers import kat_cases, pack_contiguous
-from test_gpu_parity import _engine_with, _t, _u16, _u32
+from conftest import engine_with, force_id
+from test_gpu_parity import _t, _u16, _u32
 
 pytestmark = pytest.mark.gpu
 
-FLAT_ENVS = [{"ICSUM_FLAT": "1"},
-             {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "1"},
-             {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "7"},
-             {"ICSUM_FLAT": "1", "ICSUM_FLAT_WAVES": "97"},
-             # the two-class launch (k_checksum_twoclass: short segments one per
-             # lane, long ones 16 / 8 lanes each) forced on every offsets batch;
-             # AUTO uses it for short-heavy mixes
-             {"ICSUM_TWOCLASS": "16"},
-             {"ICSUM_TWOCLASS": "8"},
-             {"ICSUM_TWOCLASS": str(16 | 32 << 8)},  # 32 segments per wave
-             {"ICSUM_TWOCLASS": str(16 | 16 << 8)}]  # 16 segments per wave
+TWO_FORCE = [{"twoclass": 16}, {"twoclass": 32}]
 
 
-@pytest.fixture(scope="module", params=FLAT_ENVS, ids=lambda e: "-".join(f"{k[6:]}{v}" for k, v in e.items()))
-def flat_engine(request):
-    yield from _engine_with(request.param)
+@pytest.fixture(scope="module", params=TWO_FORCE, ids=force_id)
+def two_csum(request):
+    yield from engine_with(request.param)
 
 
 def _sentinel(n, dtype):
@@ -55,7 +44,7 @@ def _check(eng, orc, buf, off, rng, tag=""):
     assert (_u32(sums) == orc.sum_batch(buf, n, offsets=off, init=init, odd=odd)).all(), tag
 
 
-def test_flat_kats(flat_engine):
+def test_twoclass_kats(two_csum):
     # every KAT (lengths 0-257, inits, whole segments, the 131076-byte 0xFF
     # wrap) at four alignments of the first byte
     cases = kat_cases({"rfc1071", "len", "init", "whole", "fill"})
@@ -63,12 +52,12 @@ def test_flat_kats(flat_engine):
     init = np.array([c[0] for c in cases], dtype=np.uint32)
     for lead in (0, 1, 6, 15):
         buf, off = pack_contiguous(segs, lead)
-        out = flat_engine.checksum_batch(_t(buf), offsets=_t(off), init=_t(init),
+        out = two_csum.checksum_batch(_t(buf), offsets=_t(off), init=_t(init),
                                          out=_sentinel(len(cases), __import__("torch").int16))
         assert _u16(out).tolist() == [c[2] for c in cases], f"lead={lead}"
 
 
-def test_flat_split_pieces_chain(flat_engine):
+def test_twoclass_split_pieces_chain(two_csum):
     # add(vector<string>) with parity carried across pieces (checksum.h:44-59)
     cases = kat_cases({"split"})
     maxp = max(len(p) for _, p, _, _ in cases)
@@ -77,12 +66,12 @@ def test_flat_split_pieces_chain(flat_engine):
     for k in range(maxp):
         segs = [p[k] if k < len(p) else b"" for _, p, _, _ in cases]
         buf, off = pack_contiguous(segs, 1)
-        sums = _u32(flat_engine.sum_batch(_t(buf), offsets=_t(off), init=_t(sums), odd=_t(odd))).copy()
+        sums = _u32(two_csum.sum_batch(_t(buf), offsets=_t(off), init=_t(sums), odd=_t(odd))).copy()
         odd ^= np.array([len(x) & 1 for x in segs], dtype=np.uint8)
-    assert _u16(flat_engine.fold_batch(_t(sums))).tolist() == [c[2] for c in cases]
+    assert _u16(two_csum.fold_batch(_t(sums))).tolist() == [c[2] for c in cases]
 
 
-def test_flat_mixed(flat_engine, orc):
+def test_twoclass_mixed(two_csum, orc):
     # lengths over every bin, zero-length segments, a few long ones
     rng = np.random.default_rng(0xF1A7)
     n = 6000
@@ -93,10 +82,10 @@ def test_flat_mixed(flat_engine, orc):
     segs = [rng.integers(0, 256, int(L), dtype=np.uint8).tobytes() for L in lens]
     for lead in (0, 5, 15):
         buf, off = pack_contiguous(segs, lead)
-        _check(flat_engine, orc, buf, off, rng, f"lead={lead}")
+        _check(two_csum, orc, buf, off, rng, f"lead={lead}")
 
 
-def test_flat_tiny_segments(flat_engine, orc):
+def test_twoclass_tiny_segments(two_csum, orc):
     # 0-20 byte segments: several cuts inside one 16-byte chunk, more than 64
     # cuts per tile (the cut loop's further rounds)
     rng = np.random.default_rng(0x7111)
@@ -106,10 +95,10 @@ def test_flat_tiny_segments(flat_engine, orc):
     off[1:] = np.cumsum(lens)
     off += 3
     buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
-    _check(flat_engine, orc, buf, off, rng)
+    _check(two_csum, orc, buf, off, rng)
 
 
-def test_flat_long_segments(flat_engine, orc):
+def test_twoclass_long_segments(two_csum, orc):
     # segments far longer than a share (3 MiB, 1 MiB + 1) between short ones:
     # their pieces come from many waves
     rng = np.random.default_rng(0x10E6)
@@ -121,12 +110,12 @@ def test_flat_long_segments(flat_engine, orc):
     off[1:] = np.cumsum(lens)
     off += 9
     buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
-    _check(flat_engine, orc, buf, off, rng)
+    _check(two_csum, orc, buf, off, rng)
 
 
 @pytest.mark.parametrize("lens", [[0] * 100, [0], [1], [15], [16], [17], [100_000], [0, 0, 5, 0, 0],
                                   [8192] * 3, [8191, 1, 8192, 0]])
-def test_flat_edge_batches(flat_engine, orc, lens):
+def test_twoclass_edge_batches(two_csum, orc, lens):
     # all-empty batches (every output = the folded init), single segments,
     # segments that end exactly on tile boundaries
     rng = np.random.default_rng(len(lens) * 7 + sum(lens))
@@ -135,10 +124,10 @@ def test_flat_edge_batches(flat_engine, orc, lens):
         off[1:] = np.cumsum(lens)
         off += lead
         buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
-        _check(flat_engine, orc, buf, off, rng, f"lead={lead}")
+        _check(two_csum, orc, buf, off, rng, f"lead={lead}")
 
 
-def test_flat_bimodal_large(flat_engine, orc):
+def test_twoclass_bimodal_large(two_csum, orc):
     # ACK-sized + MSS-sized segments interleaved (a TCP receive mix)
     rng = np.random.default_rng(0xACC)
     n = 150_000
@@ -147,25 +136,11 @@ def test_flat_bimodal_large(flat_engine, orc):
     off[1:] = np.cumsum(lens)
     off += 1
     buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
-    out = flat_engine.checksum_batch(_t(buf), offsets=_t(off), out=_sentinel(n, __import__("torch").int16))
+    out = two_csum.checksum_batch(_t(buf), offsets=_t(off), out=_sentinel(n, __import__("torch").int16))
     assert (_u16(out) == orc.checksum_batch(buf, n, offsets=off)).all()
 
 
-def test_flat_repeated_calls_leave_slots_clean(flat_engine, orc):
-    # the per-wave sums are left zero by k_flat_finish: the same batch twice
-    # and a different batch after it give the reference values every time
-    rng = np.random.default_rng(0x5107)
-    for rep in range(3):
-        lens = rng.integers(0, 20000, 300)
-        off = np.zeros(lens.size + 1, dtype=np.uint64)
-        off[1:] = np.cumsum(lens)
-        buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
-        for _ in range(2):
-            out = flat_engine.checksum_batch(_t(buf), offsets=_t(off))
-            assert (_u16(out) == orc.checksum_batch(buf, lens.size, offsets=off)).all(), rep
-
-
-def test_flat_config4_full_size(flat_engine):
+def test_twoclass_config4_full_size(two_csum):
     # BASELINE config 4 at full size (10.3 GB: positions past 2^31 and 2^32)
     # against the reference's digest, into a sentinel-filled output
     import hashlib
@@ -178,43 +153,26 @@ def test_flat_config4_full_size(flat_engine):
     g = golden("configs.json")["4"]
     n, seed = g["n"], g["seed"]
     off = mixed_offsets(n, seed)
-    data = flat_engine.fill_bytes(torch.empty(int(off[-1]), dtype=torch.uint8, device="cuda:0"), seed)
+    data = two_csum.fill_bytes(torch.empty(int(off[-1]), dtype=torch.uint8, device="cuda:0"), seed)
     doff = _t(off.view(np.int64))
-    init = flat_engine.pseudo_inits(n, seed, offsets=doff)
-    out = _u16(flat_engine.checksum_batch(data, offsets=doff, init=init, out=_sentinel(n, torch.int16)))
+    init = two_csum.pseudo_inits(n, seed, offsets=doff)
+    out = _u16(two_csum.checksum_batch(data, offsets=doff, init=init, out=_sentinel(n, torch.int16)))
     del data
     torch.cuda.empty_cache()
     assert out[:64].tolist() == g["out_head"]
     assert hashlib.sha256(out.tobytes()).hexdigest() == g["out_sha256"]
 
 
-def test_flat_malformed_offsets_terminate(flat_engine, orc):
-    # non-monotone offsets (a contract violation: results are undefined) must
-    # still end the call in bounded time without a fault, and leave the
-    # per-wave slots clean for the next, valid batch
-    rng = np.random.default_rng(0xBAD0)
-    n = 5000
-    off = rng.integers(0, 1 << 22, n + 1).astype(np.uint64)
-    off[-1] = 1 << 22
-    buf = rng.integers(0, 256, (1 << 22) + 16, dtype=np.uint8)
-    flat_engine.checksum_batch(_t(buf), offsets=_t(off))
-    off2 = np.sort(off)
-    off2[0] = 0
-    out = flat_engine.checksum_batch(_t(buf), offsets=_t(off2))
-    assert (_u16(out) == orc.checksum_batch(buf, n, offsets=off2)).all()
-
-
-@pytest.fixture(scope="module", params=[("16", "32"), ("16", "16"), ("16", "64"), ("1", "32")],
-                ids=lambda v: f"TWOCLASS{v[0]}-SPW{v[1]}")
+@pytest.fixture(scope="module", params=[{"twoclass": 32}, {"twoclass": 16}], ids=force_id)
 def two_engine(request):
-    yield from _engine_with({"ICSUM_TWOCLASS": request.param[0], "ICSUM_V4_SPW": request.param[1]})
+    yield from engine_with(request.param)
 
 
 @pytest.mark.parametrize("mix", ["bimodal", "ackheavy", "tricky"])
 def test_ipv4_twoclass_vs_oracle(two_engine, orc, mix):
     """Raw IPv4/TCP datagram batches through the two-class fused launch
     (k_ipv4_twoclass: <= 64-byte datagrams one per lane, the rest 16 lanes
-    each; forced with ICSUM_TWOCLASS=16, the 8-lane launch with =1): COMPUTE,
+    each, 32 datagrams per wave; forced with the twoclass hook): COMPUTE,
     VERIFY and PATCH against the oracle, patched bytes included.  "tricky"
     adds short (< 20 B), 64/65-byte edge, option-carrying and corrupted
     datagrams."""
@@ -244,3 +202,32 @@ def test_ipv4_twoclass_vs_oracle(two_engine, orc, mix):
         assert (_u16(tcp) == want[1]).all(), (mix, mode)
         assert (st.cpu().numpy() == want[2]).all(), (mix, mode)
         assert (d.cpu().numpy() == hb).all(), (mix, mode)  # PATCH wrote what the oracle wrote
+
+
+def test_auto_reaches_twoclass_from_cached_plan(engine, orc):
+    """The default dispatch: a short-heavy receive mix (3/4 ACKs among MTU
+    segments) plans on its first call and runs the two-class launches from
+    the cached plan on the next ones — checksum and fused VERIFY — with the
+    oracle's results every time."""
+    rng = np.random.default_rng(0x2C1A)
+    n = 70_000
+    lens = np.where(rng.random(n) < 0.75, 40, 1460) + rng.integers(0, 4, n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    s, ln = off[:-1].astype(np.int64), lens.astype(np.int64)
+    buf[s], buf[s + 2], buf[s + 3] = 0x45, (ln >> 8).astype(np.uint8), (ln & 255).astype(np.uint8)
+    buf[s + 9], buf[s + 32] = 6, 0x50
+    d, do = _t(buf), _t(off)
+    want = orc.checksum_batch(buf, n, offsets=off)
+    want_v = orc.ipv4_tcp_batch(buf.copy(), n, 1, offsets=off)
+    kinds = []
+    for call in range(3):
+        assert (_u16(engine.checksum_batch(d, offsets=do)) == want).all(), call
+        __import__("torch").cuda.synchronize()
+        kinds.append(engine.dispatch_info()["kernel"])
+        ip, tcp, st = engine.ipv4_tcp_batch(d, 1, offsets=do)
+        assert (_u16(ip) == want_v[0]).all() and (_u16(tcp) == want_v[1]).all(), call
+        assert (st.cpu().numpy() == want_v[2]).all(), call
+        kinds.append(engine.dispatch_info()["kernel"])
+    assert kinds[2:] == ["twoclass", "ipv4_twoclass"] * 2, kinds

@@ -52,7 +52,7 @@ def _worker(rank, port, q):
         o4 = orc.checksum_batch(d4, ms.n, offsets=off[ms.index0:ms.index0 + ms.n + 1] - off[ms.index0])
         parts4 = [None] * WORLD
         dist.all_gather_object(parts4, (ms.index0, o4.tolist(), ms.nbytes))
-        t = shard.max_over_ranks(0.25 + rank, dist, torch.device("cpu"))
+        t = shard.max_over_ranks(0.25 + rank, dist)
         if rank == 0:
             q.put((parts, parts4, t))
     finally:
