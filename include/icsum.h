@@ -199,6 +199,38 @@ int ics_tcp_wrap_headers(ics_ctx* ctx, const void* d_payloads, const uint64_t* d
                          uint64_t payload_len, uint64_t n, const ics_tcp_msg* d_msgs, void* d_hdrs,
                          uint16_t* d_ip_ck, uint16_t* d_tcp_ck, void* stream);
 
+/* ---- several batches in one launch -------------------------------------- */
+/* The receive and transmit paths hand the engine a stream of small batches —
+ * one per event-loop tick or per filled arena (the reference reads its TUN fd
+ * one datagram per call, util/tuntap/tuntap_adapter.cpp:5-21, inside the
+ * socket's event loop, util/tcp_minnow_socket/tcp_minnow_socket.h:138-164).
+ * Each launch pays a fixed ramp and drain of a few microseconds, so k such
+ * batches queued together run as ONE launch per kernel shape (batches of up
+ * to 16 per launch): results identical to k calls of ics_checksum_batch /
+ * ics_ipv4_tcp_batch on the same arguments, in any order (the batches must
+ * not overlap where PATCH writes).  Fixed-stride batches take the geometry
+ * their length picks; offsets batches take the unplanned default (no
+ * binning: call ics_checksum_batch for one large mixed batch).  The
+ * descriptor arrays are host memory, read before the call returns. */
+typedef struct ics_seg_batch {
+  const void* bytes;         /* d_bytes of ics_checksum_batch */
+  const uint64_t* offsets;   /* d_offsets (NULL: fixed stride) */
+  uint64_t stride, seg_len, n;
+  const uint32_t* init;      /* d_init (NULL = 0) */
+  uint16_t* out;             /* d_out */
+} ics_seg_batch;
+int ics_checksum_batchv(ics_ctx* ctx, const ics_seg_batch* batches, uint32_t k, void* stream);
+
+typedef struct ics_dgram_batch {
+  void* dgrams;              /* d_dgrams of ics_ipv4_tcp_batch */
+  const uint64_t* offsets;   /* d_offsets (NULL: fixed stride) */
+  uint64_t stride, dgram_len, n;
+  uint16_t* ip_ck;           /* each output may be NULL */
+  uint16_t* tcp_ck;
+  uint8_t* status;
+} ics_dgram_batch;
+int ics_ipv4_tcp_batchv(ics_ctx* ctx, const ics_dgram_batch* batches, uint32_t k, int mode, void* stream);
+
 /* ---- host-memory variants (PCIe-inclusive path) ------------------------ */
 /* Same semantics as ics_checksum_batch / ics_ipv4_tcp_batch on host
  * buffers; ics_checksum_batch_host takes segments of any length (longer than

@@ -41,6 +41,20 @@ class DispatchInfo(ctypes.Structure):
                 ("last_lps", ctypes.c_int32), ("last_unroll", ctypes.c_int32), ("last_plan", ctypes.c_int32)]
 
 
+class SegBatch(ctypes.Structure):
+    """struct ics_seg_batch (include/icsum.h): one ics_checksum_batch call's arguments."""
+    _fields_ = [("bytes", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("stride", ctypes.c_uint64),
+                ("seg_len", ctypes.c_uint64), ("n", ctypes.c_uint64), ("init", ctypes.c_void_p),
+                ("out", ctypes.c_void_p)]
+
+
+class DgramBatch(ctypes.Structure):
+    """struct ics_dgram_batch (include/icsum.h): one ics_ipv4_tcp_batch call's arguments."""
+    _fields_ = [("dgrams", ctypes.c_void_p), ("offsets", ctypes.c_void_p), ("stride", ctypes.c_uint64),
+                ("dgram_len", ctypes.c_uint64), ("n", ctypes.c_uint64), ("ip_ck", ctypes.c_void_p),
+                ("tcp_ck", ctypes.c_void_p), ("status", ctypes.c_void_p)]
+
+
 # ICS_K_* kernel ids of ics_dispatch_info_t.last_kernel
 KERNELS = {1: "checksum", 2: "small", 3: "tiny", 4: "dense", 5: "twoclass", 6: "binned", 7: "ipv4",
            8: "ipv4_twoclass", 9: "wrap", 10: "wrap_2pass", 11: "router", 12: "batchv"}
@@ -79,6 +93,8 @@ SIGNATURES = {
     "ics_memcpy_dtoh": (_int, [_p, _p, _p, ctypes.c_size_t, _p]),
     "ics_stream_synchronize": (_int, [_p, _p]),
     "ics_dispatch_info": (_int, [_p, ctypes.POINTER(DispatchInfo)]),
+    "ics_checksum_batchv": (_int, [_p, ctypes.POINTER(SegBatch), ctypes.c_uint32, _p]),
+    "ics_ipv4_tcp_batchv": (_int, [_p, ctypes.POINTER(DgramBatch), ctypes.c_uint32, _int, _p]),
     "icsw_fill_bytes": (_int, [_p, _p, _u64, _u64, _u64, _p]),
     "icsw_pseudo_inits": (_int, [_p, _p, _p, _u64, _u64, _u64, _u64, _p]),
     "icsw_ipv4_tcp_headers": (_int, [_p, _p, _u64, _u64, _u64, _u64, _u64, _p]),

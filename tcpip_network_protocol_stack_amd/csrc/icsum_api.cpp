@@ -1152,6 +1152,113 @@ int ics_tcp_wrap_headers(ics_ctx* ctx, const void* d_payloads, const uint64_t* d
   return bounds_verdict(st, ICS_OK);
 }
 
+}  // extern "C"
+
+namespace {
+// Group the batches of a multi-batch call by kernel shape and issue one
+// launch per group of up to kMaxBatchv (whose grids together stay below the
+// dispatch's work-item limit); a batch too large for that runs alone through
+// the single-batch path.
+template <typename D, typename ClassFn, typename LaunchFn, typename AloneFn>
+int run_batchv(ics_ctx* ctx, const D* b, uint32_t k, ClassFn cls_of, LaunchFn launch, AloneFn alone) {
+  constexpr uint64_t kMaxBlocks = (uint64_t(1) << 24) - 1;
+  std::vector<int> cls(k);
+  for (uint32_t j = 0; j < k; ++j) cls[j] = b[j].n ? cls_of(b[j]) : -1;
+  int last_cls = -1;
+  for (int c = 0; c <= icsum::kBvLane1; ++c) {
+    D group[icsum::kMaxBatchv];
+    int m = 0;
+    uint64_t blocks = 0;
+    auto flush = [&]() -> int {
+      if (m == 0) return ICS_OK;
+      ICS_HIP(launch(group, m, c));
+      last_cls = c;
+      m = 0;
+      blocks = 0;
+      return ICS_OK;
+    };
+    for (uint32_t j = 0; j < k; ++j) {
+      if (cls[j] != c) continue;
+      const uint64_t nb = icsum::batchv_blocks(c, b[j].n);
+      if (nb > kMaxBlocks / 4) {  // a large batch: a launch of its own, its usual path
+        if (int rc = alone(b[j])) return rc;
+        continue;
+      }
+      if (m == icsum::kMaxBatchv || blocks + nb > kMaxBlocks)
+        if (int rc = flush()) return rc;
+      group[m++] = b[j];
+      blocks += nb;
+    }
+    if (int rc = flush()) return rc;
+  }
+  if (last_cls >= 0) note(ctx, ICS_K_BATCHV, {last_cls, int(k), true, 0, 1});
+  return ICS_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int ics_checksum_batchv(ics_ctx* ctx, const ics_seg_batch* batches, uint32_t k, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (k == 0) return ICS_OK;
+  if (!batches) return fail(ICS_ERR_INVALID, "null batch array");
+  for (uint32_t j = 0; j < k; ++j)
+    if (batches[j].n && (!batches[j].bytes || !batches[j].out))
+      return fail(ICS_ERR_INVALID, "batch %u: null device buffer", j);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<icsum::BvSeg> b(k);
+  for (uint32_t j = 0; j < k; ++j)
+    b[j] = {static_cast<const uint8_t*>(batches[j].bytes), batches[j].offsets, batches[j].stride, batches[j].seg_len,
+            batches[j].n, batches[j].init, batches[j].out};
+  auto cls_of = [&](const icsum::BvSeg& x) -> int {
+    const icsum::SegSpec sp{x.bytes, x.offsets, x.stride, x.seg_len, x.n, ctx->d_zero};
+    if (!x.offsets && x.seg_len == 64 && icsum::dense_supported(sp)) return icsum::kBvDense64;
+    const icsum::Geometry g = icsum::pick_geometry(avg_len_hint(x.offsets, x.seg_len));
+    if (g.mode == icsum::kModeTiny) return icsum::kBvTiny;
+    if (g.segs > 1) return icsum::kBvSmall;
+    return g.lps >= 32 ? icsum::kBvLine64 : icsum::kBvLine16;
+  };
+  auto launch = [&](const icsum::BvSeg* g, int m, int c) {
+    return icsum::launch_checksum_batchv(g, m, c, ctx->d_zero, st);
+  };
+  auto alone = [&](const icsum::BvSeg& x) {
+    const icsum::SegSpec sp{x.bytes, x.offsets, x.stride, x.seg_len, x.n, ctx->d_zero};
+    return checksum_device(ctx, sp, x.init, nullptr, x.out, 0, st);
+  };
+  return bounds_verdict(st, run_batchv(ctx, b.data(), k, cls_of, launch, alone));
+}
+
+int ics_ipv4_tcp_batchv(ics_ctx* ctx, const ics_dgram_batch* batches, uint32_t k, int mode, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (mode < ICS_MODE_COMPUTE || mode > ICS_MODE_PATCH) return fail(ICS_ERR_INVALID, "bad mode %d", mode);
+  if (k == 0) return ICS_OK;
+  if (!batches) return fail(ICS_ERR_INVALID, "null batch array");
+  for (uint32_t j = 0; j < k; ++j)
+    if (batches[j].n && !batches[j].dgrams) return fail(ICS_ERR_INVALID, "batch %u: null datagram buffer", j);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<icsum::BvDgram> b(k);
+  for (uint32_t j = 0; j < k; ++j)
+    b[j] = {static_cast<uint8_t*>(batches[j].dgrams), batches[j].offsets, batches[j].stride, batches[j].dgram_len,
+            batches[j].n, batches[j].ip_ck, batches[j].tcp_ck, batches[j].status};
+  // the single call's unplanned choice: one lane per ACK-sized fixed-length
+  // datagram, 64-lane groups past 3.5 KB, 16-lane line grids otherwise (and
+  // for every offsets batch: mostly MTU-sized datagrams)
+  auto cls_of = [&](const icsum::BvDgram& x) -> int {
+    if (x.offsets) return icsum::kBvLine16;
+    const icsum::Geometry g = icsum::pick_geometry(x.dlen);
+    if (g.mode == icsum::kModeTiny) return icsum::kBvLane1;
+    return g.lps >= 32 ? icsum::kBvLine64 : icsum::kBvLine16;
+  };
+  auto launch = [&](const icsum::BvDgram* g, int m, int c) {
+    return icsum::launch_ipv4_batchv(g, m, c, mode, ctx->d_zero, st);
+  };
+  auto alone = [&](const icsum::BvDgram& x) {
+    return ics_ipv4_tcp_batch(ctx, x.dgrams, x.offsets, x.stride, x.dlen, x.n, mode, x.ip_ck, x.tcp_ck, x.status,
+                              stream);
+  };
+  return bounds_verdict(st, run_batchv(ctx, b.data(), k, cls_of, launch, alone));
+}
+
 int ics_tcp_wrap_headers_host(ics_ctx* ctx, const void* h_payloads, const uint64_t* h_offsets, uint64_t stride,
                               uint64_t payload_len, uint64_t n, const ics_tcp_msg* h_msgs, void* h_hdrs) {
   if (int rc = bind(ctx)) return rc;

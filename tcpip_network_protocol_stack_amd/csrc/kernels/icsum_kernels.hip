@@ -705,13 +705,14 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
 // base is aligned, the stride a multiple of 16), so byte roles never swap.
 // Measured floor for 64 MiB + 4 MiB inits + 2 MiB outputs on MI355X:
 // ≈12.4 us (tools/probe/small_probe.hip).
+// (block blk of the launch; init_step 0 reads one shared zero word)
 template <int LPS, int SEGS, bool INIT, int OUT>
-__global__ __launch_bounds__(kBlock) void k_checksum_dense(const u32x4* __restrict__ chunks,
-                                                           const uint32_t* __restrict__ init,
-                                                           void* __restrict__ out, uint64_t n) {
+__device__ __forceinline__ void checksum_dense_body(const u32x4* __restrict__ chunks, const uint32_t* __restrict__ init,
+                                                    uint32_t init_step, void* __restrict__ out, uint64_t n,
+                                                    uint32_t blk) {
   constexpr uint32_t kSegsPerWave = 64 / LPS;
   const uint32_t lane64 = threadIdx.x & 63u, lane = threadIdx.x & (LPS - 1), group = lane64 / LPS;
-  const uint64_t wave = (uint64_t(blockIdx.x) * kBlock + threadIdx.x) >> 6;
+  const uint64_t wave = (uint64_t(blk) * kBlock + threadIdx.x) >> 6;
   const uint64_t seg0 = wave * SEGS * kSegsPerWave + group;
   const uint64_t nch = n * LPS;
   u32x4 v[SEGS];
@@ -723,7 +724,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_dense(const u32x4* __restri
     ICS_CHECK16(chunks + (c < nch ? c : nch - 1), reinterpret_cast<const uint8_t*>(chunks),
                 reinterpret_cast<const uint8_t*>(chunks + nch));
     v[k] = __builtin_nontemporal_load(chunks + (c < nch ? c : nch - 1));
-    i0[k] = INIT ? init[seg < n ? seg : n - 1] : 0u;
+    i0[k] = INIT ? init[(seg < n ? seg : n - 1) * init_step] : 0u;
   }
 #pragma unroll
   for (int k = 0; k < SEGS; ++k) {
@@ -739,6 +740,13 @@ __global__ __launch_bounds__(kBlock) void k_checksum_dense(const u32x4* __restri
         static_cast<uint32_t*>(out)[seg] = sum;
     }
   }
+}
+
+template <int LPS, int SEGS, bool INIT, int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum_dense(const u32x4* __restrict__ chunks,
+                                                           const uint32_t* __restrict__ init,
+                                                           void* __restrict__ out, uint64_t n) {
+  checksum_dense_body<LPS, SEGS, INIT, OUT>(chunks, init, 1u, out, n, blockIdx.x);
 }
 
 // Bins 0..kBins-2 of a binned batch in ONE launch: nblk blocks per bin, each
@@ -1019,19 +1027,19 @@ __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, 
   }
 }
 
+// datagrams [blk * groups, ...) striding by nblk blocks (block blk of nblk:
+// a kernel of its own, or one batch's share of a multi-batch launch)
 template <int LPS, int UNROLL, bool NT, int MODE>
-__global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
-                                                     const uint64_t* __restrict__ offsets,
-                                                     uint64_t stride, uint64_t dlen, uint64_t n,
-                                                     int mode, uint16_t* __restrict__ ip_ck,
-                                                     uint16_t* __restrict__ tcp_ck,
-                                                     uint8_t* __restrict__ status, uint32_t remap,
-                                                     const uint8_t* __restrict__ zpad) {
+__device__ __forceinline__ void ipv4_body(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
+                                          uint64_t stride, uint64_t dlen, uint64_t n, int mode,
+                                          uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
+                                          uint8_t* __restrict__ status, const uint8_t* __restrict__ zpad,
+                                          uint32_t blk, uint32_t nblk) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
-  const uint64_t step = uint64_t(gridDim.x) * kGroups;
+  const uint64_t step = uint64_t(nblk) * kGroups;
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;  // zpad: 32 zero bytes
-  for (uint64_t g0 = uint64_t(block_order(remap)) * kGroups; g0 < n; g0 += step) {
+  for (uint64_t g0 = uint64_t(blk) * kGroups; g0 < n; g0 += step) {
     const uint64_t seg = g0 + threadIdx.x / LPS;
     const bool valid = seg < n;
     // offsets from a clamped index, unconditionally (a load under a divergent
@@ -1041,6 +1049,18 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
     if (!valid) e = s;
     ipv4_item<LPS, UNROLL, NT, MODE>(dg, s, e, seg, valid, lane, mode, ip_ck, tcp_ck, status, zpad, zlast);
   }
+}
+
+template <int LPS, int UNROLL, bool NT, int MODE>
+__global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
+                                                     const uint64_t* __restrict__ offsets,
+                                                     uint64_t stride, uint64_t dlen, uint64_t n,
+                                                     int mode, uint16_t* __restrict__ ip_ck,
+                                                     uint16_t* __restrict__ tcp_ck,
+                                                     uint8_t* __restrict__ status, uint32_t remap,
+                                                     const uint8_t* __restrict__ zpad) {
+  ipv4_body<LPS, UNROLL, NT, MODE>(dg, offsets, stride, dlen, n, mode, ip_ck, tcp_ck, status, zpad,
+                                   block_order(remap), gridDim.x);
 }
 
 // Two-class launch for receive mixes (ACKs among MTU datagrams): wave w
@@ -1085,6 +1105,68 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
     const uint64_t ls = lst[wv][kc][0], le = mine ? lst[wv][kc][1] : ls;
     ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[wv][kc], mine, gl, mode, ip_ck, tcp_ck, status, zpad, zlast);
   }
+}
+
+// ------------------------------------------------- multi-batch launches ---
+// The table of a multi-batch launch, by value in the kernel arguments (the
+// block offsets are scanned with scalar loads; a batch's fields are loaded
+// from the kernel-argument segment at its index — no scratch copy).
+template <typename D>
+struct BvTable {
+  D b[kMaxBatchv];
+  uint32_t block0[kMaxBatchv];  // first block of batch j (ascending; block0[0] = 0)
+  uint32_t nblk[kMaxBatchv];
+  uint32_t k;
+};
+
+// the batch that owns (logical) block blk
+template <typename D>
+__device__ __forceinline__ uint32_t bv_find(const BvTable<D>& t, uint32_t blk) {
+  uint32_t j = 0;
+#pragma unroll
+  for (uint32_t q = 1; q < uint32_t(kMaxBatchv); ++q) j += (q < t.k && blk >= t.block0[q]) ? 1u : 0u;
+  return j;
+}
+
+template <int CLS>
+__global__ __launch_bounds__(kBlock) void k_checksum_batchv(BvTable<BvSeg> t, const u32x4* __restrict__ zero16,
+                                                            uint32_t remap) {
+  const uint32_t blk = block_order(remap);  // XCD runs over the whole grid, batches in turn
+  const uint32_t j = bv_find(t, blk);
+  const BvSeg& b = t.b[j];
+  const uint32_t lb = blk - t.block0[j], nb = t.nblk[j];
+  const uint32_t* ip = b.init ? b.init : reinterpret_cast<const uint32_t*>(zero16);
+  const uint32_t is = b.init ? 1u : 0u;
+  const uint8_t* op = reinterpret_cast<const uint8_t*>(zero16);
+  const SegSrc src{b.offsets, b.stride, b.seg_len, nullptr, nullptr, -1};
+  if constexpr (CLS == kBvDense64)
+    checksum_dense_body<4, 4, true, 0>(reinterpret_cast<const u32x4*>(b.bytes), ip, is, b.out, b.n, lb);
+  else if constexpr (CLS == kBvTiny)
+    checksum_tiny_body<0>(b.bytes, src, ip, is, op, 0u, zero16, b.out, b.n, lb, nb);
+  else if constexpr (CLS == kBvSmall)
+    checksum_small_body<4, 2, 2, 0>(b.bytes, src, ip, is, op, 0u, zero16, b.out, b.n, lb, nb);
+  else if constexpr (CLS == kBvLine16)
+    checksum_body<16, 8, true, 3, 0>(b.bytes, src, ip, is, op, 0u, b.out, b.n, lb, nb);
+  else
+    checksum_body<64, 8, true, 3, 0>(b.bytes, src, ip, is, op, 0u, b.out, b.n, lb, nb);
+}
+
+template <int CLS>
+__global__ __launch_bounds__(kBlock) void k_ipv4_batchv(BvTable<BvDgram> t, int mode,
+                                                        const uint8_t* __restrict__ zpad, uint32_t remap) {
+  const uint32_t blk = block_order(remap);
+  const uint32_t j = bv_find(t, blk);
+  const BvDgram& b = t.b[j];
+  const uint32_t lb = blk - t.block0[j], nb = t.nblk[j];
+  if constexpr (CLS == kBvLane1)
+    ipv4_body<1, 4, false, 0>(b.dgrams, b.offsets, b.stride, b.dlen, b.n, mode, b.ip_ck, b.tcp_ck, b.status, zpad,
+                              lb, nb);
+  else if constexpr (CLS == kBvLine16)
+    ipv4_body<16, 8, true, 3>(b.dgrams, b.offsets, b.stride, b.dlen, b.n, mode, b.ip_ck, b.tcp_ck, b.status, zpad,
+                              lb, nb);
+  else
+    ipv4_body<64, 8, true, 3>(b.dgrams, b.offsets, b.stride, b.dlen, b.n, mode, b.ip_ck, b.tcp_ck, b.status, zpad,
+                              lb, nb);
 }
 
 // ------------------------------------------- device-side wrap (f2) -------
@@ -1887,6 +1969,65 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
   hipLaunchKernelGGL(k_tcp_hdr, dim3(uint32_t(blocks < (uint64_t(1) << 22) ? blocks : (uint64_t(1) << 22))),
                      dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n,
                      msgs, sums, hdr_out, ip_ck, tcp_ck, int(payload_only));
+  return hipGetLastError();
+}
+
+uint64_t batchv_blocks(int cls, uint64_t n) {
+  // segments per block: dense 64 groups x 4 in flight, tiny 256 lanes,
+  // small 64 groups x 2 in flight, line grids kBlock / lanes per segment
+  const uint64_t per = cls == kBvDense64 ? 256 : cls == kBvTiny || cls == kBvLane1 ? 256 : cls == kBvSmall ? 128
+                       : cls == kBvLine16 ? 16 : 4;
+  return (n + per - 1) / per;
+}
+
+namespace {
+template <typename D>
+bool bv_table(const D* b, int k, int cls, BvTable<D>& t, uint64_t& blocks) {
+  if (k < 1 || k > kMaxBatchv) return false;
+  t = {};
+  t.k = uint32_t(k);
+  blocks = 0;
+  for (int j = 0; j < k; ++j) {
+    t.b[j] = b[j];
+    const uint64_t nb = batchv_blocks(cls, b[j].n);
+    if (nb == 0) return false;
+    t.block0[j] = uint32_t(blocks);
+    t.nblk[j] = uint32_t(nb);
+    blocks += nb;
+  }
+  return blocks < (uint64_t(1) << 24);
+}
+}  // namespace
+
+hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, const void* zero16, hipStream_t st) {
+  BvTable<BvSeg> t;
+  uint64_t blocks = 0;
+  if (!bv_table(b, k, cls, t, blocks)) return hipErrorInvalidValue;
+  const u32x4* z = static_cast<const u32x4*>(zero16);
+  const dim3 grid{uint32_t(blocks), 1, 1};
+  switch (cls) {
+    case kBvDense64: hipLaunchKernelGGL(k_checksum_batchv<kBvDense64>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
+    case kBvTiny: hipLaunchKernelGGL(k_checksum_batchv<kBvTiny>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
+    case kBvSmall: hipLaunchKernelGGL(k_checksum_batchv<kBvSmall>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
+    case kBvLine16: hipLaunchKernelGGL(k_checksum_batchv<kBvLine16>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
+    case kBvLine64: hipLaunchKernelGGL(k_checksum_batchv<kBvLine64>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const void* zero16, hipStream_t st) {
+  BvTable<BvDgram> t;
+  uint64_t blocks = 0;
+  if (!bv_table(b, k, cls, t, blocks)) return hipErrorInvalidValue;
+  const uint8_t* z = static_cast<const uint8_t*>(zero16);
+  const dim3 grid{uint32_t(blocks), 1, 1};
+  switch (cls) {
+    case kBvLane1: hipLaunchKernelGGL(k_ipv4_batchv<kBvLane1>, grid, dim3(kBlock), 0, st, t, mode, z, g_xcd_remap); break;
+    case kBvLine16: hipLaunchKernelGGL(k_ipv4_batchv<kBvLine16>, grid, dim3(kBlock), 0, st, t, mode, z, g_xcd_remap); break;
+    case kBvLine64: hipLaunchKernelGGL(k_ipv4_batchv<kBvLine64>, grid, dim3(kBlock), 0, st, t, mode, z, g_xcd_remap); break;
+    default: return hipErrorInvalidValue;
+  }
   return hipGetLastError();
 }
 

@@ -106,6 +106,41 @@ bool dense_supported(const SegSpec& sp);
 hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* out, int out_kind, int segs,
                                  hipStream_t st);
 
+// ---- several batches in one launch (ics_checksum_batchv / ics_ipv4_tcp_batchv)
+// Up to kMaxBatchv batches of one kernel shape (BvClass) share a launch: the
+// grid is the concatenation of each batch's own grid, the table travels in the
+// kernel arguments (no copy), and every block finds its batch by a scan of
+// the table's block offsets.  One ramp and one drain for all of them instead
+// of one per batch ("Short batches").
+constexpr int kMaxBatchv = 16;
+struct BvSeg {  // one ics_checksum_batch call's arguments (u16 outputs)
+  const uint8_t* bytes;
+  const uint64_t* offsets;
+  uint64_t stride, seg_len, n;
+  const uint32_t* init;
+  uint16_t* out;
+};
+struct BvDgram {  // one ics_ipv4_tcp_batch call's arguments
+  uint8_t* dgrams;
+  const uint64_t* offsets;
+  uint64_t stride, dlen, n;
+  uint16_t* ip_ck;
+  uint16_t* tcp_ck;
+  uint8_t* status;
+};
+// the kernel shapes a multi-batch launch can take: the dense kernel (fixed
+// stride == length == 64 B, aligned), one lane per segment (ACK-sized fixed
+// lengths), 4-lane groups with two segments in flight (short fixed lengths),
+// the 16- and 64-lane line grids (MTU-sized / long or unknown mixes), and the
+// fused kernel's one lane per ACK-sized datagram
+enum BvClass : int { kBvDense64 = 0, kBvTiny = 1, kBvSmall = 2, kBvLine16 = 3, kBvLine64 = 4, kBvLane1 = 5 };
+// blocks one batch of n segments takes in a launch of class cls
+uint64_t batchv_blocks(int cls, uint64_t n);
+// k batches (1 <= k <= kMaxBatchv) of one class; the caller keeps the sum of
+// their batchv_blocks below 2^24 (the dispatch's work-item limit)
+hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, const void* zero16, hipStream_t st);
+hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const void* zero16, hipStream_t st);
+
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
 void set_xcd_remap(uint32_t run_log2);  // log2 XCD run length (default 10 = 1024 blocks), 0: hardware order
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);

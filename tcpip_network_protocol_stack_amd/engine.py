@@ -109,6 +109,46 @@ class Engine:
         self._check(self.lib.ics_fold_batch(self.ctx, _ptr(sums), _ptr(out), n, _stream(stream, self.device)))
         return out
 
+    def checksum_batchv(self, batches, stream=None):
+        """ics_checksum_batchv: several checksum batches in one launch per
+        kernel shape.  `batches`: dicts with keys data, n, offsets, stride,
+        seg_len, init, out (out allocated when absent); returns the outs."""
+        arr = (_lib.SegBatch * max(1, len(batches)))()
+        outs = []
+        for j, b in enumerate(batches):
+            offsets = b.get("offsets")
+            n = b.get("n")
+            if n is None:
+                n = offsets.numel() - 1 if offsets is not None else b["data"].numel() // max(b.get("stride", 1), 1)
+            out = b.get("out")
+            if out is None:
+                out = torch.empty(n, dtype=torch.int16, device=self.device)
+            arr[j] = _lib.SegBatch(_ptr(b["data"]), _ptr(offsets), b.get("stride", 0), b.get("seg_len", 0), n,
+                                   _ptr(b.get("init")), _ptr(out))
+            outs.append(out)
+        self._check(self.lib.ics_checksum_batchv(self.ctx, arr, len(batches), _stream(stream, self.device)))
+        return outs
+
+    def ipv4_tcp_batchv(self, batches, mode, stream=None):
+        """ics_ipv4_tcp_batchv: dicts with keys dgrams, n, offsets, stride,
+        dgram_len, ip_ck, tcp_ck, status (outputs allocated when absent);
+        returns [(ip_ck, tcp_ck, status), ...]."""
+        arr = (_lib.DgramBatch * max(1, len(batches)))()
+        outs = []
+        for j, b in enumerate(batches):
+            offsets = b.get("offsets")
+            n = b.get("n")
+            if n is None:
+                n = offsets.numel() - 1 if offsets is not None else b["dgrams"].numel() // max(b.get("stride", 1), 1)
+            mk = lambda dt: torch.empty(n, dtype=dt, device=self.device)  # noqa: E731
+            o = tuple(b.get(k) if b.get(k) is not None else mk(dt)
+                      for k, dt in (("ip_ck", torch.int16), ("tcp_ck", torch.int16), ("status", torch.uint8)))
+            arr[j] = _lib.DgramBatch(_ptr(b["dgrams"]), _ptr(offsets), b.get("stride", 0), b.get("dgram_len", 0), n,
+                                     _ptr(o[0]), _ptr(o[1]), _ptr(o[2]))
+            outs.append(o)
+        self._check(self.lib.ics_ipv4_tcp_batchv(self.ctx, arr, len(batches), mode, _stream(stream, self.device)))
+        return outs
+
     # ---- fused IPv4 + TCP --------------------------------------------------
     def ipv4_tcp_batch(self, dgrams, mode, n=None, offsets=None, stride=0, dgram_len=0,
                        ip_ck=None, tcp_ck=None, status=None, stream=None):

@@ -35,7 +35,7 @@ def main():
     d = torch.device("cuda", rank % ndev)  # ranks share the card on a one-GPU box
     eng = Engine(rank % ndev)
     n, seed = g["n"], g["seed"]
-    if "stride" in g:
+    if not g.get("mixed"):
         L = g["seg_len"]
         sh = shard.fixed_stride_shard(n, g["stride"], L, rank, world)
         data = torch.empty(sh.nbytes, dtype=torch.uint8, device=d)

@@ -56,8 +56,6 @@ def _sha(a):
 def geo_engine(request):
     """An engine per lane-group geometry (forced through the ICSUM_FORCE hook)."""
     force = dict(zip(("lps", "unroll", "mode", "segs"), request.param))
-    if len(request.param) == 3:
-        del force["segs"]
     gen = _engine_with(force)
     eng = next(gen)
     eng.forced = request.param

@@ -3,14 +3,16 @@
 (PCIe) rate — the numbers DESIGN.md §Measurements quotes.  bench.py stays the
 driver's single headline line (north star); this is the wider table.
 
-    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch,wrap,streams] [--iters 20]
+    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch,wrap,streams,batchv] [--iters 20]
 
 Batches that fit the 256 MiB Infinity Cache (ipv4 98 MB, tcp64 67 MB) are
 rotated over >= 4 distinct copies (>= 393 / 268 MB) so every launch reads HBM.
 Times are HIP events on the launch stream around `iters` back-to-back launches
 (median of 5 rounds); the `streams` rows issue a stream of short batches
 (configs 2, 3) on two HIP streams in turn, so one batch's drain overlaps the
-next one's ramp.  GiB = 2^30 B of algorithmic bytes (segment bytes, each
+next one's ramp; the `batchv` rows hand K = 8 such batches to ONE call
+(ics_ipv4_tcp_batchv / ics_checksum_batchv: one launch, one stream) and
+report the time per batch.  GiB = 2^30 B of algorithmic bytes (segment bytes, each
 read once); metadata (inits, offsets, outputs) is reported separately.
 """
 import argparse
@@ -100,9 +102,9 @@ def main():
     eng = Engine(0)
     eng_nobin = Engine(0)
     eng_nobin.set_binning(0)  # ICS_BINNING_SINGLE: single-geometry dispatch of offsets batches, for comparison
-    os.environ["ICSUM_PLAN_CACHE"] = "0"
-    eng_nocache = Engine(0)  # AUTO without the plan cache: every call runs the binning passes
-    del os.environ["ICSUM_PLAN_CACHE"]
+    os.environ["ICSUM_FORCE"] = "bin=1"
+    eng_nocache = Engine(0)  # binned on every call: the binning passes without the plan cache
+    del os.environ["ICSUM_FORCE"]
     dev = torch.device("cuda", 0)
 
     if "ns" in only:  # north star: 1 M x 1500 B, pseudo-header inits
@@ -237,6 +239,43 @@ def main():
                                                             out=o16[j], stream=s), args.iters * 3, K)
         emit("tcp_1Mx64_2streams", n * L, t, n * 6, entry="ics_checksum_batch", rotation=R, streams=K)
         del ds
+
+    if "batchv" in only:  # K = 8 short batches in ONE call on one stream (configs 2, 3)
+        K = 8
+        n, L, seed = 1 << 16, 1500, 0x10710002
+        bufs = []
+        for r in range(2 * K):  # two sets of K: every call reads 786 MB, beyond the 256 MiB Infinity Cache
+            d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+            eng.ipv4_tcp_headers(d, n, L, L, seed, index0=r * n)
+            eng.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)
+            bufs.append(d)
+        outs = [dict(ip_ck=torch.empty(n, dtype=torch.int16, device=dev),
+                     tcp_ck=torch.empty(n, dtype=torch.int16, device=dev),
+                     status=torch.empty(n, dtype=torch.uint8, device=dev)) for _ in range(K)]
+        sets = [[dict(dgrams=bufs[s * K + j], n=n, stride=L, dgram_len=L, **outs[j]) for j in range(K)]
+                for s in range(2)]
+        for mode, nm in ((0, "compute"), (2, "patch"), (1, "verify")):
+            t = timed(lambda i=0: eng.ipv4_tcp_batchv(sets[i % 2], mode), args.iters)
+            emit(f"ipv4_64Kix1500_{nm}_batchv{K}", n * L, t / K, n * 5, entry="ics_ipv4_tcp_batchv",
+                 batches_per_call=K, note="time per batch")
+        assert all((o["status"].cpu().numpy() == 0x0F).all() for o in outs)
+        o16 = [torch.empty(n, dtype=torch.int16, device=dev) for _ in range(K)]
+        psets = [[dict(data=bufs[s * K + j], n=n, stride=L, seg_len=L, out=o16[j]) for j in range(K)]
+                 for s in range(2)]
+        t = timed(lambda i=0: eng.checksum_batchv(psets[i % 2]), args.iters)
+        emit(f"plain_64Kix1500_batchv{K}", n * L, t / K, n * 2, entry="ics_checksum_batchv", batches_per_call=K,
+             note="time per batch")
+        del bufs, sets, psets
+        n, L, seed = 1 << 20, 64, 0x10710003
+        ds = [eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed, pos0=r * n * L)
+              for r in range(2 * K)]
+        inits = [eng.pseudo_inits(n, seed, seg_len=L, index0=r * n) for r in range(2 * K)]
+        sets = [[dict(data=ds[s * K + j], n=n, stride=L, seg_len=L, init=inits[s * K + j], out=torch.empty(n, dtype=torch.int16, device=dev))
+                 for j in range(K)] for s in range(2)]
+        t = timed(lambda i=0: eng.checksum_batchv(sets[i % 2]), args.iters)
+        emit(f"tcp_1Mx64_batchv{K}", n * L, t / K, n * 6, entry="ics_checksum_batchv", batches_per_call=K,
+             note="time per batch")
+        del ds, sets
 
     if "tcp64" in only:  # config 3: 1 M x 64 B TCP segments with pseudo inits
         n, L, seed, R = 1 << 20, 64, 0x10710003, 6

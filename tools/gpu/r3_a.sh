@@ -5,7 +5,8 @@
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-r3a}; mkdir -p $O
-timeout -k 10 840 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
+timeout -k 10 840 python -u -m pytest tests -m gpu -x -v --timeout 240 --timeout-method thread -p no:cacheprovider --durations=25 > $O/pytest.log 2>&1
 timeout -k 10 180 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-pmc --cpu-seconds 0 > $O/bench_n1.json 2> $O/bench_n1.err
 timeout -k 10 240 python3 bench.py --gpus 2 --steps 20 --warmup 5 --no-pmc --cpu-seconds 0 > $O/bench_n2.json 2> $O/bench_n2.err
 timeout -k 10 300 python3 bench.py --gpus 4 --steps 20 --warmup 5 --no-pmc --cpu-seconds 0 > $O/bench_n4.json 2> $O/bench_n4.err
+timeout -k 10 300 python3 tools/bench_configs.py --only ipv4,ns64k,tcp64,streams,batchv > $O/configs_short.jsonl 2> $O/configs_short.err
