@@ -13,7 +13,12 @@
 //            4 the two aligned 16-byte chunks holding the fields, 5 those
 //            non-temporal, 6 the aligned 64-byte blocks; 7 the whole 128-byte
 //            line holding the IPv4 header, one 16-byte store per lane of
-//            lanes 0-7, 8 the same non-temporal; junk values)
+//            lanes 0-7, 8 the same non-temporal; junk values; 9 (round 3) the
+//            64 bytes from the 32-byte sector holding the IPv4 checksum field,
+//            which hold both fields, loaded by the group's 16 lanes (one
+//            dword each), the two fields spliced in and all 64 bytes stored
+//            back: two WHOLE sectors written with the real bytes, no masked
+//            partial-sector write; checked equal to the engine's PATCH)
 //   split    v0, then a second launch that scatters the two fields from the
 //            contiguous ip_ck / tcp_ck arrays into the datagrams (split_nt:
 //            non-temporal stores; scatter: that launch alone)
@@ -128,12 +133,32 @@ __global__ __launch_bounds__(kBlock) void k_v(uint8_t* __restrict__ dg, uint64_t
     else
       *c = x;
   }
+  if (P == 9) {  // whole sectors with the fields spliced in (hlen 5 datagrams of >= 64 bytes)
+    const uint16_t ipc = fold_value(ipv4_header_sum(h));
+    const uint16_t tcv = fold_value(ipv4_pseudo(h) + tot - (tf1 & 0xffffu));
+    const uint64_t S0 = (s + 10) & ~uint64_t(31);
+    uint32_t* q = reinterpret_cast<uint32_t*>(dg + S0) + lane;  // 16 lanes: bytes [S0, S0 + 64)
+    uint32_t w = valid ? *q : 0u;
+    const uint64_t at = S0 + 4 * lane;
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      const uint64_t x = at + b;
+      uint32_t v = (w >> (8 * b)) & 0xffu;
+      if (x == s + 10) v = ipc >> 8;
+      if (x == s + 11) v = ipc & 0xffu;
+      if (x == t0 + 16) v = tcv >> 8;
+      if (x == t0 + 17) v = tcv & 0xffu;
+      w = (w & ~(0xffu << (8 * b))) | (v << (8 * b));
+    }
+    if (valid) *q = w;
+  }
   if (valid && lane == LPS - 1) {
     const uint16_t ipc = fold_value(ipv4_header_sum(h));
     uint32_t sum = ipv4_pseudo(h) + tot - (tf1 & 0xffffu);
     const uint16_t tcv = fold_value(sum);
     const uint8_t st = uint8_t(((tf0 & 0xffu) >> 4) | (h.byte(9) == 6 ? 8 : 0));
     if (P && P < 7) patch_store<P>(dg, s, t0, ipc, tcv);
+    (void)0;
     if (F & 4) {
       if (ipc == 0x1234u && tcv == 0x5678u && st == 9) status[0] = 1;  // keep the work, drop the stores
     } else {
@@ -241,7 +266,7 @@ int main() {
   };
   auto spec = [&](int c) { return SegSpec{B.d[c], nullptr, kL, kL, kN, B.zero}; };
   std::vector<V> vs;
-  vs.push_back({"engine", [&](int c) { (void)launch_ipv4_tcp(spec(c), 0, B.ip, B.tcp, B.st, g, 0, false, nullptr); }});
+  vs.push_back({"engine", [&](int c) { (void)launch_ipv4_tcp(spec(c), 0, B.ip, B.tcp, B.st, g, 0, nullptr); }});
   vs.push_back({"plain", [&](int c) { (void)launch_checksum(spec(c), nullptr, nullptr, B.ip, 0, g, 0, nullptr); }});
 #define VAR(F)                                                                                            \
   vs.push_back({"v" #F, [&](int c) {                                                                      \
@@ -250,14 +275,13 @@ int main() {
                 }});
   VAR(0) VAR(1) VAR(3) VAR(4)
 #undef VAR
-  vs.push_back({"engine_patch", [&](int c) { (void)launch_ipv4_tcp(spec(c), 2, B.ip, B.tcp, B.st, g, 0, false, nullptr); }});
-  vs.push_back({"engine_patch_wt", [&](int c) { (void)launch_ipv4_tcp(spec(c), 2, B.ip, B.tcp, B.st, g, 0, true, nullptr); }});
+  vs.push_back({"engine_patch", [&](int c) { (void)launch_ipv4_tcp(spec(c), 2, B.ip, B.tcp, B.st, g, 0, nullptr); }});
 #define PVAR(P)                                                                                           \
   vs.push_back({"p" #P, [&](int c) {                                                                      \
                   hipLaunchKernelGGL((k_v<0, P>), dim3(blocks), dim3(256), 0, nullptr, B.d[c], kL, kL, kN, B.ip, \
                                      B.tcp, B.st, 10u);                                                   \
                 }});
-  PVAR(1) PVAR(2) PVAR(3) PVAR(4) PVAR(5) PVAR(6) PVAR(7) PVAR(8)
+  PVAR(1) PVAR(2) PVAR(3) PVAR(4) PVAR(5) PVAR(6) PVAR(7) PVAR(8) PVAR(9)
 #undef PVAR
   const uint32_t sblocks = uint32_t(kN / 256);
   vs.push_back({"split", [&](int c) {
@@ -290,6 +314,22 @@ int main() {
                   hipLaunchKernelGGL(k_flat, dim3(blocks), dim3(256), 0, nullptr, B.d[c], kN, B.ip);
                 }});
 
+  {  // p9 (whole sectors, real bytes) writes exactly the engine PATCH's bytes
+    uint8_t *x = nullptr, *y = nullptr;
+    CK(hipMalloc(&x, kN * kL + 64));
+    CK(hipMalloc(&y, kN * kL + 64));
+    CK(hipMemcpy(x, B.d[0], kN * kL + 64, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(y, B.d[0], kN * kL + 64, hipMemcpyDeviceToDevice));
+    CK(launch_ipv4_tcp(SegSpec{x, nullptr, kL, kL, kN, B.zero}, 2, B.ip, B.tcp, B.st, g, 0, nullptr));
+    hipLaunchKernelGGL((k_v<0, 9>), dim3(blocks), dim3(256), 0, nullptr, y, kL, kL, kN, B.ip, B.tcp, B.st, 10u);
+    CK(hipDeviceSynchronize());
+    std::vector<uint8_t> hx(kN * kL), hy(kN * kL);
+    CK(hipMemcpy(hx.data(), x, kN * kL, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hy.data(), y, kN * kL, hipMemcpyDeviceToHost));
+    printf("{\"p9_equals_engine_patch\": %s}\n", hx == hy ? "true" : "false");
+    CK(hipFree(x));
+    CK(hipFree(y));
+  }
   for (int r = 0; r < 4000; ++r) vs[0].fn(r % kCopies);  // settle clocks
   CK(hipDeviceSynchronize());
   std::vector<std::vector<float>> t(vs.size());

@@ -10,6 +10,14 @@
 //           16 lines each)
 //   c2      two lanes per datagram, three dwords each
 //   rd      reads only (one lane per datagram, no store) — the read floor
+//   sec     round 3: four lanes per datagram load the 64-byte window from the
+//           32-byte sector holding the header start (16 B each), and the
+//           sectors holding the rewritten bytes 4..11 are stored WHOLE (two
+//           16-byte stores per sector, the new fields spliced into the bytes
+//           just loaded) instead of one masked 8-byte store: no partial-sector
+//           write reaches the memory side (dword-aligned headers, stride >= 64,
+//           so no other datagram's bytes share those sectors)
+//   rdsec   the same 64-byte window loads, no store
 // Every variant forwards (ttl--, checksum recomputed) the same datagrams, so
 // the copies start at ttl 255 and each is forwarded at most 120 times.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include router_probe.hip -o router_probe
@@ -104,6 +112,56 @@ __global__ __launch_bounds__(kBlock) void k_coop(uint8_t* __restrict__ dg, uint6
   }
 }
 
+// dword k (0..15) of the 64-byte window held 4 per lane by the group's lanes
+__device__ __forceinline__ uint32_t win_dword(const u32x4& v, uint32_t k, uint32_t base_lane) {
+  const uint32_t e = k & 3u;
+  const uint32_t mine = e == 0 ? v.x : e == 1 ? v.y : e == 2 ? v.z : v.w;  // every lane picks element k & 3
+  return uint32_t(__shfl(int(mine), int(base_lane + (k >> 2)), 64));
+}
+
+template <bool STORE>
+__global__ __launch_bounds__(kBlock) void k_sec(uint8_t* __restrict__ dg, uint64_t stride, uint64_t n,
+                                                uint8_t* __restrict__ status) {
+  constexpr uint32_t kG = kBlock / 4;
+  const uint32_t lane = threadIdx.x & 3u, base_lane = threadIdx.x & 63u & ~3u;
+  for (uint64_t i = uint64_t(blockIdx.x) * kG + threadIdx.x / 4; i - threadIdx.x / 4 < n;
+       i += uint64_t(gridDim.x) * kG) {
+    const bool valid = i < n;
+    const uint64_t s = (valid ? i : n - 1) * stride;
+    const uint64_t B = s & ~uint64_t(31);
+    u32x4* w = reinterpret_cast<u32x4*>(dg + B) + lane;
+    u32x4 v = *w;
+    const uint32_t k0 = uint32_t(s - B) >> 2;  // header dword 0 in the window (s dword-aligned)
+    uint32_t d[6];
+#pragma unroll
+    for (int k = 0; k < 6; ++k) d[k] = win_dword(v, k0 + uint32_t(k), base_lane);
+    Hdr h;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h.w[k] = d[k];
+    const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu, ttl = h.byte(8);
+    const bool fwd = valid && ver == 4 && hlen >= 5 && fold_value(ipv4_header_sum(h)) == h.be16(10) && ttl > 1;
+    if (!STORE) {
+      if (valid && lane == 0) status[i] = uint8_t(fold_value(ipv4_header_sum(h)) == h.be16(10));
+      continue;
+    }
+    h.w[2] = (h.w[2] & ~0xffu) | (ttl - 1);
+    const uint32_t c = fold_value(ipv4_header_sum(h));
+    const uint32_t w1 = h.w[1] & ~0x00800000u;
+    const uint32_t w2 = (h.w[2] & 0x0000ffffu) | ((c >> 8) << 16) | ((c & 0xffu) << 24);
+    // window dwords k0+1, k0+2 take w1, w2; this lane holds dwords 4 lane .. 4 lane + 3
+    const uint32_t a = k0 + 1;
+    u32x4 o = v;
+    o.x = (4 * lane + 0 == a) ? w1 : (4 * lane + 0 == a + 1) ? w2 : o.x;
+    o.y = (4 * lane + 1 == a) ? w1 : (4 * lane + 1 == a + 1) ? w2 : o.y;
+    o.z = (4 * lane + 2 == a) ? w1 : (4 * lane + 2 == a + 1) ? w2 : o.z;
+    o.w = (4 * lane + 3 == a) ? w1 : (4 * lane + 3 == a + 1) ? w2 : o.w;
+    // sectors touched: the ones holding window bytes 4 k0 + 4 .. 4 k0 + 11
+    const uint32_t sec_lo = (4 * k0 + 4) >> 5, sec_hi = (4 * k0 + 11) >> 5, my_sec = lane >> 1;
+    if (fwd && my_sec >= sec_lo && my_sec <= sec_hi) *w = o;
+    if (valid && lane == 0) status[i] = fwd ? 1 : 0;
+  }
+}
+
 }  // namespace
 }  // namespace icsum
 
@@ -123,7 +181,7 @@ int main() {
   CK(hipMemset(zero, 0, 64));
   for (int c = 0; c < kCopies; ++c) {
     const SegSpec sp{d[c], nullptr, kL, kL, kN, zero};
-    CK(launch_ipv4_tcp(sp, 2, nullptr, nullptr, nullptr, pick_geometry(kL), 0, false, nullptr));
+    CK(launch_ipv4_tcp(sp, 2, nullptr, nullptr, nullptr, pick_geometry(kL), 0, nullptr));
   }
   CK(hipDeviceSynchronize());
   struct V {
@@ -141,6 +199,25 @@ int main() {
   vs.push_back({"c8", [&](int c) { hipLaunchKernelGGL((k_coop<8, true>), dim3(32768), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
   vs.push_back({"rd1", [&](int c) { hipLaunchKernelGGL((k_coop<1, false>), dim3(4096), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
   vs.push_back({"rd4", [&](int c) { hipLaunchKernelGGL((k_coop<4, false>), dim3(16384), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  vs.push_back({"sec", [&](int c) { hipLaunchKernelGGL((k_sec<true>), dim3(16384), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  vs.push_back({"rdsec", [&](int c) { hipLaunchKernelGGL((k_sec<false>), dim3(16384), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  {  // the whole-sector variant writes exactly the engine's bytes
+    uint8_t *x = nullptr, *y = nullptr;
+    CK(hipMalloc(&x, kN * kL + 64));
+    CK(hipMalloc(&y, kN * kL + 64));
+    CK(hipMemcpy(x, d[0], kN * kL + 64, hipMemcpyDeviceToDevice));
+    CK(hipMemcpy(y, d[0], kN * kL + 64, hipMemcpyDeviceToDevice));
+    const SegSpec sp{x, nullptr, kL, kL, kN, zero};
+    CK(launch_router_ttl(sp, st, nullptr));
+    hipLaunchKernelGGL((k_sec<true>), dim3(16384), dim3(256), 0, nullptr, y, kL, kN, st);
+    CK(hipDeviceSynchronize());
+    std::vector<uint8_t> hx(kN * kL), hy(kN * kL);
+    CK(hipMemcpy(hx.data(), x, kN * kL, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(hy.data(), y, kN * kL, hipMemcpyDeviceToHost));
+    printf("{\"sec_equals_engine\": %s}\n", hx == hy ? "true" : "false");
+    CK(hipFree(x));
+    CK(hipFree(y));
+  }
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
