@@ -889,3 +889,28 @@ def test_dense_fixed_stride_kernel(segs, orc):
 
         torch.cuda.synchronize()
         eng.close()
+
+
+def test_force_hook_rejects_unknown_keys():
+    """ICSUM_FORCE (the test hook) fails ics_create on a key it does not know
+    or a value out of range, so a mistyped hook cannot silently test the
+    default path instead."""
+    from tcpip_network_protocol_stack_amd._lib import IcsumError
+
+    for bad in ("lps=16,bogus=1", "twoclass=8", "wrap_passes=3", "bin_plan", "lps=x"):
+        with pytest.raises(IcsumError, match="ICSUM_FORCE"):
+            next(_engine_with_raw(bad))
+    eng = next(_engine_with({"lps": 16, "unroll": 8, "mode": 3}))
+    eng.close()
+
+
+def _engine_with_raw(spec):
+    import os
+
+    from tcpip_network_protocol_stack_amd.engine import Engine
+
+    os.environ["ICSUM_FORCE"] = spec
+    try:
+        yield Engine(0)
+    finally:
+        os.environ.pop("ICSUM_FORCE", None)

@@ -38,7 +38,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n, L, seed, K = 1 << 20, 64, 0x10710003, 8
-    e4, e8 = engine(), engine(bv_dense_segs=8)
+    e4, e8, s8 = engine(), engine(bv_dense_segs=8), engine(dense_segs=8)
     big = e4.fill_bytes(torch.empty(2 * K * n * L, dtype=torch.uint8, device=dev), seed)
     binit = e4.pseudo_inits(2 * K * n, seed, seg_len=L)
     ds = [big[r * n * L:(r + 1) * n * L] for r in range(2 * K)]
@@ -53,6 +53,10 @@ def main():
                                                        init=inits[i % (2 * K)], out=outs[0])),
         "single_8M": (K, lambda i: e4.checksum_batch(big[(i % 2) * K * n * L:], n=K * n, stride=L, seg_len=L,
                                                        init=binit[(i % 2) * K * n:], out=bout)),
+        "single_1M_segs8": (1, lambda i: s8.checksum_batch(ds[i % (2 * K)], n=n, stride=L, seg_len=L,
+                                                             init=inits[i % (2 * K)], out=outs[0])),
+        "single_8M_segs8": (K, lambda i: s8.checksum_batch(big[(i % 2) * K * n * L:], n=K * n, stride=L, seg_len=L,
+                                                             init=binit[(i % 2) * K * n:], out=bout)),
         "batchv8_segs4": (K, lambda i: e4.checksum_batchv(sets[i % 2])),
         "batchv8_segs8": (K, lambda i: e8.checksum_batchv(sets[i % 2])),
     }

@@ -1,0 +1,12 @@
+#!/bin/bash
+# Driver-equivalent round-end check: GPU tests, smoke, bench N=1 (with PMC +
+# CPU baseline) and its rocprof kernel stats in the same call.
+set -euo pipefail
+cd "$GRAFT_REPO_ROOT"
+O=gpurun_out/${1:-r3full}; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest.log 2>&1
+timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
+timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
+(cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
+   -d "$GRAFT_REPO_ROOT/$O/trace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-pmc --cpu-seconds 0 --steps 20 \
+   > "$GRAFT_REPO_ROOT/$O/bench_under_rocprof.json" 2>&1)
