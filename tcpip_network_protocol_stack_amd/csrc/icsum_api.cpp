@@ -102,6 +102,7 @@ struct ics_ctx {
   uint32_t last_bin_lps = 0;     // lanes per segment of the last bin's launch (0: auto, see checksum_device)
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off)
   int bv_dense_segs = 4;         // the same in a multi-batch launch's dense class (4 or 8)
+  bool bv_dense_remap = true;    // the dense class's blocks in XCD-aware order
   int bin_plan = -1;  // -1: decided on the device per batch; forced: 0 whole, 1 split, 2 whole16, 3 wholeS
   int twoclass = 0;   // 0: auto; 16 / 32: every offsets batch through the two-class launch (that many per wave)
   // device wrap: 0 = two passes (payload sums, then a header launch) when
@@ -863,6 +864,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "last_bin_blocks") ctx->last_bin_blocks = uint32_t(v);
     else if (k == "dense_segs") ctx->dense_segs = int(v);
     else if (k == "bv_dense_segs" && (v == 4 || v == 8)) ctx->bv_dense_segs = int(v);
+    else if (k == "bv_dense_remap" && (v == 0 || v == 1)) ctx->bv_dense_remap = v != 0;
     else if (k == "twoclass" && (v == 0 || v == 16 || v == 32)) ctx->twoclass = int(v);
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
@@ -1222,7 +1224,7 @@ int ics_checksum_batchv(ics_ctx* ctx, const ics_seg_batch* batches, uint32_t k, 
     return g.lps >= 32 ? icsum::kBvLine64 : icsum::kBvLine16;
   };
   auto launch = [&](const icsum::BvSeg* g, int m, int c) {
-    return icsum::launch_checksum_batchv(g, m, c, ctx->bv_dense_segs, ctx->d_zero, st);
+    return icsum::launch_checksum_batchv(g, m, c, ctx->bv_dense_segs, ctx->bv_dense_remap, ctx->d_zero, st);
   };
   auto alone = [&](const icsum::BvSeg& x) {
     const icsum::SegSpec sp{x.bytes, x.offsets, x.stride, x.seg_len, x.n, ctx->d_zero};

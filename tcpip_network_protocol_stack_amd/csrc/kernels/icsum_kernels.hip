@@ -1999,8 +1999,8 @@ bool bv_table(const D* b, int k, int cls, int dense_segs, BvTable<D>& t, uint64_
 }
 }  // namespace
 
-hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, int dense_segs, const void* zero16,
-                                  hipStream_t st) {
+hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, int dense_segs, bool dense_remap,
+                                  const void* zero16, hipStream_t st) {
   if (cls == kBvDense64 && dense_segs != 4 && dense_segs != 8) return hipErrorInvalidValue;
   BvTable<BvSeg> t;
   uint64_t blocks = 0;
@@ -2010,9 +2010,11 @@ hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, int dense_segs
   switch (cls) {
     case kBvDense64:
       if (dense_segs == 8)
-        hipLaunchKernelGGL((k_checksum_batchv<kBvDense64, 8>), grid, dim3(kBlock), 0, st, t, z, g_xcd_remap);
+        hipLaunchKernelGGL((k_checksum_batchv<kBvDense64, 8>), grid, dim3(kBlock), 0, st, t, z,
+                           dense_remap ? g_xcd_remap : 0u);
       else
-        hipLaunchKernelGGL((k_checksum_batchv<kBvDense64, 4>), grid, dim3(kBlock), 0, st, t, z, g_xcd_remap);
+        hipLaunchKernelGGL((k_checksum_batchv<kBvDense64, 4>), grid, dim3(kBlock), 0, st, t, z,
+                           dense_remap ? g_xcd_remap : 0u);
       break;
     case kBvTiny: hipLaunchKernelGGL(k_checksum_batchv<kBvTiny>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
     case kBvSmall: hipLaunchKernelGGL(k_checksum_batchv<kBvSmall>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;

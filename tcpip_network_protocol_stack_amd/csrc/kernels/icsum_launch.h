@@ -139,8 +139,8 @@ enum BvClass : int { kBvDense64 = 0, kBvTiny = 1, kBvSmall = 2, kBvLine16 = 3, k
 uint64_t batchv_blocks(int cls, uint64_t n, int dense_segs = 4);
 // k batches (1 <= k <= kMaxBatchv) of one class; the caller keeps the sum of
 // their batchv_blocks below 2^24 (the dispatch's work-item limit)
-hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, int dense_segs, const void* zero16,
-                                  hipStream_t st);
+hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, int dense_segs, bool dense_remap,
+                                  const void* zero16, hipStream_t st);
 hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const void* zero16, hipStream_t st);
 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)

@@ -39,6 +39,7 @@ def main():
     dev = torch.device("cuda", 0)
     n, L, seed, K = 1 << 20, 64, 0x10710003, 8
     e4, e8, s8 = engine(), engine(bv_dense_segs=8), engine(dense_segs=8)
+    e4h, e8h = engine(bv_dense_remap=0), engine(bv_dense_segs=8, bv_dense_remap=0)
     big = e4.fill_bytes(torch.empty(2 * K * n * L, dtype=torch.uint8, device=dev), seed)
     binit = e4.pseudo_inits(2 * K * n, seed, seg_len=L)
     ds = [big[r * n * L:(r + 1) * n * L] for r in range(2 * K)]
@@ -59,10 +60,12 @@ def main():
                                                              init=binit[(i % 2) * K * n:], out=bout)),
         "batchv8_segs4": (K, lambda i: e4.checksum_batchv(sets[i % 2])),
         "batchv8_segs8": (K, lambda i: e8.checksum_batchv(sets[i % 2])),
+        "batchv8_segs4_hworder": (K, lambda i: e4h.checksum_batchv(sets[i % 2])),
+        "batchv8_segs8_hworder": (K, lambda i: e8h.checksum_batchv(sets[i % 2])),
     }
     # outputs agree: set 0 through every variant
     ref = [t.clone() for t in e4.checksum_batchv(sets[0])]
-    for e in (e4, e8):
+    for e in (e4, e8, e4h, e8h):
         got = e.checksum_batchv(sets[0])
         assert all(torch.equal(a, b) for a, b in zip(got, ref))
     e4.checksum_batch(big, n=K * n, stride=L, seg_len=L, init=binit, out=bout)

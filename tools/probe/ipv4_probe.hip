@@ -135,7 +135,8 @@ __global__ __launch_bounds__(kBlock) void k_v(uint8_t* __restrict__ dg, uint64_t
   }
   if (P == 9) {  // whole sectors with the fields spliced in (hlen 5 datagrams of >= 64 bytes)
     const uint16_t ipc = fold_value(ipv4_header_sum(h));
-    const uint16_t tcv = fold_value(ipv4_pseudo(h) + tot - (tf1 & 0xffffu));
+    // tcp_segment.cpp:143: the checksum field (TCP bytes 16, 17) counts as 0
+    const uint16_t tcv = fold_value(ipv4_pseudo(h) + tot - ((tf1 & 0xffu) << 8) - ((tf1 >> 8) & 0xffu));
     const uint64_t S0 = (s + 10) & ~uint64_t(31);
     uint32_t* q = reinterpret_cast<uint32_t*>(dg + S0) + lane;  // 16 lanes: bytes [S0, S0 + 64)
     uint32_t w = valid ? *q : 0u;
