@@ -1214,7 +1214,7 @@ int ics_checksum_batchv(ics_ctx* ctx, const ics_seg_batch* batches, uint32_t k, 
   std::vector<icsum::BvSeg> b(k);
   for (uint32_t j = 0; j < k; ++j)
     b[j] = {static_cast<const uint8_t*>(batches[j].bytes), batches[j].offsets, batches[j].stride, batches[j].seg_len,
-            batches[j].n, batches[j].init, batches[j].out};
+            batches[j].n, batches[j].init, batches[j].out, 0};
   auto cls_of = [&](const icsum::BvSeg& x) -> int {
     const icsum::SegSpec sp{x.bytes, x.offsets, x.stride, x.seg_len, x.n, ctx->d_zero};
     if (!x.offsets && x.seg_len == 64 && icsum::dense_supported(sp)) return icsum::kBvDense64;

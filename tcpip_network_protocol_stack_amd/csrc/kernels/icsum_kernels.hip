@@ -1119,13 +1119,16 @@ struct BvTable {
   uint32_t k;
 };
 
-// the batch that owns (logical) block blk
+// the batch that owns (logical) block blk: block0 is ascending and padded
+// with 0xFFFFFFFF past the last batch, so the batch index is the number of
+// entries 1..15 at or below blk — one scalar compare per entry, a bitmask and
+// s_bcnt1 (the uniform index keeps the descriptor load a scalar load)
 template <typename D>
 __device__ __forceinline__ uint32_t bv_find(const BvTable<D>& t, uint32_t blk) {
-  uint32_t j = 0;
+  uint32_t mask = 0;
 #pragma unroll
-  for (uint32_t q = 1; q < uint32_t(kMaxBatchv); ++q) j += (q < t.k && blk >= t.block0[q]) ? 1u : 0u;
-  return j;
+  for (uint32_t q = 1; q < uint32_t(kMaxBatchv); ++q) mask |= blk >= t.block0[q] ? (1u << q) : 0u;
+  return __builtin_amdgcn_readfirstlane(uint32_t(__builtin_popcount(mask)));
 }
 
 template <int CLS, int DSEGS = 4>
@@ -1987,6 +1990,7 @@ bool bv_table(const D* b, int k, int cls, int dense_segs, BvTable<D>& t, uint64_
   t = {};
   t.k = uint32_t(k);
   blocks = 0;
+  for (int j = k; j < kMaxBatchv; ++j) t.block0[j] = 0xFFFFFFFFu;  // no batch: never at or below a block
   for (int j = 0; j < k; ++j) {
     t.b[j] = b[j];
     const uint64_t nb = batchv_blocks(cls, b[j].n, dense_segs);

@@ -113,14 +113,15 @@ hipError_t launch_checksum_dense(const SegSpec& sp, const uint32_t* init, void* 
 // the table's block offsets.  One ramp and one drain for all of them instead
 // of one per batch ("Short batches").
 constexpr int kMaxBatchv = 16;
-struct BvSeg {  // one ics_checksum_batch call's arguments (u16 outputs)
+struct BvSeg {  // one ics_checksum_batch call's arguments (u16 outputs); 64 bytes
   const uint8_t* bytes;
   const uint64_t* offsets;
   uint64_t stride, seg_len, n;
   const uint32_t* init;
   uint16_t* out;
+  uint64_t pad;  // a power-of-two stride: the indexed descriptor address is a shift
 };
-struct BvDgram {  // one ics_ipv4_tcp_batch call's arguments
+struct BvDgram {  // one ics_ipv4_tcp_batch call's arguments; 64 bytes
   uint8_t* dgrams;
   const uint64_t* offsets;
   uint64_t stride, dlen, n;
@@ -128,6 +129,7 @@ struct BvDgram {  // one ics_ipv4_tcp_batch call's arguments
   uint16_t* tcp_ck;
   uint8_t* status;
 };
+static_assert(sizeof(BvSeg) == 64 && sizeof(BvDgram) == 64, "multi-batch descriptors: 64-byte stride");
 // the kernel shapes a multi-batch launch can take: the dense kernel (fixed
 // stride == length == 64 B, aligned), one lane per segment (ACK-sized fixed
 // lengths), 4-lane groups with two segments in flight (short fixed lengths),
