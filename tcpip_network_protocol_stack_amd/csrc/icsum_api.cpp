@@ -101,8 +101,6 @@ struct ics_ctx {
   uint32_t last_bin_blocks = 0;  // grid cap of the last bin's launch (0: one lane group per segment)
   uint32_t last_bin_lps = 0;     // lanes per segment of the last bin's launch (0: auto, see checksum_device)
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off)
-  int bv_dense_segs = 4;         // the same in a multi-batch launch's dense class (4 or 8)
-  bool bv_dense_remap = true;    // the dense class's blocks in XCD-aware order
   int bin_plan = -1;  // -1: decided on the device per batch; forced: 0 whole, 1 split, 2 whole16, 3 wholeS
   int twoclass = 0;   // 0: auto; 16 / 32: every offsets batch through the two-class launch (that many per wave)
   // device wrap: 0 = two passes (payload sums, then a header launch) when
@@ -863,8 +861,6 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "last_bin_lps") ctx->last_bin_lps = uint32_t(v);
     else if (k == "last_bin_blocks") ctx->last_bin_blocks = uint32_t(v);
     else if (k == "dense_segs") ctx->dense_segs = int(v);
-    else if (k == "bv_dense_segs" && (v == 4 || v == 8)) ctx->bv_dense_segs = int(v);
-    else if (k == "bv_dense_remap" && (v == 0 || v == 1)) ctx->bv_dense_remap = v != 0;
     else if (k == "twoclass" && (v == 0 || v == 16 || v == 32)) ctx->twoclass = int(v);
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
@@ -1164,8 +1160,7 @@ namespace {
 // dispatch's work-item limit); a batch too large for that runs alone through
 // the single-batch path.
 template <typename D, typename ClassFn, typename LaunchFn, typename AloneFn>
-int run_batchv(ics_ctx* ctx, const D* b, uint32_t k, int dense_segs, ClassFn cls_of, LaunchFn launch,
-               AloneFn alone) {
+int run_batchv(ics_ctx* ctx, const D* b, uint32_t k, ClassFn cls_of, LaunchFn launch, AloneFn alone) {
   constexpr uint64_t kMaxBlocks = (uint64_t(1) << 24) - 1;
   std::vector<int> cls(k);
   for (uint32_t j = 0; j < k; ++j) cls[j] = b[j].n ? cls_of(b[j]) : -1;
@@ -1184,7 +1179,7 @@ int run_batchv(ics_ctx* ctx, const D* b, uint32_t k, int dense_segs, ClassFn cls
     };
     for (uint32_t j = 0; j < k; ++j) {
       if (cls[j] != c) continue;
-      const uint64_t nb = icsum::batchv_blocks(c, b[j].n, dense_segs);
+      const uint64_t nb = icsum::batchv_blocks(c, b[j].n);
       if (nb > kMaxBlocks / 4) {  // a large batch: a launch of its own, its usual path
         if (int rc = alone(b[j])) return rc;
         continue;
@@ -1224,13 +1219,13 @@ int ics_checksum_batchv(ics_ctx* ctx, const ics_seg_batch* batches, uint32_t k, 
     return g.lps >= 32 ? icsum::kBvLine64 : icsum::kBvLine16;
   };
   auto launch = [&](const icsum::BvSeg* g, int m, int c) {
-    return icsum::launch_checksum_batchv(g, m, c, ctx->bv_dense_segs, ctx->bv_dense_remap, ctx->d_zero, st);
+    return icsum::launch_checksum_batchv(g, m, c, ctx->d_zero, st);
   };
   auto alone = [&](const icsum::BvSeg& x) {
     const icsum::SegSpec sp{x.bytes, x.offsets, x.stride, x.seg_len, x.n, ctx->d_zero};
     return checksum_device(ctx, sp, x.init, nullptr, x.out, 0, st);
   };
-  return bounds_verdict(st, run_batchv(ctx, b.data(), k, ctx->bv_dense_segs, cls_of, launch, alone));
+  return bounds_verdict(st, run_batchv(ctx, b.data(), k, cls_of, launch, alone));
 }
 
 int ics_ipv4_tcp_batchv(ics_ctx* ctx, const ics_dgram_batch* batches, uint32_t k, int mode, void* stream) {
@@ -1261,7 +1256,7 @@ int ics_ipv4_tcp_batchv(ics_ctx* ctx, const ics_dgram_batch* batches, uint32_t k
     return ics_ipv4_tcp_batch(ctx, x.dgrams, x.offsets, x.stride, x.dlen, x.n, mode, x.ip_ck, x.tcp_ck, x.status,
                               stream);
   };
-  return bounds_verdict(st, run_batchv(ctx, b.data(), k, 4, cls_of, launch, alone));
+  return bounds_verdict(st, run_batchv(ctx, b.data(), k, cls_of, launch, alone));
 }
 
 int ics_tcp_wrap_headers_host(ics_ctx* ctx, const void* h_payloads, const uint64_t* h_offsets, uint64_t stride,

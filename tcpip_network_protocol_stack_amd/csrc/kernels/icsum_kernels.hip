@@ -1131,7 +1131,7 @@ __device__ __forceinline__ uint32_t bv_find(const BvTable<D>& t, uint32_t blk) {
   return __builtin_amdgcn_readfirstlane(uint32_t(__builtin_popcount(mask)));
 }
 
-template <int CLS, int DSEGS = 4>
+template <int CLS>
 __global__ __launch_bounds__(kBlock) void k_checksum_batchv(BvTable<BvSeg> t, const u32x4* __restrict__ zero16,
                                                             uint32_t remap) {
   const uint32_t blk = block_order(remap);  // XCD runs over the whole grid, batches in turn
@@ -1143,7 +1143,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_batchv(BvTable<BvSeg> t, co
   const uint8_t* op = reinterpret_cast<const uint8_t*>(zero16);
   const SegSrc src{b.offsets, b.stride, b.seg_len, nullptr, nullptr, -1};
   if constexpr (CLS == kBvDense64)
-    checksum_dense_body<4, DSEGS, true, 0>(reinterpret_cast<const u32x4*>(b.bytes), ip, is, b.out, b.n, lb);
+    checksum_dense_body<4, 4, true, 0>(reinterpret_cast<const u32x4*>(b.bytes), ip, is, b.out, b.n, lb);
   else if constexpr (CLS == kBvTiny)
     checksum_tiny_body<0>(b.bytes, src, ip, is, op, 0u, zero16, b.out, b.n, lb, nb);
   else if constexpr (CLS == kBvSmall)
@@ -1975,17 +1975,17 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
   return hipGetLastError();
 }
 
-uint64_t batchv_blocks(int cls, uint64_t n, int dense_segs) {
-  // segments per block: dense 64 groups x dense_segs in flight, tiny 256
-  // lanes, small 64 groups x 2 in flight, line grids kBlock / lanes per segment
-  const uint64_t per = cls == kBvDense64 ? 64 * uint64_t(dense_segs) : cls == kBvTiny || cls == kBvLane1 ? 256
-                       : cls == kBvSmall ? 128 : cls == kBvLine16 ? 16 : 4;
+uint64_t batchv_blocks(int cls, uint64_t n) {
+  // segments per block: dense 64 groups x 4 in flight, tiny 256 lanes,
+  // small 64 groups x 2 in flight, line grids kBlock / lanes per segment
+  const uint64_t per = cls == kBvDense64 || cls == kBvTiny || cls == kBvLane1 ? 256 : cls == kBvSmall ? 128
+                       : cls == kBvLine16 ? 16 : 4;
   return (n + per - 1) / per;
 }
 
 namespace {
 template <typename D>
-bool bv_table(const D* b, int k, int cls, int dense_segs, BvTable<D>& t, uint64_t& blocks) {
+bool bv_table(const D* b, int k, int cls, BvTable<D>& t, uint64_t& blocks) {
   if (k < 1 || k > kMaxBatchv) return false;
   t = {};
   t.k = uint32_t(k);
@@ -1993,7 +1993,7 @@ bool bv_table(const D* b, int k, int cls, int dense_segs, BvTable<D>& t, uint64_
   for (int j = k; j < kMaxBatchv; ++j) t.block0[j] = 0xFFFFFFFFu;  // no batch: never at or below a block
   for (int j = 0; j < k; ++j) {
     t.b[j] = b[j];
-    const uint64_t nb = batchv_blocks(cls, b[j].n, dense_segs);
+    const uint64_t nb = batchv_blocks(cls, b[j].n);
     if (nb == 0) return false;
     t.block0[j] = uint32_t(blocks);
     t.nblk[j] = uint32_t(nb);
@@ -2003,23 +2003,14 @@ bool bv_table(const D* b, int k, int cls, int dense_segs, BvTable<D>& t, uint64_
 }
 }  // namespace
 
-hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, int dense_segs, bool dense_remap,
-                                  const void* zero16, hipStream_t st) {
-  if (cls == kBvDense64 && dense_segs != 4 && dense_segs != 8) return hipErrorInvalidValue;
+hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, const void* zero16, hipStream_t st) {
   BvTable<BvSeg> t;
   uint64_t blocks = 0;
-  if (!bv_table(b, k, cls, dense_segs, t, blocks)) return hipErrorInvalidValue;
+  if (!bv_table(b, k, cls, t, blocks)) return hipErrorInvalidValue;
   const u32x4* z = static_cast<const u32x4*>(zero16);
   const dim3 grid{uint32_t(blocks), 1, 1};
   switch (cls) {
-    case kBvDense64:
-      if (dense_segs == 8)
-        hipLaunchKernelGGL((k_checksum_batchv<kBvDense64, 8>), grid, dim3(kBlock), 0, st, t, z,
-                           dense_remap ? g_xcd_remap : 0u);
-      else
-        hipLaunchKernelGGL((k_checksum_batchv<kBvDense64, 4>), grid, dim3(kBlock), 0, st, t, z,
-                           dense_remap ? g_xcd_remap : 0u);
-      break;
+    case kBvDense64: hipLaunchKernelGGL(k_checksum_batchv<kBvDense64>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
     case kBvTiny: hipLaunchKernelGGL(k_checksum_batchv<kBvTiny>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
     case kBvSmall: hipLaunchKernelGGL(k_checksum_batchv<kBvSmall>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
     case kBvLine16: hipLaunchKernelGGL(k_checksum_batchv<kBvLine16>, grid, dim3(kBlock), 0, st, t, z, g_xcd_remap); break;
@@ -2032,7 +2023,7 @@ hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, int dense_segs
 hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const void* zero16, hipStream_t st) {
   BvTable<BvDgram> t;
   uint64_t blocks = 0;
-  if (!bv_table(b, k, cls, 4, t, blocks)) return hipErrorInvalidValue;
+  if (!bv_table(b, k, cls, t, blocks)) return hipErrorInvalidValue;
   const uint8_t* z = static_cast<const uint8_t*>(zero16);
   const dim3 grid{uint32_t(blocks), 1, 1};
   switch (cls) {

@@ -136,13 +136,11 @@ static_assert(sizeof(BvSeg) == 64 && sizeof(BvDgram) == 64, "multi-batch descrip
 // the 16- and 64-lane line grids (MTU-sized / long or unknown mixes), and the
 // fused kernel's one lane per ACK-sized datagram
 enum BvClass : int { kBvDense64 = 0, kBvTiny = 1, kBvSmall = 2, kBvLine16 = 3, kBvLine64 = 4, kBvLane1 = 5 };
-// blocks one batch of n segments takes in a launch of class cls (dense_segs:
-// segments per lane group in flight of the dense class, 4 or 8)
-uint64_t batchv_blocks(int cls, uint64_t n, int dense_segs = 4);
+// blocks one batch of n segments takes in a launch of class cls
+uint64_t batchv_blocks(int cls, uint64_t n);
 // k batches (1 <= k <= kMaxBatchv) of one class; the caller keeps the sum of
 // their batchv_blocks below 2^24 (the dispatch's work-item limit)
-hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, int dense_segs, bool dense_remap,
-                                  const void* zero16, hipStream_t st);
+hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, const void* zero16, hipStream_t st);
 hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const void* zero16, hipStream_t st);
 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)

@@ -1,8 +1,9 @@
 #!/usr/bin/env python3
 """Dev tool: config 3 (1 M x 64 B with pseudo-header inits) through the dense
 kernel — one batch per call, one 8 M-segment batch (the same bytes as eight
-batches), and eight batches per ics_checksum_batchv call with 4 or 8
-segments per lane group in flight — interleaved in one process, outputs of
+batches), and eight batches per ics_checksum_batchv call (round 3 also
+measured 8 segments per lane group in flight and hardware block order for
+the multi-batch dense class: within noise, profiles/r3_ab_batchv_config3*) — interleaved in one process, outputs of
 every variant compared.  Prints one JSON line per variant: us per 1 M-segment
 batch and the fraction of 8 TB/s of segment bytes.
 
@@ -38,8 +39,7 @@ def main():
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     n, L, seed, K = 1 << 20, 64, 0x10710003, 8
-    e4, e8, s8 = engine(), engine(bv_dense_segs=8), engine(dense_segs=8)
-    e4h, e8h = engine(bv_dense_remap=0), engine(bv_dense_segs=8, bv_dense_remap=0)
+    e4, s8 = engine(), engine(dense_segs=8)
     big = e4.fill_bytes(torch.empty(2 * K * n * L, dtype=torch.uint8, device=dev), seed)
     binit = e4.pseudo_inits(2 * K * n, seed, seg_len=L)
     ds = [big[r * n * L:(r + 1) * n * L] for r in range(2 * K)]
@@ -58,14 +58,11 @@ def main():
                                                              init=inits[i % (2 * K)], out=outs[0])),
         "single_8M_segs8": (K, lambda i: s8.checksum_batch(big[(i % 2) * K * n * L:], n=K * n, stride=L, seg_len=L,
                                                              init=binit[(i % 2) * K * n:], out=bout)),
-        "batchv8_segs4": (K, lambda i: e4.checksum_batchv(sets[i % 2])),
-        "batchv8_segs8": (K, lambda i: e8.checksum_batchv(sets[i % 2])),
-        "batchv8_segs4_hworder": (K, lambda i: e4h.checksum_batchv(sets[i % 2])),
-        "batchv8_segs8_hworder": (K, lambda i: e8h.checksum_batchv(sets[i % 2])),
+        "batchv8": (K, lambda i: e4.checksum_batchv(sets[i % 2])),
     }
     # outputs agree: set 0 through every variant
     ref = [t.clone() for t in e4.checksum_batchv(sets[0])]
-    for e in (e4, e8, e4h, e8h):
+    for e in (e4,):
         got = e.checksum_batchv(sets[0])
         assert all(torch.equal(a, b) for a, b in zip(got, ref))
     e4.checksum_batch(big, n=K * n, stride=L, seg_len=L, init=binit, out=bout)
