@@ -171,3 +171,49 @@ def test_round2_dispatches_clean_and_identical(engine, force):
         torch.cuda.synchronize()
     finally:
         dbg.close()
+
+
+def test_batchv_clean_and_identical(dbg, engine):
+    """The multi-batch launches (ics_checksum_batchv / ics_ipv4_tcp_batchv)
+    under the bounds-checked build: every kernel shape they take (dense,
+    tiny, small, 16- and 64-lane line grids, one lane per ACK datagram),
+    clean and equal to the release library's."""
+    rng = np.random.default_rng(0xB0B)
+    bufs = []
+    for stride, L, n, lead in ((1500, 1500, 500, 0), (64, 64, 3000, 0), (40, 40, 2000, 0), (72, 64, 900, 3),
+                               (9000, 9000, 40, 0), (130, 128, 700, 1)):
+        bufs.append((rng.integers(0, 256, lead + n * stride + 16, dtype=np.uint8), stride, L, n, lead))
+    lens = rng.choice([0, 1, 40, 64, 576, 1500, 9000], 800)
+    off = np.zeros(lens.size + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    obuf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+
+    def batches():
+        out = []
+        for b, stride, L, n, lead in bufs:
+            d = _t(b)
+            out.append(dict(data=d[lead:] if lead else d, n=n, stride=stride, seg_len=L))
+        out.append(dict(data=_t(obuf), offsets=_t(off)))
+        return out
+
+    got = dbg.checksum_batchv(batches())
+    want = engine.checksum_batchv(batches())
+    for g, w in zip(got, want):
+        assert (_u(g, np.uint16) == _u(w, np.uint16)).all()
+    dg = []
+    for L, n in ((1500, 300), (40, 1500), (9000, 30)):
+        b = rng.integers(0, 256, n * L + 16, dtype=np.uint8)
+        b[0:n * L:L] = 0x45
+        dg.append((b, L, n))
+    for mode in (0, 1, 2):
+        d1 = [dict(dgrams=_t(b), n=n, stride=L, dgram_len=L) for b, L, n in dg] + \
+             [dict(dgrams=_t(obuf), offsets=_t(off))]
+        d2 = [dict(dgrams=_t(b), n=n, stride=L, dgram_len=L) for b, L, n in dg] + \
+             [dict(dgrams=_t(obuf), offsets=_t(off))]
+        r1 = dbg.ipv4_tcp_batchv(d1, mode)
+        r2 = engine.ipv4_tcp_batchv(d2, mode)
+        for x, y in zip(r1, r2):
+            for a, c in zip(x, y):
+                assert (a.cpu().numpy() == c.cpu().numpy()).all(), mode
+        for a, c in zip(d1, d2):
+            assert (a["dgrams"].cpu().numpy() == c["dgrams"].cpu().numpy()).all(), mode
