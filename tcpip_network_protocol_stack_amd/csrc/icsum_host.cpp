@@ -1,0 +1,339 @@
+// icsum_host.cpp — the host-memory (PCIe-inclusive) path behind the C-ABI's
+// *_host entry points: batches in host memory are cut into chunks that fit
+// the context's staging slots, and the slots take turns (one stream each) so
+// the copies, the kernels and the host-side stores of consecutive chunks
+// overlap.  The kernels are the device path's (icsum_dispatch.cpp's
+// geometry choice); there is no CPU arithmetic beyond folding the pieces of a
+// segment longer than a slot.
+#include <algorithm>
+#include <cstring>
+
+#include "icsum_ctx.h"
+
+namespace icsum::detail {
+namespace {
+
+int ensure_staging(ics_ctx* ctx) {
+  if (ctx->staged) return ICS_OK;
+  for (int k = 0; k < ctx->nslots; ++k) {
+    ICS_HIP(hipStreamCreateWithFlags(&ctx->st[k], hipStreamNonBlocking));
+    ICS_HIP(hipEventCreateWithFlags(&ctx->ev[k], hipEventDisableTiming));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_in[k]), ctx->slot_bytes, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_in[k]), ctx->slot_bytes));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_off[k]), (ics_ctx::kSlotSegs + 1) * 8, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_off[k]), (ics_ctx::kSlotSegs + 1) * 8));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_init[k]), ics_ctx::kSlotSegs * 4, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_init[k]), ics_ctx::kSlotSegs * 4));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_out[k]), ics_ctx::kSlotSegs * 5, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_out[k]), ics_ctx::kSlotSegs * 5));
+  }
+  ctx->staged = true;
+  return ICS_OK;
+}
+
+int ensure_wrap_staging(ics_ctx* ctx) {
+  if (ctx->wrap_staged) return ICS_OK;
+  for (int k = 0; k < ctx->nslots; ++k) {
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_msg[k]), ics_ctx::kWrapSlotSegs * sizeof(ics_tcp_msg), 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_msg[k]), ics_ctx::kWrapSlotSegs * sizeof(ics_tcp_msg)));
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_hdr[k]), ics_ctx::kWrapSlotSegs * 40, 0));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_hdr[k]), ics_ctx::kWrapSlotSegs * 40));
+    ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_sums[k]), ics_ctx::kWrapSlotSegs * 4));
+  }
+  ctx->wrap_staged = true;
+  return ICS_OK;
+}
+
+// One staged chunk of segments [i0, i1) covering bytes [b0, b1).  A segment
+// longer than a staging slot goes through the slots as PIECES: chunks with
+// piece = true, i1 = i0 + 1 and [b0, b1) a slot-sized part of that one
+// segment (pos = the part's offset inside it).
+struct Chunk {
+  uint64_t i0, i1, b0, b1;
+  bool piece = false, last = false;
+  uint64_t pos = 0;
+};
+
+// Next chunk starting at segment i0 (whose first `pos` bytes were already
+// staged as pieces) that fits the slot.
+int next_chunk(const ics_ctx* ctx, const uint64_t* offsets, uint64_t stride, uint64_t seg_len, uint64_t n,
+               uint64_t i0, uint64_t pos, bool allow_pieces, uint64_t cap_n, Chunk* c) {
+  const uint64_t cap_b = ctx->slot_bytes;
+  const uint64_t s0 = offsets ? offsets[i0] : i0 * stride;
+  const uint64_t len0 = offsets ? offsets[i0 + 1] - s0 : seg_len;
+  if (pos || len0 > cap_b) {  // segment i0 does not fit a slot: its next piece
+    if (!allow_pieces)
+      return fail(ICS_ERR_INVALID, "datagram %llu (%llu bytes) exceeds the %zu-byte staging slot",
+                  (unsigned long long)i0, (unsigned long long)len0, ctx->slot_bytes);
+    const uint64_t take = std::min<uint64_t>(cap_b, len0 - pos);
+    *c = {i0, i0 + 1, s0 + pos, s0 + pos + take, true, pos + take == len0, pos};
+    return ICS_OK;
+  }
+  if (!offsets) {
+    const uint64_t per = std::max<uint64_t>(stride, seg_len);
+    uint64_t k = per ? cap_b / per : cap_n;
+    if (k == 0) k = 1;  // stride > slot but the segment itself fits
+    k = std::min<uint64_t>({k, cap_n, n - i0});
+    *c = {i0, i0 + k, i0 * stride, (i0 + k - 1) * stride + seg_len};
+    return ICS_OK;
+  }
+  const uint64_t b0 = offsets[i0];
+  uint64_t i1 = i0;
+  while (i1 < n && i1 - i0 < cap_n && offsets[i1 + 1] - b0 <= cap_b) ++i1;
+  *c = {i0, i1, b0, offsets[i1]};
+  return ICS_OK;
+}
+
+// InternetChecksum::value() of a raw sum (util/tools/checksum.h:31-41)
+uint16_t fold_value(uint32_t sum) {
+  while (sum > 0xFFFFu) sum = (sum >> 16) + (sum & 0xFFFFu);
+  return uint16_t(~sum & 0xFFFFu);
+}
+
+// A piece is summed on the device as sub-pieces of this many bytes (one lane
+// group each, so a 32 MiB piece is 512 segments of work, not one long one);
+// even, so every sub-piece starts with the piece's parity.
+constexpr uint64_t kSubPiece = uint64_t(64) << 10;
+
+// Is [p, p+bytes) page-locked host memory the DMA engines can read directly?
+bool host_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory is not an error for us
+    return false;
+  }
+  return a.type == hipMemoryTypeHost;
+}
+
+// memcpy split over the context's copy workers: a single core copies pageable
+// memory into the pinned slots at ~10-20 GB/s, below what PCIe Gen5 x16 moves
+void par_memcpy(ics_ctx* ctx, void* dst, const void* src, size_t n) {
+  constexpr size_t kMinPerThread = size_t(4) << 20;
+  const size_t t = std::min<size_t>(ctx->copy_threads, std::max<size_t>(1, n / kMinPerThread));
+  if (t <= 1) {
+    std::memcpy(dst, src, n);
+    return;
+  }
+  if (!ctx->copy_pool) ctx->copy_pool = std::make_unique<icsum::detail::WorkerPool>(ctx->copy_threads - 1);
+  ctx->copy_pool->run(n, t, [=](size_t a, size_t b) {
+    std::memcpy(static_cast<char*>(dst) + a, static_cast<const char*>(src) + a, b - a);
+  });
+}
+
+// fn(j0, j1) over [0, m) datagrams on the copy workers (host-side stores into
+// the caller's batch at retire), serially below 16 Ki datagrams per range
+template <typename Fn>
+void host_ranges(ics_ctx* ctx, uint64_t m, Fn&& fn) {
+  constexpr uint64_t kMinPerThread = 16384;
+  const size_t t = std::min<size_t>(ctx->copy_threads, std::max<uint64_t>(1, m / kMinPerThread));
+  if (t <= 1) {
+    fn(size_t(0), size_t(m));
+    return;
+  }
+  if (!ctx->copy_pool) ctx->copy_pool = std::make_unique<icsum::detail::WorkerPool>(ctx->copy_threads - 1);
+  ctx->copy_pool->run(m, t, fn);
+}
+
+// ICS_MODE_PATCH's stores (k_ipv4_tcp, mode 2) applied on the host from a
+// COMPUTE pass's results: for every datagram of >= 20 bytes the IPv4
+// checksum goes to bytes 10..11; when >= 18 bytes follow the header
+// (4 * hlen clamped to [20, len]) the TCP checksum goes to bytes 16..17 of
+// the TCP header.  Both big-endian.  `res` = the slot's results: m ip u16,
+// m tcp u16, m status bytes.
+void host_patch_fields(uint8_t* bytes, const uint64_t* offsets, uint64_t stride, uint64_t dlen, const Chunk& c,
+                       const uint8_t* res, uint64_t j0, uint64_t j1) {
+  const uint64_t m = c.i1 - c.i0;
+  const uint16_t* ip = reinterpret_cast<const uint16_t*>(res);
+  const uint16_t* tcp = ip + m;
+  for (uint64_t j = j0; j < j1; ++j) {
+    const uint64_t i = c.i0 + j;
+    const uint64_t s = offsets ? offsets[i] : i * stride;
+    const uint64_t len = offsets ? offsets[i + 1] - s : dlen;
+    if (len < 20) continue;
+    uint8_t* d = bytes + s;
+    d[10] = uint8_t(ip[j] >> 8);
+    d[11] = uint8_t(ip[j]);
+    uint64_t off = 4u * (d[0] & 0x0fu);
+    if (off < 20) off = 20;
+    if (off > len) off = len;
+    if (len - off >= 18) {
+      d[off + 16] = uint8_t(tcp[j] >> 8);
+      d[off + 17] = uint8_t(tcp[j]);
+    }
+  }
+}
+
+}  // namespace
+
+void free_staging(ics_ctx* ctx) {
+  for (int k = 0; k < ics_ctx::kMaxSlots; ++k) {
+    if (ctx->st[k]) (void)hipStreamSynchronize(ctx->st[k]);
+    if (ctx->h_in[k]) (void)hipHostFree(ctx->h_in[k]);
+    if (ctx->d_in[k]) (void)hipFree(ctx->d_in[k]);
+    if (ctx->h_off[k]) (void)hipHostFree(ctx->h_off[k]);
+    if (ctx->d_off[k]) (void)hipFree(ctx->d_off[k]);
+    if (ctx->h_init[k]) (void)hipHostFree(ctx->h_init[k]);
+    if (ctx->d_init[k]) (void)hipFree(ctx->d_init[k]);
+    if (ctx->h_out[k]) (void)hipHostFree(ctx->h_out[k]);
+    if (ctx->d_out[k]) (void)hipFree(ctx->d_out[k]);
+    if (ctx->h_msg[k]) (void)hipHostFree(ctx->h_msg[k]);
+    if (ctx->d_msg[k]) (void)hipFree(ctx->d_msg[k]);
+    if (ctx->h_hdr[k]) (void)hipHostFree(ctx->h_hdr[k]);
+    if (ctx->d_hdr[k]) (void)hipFree(ctx->d_hdr[k]);
+    if (ctx->d_sums[k]) (void)hipFree(ctx->d_sums[k]);
+    if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
+    if (ctx->st[k]) (void)hipStreamDestroy(ctx->st[k]);
+  }
+  ctx->staged = false;
+  ctx->wrap_staged = false;
+}
+
+// kind 0: checksum batch (u16 out); kind 1: ipv4_tcp batch (ip u16, tcp u16, status u8);
+// kind 2: tcp wrap (40 header bytes per datagram back, written into h_bytes).
+// The slots take turns, one stream each: while the GPU moves and sums chunk
+// k, the host prepares chunk k+1.  Pinned user buffers are DMA'd directly (no
+// host copy); pageable ones are staged through the pinned slots by par_memcpy.
+int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets,
+                  uint64_t stride, uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode,
+                  uint16_t* out_a, uint16_t* out_b, uint8_t* out_c, const ics_tcp_msg* h_msgs) {
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  if (int rc = ensure_staging(ctx)) return rc;
+  if (kind == 2)
+    if (int rc = ensure_wrap_staging(ctx)) return rc;
+  const bool direct = host_pinned(h_bytes);
+  Chunk pending[ics_ctx::kMaxSlots];
+  bool busy[ics_ctx::kMaxSlots] = {};
+  uint32_t piece_sum = 0;  // running sum of the long segment whose pieces are in flight
+  auto retire = [&](int k) -> int {
+    if (!busy[k]) return ICS_OK;
+    ICS_HIP(hipEventSynchronize(ctx->ev[k]));
+    const Chunk& c = pending[k];
+    const uint64_t m = c.i1 - c.i0;
+    if (c.piece) {
+      // raw u32 sums of the piece's sub-pieces; uint32 addition is
+      // associative, so sum_ of the whole segment = init + every part's sum
+      // (each summed with its own start parity), wrap included
+      const uint64_t parts = (c.b1 - c.b0 + kSubPiece - 1) / kSubPiece;
+      const uint32_t* raw = reinterpret_cast<const uint32_t*>(ctx->h_out[k]);
+      for (uint64_t j = 0; j < parts; ++j) piece_sum += raw[j];
+      if (c.last) {
+        out_a[c.i0] = fold_value((h_init ? h_init[c.i0] : 0u) + piece_sum);
+        piece_sum = 0;
+      }
+    } else if (kind == 0) {
+      std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
+    } else if (kind == 2 && mode == 1) {  // payload-only: headers to the caller's array
+      std::memcpy(reinterpret_cast<uint8_t*>(out_c) + 40 * c.i0, ctx->h_hdr[k], m * 40);
+    } else if (kind == 2) {  // 40 header bytes into each datagram of the caller's batch
+      uint8_t* bytes = static_cast<uint8_t*>(h_bytes);
+      host_ranges(ctx, m, [&](size_t j0, size_t j1) {
+        for (uint64_t j = j0; j < j1; ++j) {
+          const uint64_t i = c.i0 + j;
+          const uint64_t s0 = h_offsets ? h_offsets[i] : i * stride;
+          const uint64_t len = h_offsets ? h_offsets[i + 1] - s0 : seg_len;
+          if (len >= 40) std::memcpy(bytes + s0, ctx->h_hdr[k] + 40 * j, 40);
+        }
+      });
+    } else {
+      if (out_a) std::memcpy(out_a + c.i0, ctx->h_out[k], m * 2);
+      if (out_b) std::memcpy(out_b + c.i0, ctx->h_out[k] + m * 2, m * 2);
+      if (out_c) std::memcpy(out_c + c.i0, ctx->h_out[k] + m * 4, m);
+      if (mode == ICS_MODE_PATCH)  // scattered 2-byte stores into the caller's batch
+        host_ranges(ctx, m, [&](size_t j0, size_t j1) {
+          host_patch_fields(static_cast<uint8_t*>(h_bytes), h_offsets, stride, seg_len, c, ctx->h_out[k], j0, j1);
+        });
+    }
+    busy[k] = false;
+    return ICS_OK;
+  };
+  uint64_t i0 = 0, pos = 0;
+  int slot = 0;
+  while (i0 < n) {
+    Chunk c;
+    if (int rc = next_chunk(ctx, h_offsets, stride, seg_len, n, i0, pos, kind == 0,
+                            kind == 2 ? ics_ctx::kWrapSlotSegs : ics_ctx::kSlotSegs, &c))
+      return rc;
+    if (int rc = retire(slot)) return rc;
+    const uint64_t m = c.i1 - c.i0, nb = c.b1 - c.b0;
+    uint8_t* src = static_cast<uint8_t*>(h_bytes) + c.b0;
+    if (!direct) {
+      par_memcpy(ctx, ctx->h_in[slot], src, nb);
+      src = ctx->h_in[slot];
+    }
+    hipStream_t st = ctx->st[slot];
+    ICS_HIP(hipMemcpyAsync(ctx->d_in[slot], src, nb, hipMemcpyHostToDevice, st));
+    if (c.piece) {
+      // ics_sum_batch over the piece's sub-pieces: raw sums, parity = the
+      // piece's offset in its segment (checksum.h:24-26 carried across add()s)
+      const uint64_t parts = (nb + kSubPiece - 1) / kSubPiece;
+      for (uint64_t j = 0; j <= parts; ++j) ctx->h_off[slot][j] = std::min<uint64_t>(j * kSubPiece, nb);
+      uint8_t* odd = reinterpret_cast<uint8_t*>(ctx->h_init[slot]);
+      std::memset(odd, int(c.pos & 1), parts);
+      ICS_HIP(hipMemcpyAsync(ctx->d_off[slot], ctx->h_off[slot], (parts + 1) * 8, hipMemcpyHostToDevice, st));
+      ICS_HIP(hipMemcpyAsync(ctx->d_init[slot], odd, parts, hipMemcpyHostToDevice, st));
+      const icsum::SegSpec sp{ctx->d_in[slot], ctx->d_off[slot], 0, 0, parts, ctx->d_zero};
+      ICS_HIP(icsum::launch_checksum(sp, nullptr, reinterpret_cast<const uint8_t*>(ctx->d_init[slot]),
+                                     ctx->d_out[slot], 1, geometry_for(ctx, kSubPiece), 0, st));
+      ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], parts * 4, hipMemcpyDeviceToHost, st));
+      ICS_HIP(hipEventRecord(ctx->ev[slot], st));
+      pending[slot] = c;
+      busy[slot] = true;
+      if (c.last) {
+        i0 = c.i1;
+        pos = 0;
+      } else {
+        pos = c.pos + nb;
+      }
+      slot = (slot + 1) % ctx->nslots;
+      continue;
+    }
+    const uint64_t* d_off = nullptr;
+    if (h_offsets) {
+      for (uint64_t j = 0; j <= m; ++j) ctx->h_off[slot][j] = h_offsets[c.i0 + j] - c.b0;
+      ICS_HIP(hipMemcpyAsync(ctx->d_off[slot], ctx->h_off[slot], (m + 1) * 8, hipMemcpyHostToDevice, st));
+      d_off = ctx->d_off[slot];
+    }
+    const icsum::SegSpec sp{ctx->d_in[slot], d_off, stride, seg_len, m, ctx->d_zero};
+    const uint64_t avg = h_offsets ? nb / m : seg_len;
+    const icsum::Geometry g = geometry_for(ctx, avg);
+    if (kind == 2) {
+      std::memcpy(ctx->h_msg[slot], h_msgs + c.i0, m * sizeof(ics_tcp_msg));
+      ICS_HIP(hipMemcpyAsync(ctx->d_msg[slot], ctx->h_msg[slot], m * sizeof(ics_tcp_msg), hipMemcpyHostToDevice, st));
+      ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(ctx->d_msg[slot]),
+                                     reinterpret_cast<uint32_t*>(ctx->d_hdr[slot]), nullptr, nullptr, mode == 1,
+                                     wrap_two_pass(ctx, true, m) ? ctx->d_sums[slot] : nullptr, ipv4_geometry(g),
+                                     0, st));
+      ICS_HIP(hipMemcpyAsync(ctx->h_hdr[slot], ctx->d_hdr[slot], m * 40, hipMemcpyDeviceToHost, st));
+    } else if (kind == 0) {
+      const uint32_t* d_init = nullptr;
+      if (h_init) {
+        std::memcpy(ctx->h_init[slot], h_init + c.i0, m * 4);
+        ICS_HIP(hipMemcpyAsync(ctx->d_init[slot], ctx->h_init[slot], m * 4, hipMemcpyHostToDevice, st));
+        d_init = ctx->d_init[slot];
+      }
+      ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, ctx->d_out[slot], 0, g, 0, st));
+      ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 2, hipMemcpyDeviceToHost, st));
+    } else {
+      uint16_t* a = reinterpret_cast<uint16_t*>(ctx->d_out[slot]);
+      uint16_t* b = a + m;
+      uint8_t* s = ctx->d_out[slot] + m * 4;
+      // PATCH from host memory: the device computes (COMPUTE gives the very
+      // values PATCH stores) and only the 5-byte results come back; the two
+      // fields are written into the caller's bytes on the host at retire,
+      // instead of copying every patched byte back over PCIe
+      const int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;
+      ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, ipv4_geometry(g), 0, st));
+      ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 5, hipMemcpyDeviceToHost, st));
+    }
+    ICS_HIP(hipEventRecord(ctx->ev[slot], st));
+    pending[slot] = c;
+    busy[slot] = true;
+    i0 = c.i1;
+    slot = (slot + 1) % ctx->nslots;
+  }
+  for (int k = 0; k < ctx->nslots; ++k)  // oldest first
+    if (int rc = retire((slot + k) % ctx->nslots)) return rc;
+  return bounds_verdict(ctx->st[0], ICS_OK);
+}
+
+}  // namespace icsum::detail

@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kBlock) void k_bin_plan(uint32_t* __restrict__ meta
     meta[kBinMetaPlan] = plan;
     const uint64_t avg = n ? total / n : 0;
     meta[kBinMetaAvgLen] = uint32_t(avg < 0xFFFFFFFFull ? avg : 0xFFFFFFFFull);
-    // the host's plan cache (icsum_api.cpp), one 8-byte store to page-locked
+    // the host's plan cache (icsum_dispatch.cpp), one 8-byte store to page-locked
     // host memory: the plan (bits 0-3), the share of bin-0 (<= 144-byte)
     // segments in sixteenths (bits 4-7), the batch size (bits 8-39), the
     // share of bytes in segments over 1920 bytes in sixteenths (bits 40-43)

@@ -1,5 +1,5 @@
 // icsum_launch.h — internal launcher interface between the C-ABI layer
-// (icsum_api.cpp) and the HIP kernels (icsum_kernels.hip).  Not installed.
+// (icsum_api.cpp, icsum_dispatch.cpp, icsum_host.cpp) and the HIP kernels (icsum_kernels.hip).  Not installed.
 #pragma once
 
 #include <hip/hip_runtime_api.h>
