@@ -3,7 +3,8 @@
 segments (1 M x 1460-1463 B, or 1 M x 40-43 B) through the binned dispatch
 (split plan forced), through the single long-segment launch, and through a
 single launch with the bin's own geometry (one lane group per segment, no
-list, no grid stride); interleaved in one process.
+list, no grid stride); interleaved in one process.  (Round 1 also ran the
+bin's geometry on a capped grid, a knob since removed: profiles/r1_ab_bins*.)
 
     python tools/ab_bins.py [--rounds 5]
 """
@@ -19,28 +20,14 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from tcpip_network_protocol_stack_amd.engine import Engine  # noqa: E402
+from _force import engine, geometry  # noqa: E402
 
 VARIANTS = {
-    "binned_split": {"ICSUM_BIN": "1", "ICSUM_BIN_PLAN": "1"},
-    "single_64x8": {"ICSUM_BIN": "0"},
-    "single_16x8m3": {"ICSUM_BIN": "0", "ICSUM_LPS": "16", "ICSUM_UNROLL": "8", "ICSUM_MODE": "3"},
-    "single_4x2s2": {"ICSUM_BIN": "0", "ICSUM_LPS": "4", "ICSUM_UNROLL": "2", "ICSUM_MODE": "2", "ICSUM_SEGS": "2"},
-    # the bin's geometry on a capped grid (grid stride, no list): isolates the stride from the list
-    "single_16x8m3_cap2k": {"ICSUM_BIN": "0", "ICSUM_LPS": "16", "ICSUM_UNROLL": "8", "ICSUM_MODE": "3",
-                            "ICSUM_MAX_BLOCKS": "2048"},
-    "single_16x8m3_cap8k": {"ICSUM_BIN": "0", "ICSUM_LPS": "16", "ICSUM_UNROLL": "8", "ICSUM_MODE": "3",
-                            "ICSUM_MAX_BLOCKS": "8192"},
+    "binned_split": {"bin": 1, "bin_plan": 1},
+    "single_64x8": {"bin": 0},
+    "single_16x8m3": {"bin": 0, **geometry(16, 8, 3)},
+    "single_4x2s2": {"bin": 0, **geometry(4, 2, 2, segs=2)},
 }
-
-
-def engine(env):
-    os.environ.update(env)
-    try:
-        return Engine(0)
-    finally:
-        for k in env:
-            del os.environ[k]
 
 
 def main():
@@ -49,7 +36,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    engs = {k: engine(v) for k, v in VARIANTS.items()}
+    engs = {k: engine(**v) for k, v in VARIANTS.items()}
     st = torch.cuda.current_stream()
     rng = np.random.default_rng(0x1460)
     n = 1 << 20
@@ -63,8 +50,7 @@ def main():
         doff = torch.from_numpy(off).to(dev)
         ref = e0.checksum_batch(d, offsets=doff)
         torch.cuda.synchronize()
-        names = [k for k in engs if not (kind == "mss_1460" and k == "single_4x2s2")
-                 and not (kind == "ack_40" and "cap" in k)]
+        names = [k for k in engs if not (kind == "mss_1460" and k == "single_4x2s2")]
         times = {k: [] for k in names}
         for r in range(args.rounds):
             for k in names if r % 2 == 0 else names[::-1]:

@@ -1,7 +1,6 @@
 #!/usr/bin/env python3
 """Dev tool: interleaved in-process A/B of the host-memory pipeline's staging
-(ICSUM_HOST_SLOTS slots of ICSUM_HOST_SLOT_MB each; a trailing "b", e.g.
-3x32b, adds ICSUM_HOST_BLOCKING_SYNC=1) on the PCIe-inclusive
+(ICSUM_HOST_SLOTS slots of ICSUM_HOST_SLOT_MB each) on the PCIe-inclusive
 row of tools/bench_configs.py (256 Ki x 1500 B from pinned and from pageable
 host memory, u16 results back), next to a bare H2D copy of the same bytes.
 
@@ -23,9 +22,8 @@ import torch  # noqa: E402
 from tcpip_network_protocol_stack_amd.engine import Engine  # noqa: E402
 
 
-def engine(slots, mb, blocking):
-    env = {"ICSUM_HOST_SLOTS": str(slots), "ICSUM_HOST_SLOT_MB": str(mb),
-           "ICSUM_HOST_BLOCKING_SYNC": "1" if blocking else "0"}
+def engine(slots, mb):
+    env = {"ICSUM_HOST_SLOTS": str(slots), "ICSUM_HOST_SLOT_MB": str(mb)}
     os.environ.update(env)
     try:
         return Engine(0)
@@ -42,8 +40,7 @@ def main():
     from oracle import oracle as orc  # workload bytes only (spec generator)
 
     n, L, seed = 1 << 18, 1500, 0x10710000
-    variants = [(int(v.split("x")[0]), int(v.split("x")[1].rstrip("b")), v.endswith("b"))
-                for v in args.variants.split(",")]
+    variants = [(int(v.split("x")[0]), int(v.split("x")[1])) for v in args.variants.split(",")]
     engs = {v: engine(*v) for v in variants}
     bufs = {}
     for pinned in (True, False):
@@ -71,7 +68,7 @@ def main():
         copy_ts.append(time.perf_counter() - t0)
     for (v, p), ts in times.items():
         med = statistics.median(ts)
-        print(json.dumps({"slots": v[0], "slot_MB": v[1], "blocking_sync": v[2], "pinned": p, "med_ms": round(med * 1e3, 3),
+        print(json.dumps({"slots": v[0], "slot_MB": v[1], "pinned": p, "med_ms": round(med * 1e3, 3),
                           "GB_s": round(n * L / med / 1e9, 2)}), flush=True)
     med = statistics.median(copy_ts)
     print(json.dumps({"bare_h2d_copy": True, "med_ms": round(med * 1e3, 3), "GB_s": round(n * L / med / 1e9, 2)}))

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Dev A/B: lane-group geometry of the fused IPv4/TCP kernel on BASELINE
 config 2 (64 Ki x 1500 B, 6 rotated copies), COMPUTE / VERIFY / PATCH,
-engines with forced ICSUM_LPS/UNROLL/MODE interleaved in one process."""
+engines with forced geometries (ICSUM_FORCE lps/unroll/mode) interleaved in one process."""
 import json
 import os
 import statistics
@@ -13,22 +13,12 @@ sys.path.insert(0, ROOT)
 
 import torch  # noqa: E402
 
-from tcpip_network_protocol_stack_amd.engine import Engine  # noqa: E402
-
-
-def engine(lps, unroll, mode):
-    env = {"ICSUM_LPS": str(lps), "ICSUM_UNROLL": str(unroll), "ICSUM_MODE": str(mode)}
-    os.environ.update(env)
-    try:
-        return Engine(0)
-    finally:
-        for k in env:
-            del os.environ[k]
+from _force import engine, geometry  # noqa: E402
 
 
 def main():
     variants = [v for v in (sys.argv[1] if len(sys.argv) > 1 else "16x8x3,32x4x3,16x6x3,32x3x3,16x5x3").split(",")]
-    engs = {v: engine(*map(int, v.split("x"))) for v in variants}
+    engs = {v: engine(**geometry(*map(int, v.split("x")))) for v in variants}
     dev = torch.device("cuda", 0)
     n, L, seed, R = 1 << 16, 1500, 0x10710002, 6
     base = engs[variants[0]]

@@ -17,17 +17,13 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from tcpip_network_protocol_stack_amd.engine import Engine  # noqa: E402
+from _force import engine, geometry  # noqa: E402
 
 PEAK = 8.0e12
 
 
-def engine_with(lps, unroll, mode, nt=1):
-    os.environ.update(ICSUM_LPS=str(lps), ICSUM_UNROLL=str(unroll), ICSUM_MODE=str(mode), ICSUM_NT=str(nt))
-    try:
-        return Engine(0)
-    finally:
-        for k in ("ICSUM_LPS", "ICSUM_UNROLL", "ICSUM_MODE", "ICSUM_NT"):
-            del os.environ[k]
+def engine_with(lps, unroll, mode):
+    return engine(**geometry(lps, unroll, mode))
 
 
 def timed(fn, iters=20, rounds=5):
@@ -73,9 +69,9 @@ def batch(eng, n, ack_frac, seed):
 def main():
     eng = Engine(0)
     forced = {f"{l}x{u}m{m}": engine_with(l, u, m) for l, u, m in ((4, 2, 2), (8, 2, 2), (8, 4, 3), (8, 8, 3), (16, 4, 3), (16, 8, 3), (32, 8, 3))}
-    if os.environ.get("AB_LANE1"):  # one lane per datagram (LPS 1, 16-byte grid), NT and default-policy loads
+    if os.environ.get("AB_LANE1"):  # one lane per datagram (mode 4: the IPv4 kernel's default-policy lane1 shape)
         forced = {k: forced[k] for k in ("4x2m2", "8x8m3")}
-        forced.update({"1x4m0": engine_with(1, 4, 0), "1x4m0c": engine_with(1, 4, 0, 0), "1x8m0": engine_with(1, 8, 0)})
+        forced.update({"1x4m4": engine_with(1, 4, 4)})
     fracs = [float(a) for a in sys.argv[1].split(",")] if len(sys.argv) > 1 else (0.5, 0.0)
     for ack_frac in fracs:
         n = 1 << 20

@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """Dev tool: interleaved in-process A/B of the binned dispatch's last-bin
-launch: its grid cap (ICSUM_LAST_BIN_BLOCKS; 0 = one lane group per segment of
-the batch), its lanes per segment (--var ICSUM_LAST_BIN_LPS --caps 64,32) or
-the plan (--var ICSUM_BIN_PLAN --caps 0,1,2,-1; -1 = decided on the device).  Workloads: BASELINE config 4 (1 M mixed 64 B-64 KiB,
+launch, each value an ICSUM_FORCE key: its grid cap (last_bin_blocks; 0 = one
+lane group per segment of the batch), its lanes per segment (--var
+last_bin_lps --caps 64,32) or the plan (--var bin_plan --caps=0,1,2,3,-1; -1 =
+decided on the device; --var bin --caps=-1,1 compares the plan cache with
+binning on every call).  Workloads: BASELINE config 4 (1 M mixed 64 B-64 KiB,
 whole-batch plan), the 2 M bimodal 40 B / 1460 B batch (split plan, empty last
 bin) and 2 M segments of 4-6 KiB (whole-batch plan with > 1 M segments).
 
@@ -20,18 +22,15 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from tcpip_network_protocol_stack_amd.engine import Engine, mixed_offsets  # noqa: E402
+from tcpip_network_protocol_stack_amd.engine import mixed_offsets  # noqa: E402
+from _force import engine as forced  # noqa: E402
 
 
-VAR = "ICSUM_LAST_BIN_BLOCKS"
+VAR = "last_bin_blocks"
 
 
 def engine(cap):
-    os.environ[VAR] = str(cap)
-    try:
-        return Engine(0)
-    finally:
-        del os.environ[VAR]
+    return forced(**{VAR: cap})
 
 
 def batch(kind, dev, eng):
@@ -58,7 +57,7 @@ def main():
     ap.add_argument("--caps", default="0,262144,131072")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
-    ap.add_argument("--var", default="ICSUM_LAST_BIN_BLOCKS")
+    ap.add_argument("--var", default="last_bin_blocks", help="ICSUM_FORCE key")
     ap.add_argument("--workloads", default="config4,bimodal,long2m", help="config4,bimodal,long2m,mss,ack")
     args = ap.parse_args()
     global VAR

@@ -1,9 +1,10 @@
 #!/usr/bin/env python3
 """Dev A/B: device-resident OFFSETS batches below the binning threshold
-(ICSUM_BIN_MIN, 64 Ki segments) run as one launch with the unknown-mix
-(64-lane) geometry.  Compares, interleaved in one process: the default, a
-lower ICSUM_BIN_MIN (binning + the plan cache, so repeat calls on the same
-offsets run the cached plan's single launch), and the best fixed geometry for
+(bin_min, 64 Ki segments) run as one launch, its geometry from the plan
+cache.  Compares, interleaved in one process: the default, a lower bin_min
+(ICSUM_FORCE bin_min=1024: binning + the plan cache, so repeat calls on the
+same offsets run the cached plan's single launch), binning on every call
+(bin=1: no plan cache), and the best fixed geometry for
 the length (forced), for 4-32 Ki segments of 64 / 576 / 1500 bytes."""
 import json
 import os
@@ -16,23 +17,12 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from tcpip_network_protocol_stack_amd.engine import Engine  # noqa: E402
-
-
-def engine(**env):
-    for k, v in env.items():
-        os.environ[k] = str(v)
-    try:
-        return Engine(0)
-    finally:
-        for k in env:
-            del os.environ[k]
+from _force import engine  # noqa: E402
 
 
 def main():
     dev = torch.device("cuda", 0)
-    engs = {"default": Engine(0), "binmin1k": engine(ICSUM_BIN_MIN=1024),
-            "binmin1k_nocache": engine(ICSUM_BIN_MIN=1024, ICSUM_PLAN_CACHE=0)}
+    engs = {"default": engine(), "binmin1k": engine(bin_min=1024), "binned_nocache": engine(bin=1)}
     for n in (8192, 16384, 32768, 65535):
         for L in (64, 576, 1500):
             R = max(2, (400 << 20) // (n * L) + 1)

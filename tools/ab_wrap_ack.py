@@ -1,8 +1,8 @@
 #!/usr/bin/env python3
 """Dev tool: the device wrap (ics_tcp_wrap_batch, in place) of pure-ACK and
 short messages — 1 M datagrams of 40-56 bytes, packed offsets — at the
-default geometry (16-lane groups) and one lane per datagram (forced
-ICSUM_LPS=1 ICSUM_UNROLL=4 ICSUM_MODE=0 ICSUM_NT=0); outputs compared."""
+default geometry (16-lane groups before the plan lands) and one lane per
+datagram (ICSUM_FORCE lps=1,unroll=4,mode=4); outputs compared."""
 import json
 import os
 import statistics
@@ -14,21 +14,12 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE, Engine  # noqa: E402
-
-
-def engine(env):
-    os.environ.update(env)
-    try:
-        return Engine(0)
-    finally:
-        for k in env:
-            del os.environ[k]
+from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE  # noqa: E402
+from _force import engine, geometry  # noqa: E402
 
 
 def main():
-    engs = {"default": engine({}), "lane1": engine({"ICSUM_LPS": "1", "ICSUM_UNROLL": "4", "ICSUM_MODE": "0",
-                                                    "ICSUM_NT": "0"})}
+    engs = {"default": engine(), "lane1": engine(**geometry(1, 4, 4))}
     rng = np.random.default_rng(0x3A)
     n = 1 << 20
     for name, lens in (("acks_40B", np.full(n, 40)), ("short_40_56B", rng.integers(40, 57, n))):

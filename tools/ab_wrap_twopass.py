@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Dev A/B: the device wrap as two passes (payload sums, then a header launch;
-ICSUM_WRAP_PASSES=2) vs the one-pass kernel that stores the headers inside the
-payload stream (ICSUM_WRAP_PASSES=1), beside the plain checksum of the same
+ICSUM_FORCE wrap_passes=2) vs the one-pass kernel that stores the headers inside the
+payload stream (wrap_passes=1), beside the plain checksum of the same
 payloads (the default picks two passes for headers apart, one in place).
 1 M x 1000-byte payloads / 1040-byte datagrams, interleaved rounds in one
 process; also 64 Ki x 1500 B (config 2's shape)."""
@@ -16,16 +16,14 @@ sys.path.insert(0, ROOT)
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE, Engine  # noqa: E402
+from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE  # noqa: E402
+from _force import engine  # noqa: E402
 
 
 def main():
     dev = torch.device("cuda", 0)
-    os.environ["ICSUM_WRAP_PASSES"] = "2"
-    two = Engine(0)
-    os.environ["ICSUM_WRAP_PASSES"] = "1"
-    one = Engine(0)
-    del os.environ["ICSUM_WRAP_PASSES"]
+    two = engine(wrap_passes=2)
+    one = engine(wrap_passes=1)
     for n, L in ((1 << 20, 1040), (1 << 16, 1500)):
         P, R = L - 40, max(3, (600 << 20) // (n * L) + 1)
         rng = np.random.default_rng(6)

@@ -1,6 +1,7 @@
 """Dev probe: mixed-length offsets batches through the binned and the
 single-geometry dispatch (run under rocprofv3 --kernel-trace to split the
-time per bin kernel).  ICSUM_BIN / ICSUM_BIN_BLOCKS come from the environment.
+time per bin kernel).  The dispatch comes from ICSUM_FORCE in the environment
+(e.g. bin=0 / bin=1,bin_blocks=8192).
 
     python tools/bin_probe.py {mixed|long|bimodal|mss|ack} [iters]
 """

@@ -6,4 +6,4 @@ cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-tiny2}; mkdir -p $O
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread > $O/pytest.log 2>&1
 timeout -k 10 300 python3 -u tools/ab_tiny.py > $O/ab_tiny.jsonl 2> $O/ab_tiny.err
-timeout -k 10 300 python3 -u tools/ab_lastbin.py --var ICSUM_PLAN_CACHE --caps 1,0 --workloads ack,bimodal,config4,mss > $O/ab_cache.jsonl 2> $O/ab_cache.err
+timeout -k 10 300 python3 -u tools/ab_lastbin.py --var bin --caps=-1,1 --workloads ack,bimodal,config4,mss > $O/ab_cache.jsonl 2> $O/ab_cache.err

@@ -1,12 +1,12 @@
 #!/usr/bin/env python3
-"""Dev tool: interleaved in-process A/B of kernel geometries (LPS, UNROLL, NT,
-grid cap) on the BASELINE workloads (cdna_hip_programming.md §5.4 rule 24).
+"""Dev tool: interleaved in-process A/B of kernel geometries (LPS, UNROLL,
+MODE, SEGS through ICSUM_FORCE; the load policy follows the geometry table)
+on the BASELINE workloads (cdna_hip_programming.md §5.4 rule 24).
 
     python tools/sweep_geometry.py [--workloads ns,tcp64,jumbo,mixed] [--rounds 5]
 Prints one JSON line per (workload, variant) with median/min kernel GB/s.
 """
 import argparse
-import itertools
 import json
 import os
 import statistics
@@ -19,6 +19,7 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from tcpip_network_protocol_stack_amd.engine import Engine, mixed_offsets  # noqa: E402
+from _force import engine, geometry  # noqa: E402
 
 WL = {"ns": (1 << 20, 1500), "tcp64": (1 << 20, 64), "jumbo": (1 << 20, 9000), "mixed": (1 << 20, None),
       "s128": (1 << 20, 128), "s256": (1 << 20, 256), "s576": (1 << 20, 576), "s3000": (1 << 19, 3000),
@@ -28,37 +29,24 @@ WL = {"ns": (1 << 20, 1500), "tcp64": (1 << 20, 64), "jumbo": (1 << 20, 9000), "
       "s1400": (1 << 20, 1400), "s1536": (1 << 20, 1536), "s1600": (1 << 20, 1600), "s1800": (1 << 20, 1800)}
 
 
-def make_engine(lps, unroll, nt, line, segs, cap):
-    env = {"ICSUM_LPS": str(lps), "ICSUM_UNROLL": str(unroll), "ICSUM_NT": str(int(nt)),
-           "ICSUM_MODE": str(int(line)), "ICSUM_SEGS": str(segs), "ICSUM_MAX_BLOCKS": str(cap)}
-    old = {k: os.environ.get(k) for k in env}
-    os.environ.update(env)
-    try:
-        return Engine(0)
-    finally:
-        for k, v in old.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+def make_engine(lps, unroll, mode, segs):
+    return engine(**geometry(lps, unroll, mode, segs=segs if segs > 1 else None))
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--workloads", default="ns,tcp64,jumbo,mixed")
     ap.add_argument("--variants", default="")
-    ap.add_argument("--caps", default="0")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=10)
     args = ap.parse_args()
-    # LPSxUNROLLxNT[xMODE[xSEGS]]
+    # LPSxUNROLL[xMODE[xSEGS]]
     def parse_variant(v):
         parts = [int(x) for x in v.split("x")]
-        return tuple(parts + [1, 0, 1][len(parts) - 2:])[:5]  # defaults: NT 1, MODE 0, SEGS 1
+        return tuple(parts + [3, 1][len(parts) - 2:])[:4]  # defaults: MODE 3 (line grid), SEGS 1
 
     variants = [parse_variant(v) for v in args.variants.split(",") if v] or [
-        (16, 6, 1, 0, 1), (16, 8, 1, 1, 1), (32, 4, 1, 1, 1), (64, 8, 1, 1, 1)]
-    caps = [int(c) for c in args.caps.split(",")]
+        (16, 8, 3, 1), (32, 8, 3, 1), (64, 8, 3, 1), (4, 2, 2, 2)]
     base = Engine(0)
     for wl in args.workloads.split(","):
         n, L = WL[wl]
@@ -75,8 +63,8 @@ def main():
         ref = base.checksum_batch(data, n=n, offsets=doff, stride=L or 0, seg_len=L or 0, init=init)
         torch.cuda.synchronize()
         engines = {}
-        for (lps, u, nt, line, segs), cap in itertools.product(variants, caps):
-            engines[(lps, u, nt, line, segs, cap)] = make_engine(lps, u, nt, line, segs, cap)
+        for lps, u, mode, segs in variants:
+            engines[(lps, u, mode, segs)] = make_engine(lps, u, mode, segs)
         times = {k: [] for k in engines}
         st = torch.cuda.current_stream()
         for r in range(args.rounds):
@@ -93,7 +81,7 @@ def main():
                     assert torch.equal(out, ref), f"variant {k} mismatch"
         for k, ts in times.items():
             med = statistics.median(ts)
-            print(json.dumps({"workload": wl, "lps": k[0], "unroll": k[1], "nt": k[2], "mode": k[3], "segs": k[4], "cap": k[5],
+            print(json.dumps({"workload": wl, "lps": k[0], "unroll": k[1], "mode": k[2], "segs": k[3],
                               "med_us": round(med * 1e6, 1), "med_GBs": round(total / med / 1e9, 1),
                               "best_GBs": round(total / min(ts) / 1e9, 1)}), flush=True)
         for e in engines.values():
