@@ -20,6 +20,7 @@ icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len) {
   if (ctx->force_lps) g = {ctx->force_lps, ctx->force_unroll ? ctx->force_unroll : g.unroll, g.nt, g.mode, 1};
   if (ctx->force_mode >= 0) g.mode = ctx->force_mode;
   if (ctx->force_segs > 0) g.segs = ctx->force_segs;
+  if (!icsum::geometry_supported(g)) g.nt = !g.nt;  // a forced shape exists with one load policy
   if (!icsum::geometry_supported(g)) g = icsum::pick_geometry(avg_len);
   return g;
 }
