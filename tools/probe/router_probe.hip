@@ -18,8 +18,10 @@
 //           write reaches the memory side (dword-aligned headers, stride >= 64,
 //           so no other datagram's bytes share those sectors)
 //   rdsec   the same 64-byte window loads, no store
+//   rt*     the shipped two-lane structure with a 4-byte store of bytes 8..11
+//           (w4) and / or 20-byte reads of aligned headers (r20), see k_rt
 // Every variant forwards (ttl--, checksum recomputed) the same datagrams, so
-// the copies start at ttl 255 and each is forwarded at most 120 times.
+// the copies start at ttl 255 and each is forwarded at most 240 times.
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../../include router_probe.hip -o router_probe
 #include "../../tcpip_network_protocol_stack_amd/csrc/kernels/icsum_kernels.hip"
 
@@ -162,6 +164,71 @@ __global__ __launch_bounds__(kBlock) void k_sec(uint8_t* __restrict__ dg, uint64
   }
 }
 
+// round 3 (later): the shipped kernel's two lanes per datagram, with
+//   W4      for a dword-aligned header whose reserved flag bit is clear (the
+//           flags byte then re-serializes to itself), ONE aligned 4-byte store
+//           of bytes 8..11 (ttl - 1, protocol, checksum) instead of the 8-byte
+//           store of bytes 4..11: it never straddles a 32-byte sector
+//   READ20  lane 1's third dword (header bytes 20..23, only needed to realign
+//           an unaligned header) re-reads dword 4 when the header is aligned
+template <bool READ20, bool W4>
+__global__ __launch_bounds__(kBlock) void k_rt(uint8_t* __restrict__ dg, uint64_t stride, uint64_t n,
+                                               uint8_t* __restrict__ status, const uint32_t* __restrict__ zpad) {
+  constexpr uint32_t kG = kBlock / 2;
+  const uint32_t lane = threadIdx.x & 1u;
+  const uint64_t step = uint64_t(gridDim.x) * kG;
+  for (uint64_t g0 = uint64_t(blockIdx.x) * kG; g0 < n; g0 += step) {
+    const uint64_t i = g0 + threadIdx.x / 2;
+    const bool valid = i < n;
+    uint64_t s, e;
+    seg_bounds(nullptr, stride, stride, valid ? i : n - 1, s, e);
+    const bool hdr = valid && e - s >= 20;
+    uint8_t* p = dg + s;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+    const uint32_t* q = hdr ? reinterpret_cast<const uint32_t*>(p - sh) : zpad;
+    const uint32_t* last = hdr ? last_dword(dg + e) : zpad + 7;
+    uint32_t mine[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      uint32_t idx = lane + 2u * k;
+      if (READ20 && k == 2 && sh == 0) idx = 4;
+      const uint32_t* a = q + idx;
+      mine[k] = *(a < last ? a : last);
+    }
+    const int pair = int(threadIdx.x & 63u & ~1u);
+    uint32_t d[6];
+#pragma unroll
+    for (int w = 0; w < 6; ++w) d[w] = uint32_t(__shfl(int(mine[w / 2]), pair + (w & 1), 64));
+    if (valid && lane == 0) {
+      uint8_t st = 0;
+      if (hdr) {
+        Hdr h;
+#pragma unroll
+        for (int k = 0; k < 5; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+        const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu, ttl = h.byte(8);
+        if (ver == 4 && hlen >= 5 && fold_value(ipv4_header_sum(h)) == h.be16(10) && ttl > 1) {
+          h.w[2] = (h.w[2] & ~0xffu) | (ttl - 1);
+          const uint32_t c = fold_value(ipv4_header_sum(h));
+          const uint32_t w2 = (h.w[2] & 0x0000ffffu) | ((c >> 8) << 16) | ((c & 0xffu) << 24);
+          if (W4 && sh == 0 && (h.byte(6) & 0x80u) == 0) {
+            *reinterpret_cast<uint32_t*>(p + 8) = w2;
+          } else if (sh == 0) {
+            uint32_t* o = reinterpret_cast<uint32_t*>(p + 4);
+            o[0] = h.w[1] & ~0x00800000u;
+            o[1] = w2;
+          } else {
+            p[6] = uint8_t(h.byte(6) & 0x7fu);
+            p[8] = uint8_t(ttl - 1);
+            store_be16(p + 10, c);
+          }
+          st = 1;
+        }
+      }
+      status[i] = st;
+    }
+  }
+}
+
 }  // namespace
 }  // namespace icsum
 
@@ -201,6 +268,11 @@ int main() {
   vs.push_back({"rd4", [&](int c) { hipLaunchKernelGGL((k_coop<4, false>), dim3(16384), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
   vs.push_back({"sec", [&](int c) { hipLaunchKernelGGL((k_sec<true>), dim3(16384), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
   vs.push_back({"rdsec", [&](int c) { hipLaunchKernelGGL((k_sec<false>), dim3(16384), dim3(256), 0, nullptr, d[c], kL, kN, st); }});
+  const uint32_t rt_blocks = uint32_t(std::min<uint64_t>((kN * 2 + kBlock - 1) / kBlock, 65536));
+  vs.push_back({"rt", [&](int c) { hipLaunchKernelGGL((k_rt<false, false>), dim3(rt_blocks), dim3(kBlock), 0, nullptr, d[c], kL, kN, st, reinterpret_cast<const uint32_t*>(zero)); }});
+  vs.push_back({"rt_w4", [&](int c) { hipLaunchKernelGGL((k_rt<false, true>), dim3(rt_blocks), dim3(kBlock), 0, nullptr, d[c], kL, kN, st, reinterpret_cast<const uint32_t*>(zero)); }});
+  vs.push_back({"rt_r20", [&](int c) { hipLaunchKernelGGL((k_rt<true, false>), dim3(rt_blocks), dim3(kBlock), 0, nullptr, d[c], kL, kN, st, reinterpret_cast<const uint32_t*>(zero)); }});
+  vs.push_back({"rt_w4_r20", [&](int c) { hipLaunchKernelGGL((k_rt<true, true>), dim3(rt_blocks), dim3(kBlock), 0, nullptr, d[c], kL, kN, st, reinterpret_cast<const uint32_t*>(zero)); }});
   {  // the whole-sector variant writes exactly the engine's bytes
     uint8_t *x = nullptr, *y = nullptr;
     CK(hipMalloc(&x, kN * kL + 64));
@@ -210,6 +282,21 @@ int main() {
     const SegSpec sp{x, nullptr, kL, kL, kN, zero};
     CK(launch_router_ttl(sp, st, nullptr));
     hipLaunchKernelGGL((k_sec<true>), dim3(16384), dim3(256), 0, nullptr, y, kL, kN, st);
+    CK(hipDeviceSynchronize());
+    {  // and the 4-byte-store / 20-byte-read variant, on a third copy
+      uint8_t* z = nullptr;
+      CK(hipMalloc(&z, kN * kL + 64));
+      CK(hipMemcpy(z, d[0], kN * kL + 64, hipMemcpyDeviceToDevice));
+      const uint32_t rb = uint32_t(std::min<uint64_t>((kN * 2 + kBlock - 1) / kBlock, 65536));
+      hipLaunchKernelGGL((k_rt<true, true>), dim3(rb), dim3(kBlock), 0, nullptr, z, kL, kN, st,
+                         reinterpret_cast<const uint32_t*>(zero));
+      CK(hipDeviceSynchronize());
+      std::vector<uint8_t> hx(kN * kL), hz(kN * kL);
+      CK(hipMemcpy(hx.data(), x, kN * kL, hipMemcpyDeviceToHost));
+      CK(hipMemcpy(hz.data(), z, kN * kL, hipMemcpyDeviceToHost));
+      printf("{\"rt_w4_r20_equals_engine\": %s}\n", hx == hz ? "true" : "false");
+      CK(hipFree(z));
+    }
     CK(hipDeviceSynchronize());
     std::vector<uint8_t> hx(kN * kL), hy(kN * kL);
     CK(hipMemcpy(hx.data(), x, kN * kL, hipMemcpyDeviceToHost));
@@ -225,15 +312,15 @@ int main() {
   for (int k = 0; k < 400; ++k) hipLaunchKernelGGL((k_coop<4, false>), dim3(16384), dim3(256), 0, nullptr, d[k % kCopies], kL, kN, st);
   CK(hipDeviceSynchronize());
   std::vector<std::vector<float>> t(vs.size());
-  for (int r = 0; r < 4; ++r) {
+  for (int r = 0; r < 12; ++r) {
     for (size_t v = 0; v < vs.size(); ++v) {
       CK(hipEventRecord(a, nullptr));
-      for (int k = 0; k < 6; ++k) vs[v].fn(k % kCopies);
+      for (int k = 0; k < 12; ++k) vs[v].fn(k % kCopies);
       CK(hipEventRecord(b, nullptr));
       CK(hipEventSynchronize(b));
       float ms = 0;
       CK(hipEventElapsedTime(&ms, a, b));
-      t[v].push_back(ms * 1e3f / 6);
+      t[v].push_back(ms * 1e3f / 12);
     }
   }
   std::vector<uint8_t> h(kN);
