@@ -3,7 +3,7 @@
 (PCIe) rate — the numbers DESIGN.md §Measurements quotes.  bench.py stays the
 driver's single headline line (north star); this is the wider table.
 
-    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch,wrap,streams,batchv] [--iters 20]
+    python tools/bench_configs.py [--only ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,ns64k,hostpatch,wrap,streams,batchv,stack] [--iters 20]
 
 Batches that fit the 256 MiB Infinity Cache (ipv4 98 MB, tcp64 67 MB) are
 rotated over >= 4 distinct copies (>= 393 / 268 MB) so every launch reads HBM.
@@ -408,6 +408,74 @@ def main():
                 ts.append(time.perf_counter() - t0)
             emit(f"wrap_host_256Kix1040_{'pinned' if pinned else 'pageable'}", nh * L, statistics.median(ts), nh * 68,
                  entry="ics_tcp_wrap_batch_host", note="H2D payloads + kernel + D2H of the 40 header bytes")
+
+    if "stack" in only:  # one stack tick: transmit wrap and receive VERIFY on their own buffers, interleaved
+        # (with one plan-cache entry each call evicted the other's plan; the keyed slots must
+        # leave each call's time and launch exactly what it is when the call runs alone)
+        from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE
+
+        n, seed = 1 << 18, 0x10710007
+        rng = np.random.default_rng(seed)
+        rl = np.where(rng.random(n) < 0.5, 40, 1500)  # received: half pure ACKs, half MTU segments
+        roff = np.zeros(n + 1, dtype=np.uint64)
+        roff[1:] = np.cumsum(rl)
+        tl = 40 + rng.integers(0, 1001, n)  # transmitted: payloads of 0..1000 bytes behind 40 bytes of room
+        toff = np.zeros(n + 1, dtype=np.uint64)
+        toff[1:] = np.cumsum(tl)
+        rx = eng.fill_bytes(torch.empty(int(roff[-1]) + 16, dtype=torch.uint8, device=dev), seed)
+        tx = eng.fill_bytes(torch.empty(int(toff[-1]) + 16, dtype=torch.uint8, device=dev), seed + 1)
+        drof = torch.from_numpy(roff.view(np.int64)).to(dev)
+        dtof = torch.from_numpy(toff.view(np.int64)).to(dev)
+        m = np.zeros(n, dtype=TCP_MSG_DTYPE)
+        for f, hi in (("src", 2**32), ("dst", 2**32), ("seqno", 2**32), ("ackno", 2**32), ("src_port", 2**16),
+                      ("dst_port", 2**16), ("window", 2**16)):
+            m[f] = rng.integers(0, hi, n, dtype=np.uint64)
+        m["flags"], m["ttl"] = 0x10, 128
+        dm = torch.from_numpy(m.view(np.uint8).copy()).to(dev)
+        ip = torch.empty(n, dtype=torch.int16, device=dev)
+        tcp = torch.empty(n, dtype=torch.int16, device=dev)
+        stt = torch.empty(n, dtype=torch.uint8, device=dev)
+
+        def verify():
+            eng.ipv4_tcp_batch(rx, 1, n=n, offsets=drof, ip_ck=ip, tcp_ck=tcp, status=stt)
+
+        def wrap():
+            eng.tcp_wrap_batch(tx, dm, n=n, offsets=dtof)
+
+        def per_call(fn, other, calls):
+            """median of per-call HIP-event times of fn, each call alone or right after `other`"""
+            st = torch.cuda.current_stream()
+            evs = []
+            for _ in range(calls):
+                if other:
+                    other()
+                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record(st)
+                fn()
+                b.record(st)
+                evs.append((a, b))
+            torch.cuda.synchronize()
+            return statistics.median(a.elapsed_time(b) / 1e3 for a, b in evs), eng.dispatch_info()
+
+        for _ in range(4):  # both keys miss once, then their plans land
+            verify()
+            wrap()
+        torch.cuda.synchronize()
+        calls = args.iters * args.rounds
+        rows = {}
+        for name, fn, other in (("verify_alone", verify, None), ("verify_after_wrap", verify, wrap),
+                                ("wrap_alone", wrap, None), ("wrap_after_verify", wrap, verify)):
+            before = eng.dispatch_info()
+            t, info = per_call(fn, other, calls)
+            rows[name] = t
+            nbytes = int(roff[-1]) if fn is verify else int(toff[-1])
+            emit(f"stack_tick_{name}", nbytes, t, n * (5 if fn is verify else 28),
+                 entry="ics_ipv4_tcp_batch VERIFY" if fn is verify else "ics_tcp_wrap_batch",
+                 last_kernel=info["kernel"], last_plan=info["plan"],
+                 plan_hits=info["plan_hits"] - before["plan_hits"],
+                 plan_misses=info["plan_misses"] - before["plan_misses"],
+                 note="median per-call HIP-event time; 256 Ki datagrams, packed offsets")
+        del rx, tx
     eng.close()
 
 
