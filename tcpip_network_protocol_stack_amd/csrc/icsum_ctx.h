@@ -156,6 +156,14 @@ struct ics_ctx {
   // wrap from host memory (allocated on first use): per slot up to
   // kWrapSlotSegs messages in, 40 header bytes per datagram back
   static constexpr size_t kWrapSlotSegs = size_t(1) << 18;
+  // a host-memory batch of at most this many bytes that fits one slot is not
+  // copied to the device: the kernel reads it (and its offsets, inits or
+  // messages) straight from page-locked memory over PCIe and writes its
+  // results straight into the pinned result area — one launch and one
+  // synchronisation per call instead of DMA copies on either side, which is
+  // what a per-tick TUN / socket batch pays for ("Per-tick host
+  // batches"); ICSUM_FORCE zero_copy_max=0 turns it off (tests)
+  uint64_t zero_copy_max = uint64_t(768) << 10;
   bool wrap_staged = false;
   uint8_t* h_msg[kMaxSlots] = {};
   uint8_t* d_msg[kMaxSlots] = {};

@@ -507,6 +507,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "twoclass" && (v == 0 || v == 16 || v == 32)) ctx->twoclass = int(v);
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
+    else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);
     else return fail(ICS_ERR_INVALID, "ICSUM_FORCE: unknown or out-of-range '%s'", item.c_str());
   }
   return ICS_OK;

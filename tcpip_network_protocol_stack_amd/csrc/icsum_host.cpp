@@ -13,6 +13,22 @@
 namespace icsum::detail {
 namespace {
 
+// Is p page-locked host memory the DMA engines can read directly, and can a
+// kernel address it at the same address (hipHostMalloc memory under the
+// unified address space; a registered range mapped elsewhere is only DMA'd)?
+struct Pinned {
+  bool dma = false, kernel = false;
+};
+Pinned host_pinned(const void* p) {
+  hipPointerAttribute_t a{};
+  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+    (void)hipGetLastError();  // pageable memory is not an error for us
+    return {};
+  }
+  const bool host = a.type == hipMemoryTypeHost;
+  return {host, host && a.devicePointer == p};
+}
+
 int ensure_staging(ics_ctx* ctx) {
   if (ctx->staged) return ICS_OK;
   for (int k = 0; k < ctx->nslots; ++k) {
@@ -26,6 +42,10 @@ int ensure_staging(ics_ctx* ctx) {
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_init[k]), ics_ctx::kSlotSegs * 4));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_out[k]), ics_ctx::kSlotSegs * 5, 0));
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_out[k]), ics_ctx::kSlotSegs * 5));
+    // the zero-copy path hands these very addresses to kernels
+    for (const void* h : {static_cast<const void*>(ctx->h_in[k]), static_cast<const void*>(ctx->h_off[k]),
+                          static_cast<const void*>(ctx->h_init[k]), static_cast<const void*>(ctx->h_out[k])})
+      if (!host_pinned(h).kernel) ctx->zero_copy_max = 0;
   }
   ctx->staged = true;
   return ICS_OK;
@@ -39,6 +59,7 @@ int ensure_wrap_staging(ics_ctx* ctx) {
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_hdr[k]), ics_ctx::kWrapSlotSegs * 40, 0));
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_hdr[k]), ics_ctx::kWrapSlotSegs * 40));
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_sums[k]), ics_ctx::kWrapSlotSegs * 4));
+    if (!host_pinned(ctx->h_msg[k]).kernel || !host_pinned(ctx->h_hdr[k]).kernel) ctx->zero_copy_max = 0;
   }
   ctx->wrap_staged = true;
   return ICS_OK;
@@ -95,15 +116,6 @@ uint16_t fold_value(uint32_t sum) {
 // even, so every sub-piece starts with the piece's parity.
 constexpr uint64_t kSubPiece = uint64_t(64) << 10;
 
-// Is [p, p+bytes) page-locked host memory the DMA engines can read directly?
-bool host_pinned(const void* p) {
-  hipPointerAttribute_t a{};
-  if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-    (void)hipGetLastError();  // pageable memory is not an error for us
-    return false;
-  }
-  return a.type == hipMemoryTypeHost;
-}
 
 // memcpy split over the context's copy workers: a single core copies pageable
 // memory into the pinned slots at ~10-20 GB/s, below what PCIe Gen5 x16 moves
@@ -193,6 +205,10 @@ void free_staging(ics_ctx* ctx) {
 // The slots take turns, one stream each: while the GPU moves and sums chunk
 // k, the host prepares chunk k+1.  Pinned user buffers are DMA'd directly (no
 // host copy); pageable ones are staged through the pinned slots by par_memcpy.
+// A batch of at most ctx->zero_copy_max bytes in one chunk is not DMA'd at
+// all: the kernel reads the pinned bytes, offsets, inits and messages over
+// PCIe and writes its results into the pinned result area (one launch, one
+// synchronisation).
 int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets,
                   uint64_t stride, uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode,
                   uint16_t* out_a, uint16_t* out_b, uint8_t* out_c, const ics_tcp_msg* h_msgs) {
@@ -200,7 +216,8 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   if (int rc = ensure_staging(ctx)) return rc;
   if (kind == 2)
     if (int rc = ensure_wrap_staging(ctx)) return rc;
-  const bool direct = host_pinned(h_bytes);
+  const Pinned pin = host_pinned(h_bytes);
+  const bool direct = pin.dma;
   Chunk pending[ics_ctx::kMaxSlots];
   bool busy[ics_ctx::kMaxSlots] = {};
   uint32_t piece_sum = 0;  // running sum of the long segment whose pieces are in flight
@@ -255,13 +272,24 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       return rc;
     if (int rc = retire(slot)) return rc;
     const uint64_t m = c.i1 - c.i0, nb = c.b1 - c.b0;
+    const bool zc = !c.piece && c.i0 == 0 && c.i1 == n && nb <= ctx->zero_copy_max;
     uint8_t* src = static_cast<uint8_t*>(h_bytes) + c.b0;
-    if (!direct) {
+    if (zc ? !pin.kernel : !direct) {
       par_memcpy(ctx, ctx->h_in[slot], src, nb);
       src = ctx->h_in[slot];
     }
     hipStream_t st = ctx->st[slot];
-    ICS_HIP(hipMemcpyAsync(ctx->d_in[slot], src, nb, hipMemcpyHostToDevice, st));
+    if (!zc) ICS_HIP(hipMemcpyAsync(ctx->d_in[slot], src, nb, hipMemcpyHostToDevice, st));
+    // where the kernel finds the chunk's inputs and leaves its results
+    uint8_t* const in = zc ? src : ctx->d_in[slot];
+    uint8_t* const res = zc ? ctx->h_out[slot] : ctx->d_out[slot];
+    auto h2d = [&](void* d, const void* h, size_t bytes, const void** where) -> hipError_t {
+      *where = zc ? h : d;
+      return zc ? hipSuccess : hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
+    };
+    auto d2h = [&](void* h, const void* d, size_t bytes) -> hipError_t {
+      return zc ? hipSuccess : hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, st);
+    };
     if (c.piece) {
       // ics_sum_batch over the piece's sub-pieces: raw sums, parity = the
       // piece's offset in its segment (checksum.h:24-26 carried across add()s)
@@ -290,40 +318,44 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
     const uint64_t* d_off = nullptr;
     if (h_offsets) {
       for (uint64_t j = 0; j <= m; ++j) ctx->h_off[slot][j] = h_offsets[c.i0 + j] - c.b0;
-      ICS_HIP(hipMemcpyAsync(ctx->d_off[slot], ctx->h_off[slot], (m + 1) * 8, hipMemcpyHostToDevice, st));
-      d_off = ctx->d_off[slot];
+      const void* w = nullptr;
+      ICS_HIP(h2d(ctx->d_off[slot], ctx->h_off[slot], (m + 1) * 8, &w));
+      d_off = static_cast<const uint64_t*>(w);
     }
-    const icsum::SegSpec sp{ctx->d_in[slot], d_off, stride, seg_len, m, ctx->d_zero};
+    const icsum::SegSpec sp{in, d_off, stride, seg_len, m, ctx->d_zero};
     const uint64_t avg = h_offsets ? nb / m : seg_len;
     const icsum::Geometry g = geometry_for(ctx, avg);
     if (kind == 2) {
       std::memcpy(ctx->h_msg[slot], h_msgs + c.i0, m * sizeof(ics_tcp_msg));
-      ICS_HIP(hipMemcpyAsync(ctx->d_msg[slot], ctx->h_msg[slot], m * sizeof(ics_tcp_msg), hipMemcpyHostToDevice, st));
-      ICS_HIP(icsum::launch_tcp_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(ctx->d_msg[slot]),
-                                     reinterpret_cast<uint32_t*>(ctx->d_hdr[slot]), nullptr, nullptr, mode == 1,
+      const void* msgs = nullptr;
+      ICS_HIP(h2d(ctx->d_msg[slot], ctx->h_msg[slot], m * sizeof(ics_tcp_msg), &msgs));
+      uint8_t* hdr = zc ? ctx->h_hdr[slot] : ctx->d_hdr[slot];
+      ICS_HIP(icsum::launch_tcp_wrap(sp, static_cast<const icsum::TcpMsg*>(msgs), reinterpret_cast<uint32_t*>(hdr),
+                                     nullptr, nullptr, mode == 1,
                                      wrap_two_pass(ctx, true, m) ? ctx->d_sums[slot] : nullptr, ipv4_geometry(g),
                                      0, st));
-      ICS_HIP(hipMemcpyAsync(ctx->h_hdr[slot], ctx->d_hdr[slot], m * 40, hipMemcpyDeviceToHost, st));
+      ICS_HIP(d2h(ctx->h_hdr[slot], ctx->d_hdr[slot], m * 40));
     } else if (kind == 0) {
       const uint32_t* d_init = nullptr;
       if (h_init) {
         std::memcpy(ctx->h_init[slot], h_init + c.i0, m * 4);
-        ICS_HIP(hipMemcpyAsync(ctx->d_init[slot], ctx->h_init[slot], m * 4, hipMemcpyHostToDevice, st));
-        d_init = ctx->d_init[slot];
+        const void* w = nullptr;
+        ICS_HIP(h2d(ctx->d_init[slot], ctx->h_init[slot], m * 4, &w));
+        d_init = static_cast<const uint32_t*>(w);
       }
-      ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, ctx->d_out[slot], 0, g, 0, st));
-      ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 2, hipMemcpyDeviceToHost, st));
+      ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, res, 0, g, 0, st));
+      ICS_HIP(d2h(ctx->h_out[slot], ctx->d_out[slot], m * 2));
     } else {
-      uint16_t* a = reinterpret_cast<uint16_t*>(ctx->d_out[slot]);
+      uint16_t* a = reinterpret_cast<uint16_t*>(res);
       uint16_t* b = a + m;
-      uint8_t* s = ctx->d_out[slot] + m * 4;
+      uint8_t* s = res + m * 4;
       // PATCH from host memory: the device computes (COMPUTE gives the very
       // values PATCH stores) and only the 5-byte results come back; the two
       // fields are written into the caller's bytes on the host at retire,
       // instead of copying every patched byte back over PCIe
       const int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;
       ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, ipv4_geometry(g), 0, st));
-      ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], m * 5, hipMemcpyDeviceToHost, st));
+      ICS_HIP(d2h(ctx->h_out[slot], ctx->d_out[slot], m * 5));
     }
     ICS_HIP(hipEventRecord(ctx->ev[slot], st));
     pending[slot] = c;

@@ -1,0 +1,120 @@
+"""GPU: the host-memory entry points on per-tick batch sizes (the TUN /
+socket event loop's few datagrams per tick, util/tuntap/tuntap_adapter.cpp:5-21
+inside util/tcp_minnow_socket/tcp_minnow_socket.h:138-164).
+
+A host batch that fits one staging chunk and at most `zero_copy_max` bytes
+is not DMA'd: the kernel reads the page-locked bytes (the caller's own when
+they are page-locked, the staging slot's otherwise), offsets, inits and
+messages over PCIe and writes its results into the page-locked result area
+(icsum_host.cpp, DESIGN.md §6 "Per-tick host batches").  Every case runs on
+three engines — the default threshold, zero-copy off (zero_copy_max=0: the
+DMA path on the same sizes) and zero-copy for every one-chunk batch
+(zero_copy_max=2^30) — against the oracle, from pageable and page-locked
+memory, at odd starts, with the calls of different sizes and kinds
+interleaved on one engine so a result area reused between calls cannot
+pass on stale results."""
+import numpy as np
+import pytest
+
+from helpers import pack_contiguous
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=["auto", "0", str(1 << 30)])
+def zeng(request):
+    from conftest import engine_with
+
+    yield from engine_with(None if request.param == "auto" else {"zero_copy_max": request.param})
+
+
+def _host(buf, pinned):
+    import torch
+
+    h = torch.empty(buf.size, dtype=torch.uint8, pin_memory=pinned).numpy()
+    h[:] = buf
+    return h
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_zc_checksum_fixed_and_offsets(zeng, orc, pinned):
+    rng = np.random.default_rng(41)
+    for n in (1, 2, 17, 300, 5000):
+        L = 1500
+        buf = _host(rng.integers(0, 256, n * L + 3, dtype=np.uint8), pinned)
+        init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        got = zeng.checksum_batch_host(buf, n, stride=L, seg_len=L - 1, init=init)
+        assert (got == orc.checksum_batch(buf, n, stride=L, seg_len=L - 1, init=init)).all(), n
+        lens = rng.integers(0, 3000, n)
+        segs = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in lens]
+        b2, off = pack_contiguous(segs, 3)
+        h2 = _host(b2, pinned)
+        got = zeng.checksum_batch_host(h2, n, offsets=off)
+        assert (got == orc.checksum_batch(b2, n, offsets=off)).all(), n
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("lead", [0, 3])
+def test_zc_ipv4_every_mode(zeng, orc, pinned, lead):
+    from test_gpu_parity import _random_datagrams
+
+    rng = np.random.default_rng(7 + lead)
+    for n in (1, 7, 300):
+        segs = _random_datagrams(rng, n)
+        buf, off = pack_contiguous(segs, lead)
+        for mode in (0, 1, 2):
+            h = _host(buf, pinned)
+            ip, tcp, st = zeng.ipv4_tcp_batch_host(h, n, mode, offsets=off)
+            hb = buf.copy()
+            w = orc.ipv4_tcp_batch(hb, n, mode, offsets=off)
+            assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), (n, mode)
+            assert (h == hb).all(), (n, mode)
+    # fixed stride, MTU-sized: PATCH, then VERIFY over the patched bytes
+    n, L = 64, 1500
+    data = orc.fill_bytes(0x10710002, 0, n * L)
+    h = _host(data, pinned)
+    zeng.ipv4_tcp_batch_host(h, n, 2, stride=L, dgram_len=L)
+    ip, tcp, st = zeng.ipv4_tcp_batch_host(h, n, 1, stride=L, dgram_len=L)
+    w = orc.ipv4_tcp_batch(h.copy(), n, 1, stride=L, dgram_len=L)
+    assert (st == w[2]).all() and (tcp == w[1]).all() and (ip == w[0]).all()
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_zc_wrap_in_place_and_headers_apart(zeng, orc, pinned):
+    from test_gpu_wrap import _oracle_wire, _random_batch
+
+    rng = np.random.default_rng(99)
+    for n in (1, 33, 500):
+        segs, m = _random_batch(rng, n)
+        want = _oracle_wire(orc, segs, m)
+        buf, off = pack_contiguous(segs, 1)
+        h = _host(buf, pinned)
+        zeng.tcp_wrap_batch_host(h, m, n, offsets=off)
+        for i, w in enumerate(want):
+            assert h[off[i]:off[i + 1]].tobytes() == w, (n, i)
+        pays = [s[40:] for s in segs]
+        pb, poff = pack_contiguous(pays, 2)
+        hdrs = zeng.tcp_wrap_headers_host(_host(pb, pinned), m, n, offsets=poff)
+        for i, w in enumerate(want):
+            assert hdrs[40 * i:40 * i + 40].tobytes() == w[:40], (n, i)
+
+
+def test_zc_interleaved_calls_no_stale_results(zeng, orc):
+    """Calls of different kinds and sizes in turn on one engine (the result
+    areas of the staging slots are reused): each one equals the oracle."""
+    from test_gpu_parity import _random_datagrams
+
+    rng = np.random.default_rng(5)
+    for r in range(12):
+        n = int(rng.integers(1, 40))
+        if r % 3 == 0:
+            buf = rng.integers(0, 256, n * 576, dtype=np.uint8)
+            got = zeng.checksum_batch_host(buf, n, stride=576, seg_len=576)
+            assert (got == orc.checksum_batch(buf, n, stride=576, seg_len=576)).all(), r
+        else:
+            segs = _random_datagrams(rng, n)
+            buf, off = pack_contiguous(segs, r % 4)
+            mode = r % 3
+            ip, tcp, st = zeng.ipv4_tcp_batch_host(buf.copy(), n, mode, offsets=off)
+            w = orc.ipv4_tcp_batch(buf.copy(), n, mode, offsets=off)
+            assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), r

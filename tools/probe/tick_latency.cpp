@@ -1,0 +1,143 @@
+// tick_latency.cpp — dev tool: wall time of ONE host-memory engine call per
+// batch, the way a TUN / socket event loop calls it each tick
+// (util/tuntap/tuntap_adapter.cpp:5-21 inside
+// util/tcp_minnow_socket/tcp_minnow_socket.h:138-164: a few datagrams per
+// tick, results needed before the next).  Loads one or more builds of
+// libicsum.so side by side (dlopen, RTLD_LOCAL) and times them interleaved on
+// the same buffers; every build's outputs must equal the first's.
+//   g++ -O2 -std=c++17 -I../../include tick_latency.cpp -o tick_latency -ldl
+//   tick_latency libA.so [libB.so ...]
+#include <dlfcn.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <chrono>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "icsum.h"
+
+namespace {
+
+struct Lib {
+  std::string path;
+  ics_ctx* ctx = nullptr;
+  int (*create)(int, ics_ctx**);
+  int (*destroy)(ics_ctx*);
+  int (*host_alloc)(ics_ctx*, void**, size_t);
+  int (*checksum_host)(ics_ctx*, const void*, const uint64_t*, uint64_t, uint64_t, const uint32_t*, uint16_t*,
+                       uint64_t);
+  int (*ipv4_host)(ics_ctx*, void*, const uint64_t*, uint64_t, uint64_t, uint64_t, int, uint16_t*, uint16_t*,
+                   uint8_t*);
+  int (*wrap_host)(ics_ctx*, void*, const uint64_t*, uint64_t, uint64_t, uint64_t, const ics_tcp_msg*);
+  const char* (*last_error)();
+};
+
+template <typename F>
+void sym(void* h, const char* name, F& f) {
+  f = reinterpret_cast<F>(dlsym(h, name));
+  if (!f) {
+    fprintf(stderr, "missing %s\n", name);
+    exit(1);
+  }
+}
+
+Lib open_lib(const char* path) {
+  Lib l;
+  l.path = path;
+  void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  if (!h) {
+    fprintf(stderr, "dlopen %s: %s\n", path, dlerror());
+    exit(1);
+  }
+  sym(h, "ics_create", l.create);
+  sym(h, "ics_destroy", l.destroy);
+  sym(h, "ics_host_alloc", l.host_alloc);
+  sym(h, "ics_checksum_batch_host", l.checksum_host);
+  sym(h, "ics_ipv4_tcp_batch_host", l.ipv4_host);
+  sym(h, "ics_tcp_wrap_batch_host", l.wrap_host);
+  sym(h, "ics_last_error", l.last_error);
+  if (l.create(0, &l.ctx) != ICS_OK) {
+    fprintf(stderr, "ics_create: %s\n", l.last_error());
+    exit(1);
+  }
+  return l;
+}
+
+void check(const Lib& l, int rc) {
+  if (rc != ICS_OK) {
+    fprintf(stderr, "%s: %s\n", l.path.c_str(), l.last_error());
+    exit(1);
+  }
+}
+
+using clk = std::chrono::steady_clock;
+
+double pct(std::vector<double> v, double p) {
+  std::sort(v.begin(), v.end());
+  return v[size_t(p * double(v.size() - 1))];
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    fprintf(stderr, "usage: %s lib.so [lib.so ...]\n", argv[0]);
+    return 2;
+  }
+  std::vector<Lib> libs;
+  for (int i = 1; i < argc; ++i) libs.push_back(open_lib(argv[i]));
+  constexpr uint64_t kL = 1500, kMaxN = 4096;
+  std::vector<uint8_t> pageable(kMaxN * kL);
+  std::mt19937_64 rng(7);
+  for (auto& b : pageable) b = uint8_t(rng());
+  uint8_t* pinned = nullptr;
+  check(libs[0], libs[0].host_alloc(libs[0].ctx, reinterpret_cast<void**>(&pinned), kMaxN * kL));
+  memcpy(pinned, pageable.data(), kMaxN * kL);
+  std::vector<ics_tcp_msg> msgs(kMaxN);
+  for (uint64_t i = 0; i < kMaxN; ++i) {
+    msgs[i] = ics_tcp_msg{0x0a000001u, 0x0a000002u, uint32_t(rng()), uint32_t(rng()), 40000, 80, 64000, 0x10, 128,
+                          0, 0};
+  }
+  const uint64_t sizes[] = {1, 4, 16, 64, 256, 512, 1024, 4096};
+  const char* ops[] = {"verify", "checksum", "wrap"};
+  const int rounds = 5, calls = 200;
+  for (const char* op : ops)
+    for (int mem = 0; mem < 2; ++mem)
+      for (uint64_t n : sizes) {
+        uint8_t* src = mem ? pinned : pageable.data();
+        std::vector<std::vector<double>> t(libs.size());
+        std::vector<std::vector<uint8_t>> res(libs.size(), std::vector<uint8_t>(n * kL + n * 5));
+        for (int r = 0; r < rounds; ++r)
+          for (size_t k = 0; k < libs.size(); ++k) {
+            const Lib& l = libs[k];
+            uint16_t* a = reinterpret_cast<uint16_t*>(res[k].data());
+            uint16_t* b = a + n;
+            uint8_t* st = reinterpret_cast<uint8_t*>(b + n);
+            for (int c = 0; c < calls + 10; ++c) {
+              const auto t0 = clk::now();
+              if (op[0] == 'v')
+                check(l, l.ipv4_host(l.ctx, src, nullptr, kL, kL, n, ICS_MODE_VERIFY, a, b, st));
+              else if (op[0] == 'c')
+                check(l, l.checksum_host(l.ctx, src, nullptr, kL, kL, nullptr, a, n));
+              else
+                check(l, l.wrap_host(l.ctx, src, nullptr, kL, kL, n, msgs.data()));
+              if (c >= 10) t[k].push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+            }
+            if (op[0] == 'w') memcpy(res[k].data() + n * 5, src, n * kL);  // the wrapped wire bytes
+          }
+        for (size_t k = 0; k < libs.size(); ++k) {
+          const bool same = res[k] == res[0];
+          printf("{\"op\": \"%s\", \"mem\": \"%s\", \"n\": %llu, \"bytes\": %llu, \"lib\": \"%s\", \"p10_us\": %.2f, "
+                 "\"p50_us\": %.2f, \"p90_us\": %.2f, \"same_as_first\": %s}\n",
+                 op, mem ? "pinned" : "pageable", (unsigned long long)n, (unsigned long long)(n * kL),
+                 libs[k].path.c_str(), pct(t[k], 0.1), pct(t[k], 0.5), pct(t[k], 0.9), same ? "true" : "false");
+          fflush(stdout);
+        }
+      }
+  for (auto& l : libs) l.destroy(l.ctx);
+  return 0;
+}
