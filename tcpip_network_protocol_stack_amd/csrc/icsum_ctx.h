@@ -163,7 +163,12 @@ struct ics_ctx {
   // synchronisation per call instead of DMA copies on either side, which is
   // what a per-tick TUN / socket batch pays for ("Per-tick host
   // batches"); ICSUM_FORCE zero_copy_max=0 turns it off (tests)
-  uint64_t zero_copy_max = uint64_t(768) << 10;
+  uint64_t zero_copy_max = uint64_t(2) << 20;
+  // ... and it ends in a completion word its slot's stream writes after the
+  // kernel (k_host_flag), which the caller spins on: ~3.7 us less than
+  // waiting for the stream's completion signal (tools/probe/sync_probe.hip)
+  uint64_t* h_flag = nullptr;  // kMaxSlots words, 64 bytes apart, coherent page-locked
+  uint64_t flag_ticket = 0;
   bool wrap_staged = false;
   uint8_t* h_msg[kMaxSlots] = {};
   uint8_t* d_msg[kMaxSlots] = {};

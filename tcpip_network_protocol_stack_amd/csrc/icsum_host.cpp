@@ -6,6 +6,7 @@
 // geometry choice); there is no CPU arithmetic beyond folding the pieces of a
 // segment longer than a slot.
 #include <algorithm>
+#include <chrono>
 #include <cstring>
 
 #include "icsum_ctx.h"
@@ -47,6 +48,9 @@ int ensure_staging(ics_ctx* ctx) {
                           static_cast<const void*>(ctx->h_init[k]), static_cast<const void*>(ctx->h_out[k])})
       if (!host_pinned(h).kernel) ctx->zero_copy_max = 0;
   }
+  ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_flag), ics_ctx::kMaxSlots * 64, hipHostMallocCoherent));
+  std::memset(ctx->h_flag, 0, ics_ctx::kMaxSlots * 64);
+  if (!host_pinned(ctx->h_flag).kernel) ctx->zero_copy_max = 0;
   ctx->staged = true;
   return ICS_OK;
 }
@@ -175,6 +179,22 @@ void host_patch_fields(uint8_t* bytes, const uint64_t* offsets, uint64_t stride,
   }
 }
 
+// Wait for a zero-copy chunk: spin on its completion word (k_host_flag) for
+// up to a millisecond — a zero-copy chunk is at most zero_copy_max bytes, tens
+// of microseconds over PCIe — then block on the slot's stream, which also
+// surfaces a kernel fault as a HIP error instead of a hang.
+int wait_flag(ics_ctx* ctx, int k, uint64_t v) {
+  const uint64_t* f = ctx->h_flag + 8 * k;
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1;; ++i) {
+    if (__atomic_load_n(f, __ATOMIC_ACQUIRE) >= v) return ICS_OK;
+    if ((i & 1023) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(1)) break;
+  }
+  ICS_HIP(hipStreamSynchronize(ctx->st[k]));
+  if (__atomic_load_n(f, __ATOMIC_ACQUIRE) >= v) return ICS_OK;
+  return fail(ICS_ERR_HIP, "host path: slot %d's completion word was not written", k);
+}
+
 }  // namespace
 
 void free_staging(ics_ctx* ctx) {
@@ -196,6 +216,8 @@ void free_staging(ics_ctx* ctx) {
     if (ctx->ev[k]) (void)hipEventDestroy(ctx->ev[k]);
     if (ctx->st[k]) (void)hipStreamDestroy(ctx->st[k]);
   }
+  if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
+  ctx->h_flag = nullptr;
   ctx->staged = false;
   ctx->wrap_staged = false;
 }
@@ -220,10 +242,15 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   const bool direct = pin.dma;
   Chunk pending[ics_ctx::kMaxSlots];
   bool busy[ics_ctx::kMaxSlots] = {};
+  uint64_t flag_of[ics_ctx::kMaxSlots] = {};  // zero-copy chunk: its completion word's value (0: event)
   uint32_t piece_sum = 0;  // running sum of the long segment whose pieces are in flight
   auto retire = [&](int k) -> int {
     if (!busy[k]) return ICS_OK;
-    ICS_HIP(hipEventSynchronize(ctx->ev[k]));
+    if (flag_of[k]) {
+      if (int rc = wait_flag(ctx, k, flag_of[k])) return rc;
+    } else {
+      ICS_HIP(hipEventSynchronize(ctx->ev[k]));
+    }
     const Chunk& c = pending[k];
     const uint64_t m = c.i1 - c.i0;
     if (c.piece) {
@@ -304,6 +331,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
                                      ctx->d_out[slot], 1, geometry_for(ctx, kSubPiece), 0, st));
       ICS_HIP(hipMemcpyAsync(ctx->h_out[slot], ctx->d_out[slot], parts * 4, hipMemcpyDeviceToHost, st));
       ICS_HIP(hipEventRecord(ctx->ev[slot], st));
+      flag_of[slot] = 0;
       pending[slot] = c;
       busy[slot] = true;
       if (c.last) {
@@ -357,7 +385,13 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, ipv4_geometry(g), 0, st));
       ICS_HIP(d2h(ctx->h_out[slot], ctx->d_out[slot], m * 5));
     }
-    ICS_HIP(hipEventRecord(ctx->ev[slot], st));
+    if (zc) {
+      flag_of[slot] = ++ctx->flag_ticket;
+      ICS_HIP(icsum::launch_host_flag(ctx->h_flag + 8 * slot, flag_of[slot], st));
+    } else {
+      flag_of[slot] = 0;
+      ICS_HIP(hipEventRecord(ctx->ev[slot], st));
+    }
     pending[slot] = c;
     busy[slot] = true;
     i0 = c.i1;

@@ -784,6 +784,14 @@ __global__ __launch_bounds__(kBlock) void k_checksum_bins(const uint8_t* __restr
 #define ICS_GRID_STRIDE(i, n) \
   for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < (n); i += uint64_t(gridDim.x) * blockDim.x)
 
+// Completion word of a host-memory call: stream order puts it behind the
+// call's kernels (whose results a kernel boundary has already made visible),
+// and the host spins on the page-locked word instead of waiting for the
+// stream's completion signal ("Per-tick host batches").
+__global__ void k_host_flag(uint64_t* flag, uint64_t v) {
+  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 __global__ void k_fold(const uint32_t* __restrict__ sum, uint16_t* __restrict__ out, uint64_t n) {
   ICS_GRID_STRIDE(i, n) out[i] = fold_value(sum[i]);
 }
@@ -2049,6 +2057,11 @@ bool geometry_supported(Geometry g) {
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   return false;
+}
+
+hipError_t launch_host_flag(uint64_t* flag, uint64_t v, hipStream_t st) {
+  hipLaunchKernelGGL(k_host_flag, dim3(1), dim3(1), 0, st, flag, v);
+  return hipGetLastError();
 }
 
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st) {

@@ -146,6 +146,9 @@ hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
 void set_xcd_remap(uint32_t run_log2);  // log2 XCD run length (default 10 = 1024 blocks), 0: hardware order
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
+// one thread stores v into *flag (page-locked, coherent host memory) with
+// system-scope release, behind the stream's earlier work
+hipError_t launch_host_flag(uint64_t* flag, uint64_t v, hipStream_t st);
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
 // fused IPv4 + TCP for receive mixes: datagrams of <= 64 bytes one per lane,
