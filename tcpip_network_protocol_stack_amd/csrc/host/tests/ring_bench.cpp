@@ -22,7 +22,9 @@
 // one arena at a time vs a DatagramTxRing.
 // `verify` times the engine side alone: [readers] threads verifying their
 // own 24 MB arena `passes` times (how concurrent engines share PCIe).
-//   build/ring_bench [passes] [seqpacket|udp|tx|verify] [writers] [readers]
+// `tick` times the per-tick calls of a stack (1-256 datagrams per call)
+// against the per-object CPU path on the drop-in types.
+//   build/ring_bench [passes] [seqpacket|udp|tx|verify|unwrap|tick] [writers] [readers]
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <sys/socket.h>
@@ -306,6 +308,84 @@ int main(int argc, char** argv)
                     double(passes) * double(arena.size()) / sec / 1e6,
                     double(passes) * double(arena.bytes()) / sec / 1e9, ok);
         return ok == (passes + 1) * arena.size() ? 0 : 2;
+    }
+    if (argc > 2 && std::string(argv[2]) == "tick") {
+        // the stack's per-tick calls: the reference reads its TUN fd one
+        // datagram per call (util/tuntap/tuntap_adapter.cpp:5-21) inside the
+        // socket's event loop (util/tcp_minnow_socket/tcp_minnow_socket.h:
+        // 138-164), so a tick carries a few datagrams.  Per tick of k MTU
+        // datagrams: the arena's unwrap (GPU verify + host parse + gates) and
+        // the engine's wrap, against the per-object path on the drop-in types
+        // (parse + unwrap_tcp_in_ip, wrap_tcp_in_ip + serialize) on this core.
+        icsum::BatchEngine eng(0);
+        TCPOverIPv4Adapter a, b;
+        a.config_mut().source = Address{"10.1.2.3", 4321};
+        a.config_mut().destination = Address{"10.9.8.7", 80};
+        b.config_mut().source = Address{"10.9.8.7", 80};
+        b.config_mut().destination = Address{"10.1.2.3", 4321};
+        std::mt19937_64 rng(0x1073);
+        std::vector<TCPMessage> msgs(256);
+        for (auto& m : msgs) {
+            m.sender.seqno = Wrap32{static_cast<uint32_t>(rng())};
+            m.sender.payload.resize(1460);
+            for (auto& c : m.sender.payload) c = static_cast<char>(rng());
+            m.receiver.ackno = Wrap32{static_cast<uint32_t>(rng())};
+            m.receiver.window_size = 65535;
+        }
+        auto p50 = [](std::vector<double> v) {
+            std::sort(v.begin(), v.end());
+            return v[v.size() / 2];
+        };
+        using clk = std::chrono::steady_clock;
+        auto us = [](clk::time_point t0) { return std::chrono::duration<double, std::micro>(clk::now() - t0).count(); };
+        const size_t iters = passes < 50 ? 2000 : passes;
+        for (size_t k : {1, 4, 16, 64, 256}) {
+            const std::vector<TCPMessage> km(msgs.begin(), msgs.begin() + static_cast<std::ptrdiff_t>(k));
+            icsum::DatagramBatch arena(eng, size_t(1) << 20, k);
+            std::vector<std::string> wires;
+            for (const auto& d : eng.wrap(a, km)) {
+                std::string w;
+                for (const auto& piece : serialize(d)) w += piece;
+                arena.push(w);
+                wires.push_back(w);
+            }
+            std::vector<double> t_unwrap, t_wrap, t_cpu_unwrap, t_cpu_wrap;
+            size_t ok = 0, cpu_ok = 0;
+            for (size_t it = 0; it < iters + 20; ++it) {
+                auto t0 = clk::now();
+                for (const auto& m : arena.unwrap(b)) ok += m.has_value();
+                const double u = us(t0);
+                t0 = clk::now();
+                const auto dg = eng.wrap(a, km);
+                const double w = us(t0);
+                t0 = clk::now();
+                for (const auto& wire : wires) {
+                    InternetDatagram d;
+                    if (parse(d, std::vector<std::string>{wire})) cpu_ok += b.unwrap_tcp_in_ip(d).has_value();
+                }
+                const double cu = us(t0);
+                t0 = clk::now();
+                size_t bytes = 0;
+                for (const auto& m : km) {
+                    const InternetDatagram d = a.wrap_tcp_in_ip(m);
+                    for (const auto& piece : serialize(d)) bytes += piece.size();
+                }
+                const double cw = us(t0);
+                if (dg.size() != k || bytes != k * 1500) return 3;
+                if (it >= 20) {
+                    t_unwrap.push_back(u);
+                    t_wrap.push_back(w);
+                    t_cpu_unwrap.push_back(cu);
+                    t_cpu_wrap.push_back(cw);
+                }
+            }
+            std::printf("{\"mode\": \"tick\", \"datagrams\": %zu, \"iters\": %zu, \"unwrap_us\": %.2f, \"wrap_us\": %.2f, "
+                        "\"cpu_unwrap_us\": %.2f, \"cpu_wrap_us\": %.2f, \"accepted\": %zu, \"cpu_accepted\": %zu}\n",
+                        k, iters, p50(t_unwrap), p50(t_wrap), p50(t_cpu_unwrap), p50(t_cpu_wrap), ok, cpu_ok);
+            std::fflush(stdout);
+            if (ok != (iters + 20) * k || cpu_ok != ok) return 2;
+        }
+        return 0;
     }
     if (argc > 2 && std::string(argv[2]) == "csum") {
         // BatchEngine::checksum over 16 Ki 1480-byte segments and

@@ -103,7 +103,9 @@ int main(int argc, char** argv) {
                           0, 0};
   }
   const uint64_t sizes[] = {1, 4, 16, 64, 256, 512, 1024, 4096};
-  const char* ops[] = {"verify", "checksum", "wrap"};
+  const char* ops[] = {"verify", "verify_off", "checksum", "wrap"};
+  std::vector<uint64_t> offs(kMaxN + 1);
+  for (uint64_t i = 0; i <= kMaxN; ++i) offs[i] = i * kL;
   const int rounds = 5, calls = 200;
   for (const char* op : ops)
     for (int mem = 0; mem < 2; ++mem)
@@ -119,7 +121,9 @@ int main(int argc, char** argv) {
             uint8_t* st = reinterpret_cast<uint8_t*>(b + n);
             for (int c = 0; c < calls + 10; ++c) {
               const auto t0 = clk::now();
-              if (op[0] == 'v')
+              if (!strcmp(op, "verify_off"))
+                check(l, l.ipv4_host(l.ctx, src, offs.data(), 0, 0, n, ICS_MODE_VERIFY, a, b, st));
+              else if (op[0] == 'v')
                 check(l, l.ipv4_host(l.ctx, src, nullptr, kL, kL, n, ICS_MODE_VERIFY, a, b, st));
               else if (op[0] == 'c')
                 check(l, l.checksum_host(l.ctx, src, nullptr, kL, kL, nullptr, a, n));
