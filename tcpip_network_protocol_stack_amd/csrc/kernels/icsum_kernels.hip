@@ -995,9 +995,16 @@ __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, 
       if (e - t0 >= 18) load_tcp_fields(dg + t0, last, tf0, tf1);
     }
   }
-  if (__any(redo)) {  // wave-uniform; groups without options re-sum the same bytes
-    ev = od = 0;
-    seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
+  if (__any(redo)) {  // wave-uniform
+    // The stream summed [s + 20, e); the TCP part starts at t0 = s + 4 hlen
+    // (or is empty when the header claims more than the datagram holds).
+    // Byte roles are by absolute address and 4 hlen - 20 is even, so the
+    // options' own even / odd sums (at most 40 bytes, a few masked chunks
+    // per group) come off exactly — no second pass over the payload.
+    uint32_t oe = 0, oo = 0;
+    if (redo) range_sums_masked<LPS, 1, false>(dg, s + 20, t0, lane, oe, oo);
+    ev -= oe;
+    od -= oo;
   }
   const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(t0) & 1u));
   if (valid && lane == LPS - 1) {
