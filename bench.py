@@ -25,7 +25,12 @@ Prints ONE JSON line (rank 0) with `roofline` (HIP-event kernel time vs the
 8 TB/s HBM peak; PMC traffic from a rocprofv3 child pass) and `cpu_baseline`
 (the reference's own InternetChecksum, compiled from /root/reference into
 oracle/_ref/, over the same bytes — the whole NS batch — on every CPU this
-process may use, outputs compared with the GPU's).
+process may use, outputs compared with the GPU's).  At N=1 it also carries
+`host_inclusive` (north_star: the path starts and ends in host memory): the
+same NS batch through ics_checksum_batch_host from page-locked memory (H2D,
+kernel and D2H pipelined; GB/s, outputs compared with the device run's), and
+the per-call latency of a per-tick host batch of 1 and 16 segments (one
+zero-copy launch and a completion word; ctypes call, preallocated outputs).
 """
 import argparse
 import csv
@@ -74,6 +79,7 @@ def parse():
     ap.add_argument("--no-config5", action="store_true",
                     help="skip the BASELINE config-5 strong-scaling sub-measurement")
     ap.add_argument("--config5-steps", type=int, default=0, help="timed steps of config 5 (0 = --steps)")
+    ap.add_argument("--no-host", action="store_true", help="skip the host_inclusive sub-object")
     return ap.parse_args()
 
 
@@ -218,6 +224,43 @@ def cpu_baseline(data_d, init_d, out_d, seg, budget_s, threads=0):
                       f"in {el1:.1f} s; all {n} outputs bit-identical to the GPU's: {match}"}
 
 
+def host_inclusive(eng, data, init, out, n, seg, passes=3, calls=300):
+    """The PCIe-inclusive rate of the same batch and the latency of per-tick
+    host calls ("Host-inclusive" and "Per-tick host batches")."""
+    import numpy as np
+    import torch
+
+    h = torch.empty(data.numel(), dtype=torch.uint8, pin_memory=True)
+    h.copy_(data)
+    hn = h.numpy()
+    hi = init.cpu().numpy()
+    want = out.cpu().numpy().view(np.uint16)
+    got = eng.checksum_batch_host(hn, n, stride=seg, seg_len=seg, init=hi)  # staging set up before the clock
+    same = bool((got == want).all())
+    t0 = time.perf_counter()
+    for _ in range(passes):
+        eng.checksum_batch_host(hn, n, stride=seg, seg_len=seg, init=hi)
+    el = time.perf_counter() - t0
+    tick = {}
+    res = np.empty(16, dtype=np.uint16)
+    for k in (1, 16):
+        ts = []
+        for c in range(calls + 20):
+            t1 = time.perf_counter()
+            rc = eng.lib.ics_checksum_batch_host(eng.ctx, hn.ctypes.data, None, seg, seg, hi.ctypes.data,
+                                                 res.ctypes.data, k)
+            if c >= 20:
+                ts.append(time.perf_counter() - t1)
+            if rc:
+                raise RuntimeError(f"ics_checksum_batch_host: {rc}")
+        same = same and bool((res[:k] == want[:k]).all())
+        tick[f"segments_{k}_us"] = round(sorted(ts)[len(ts) // 2] * 1e6, 2)
+    del h
+    return {"entry": "ics_checksum_batch_host", "memory": "page-locked", "bytes": n * seg, "passes": passes,
+            "GB_s": round(n * seg * passes / el / 1e9, 2), "outputs_equal_device": same,
+            "tick_p50": tick, "tick_note": f"{seg}-byte segments, {calls} ctypes calls, preallocated outputs"}
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -335,6 +378,9 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(data, init, out, seg, args.cpu_seconds, args.cpu_threads)
+    host = None
+    if rank == 0 and world == 1 and not args.no_host:
+        host = host_inclusive(eng, data, init, out, n, seg)
     del data, init, out
 
     # BASELINE config 5: 8 M x 9000 B sharded over the N GPUs (strong scaling)
@@ -389,6 +435,7 @@ def main():
                          "traffic_source": traffic_src},
             "cpu_baseline": cpu,
             "config5": config5,
+            "host_inclusive": host,
         }
         print(json.dumps(line), flush=True)
     eng.close()
