@@ -99,6 +99,23 @@ void run() {
   CK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
   const Geometry geo{16, 8, true, 3};
   uint64_t ticket = 0;
+  {  // host-side costs of one call: pointer query, launch issue
+    std::vector<double> pq, li;
+    for (int i = 0; i < 2000; ++i) {
+      hipPointerAttribute_t a{};
+      auto t0 = clk::now();
+      CK(hipPointerGetAttributes(&a, h_out));
+      pq.push_back(us_since(t0));
+      const SegSpec sp{d_dg, nullptr, kL, kL, 1, zero};
+      uint16_t* ip = reinterpret_cast<uint16_t*>(h_out);
+      t0 = clk::now();
+      CK(launch_ipv4_tcp(sp, 1, ip, ip + 1, h_out + 4, geo, 0, st));
+      li.push_back(us_since(t0));
+      CK(hipStreamSynchronize(st));
+    }
+    printf("{\"host_cost\": true, \"pointer_query_p50_us\": %.3f, \"launch_issue_p50_us\": %.3f}\n", pct(pq, 0.5),
+           pct(li, 0.5));
+  }
   const char* names[] = {"sync", "evsync", "evquery", "flagk", "wvalue", "lastblk"};
   for (uint64_t n : {1ull, 16ull, 256ull, 4096ull}) {
     const SegSpec sp{d_dg, nullptr, kL, kL, n, zero};
