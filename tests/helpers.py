@@ -62,3 +62,29 @@ def oracle_wrap_wire(orc, payload, r):
     _, _, st, w = orc.ipv4_tcp(bytes(b), 2)
     assert st & 0x03 == 0x03
     return w
+
+
+# ---- tests/golden/endtoend_capture.npz (oracle/make_endtoend_capture.py)
+def endtoend_capture():
+    """The frames the unmodified reference stack exchanged in BASELINE config
+    1 (128 KiB transfer), as captured on the relay: (frames uint8 buffer,
+    frame offsets n+1, direction, offsets n_ip+1 of the IPv4 datagrams inside
+    the frames — each starts 14 bytes into its EthernetFrame, so the starts
+    are unaligned exactly as a receive arena of frames holds them)."""
+    import os
+
+    z = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "endtoend_capture.npz"),
+                allow_pickle=False)
+    frames, off, direction = z["frames"], z["offsets"].astype(np.uint64), z["direction"]
+    ip = [i for i in range(len(off) - 1) if frames[off[i] + 12] == 0x08 and frames[off[i] + 13] == 0x00]
+    # IPv4 datagram k = [its frame's start + 14, the frame's end)
+    starts = np.array([off[i] + 14 for i in ip], dtype=np.uint64)
+    ends = np.array([off[i + 1] for i in ip], dtype=np.uint64)
+    buf = np.concatenate([frames, np.zeros(16, dtype=np.uint8)])
+    return buf, off, direction, starts, ends
+
+
+def ip_packed(buf, starts, ends, lead=0):
+    """The captured IPv4 datagrams back to back (the IP layer's receive arena)."""
+    segs = [buf[int(s):int(e)].tobytes() for s, e in zip(starts, ends)]
+    return pack_contiguous(segs, lead)

@@ -8,11 +8,16 @@ server: it learns the first two peers that say hello (endtoend sends three
 empty datagrams first, endtoend.cpp:258-261) and forwards every non-empty
 datagram from one to the other.
 
-    python tools/endtoend_run.py BINARY [--bytes N] [--seed S] [--timeout T]
+    python tools/endtoend_run.py BINARY [--bytes N] [--seed S] [--timeout T] [--capture FILE.npz]
 
 prints one JSON line: ok (server stdout == client stdin), transfer_s (client start
 until the server has written every byte), wall_s (both processes exited; includes the
 TCP close linger of tcp_minnow_socket), bytes.
+
+--capture keeps every frame the relay forwards (the serialized EthernetFrames
+the two routers exchange, endtoend.cpp:118-124) in forwarding order: `frames`
+(uint8, back to back), `offsets` (uint64, n + 1), `direction` (uint8: 0 from
+the first peer — the server — to the second, 1 back), saved with numpy.
 """
 import argparse
 import json
@@ -51,6 +56,8 @@ class Bounce(threading.Thread):
         self.port = self.sock.getsockname()[1]
         self.peers = []
         self.forwarded = 0
+        self.captured = []  # (direction, frame) when capturing
+        self.capture = False
         self.stop = threading.Event()
 
     def run(self):
@@ -69,12 +76,15 @@ class Bounce(threading.Thread):
                         other = self.peers[1 - self.peers.index(addr)]
                         self.sock.sendto(data, other)
                         self.forwarded += 1
+                        if self.capture:
+                            self.captured.append((self.peers.index(addr), data))
         self.sock.close()
 
 
-def run(binary, nbytes, seed, timeout):
+def run(binary, nbytes, seed, timeout, capture=None):
     payload = seeded_bytes(nbytes, seed)
     bounce = Bounce()
+    bounce.capture = capture is not None
     bounce.start()
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "client.in")
@@ -109,6 +119,14 @@ def run(binary, nbytes, seed, timeout):
             got = f.read()
     bounce.stop.set()
     bounce.join()
+    if capture:
+        import numpy as np
+
+        frames = [f for _, f in bounce.captured]
+        off = np.zeros(len(frames) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(f) for f in frames])
+        np.savez(capture, frames=np.frombuffer(b"".join(frames), dtype=np.uint8), offsets=off,
+                 direction=np.array([d for d, _ in bounce.captured], dtype=np.uint8))
     return {"ok": got == payload, "bytes": nbytes, "received": len(got),
             "transfer_s": None if t_data is None else round(t_data, 3), "wall_s": round(wall, 3),
             "frames_relayed": bounce.forwarded, "client_rc": client.returncode, "server_rc": server.returncode,
@@ -121,8 +139,9 @@ def main():
     ap.add_argument("--bytes", type=int, default=1 << 20)
     ap.add_argument("--seed", type=int, default=0x10710001)
     ap.add_argument("--timeout", type=float, default=120.0)
+    ap.add_argument("--capture", default=None, help="save the relayed frames (.npz)")
     a = ap.parse_args()
-    r = run(a.binary, a.bytes, a.seed, a.timeout)
+    r = run(a.binary, a.bytes, a.seed, a.timeout, a.capture)
     print(json.dumps(r), flush=True)
     sys.exit(0 if r["ok"] else 1)
 
