@@ -59,3 +59,20 @@ def test_config1_endtoend_1MiB_bit_exact(built):
     rc_ref, r = _run(REFBIN)
     assert rc_ref == 0 and r["ok"], r
     print(json.dumps({"dropin": d, "reference": r}))
+
+
+def test_config1_corrupted_frames_dropped_and_retransmitted(built):
+    """SURVEY §5 failure path: a checksum failure is a loss that TCP recovers.
+    The relay flips one random bit past the Ethernet header of 5 % of the IPv4
+    frames; the drop-in's parse must reject every one of them (IPv4 header
+    checksum or TCP checksum, util/ipv4_header/ipv4_header.cpp:53-58,
+    util/tcp_segment/tcp_segment.cpp:11-18 — the reserved flag bit alone is
+    not covered by the checksum and changes nothing the payload depends on),
+    and the retransmissions must still deliver 64 KiB bit-exact — as with the
+    unmodified reference build under the same seed."""
+    for binary in (os.path.join(built, "endtoend"), REFBIN):
+        r = subprocess.run([sys.executable, RUN, binary, "--bytes", str(64 << 10), "--corrupt", "0.05",
+                            "--timeout", "90"], capture_output=True, text=True, timeout=240)
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert r.returncode == 0 and d["ok"] and d["received"] == 64 << 10, (binary, d)
+        assert d["frames_corrupted"] >= 2, d

@@ -9,6 +9,7 @@ empty datagrams first, endtoend.cpp:258-261) and forwards every non-empty
 datagram from one to the other.
 
     python tools/endtoend_run.py BINARY [--bytes N] [--seed S] [--timeout T] [--capture FILE.npz]
+                                 [--corrupt P]
 
 prints one JSON line: ok (server stdout == client stdin), transfer_s (client start
 until the server has written every byte), wall_s (both processes exited; includes the
@@ -18,6 +19,11 @@ TCP close linger of tcp_minnow_socket), bytes.
 the two routers exchange, endtoend.cpp:118-124) in forwarding order: `frames`
 (uint8, back to back), `offsets` (uint64, n + 1), `direction` (uint8: 0 from
 the first peer — the server — to the second, 1 back), saved with numpy.
+
+--corrupt P flips one random bit past the Ethernet header of a fraction P of
+the IPv4 frames (seeded): the stack must drop each one at its checksum check
+(a checksum failure is a loss) and TCP must retransmit, so the
+transfer still arrives bit-exact; the line reports how many were flipped.
 """
 import argparse
 import json
@@ -58,6 +64,9 @@ class Bounce(threading.Thread):
         self.forwarded = 0
         self.captured = []  # (direction, frame) when capturing
         self.capture = False
+        self.corrupt = 0.0
+        self.flipped = 0
+        self.rng = None
         self.stop = threading.Event()
 
     def run(self):
@@ -74,6 +83,13 @@ class Bounce(threading.Thread):
                         self.peers.append(addr)
                     if data and len(self.peers) == 2 and addr in self.peers:
                         other = self.peers[1 - self.peers.index(addr)]
+                        if self.corrupt and len(data) > 14 and data[12:14] == b"\x08\x00" and \
+                                self.rng.random() < self.corrupt:
+                            b = bytearray(data)
+                            bit = self.rng.randrange(8 * (len(b) - 14))
+                            b[14 + bit // 8] ^= 1 << (bit % 8)
+                            data = bytes(b)
+                            self.flipped += 1
                         self.sock.sendto(data, other)
                         self.forwarded += 1
                         if self.capture:
@@ -81,10 +97,15 @@ class Bounce(threading.Thread):
         self.sock.close()
 
 
-def run(binary, nbytes, seed, timeout, capture=None):
+def run(binary, nbytes, seed, timeout, capture=None, corrupt=0.0):
     payload = seeded_bytes(nbytes, seed)
     bounce = Bounce()
     bounce.capture = capture is not None
+    if corrupt:
+        import random
+
+        bounce.corrupt = corrupt
+        bounce.rng = random.Random(seed)
     bounce.start()
     with tempfile.TemporaryDirectory() as td:
         src = os.path.join(td, "client.in")
@@ -129,7 +150,7 @@ def run(binary, nbytes, seed, timeout, capture=None):
                  direction=np.array([d for d, _ in bounce.captured], dtype=np.uint8))
     return {"ok": got == payload, "bytes": nbytes, "received": len(got),
             "transfer_s": None if t_data is None else round(t_data, 3), "wall_s": round(wall, 3),
-            "frames_relayed": bounce.forwarded, "client_rc": client.returncode, "server_rc": server.returncode,
+            "frames_relayed": bounce.forwarded, "frames_corrupted": bounce.flipped, "client_rc": client.returncode, "server_rc": server.returncode,
             "binary": binary}
 
 
@@ -140,8 +161,9 @@ def main():
     ap.add_argument("--seed", type=int, default=0x10710001)
     ap.add_argument("--timeout", type=float, default=120.0)
     ap.add_argument("--capture", default=None, help="save the relayed frames (.npz)")
+    ap.add_argument("--corrupt", type=float, default=0.0, help="fraction of IPv4 frames with one bit flipped")
     a = ap.parse_args()
-    r = run(a.binary, a.bytes, a.seed, a.timeout, a.capture)
+    r = run(a.binary, a.bytes, a.seed, a.timeout, a.capture, a.corrupt)
     print(json.dumps(r), flush=True)
     sys.exit(0 if r["ok"] else 1)
 
