@@ -118,9 +118,14 @@ struct ics_ctx {
   // ics_ipv4_tcp_batch: from this share of <= 144-byte datagrams (sixteenths,
   // the plan word's bits 4-7) an offsets batch runs 8-lane groups
   static constexpr uint32_t kIpv4ShortMix16 = 5;
-  // ... and from this share up the two-class launch (k_ipv4_twoclass, 32
-  // datagrams per wave), which beats the 8-lane groups from 5/16 ACKs up
-  static constexpr uint32_t kIpv4TwoClass16 = 5;
+  // ... and from this share up the two-class launch (k_ipv4_twoclass, block
+  // lists, 16 datagrams per wave in the bounds pass), which beats 16 x 4
+  // groups from 3/16 ACKs up (1 M datagrams VERIFY, tools/ab_mix_split.py,
+  // profiles/r3_mix_twoclass_ab.jsonl: 1/8 200.2 vs 198.5 us, 3/16 187.3 vs
+  // 191.4, 1/4 176.0 vs 185.4, 5/16 164.3 vs 184.2)
+  static constexpr uint32_t kIpv4TwoClass16 = 3;
+  // ... with 32 datagrams per wave (128 per block) from this share up
+  static constexpr uint32_t kIpv4TwoClassWide16 = 11;
   // the plain checksum's short-mix threshold (short_mix: the two-class
   // launch); raw-datagram ACK shares, AUTO vs two-class at 16 per wave
   // (tools/ab_ipv4_mix.py plain rows): 3/8 156.1 vs 144.1 us, 5/16 163.6 vs

@@ -292,6 +292,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   // kernels running behind the first and every 16th launch (DESIGN.md §4,
   // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
   bool two = false;
+  int spw = 16;
   PlanReq req;
   int plan_used = -1;
   if (d_offsets && !forced_geometry(ctx) && !ctx->twoclass && n >= ics_ctx::kSmallPlanMin && n <= 0xFFFFFFFFull) {
@@ -306,18 +307,23 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
       g = ipv4_geometry({8, 8, true, 3, 1});  // ACK + MTU mixes past the two-class grid's limit
     else if (hit)
       g = ipv4_geometry({16, 4, true, 3, 1});  // MTU + a few ACKs: shorter unroll, 1-4 % (1 M datagrams)
-    // the two-class launch, 32 datagrams per wave.  1 M datagrams VERIFY,
-    // 8-lane groups vs two-class at 64 / 32 / 16 per wave (tools/ab_ipv4_mix.py):
-    // 3/4 ACKs 127.3 vs 85.3 / 83.7 / 98.9 us, 1/2 157.9 vs 154.0 / 139.8 /
-    // 149.7, 7/16 166.0 vs 169.7 / 153.8 / 164.3, 5/16 183.1 vs 201.0 / 181.1 / 185.5
+    // the two-class launch (block lists, ics_ctx::kIpv4TwoClass16 for the
+    // crossover against 16 x 4 groups; round 2's per-wave version beat the
+    // 8-lane groups from 5/16 ACKs up, tools/ab_ipv4_mix.py)
     two = hit && plan != icsum::kPlanWholeBatchSmall && mix.short16 >= ics_ctx::kIpv4TwoClass16 && mix.long16 == 0;
+    // ACK-heavy mixes: 128 datagrams per block, so the block's one short
+    // pass carries more of them (3/4 ACKs 78.4 -> 75.4 us, mix_probe blk32)
+    spw = mix.short16 >= ics_ctx::kIpv4TwoClassWide16 ? 32 : 16;
     plan_used = hit ? int(plan) : -1;
   }
-  if (d_offsets && ctx->twoclass) two = true;  // test hook
+  if (d_offsets && ctx->twoclass) {  // test hook
+    two = true;
+    spw = ctx->twoclass;
+  }
   hipError_t le = hipErrorInvalidValue;
   if (two) {
-    le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, st);
-    if (le != hipErrorInvalidValue) note(ctx, ICS_K_IPV4_TWOCLASS, {16, 32, true, 3, 1}, plan_used);
+    le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, spw, st);
+    if (le != hipErrorInvalidValue) note(ctx, ICS_K_IPV4_TWOCLASS, {16, spw, true, 3, 1}, plan_used);
   }
   if (le == hipErrorInvalidValue) {
     le = icsum::launch_ipv4_tcp(sp, mode, d_ip_ck, d_tcp_ck, d_status, g, 0, st);

@@ -1078,47 +1078,77 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                    block_order(remap), gridDim.x);
 }
 
-// Two-class launch for receive mixes (ACKs among MTU datagrams): wave w
-// takes datagrams [64 w, 64 w + 64); those of <= 64 bytes one per lane, the
-// rest 16 lanes each from a per-wave LDS list, four at a time.
+// Two-class launch for receive mixes (ACKs among MTU datagrams): block b
+// takes datagrams [4 SPW b, 4 SPW b + 4 SPW), wave w reads the bounds of SPW
+// of them and appends each to the block's short (<= 64 bytes) or long list
+// in LDS.  Wave 0 then verifies the short ones one per lane, 64 per pass,
+// while the other waves — and wave 0 once its short passes are done — claim
+// the long ones four at a time (16 lanes each) from an LDS counter.  A wave
+// that verified both classes in turn spent a whole memory round trip on its
+// short phase for a fraction of a long round's bytes; with the classes
+// split over the block's waves only one wave does (½-ACK
+// VERIFY of 1 M datagrams 135.5 -> 129.1 us, ¼-ACK 189.7 -> 177.8 us).
 template <int SPW>
 __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
                                                           uint64_t stride, uint64_t dlen, uint64_t n, int mode,
                                                           uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
                                                           uint8_t* __restrict__ status,
                                                           const uint8_t* __restrict__ zpad) {
-  __shared__ uint64_t lst[kBlock / 64][64][2];
-  __shared__ uint32_t lseg[kBlock / 64][64];
+  constexpr uint32_t kPer = (kBlock / 64) * SPW;
+  __shared__ uint64_t lst[kPer][2], sst[kPer][2];  // the block's long / short datagrams' {start, end}
+  __shared__ uint32_t lseg[kPer], sseg[kPer];
+  __shared__ uint32_t cnt[3];  // long, short, long claimed
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
-  // SPW datagrams per wave (lanes >= SPW idle in the short phase)
+  if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
+  __syncthreads();
   const uint64_t seg = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
   const bool valid = seg < n && lane < SPW;
   uint64_t s, e;
   seg_bounds(offsets, stride, dlen, seg < n ? seg : n - 1, s, e);
   if (!valid) e = s;
   const bool is_short = e - s <= 64;
-  const uint64_t lmask = __ballot(valid && !is_short);
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(lmask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(lmask), 0u));
-  if (valid && !is_short) {
-    lst[wv][rank][0] = s;
-    lst[wv][rank][1] = e;
-    lseg[wv][rank] = uint32_t(seg);
+  const uint64_t lmask = __ballot(valid && !is_short), smask = __ballot(valid && is_short);
+  uint32_t lbase = 0, sbase = 0;
+  if (lane == 0) {
+    lbase = atomicAdd(&cnt[0], uint32_t(__builtin_popcountll(lmask)));
+    sbase = atomicAdd(&cnt[1], uint32_t(__builtin_popcountll(smask)));
   }
-  // short datagrams: one lane each (the long lanes run an empty item)
-  ipv4_item<1, 4, false, 0>(dg, s, is_short ? e : s, seg, valid && is_short, 0u, mode, ip_ck, tcp_ck, status,
-                            zpad, zlast);
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  const uint32_t nlong = uint32_t(__builtin_popcountll(lmask));
+  lbase = __builtin_amdgcn_readfirstlane(lbase);
+  sbase = __builtin_amdgcn_readfirstlane(sbase);
+  const uint32_t lr = __builtin_amdgcn_mbcnt_hi(uint32_t(lmask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(lmask), 0u));
+  const uint32_t sr = __builtin_amdgcn_mbcnt_hi(uint32_t(smask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(smask), 0u));
+  if (valid && !is_short) {
+    lst[lbase + lr][0] = s;
+    lst[lbase + lr][1] = e;
+    lseg[lbase + lr] = uint32_t(seg);
+  }
+  if (valid && is_short) {
+    sst[sbase + sr][0] = s;
+    sst[sbase + sr][1] = e;
+    sseg[sbase + sr] = uint32_t(seg);
+  }
+  __syncthreads();
+  const uint32_t nlong = cnt[0], nshort = cnt[1];
+  if (wv == 0)
+    for (uint32_t r0 = 0; r0 < nshort; r0 += 64) {  // uniform
+      const uint32_t k = r0 + lane;
+      const bool mine = k < nshort;
+      const uint32_t kc = mine ? k : 0u;
+      const uint64_t ss = sst[kc][0], se = mine ? sst[kc][1] : ss;
+      ipv4_item<1, 4, false, 0>(dg, ss, se, sseg[kc], mine, 0u, mode, ip_ck, tcp_ck, status, zpad, zlast);
+    }
   const uint32_t g = lane >> 4, gl = lane & 15u;
-  for (uint32_t r0 = 0; r0 < nlong; r0 += 4) {  // uniform
+  for (;;) {
+    uint32_t r0 = 0;
+    if (lane == 0) r0 = atomicAdd(&cnt[2], 4u);
+    r0 = __builtin_amdgcn_readfirstlane(r0);
+    if (r0 >= nlong) break;  // uniform
     const uint32_t k = r0 + g;
     const bool mine = k < nlong;
     const uint32_t kc = mine ? k : 0u;
-    const uint64_t ls = lst[wv][kc][0], le = mine ? lst[wv][kc][1] : ls;
-    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[wv][kc], mine, gl, mode, ip_ck, tcp_ck, status, zpad, zlast);
+    const uint64_t ls = lst[kc][0], le = mine ? lst[kc][1] : ls;
+    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[kc], mine, gl, mode, ip_ck, tcp_ck, status, zpad, zlast);
   }
 }
 
@@ -1960,14 +1990,19 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 }
 
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                hipStream_t st) {
-  constexpr uint64_t kSpw = 32;  // datagrams per wave (measured best over 16 / 32 / 64)
-  const uint64_t per_block = uint64_t(kBlock / 64) * kSpw;
+                                int spw, hipStream_t st) {
+  if (spw != 16 && spw != 32) return hipErrorInvalidValue;
+  const uint64_t per_block = uint64_t(kBlock / 64) * uint64_t(spw);
   const uint64_t blocks = (sp.n + per_block - 1) / per_block;
   if (sp.list || blocks == 0 || blocks > (uint64_t(1) << 24)) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_ipv4_twoclass<kSpw>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes),
-                     sp.offsets, sp.stride, sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status,
-                     static_cast<const uint8_t*>(sp.zero16));
+  uint8_t* const dg = const_cast<uint8_t*>(sp.bytes);
+  const uint8_t* const z = static_cast<const uint8_t*>(sp.zero16);
+  if (spw == 16)
+    hipLaunchKernelGGL(k_ipv4_twoclass<16>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, dg, sp.offsets, sp.stride,
+                       sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z);
+  else
+    hipLaunchKernelGGL(k_ipv4_twoclass<32>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, dg, sp.offsets, sp.stride,
+                       sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z);
   return hipGetLastError();
 }
 

@@ -151,10 +151,12 @@ hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream
 hipError_t launch_host_flag(uint64_t* flag, uint64_t v, hipStream_t st);
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
-// fused IPv4 + TCP for receive mixes: datagrams of <= 64 bytes one per lane,
-// the rest 16 lanes each (k_ipv4_twoclass, one wave per 32 datagrams)
+// fused IPv4 + TCP for receive mixes: each block's datagrams of <= 64 bytes
+// one per lane on one wave, the rest 16 lanes each claimed by every wave
+// (k_ipv4_twoclass); spw (16 or 32) datagrams per wave in the bounds pass,
+// i.e. 64 or 128 per block
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                hipStream_t st);
+                                int spw, hipStream_t st);
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg

@@ -171,8 +171,9 @@ def two_engine(request):
 @pytest.mark.parametrize("mix", ["bimodal", "ackheavy", "tricky"])
 def test_ipv4_twoclass_vs_oracle(two_engine, orc, mix):
     """Raw IPv4/TCP datagram batches through the two-class fused launch
-    (k_ipv4_twoclass: <= 64-byte datagrams one per lane, the rest 16 lanes
-    each, 32 datagrams per wave; forced with the twoclass hook): COMPUTE,
+    (k_ipv4_twoclass: the block's <= 64-byte datagrams one per lane on one
+    wave, the rest 16 lanes each claimed by every wave; forced with the
+    twoclass hook): COMPUTE,
     VERIFY and PATCH against the oracle, patched bytes included.  "tricky"
     adds short (< 20 B), 64/65-byte edge, option-carrying and corrupted
     datagrams."""

@@ -1,15 +1,19 @@
-// mix_probe.hip — dev tool: the two-class IPv4 launch (k_ipv4_twoclass) on a
-// received ACK/MTU mix, against variants of its shape.  One call over 1 M
-// datagrams (40-byte ACKs and 1500-byte segments, valid headers) runs ≈ 14 %
-// slower than the same datagrams repacked by class and verified in two calls
-// (tools/ab_mix_split.py).  Variants (all VERIFY, outputs compared with the
-// shipped kernel's):
-//   ship     k_ipv4_twoclass<32> as shipped (78 VGPRs: 6 waves per SIMD)
-//   u6       long class 16 lanes x 6 loads in flight (fewer VGPRs)
-//   occ8     the shipped body under __launch_bounds__(256, 8): 8 waves per SIMD
-//   u6occ8   both
-//   spw16    16 datagrams per wave
-// Launches are timed interleaved (20 launches x 7 rounds, HIP events).
+// mix_probe.hip — dev tool: the two-class IPv4 launch on a received ACK/MTU
+// mix (1 M datagrams, 40-byte ACKs and 1500-byte segments, valid headers;
+// the ACK shares on the command line), against shapes around it.  VERIFY,
+// outputs compared with the library kernel's, launches timed interleaved
+// (20 launches x 7 rounds, HIP events).
+//   ship     launch_ipv4_twoclass (since round 3 the block-list kernel, 16
+//            datagrams per wave; before that the per-wave one, = spw16's body
+//            at 32 per wave)
+//   spw16    the round-2 per-wave kernel at 16 datagrams per wave: the wave
+//            verifies its short datagrams, then its long ones 4 at a time
+//   blk*     block lists: wave 0 verifies the block's short datagrams, every
+//            wave claims groups of 4 long ones from an LDS counter (* =
+//            datagrams per wave in the bounds pass)
+//   blkq*    one LDS queue of short passes and long groups claimed by every wave
+// (round 3, first runs: long class 16 x 6 and 8 waves / SIMD by launch
+// bounds were slower than the per-wave kernel and are gone from the list)
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 mix_probe.hip -o mix_probe
 #include "../../tcpip_network_protocol_stack_amd/csrc/kernels/icsum_kernels.hip"
 
@@ -71,6 +75,144 @@ __device__ __forceinline__ void twoclass_body(uint8_t* __restrict__ dg, const ui
   }
 }
 
+// block lists: the block's 4 x SPW datagrams go to one long and one short
+// list in LDS; wave 0 verifies the short ones (one lane each, 64 per pass),
+// every wave claims groups of 4 long ones (16 lanes each) from an LDS counter
+// — wave 0 joining once its short passes are done
+template <int SPW>
+__global__ __launch_bounds__(kBlock) void k_mix_blk(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
+                                                    uint64_t n, int mode, uint16_t* __restrict__ ip_ck,
+                                                    uint16_t* __restrict__ tcp_ck, uint8_t* __restrict__ status,
+                                                    const uint8_t* __restrict__ zpad) {
+  constexpr uint32_t kPer = (kBlock / 64) * SPW;
+  __shared__ uint64_t lst[kPer][2];
+  __shared__ uint32_t lseg[kPer];
+  __shared__ uint64_t sst[kPer][2];
+  __shared__ uint32_t sseg[kPer];
+  __shared__ uint32_t cnt[3];  // long, short, long claimed
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
+  if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t seg = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
+  const bool valid = seg < n && lane < SPW;
+  uint64_t s, e;
+  seg_bounds(offsets, 0, 0, seg < n ? seg : n - 1, s, e);
+  if (!valid) e = s;
+  const bool is_short = e - s <= 64;
+  const uint64_t lmask = __ballot(valid && !is_short), smask = __ballot(valid && is_short);
+  uint32_t lbase = 0, sbase = 0;
+  if (lane == 0) {
+    lbase = atomicAdd(&cnt[0], uint32_t(__builtin_popcountll(lmask)));
+    sbase = atomicAdd(&cnt[1], uint32_t(__builtin_popcountll(smask)));
+  }
+  lbase = __builtin_amdgcn_readfirstlane(lbase);
+  sbase = __builtin_amdgcn_readfirstlane(sbase);
+  const uint32_t lr = __builtin_amdgcn_mbcnt_hi(uint32_t(lmask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(lmask), 0u));
+  const uint32_t sr = __builtin_amdgcn_mbcnt_hi(uint32_t(smask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(smask), 0u));
+  if (valid && !is_short) {
+    lst[lbase + lr][0] = s;
+    lst[lbase + lr][1] = e;
+    lseg[lbase + lr] = uint32_t(seg);
+  }
+  if (valid && is_short) {
+    sst[sbase + sr][0] = s;
+    sst[sbase + sr][1] = e;
+    sseg[sbase + sr] = uint32_t(seg);
+  }
+  __syncthreads();
+  const uint32_t nlong = cnt[0], nshort = cnt[1];
+  if (wv == 0)
+    for (uint32_t r0 = 0; r0 < nshort; r0 += 64) {  // uniform
+      const uint32_t k = r0 + lane;
+      const bool mine = k < nshort;
+      const uint32_t kc = mine ? k : 0u;
+      const uint64_t ss = sst[kc][0], se = mine ? sst[kc][1] : ss;
+      ipv4_item<1, 4, false, 0>(dg, ss, se, sseg[kc], mine, 0u, mode, ip_ck, tcp_ck, status, zpad, zlast);
+    }
+  const uint32_t g = lane >> 4, gl = lane & 15u;
+  for (;;) {
+    uint32_t r0 = 0;
+    if (lane == 0) r0 = atomicAdd(&cnt[2], 4u);
+    r0 = __builtin_amdgcn_readfirstlane(r0);
+    if (r0 >= nlong) break;
+    const uint32_t k = r0 + g;
+    const bool mine = k < nlong;
+    const uint32_t kc = mine ? k : 0u;
+    const uint64_t ls = lst[kc][0], le = mine ? lst[kc][1] : ls;
+    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[kc], mine, gl, mode, ip_ck, tcp_ck, status, zpad, zlast);
+  }
+}
+
+// one LDS work queue per block: short passes (64 short datagrams, one lane
+// each) first, then groups of 4 long datagrams (16 lanes each); every wave
+// claims the next item until the queue is empty
+template <int SPW>
+__global__ __launch_bounds__(kBlock) void k_mix_blkq(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
+                                                     uint64_t n, int mode, uint16_t* __restrict__ ip_ck,
+                                                     uint16_t* __restrict__ tcp_ck, uint8_t* __restrict__ status,
+                                                     const uint8_t* __restrict__ zpad) {
+  constexpr uint32_t kPer = (kBlock / 64) * SPW;
+  __shared__ uint64_t lst[kPer][2];
+  __shared__ uint32_t lseg[kPer];
+  __shared__ uint64_t sst[kPer][2];
+  __shared__ uint32_t sseg[kPer];
+  __shared__ uint32_t cnt[3];
+  const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
+  if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
+  __syncthreads();
+  const uint64_t seg = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
+  const bool valid = seg < n && lane < SPW;
+  uint64_t s, e;
+  seg_bounds(offsets, 0, 0, seg < n ? seg : n - 1, s, e);
+  if (!valid) e = s;
+  const bool is_short = e - s <= 64;
+  const uint64_t lmask = __ballot(valid && !is_short), smask = __ballot(valid && is_short);
+  uint32_t lbase = 0, sbase = 0;
+  if (lane == 0) {
+    lbase = atomicAdd(&cnt[0], uint32_t(__builtin_popcountll(lmask)));
+    sbase = atomicAdd(&cnt[1], uint32_t(__builtin_popcountll(smask)));
+  }
+  lbase = __builtin_amdgcn_readfirstlane(lbase);
+  sbase = __builtin_amdgcn_readfirstlane(sbase);
+  const uint32_t lr = __builtin_amdgcn_mbcnt_hi(uint32_t(lmask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(lmask), 0u));
+  const uint32_t sr = __builtin_amdgcn_mbcnt_hi(uint32_t(smask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(smask), 0u));
+  if (valid && !is_short) {
+    lst[lbase + lr][0] = s;
+    lst[lbase + lr][1] = e;
+    lseg[lbase + lr] = uint32_t(seg);
+  }
+  if (valid && is_short) {
+    sst[sbase + sr][0] = s;
+    sst[sbase + sr][1] = e;
+    sseg[sbase + sr] = uint32_t(seg);
+  }
+  __syncthreads();
+  const uint32_t nlong = cnt[0], nshort = cnt[1];
+  const uint32_t spass = (nshort + 63) / 64, items = spass + (nlong + 3) / 4;
+  const uint32_t g = lane >> 4, gl = lane & 15u;
+  for (;;) {
+    uint32_t it = 0;
+    if (lane == 0) it = atomicAdd(&cnt[2], 1u);
+    it = __builtin_amdgcn_readfirstlane(it);
+    if (it >= items) break;
+    if (it < spass) {
+      const uint32_t k = it * 64 + lane;
+      const bool mine = k < nshort;
+      const uint32_t kc = mine ? k : 0u;
+      const uint64_t ss = sst[kc][0], se = mine ? sst[kc][1] : ss;
+      ipv4_item<1, 4, false, 0>(dg, ss, se, sseg[kc], mine, 0u, mode, ip_ck, tcp_ck, status, zpad, zlast);
+    } else {
+      const uint32_t k = (it - spass) * 4 + g;
+      const bool mine = k < nlong;
+      const uint32_t kc = mine ? k : 0u;
+      const uint64_t ls = lst[kc][0], le = mine ? lst[kc][1] : ls;
+      ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[kc], mine, gl, mode, ip_ck, tcp_ck, status, zpad, zlast);
+    }
+  }
+}
+
 template <int SPW, int LU>
 __global__ __launch_bounds__(kBlock) void k_mix(uint8_t* dg, const uint64_t* offsets, uint64_t n, int mode,
                                                 uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
@@ -85,11 +227,11 @@ __global__ __launch_bounds__(kBlock, 8) void k_mix_occ8(uint8_t* dg, const uint6
   twoclass_body<SPW, LU>(dg, offsets, n, mode, ip_ck, tcp_ck, status, zpad);
 }
 
-void run() {
+void run(double ack) {
   constexpr uint64_t kN = 1 << 20;
   std::mt19937_64 rng(11);
   std::vector<uint64_t> off(kN + 1, 0);
-  for (uint64_t i = 0; i < kN; ++i) off[i + 1] = off[i] + ((rng() & 1) ? 40 : 1500);
+  for (uint64_t i = 0; i < kN; ++i) off[i + 1] = off[i] + (double(rng() >> 11) * 0x1.0p-53 < ack ? 40 : 1500);
   const uint64_t bytes = off[kN];
   std::vector<uint8_t> h(bytes + 16);
   for (auto& b : h) b = uint8_t(rng());
@@ -123,11 +265,14 @@ void run() {
   };
   auto grid = [](int spw) { return dim3(uint32_t((kN + uint64_t(4 * spw) - 1) / uint64_t(4 * spw))); };
   std::vector<V> vs = {
-      {"ship", [&] { CK(launch_ipv4_twoclass(sp, 1, ip, tcp, st, nullptr)); }},
-      {"u6", [&] { hipLaunchKernelGGL((k_mix<32, 6>), grid(32), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
-      {"occ8", [&] { hipLaunchKernelGGL((k_mix_occ8<32, 8>), grid(32), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
-      {"u6occ8", [&] { hipLaunchKernelGGL((k_mix_occ8<32, 6>), grid(32), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
+      {"ship", [&] { CK(launch_ipv4_twoclass(sp, 1, ip, tcp, st, 16, nullptr)); }},
       {"spw16", [&] { hipLaunchKernelGGL((k_mix<16, 8>), grid(16), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
+      {"blk32", [&] { hipLaunchKernelGGL((k_mix_blk<32>), grid(32), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
+      {"blk16", [&] { hipLaunchKernelGGL((k_mix_blk<16>), grid(16), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
+      {"blkq16", [&] { hipLaunchKernelGGL((k_mix_blkq<16>), grid(16), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
+      {"blkq24", [&] { hipLaunchKernelGGL((k_mix_blkq<24>), grid(24), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
+      {"blkq32", [&] { hipLaunchKernelGGL((k_mix_blkq<32>), grid(32), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
+      {"blk24", [&] { hipLaunchKernelGGL((k_mix_blk<24>), grid(24), dim3(kBlock), 0, nullptr, d, doff, kN, 1, ip, tcp, st, z); }},
   };
   std::vector<uint8_t> want(kN * 5), got(kN * 5);
   vs[0].f();
@@ -168,15 +313,23 @@ void run() {
     }
   for (size_t v = 0; v < vs.size(); ++v) {
     std::sort(t[v].begin(), t[v].end());
-    printf("{\"variant\": \"%s\", \"us_median\": %.2f, \"us_min\": %.2f, \"bytes\": %llu, \"accepted\": %zu}\n",
-           vs[v].name, t[v][t[v].size() / 2], t[v][0], (unsigned long long)bytes, accept);
+    printf("{\"ack_share\": %.2f, \"variant\": \"%s\", \"us_median\": %.2f, \"us_min\": %.2f, \"bytes\": %llu, "
+           "\"accepted\": %zu}\n",
+           ack, vs[v].name, t[v][t[v].size() / 2], t[v][0], (unsigned long long)bytes, accept);
   }
+  fflush(stdout);
+  CK(hipEventDestroy(a));
+  CK(hipEventDestroy(b));
+  for (void* p : {static_cast<void*>(d), static_cast<void*>(doff), zero, static_cast<void*>(ip),
+                  static_cast<void*>(tcp), static_cast<void*>(st), static_cast<void*>(ref)})
+    CK(hipFree(p));
 }
 
 }  // namespace
 }  // namespace icsum
 
-int main() {
-  icsum::run();
+int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i) icsum::run(atof(argv[i]));
+  if (argc < 2) icsum::run(0.5);
   return 0;
 }
