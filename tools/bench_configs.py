@@ -319,6 +319,23 @@ def main():
                            "_auto_nocache": "auto, binning passes every call"}[tag])
         del d
 
+    if "rxmix" in only:  # received traffic: raw IPv4/TCP datagrams, ACKs among MTU segments, valid headers
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        from ab_ipv4_mix import batch
+
+        n = 1 << 20
+        ip = torch.empty(n, dtype=torch.int16, device=dev)
+        tcp = torch.empty(n, dtype=torch.int16, device=dev)
+        stt = torch.empty(n, dtype=torch.uint8, device=dev)
+        for af in (0.25, 0.5, 0.75):
+            d, doff, nbytes = batch(eng, n, af, 11)
+            t = timed(lambda i=0: eng.ipv4_tcp_batch(d, 1, n=n, offsets=doff, ip_ck=ip, tcp_ck=tcp, status=stt),
+                      args.iters)
+            info = eng.dispatch_info()
+            emit(f"rxmix_1M_{int(af * 100)}pct_acks_verify", nbytes, t, n * 13, entry="ics_ipv4_tcp_batch VERIFY",
+                 last_kernel=info["kernel"], datagrams_per_wave=info["unroll"])
+            del d
+
     if "jumbo" in only:  # config 5 per-GPU shard (weak scaling unit): 1 M x 9000 B
         n, L, seed = 1 << 20, 9000, 0x10710005
         d = eng.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device=dev), seed)

@@ -10,4 +10,4 @@ timeout -k 10 300 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.jso
 (cd /tmp && export TMPDIR=/tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv \
    -d "$GRAFT_REPO_ROOT/$O/trace" -o run -- python3 "$GRAFT_REPO_ROOT/bench.py" --no-pmc --no-host --cpu-seconds 0 --steps 20 \
    > "$GRAFT_REPO_ROOT/$O/bench_under_rocprof.json" 2>&1)
-timeout -k 10 600 python3 tools/bench_configs.py --only ns,ipv4,ns64k,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,wrap,streams,batchv,stack > $O/configs.jsonl 2> $O/configs.err
+timeout -k 10 600 python3 tools/bench_configs.py --only ns,ipv4,ns64k,tcp64,mixed,bimodal,jumbo,jumbo_all,host,router,wrap,streams,batchv,stack,rxmix > $O/configs.jsonl 2> $O/configs.err
