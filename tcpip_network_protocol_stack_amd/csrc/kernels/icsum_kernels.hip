@@ -611,87 +611,110 @@ __global__ __launch_bounds__(kBlock) void k_checksum_tiny(const uint8_t* __restr
 }
 
 // Two-class launch for receive mixes (ACKs among MTU segments), no binning
-// pass: wave w reads the bounds of segments [64 w, 64 w + 64), finishes the
-// short ones (<= 4 chunks) one per lane as k_checksum_tiny does, then its
-// long ones LONG_LPS lanes each (the line grid, unroll 8), 64 / LONG_LPS at a
-// time from a per-wave LDS list.
+// pass: block b takes segments [4 SPW b, 4 SPW b + 4 SPW); wave w reads the
+// bounds of SPW of them and appends each to the block's short (<= 4 chunks)
+// or long list in LDS.  Wave 0 then finishes the short ones one per lane (64
+// per pass, as k_checksum_tiny does), while every wave — wave 0 once its
+// short passes are done — claims the long ones 64 / LONG_LPS at a time from
+// an LDS counter (LONG_LPS lanes each, the line grid, unroll 8).  The fused
+// IPv4 launch's block lists (k_ipv4_twoclass); 2 M x 40 / 1460 B 230.8 ->
+// 224.8 us against the per-wave version (tools/probe/csum_mix_probe.hip).
 template <int LONG_LPS, int SPW, int OUT>
 __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __restrict__ bytes, SegSrc src,
                                                               const uint32_t* __restrict__ init, uint32_t init_step,
                                                               const uint8_t* __restrict__ odd, uint32_t odd_step,
                                                               const u32x4* __restrict__ zero16,
                                                               void* __restrict__ out, uint64_t n) {
-  __shared__ uint64_t lst[kBlock / 64][64][2];  // per wave: the long segments' {start, end}
-  __shared__ uint32_t lseg[kBlock / 64][64];
+  constexpr uint32_t kPer = (kBlock / 64) * SPW;
+  __shared__ uint64_t lst[kPer][2], sst[kPer][2];  // the block's long / short segments' {start, end}
+  __shared__ uint32_t lseg[kPer], sseg[kPer];
+  __shared__ uint32_t cnt[3];  // long, short, long claimed
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
+  __syncthreads();
   const Work w{n, nullptr};
-  // SPW segments per wave (lanes >= SPW idle in the short phase): fewer
-  // long segments per wave, so shorter-lived waves when long ones abound
   const uint64_t gi = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
   uint64_t seg, s, e;
   src_locate(src, w, gi, n, seg, s, e);
   const bool valid = gi < n && lane < SPW;
   const uint64_t a0 = s & ~uint64_t(15);
-  const uint64_t span = e > s ? e - a0 : 0;
-  const uint32_t nch = uint32_t((span + 15) >> 4);
+  const uint32_t nch = uint32_t(((e > s ? e - a0 : 0) + 15) >> 4);
   const bool is_short = nch <= 4;
-  // short segments: one lane each (long lanes load the zero block)
-  const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(bytes + a0);
-  u32x4 v[4];
-#pragma unroll
-  for (int u = 0; u < 4; ++u) {
-    const u32x4* q = nch && is_short ? p + (uint32_t(u) < nch ? uint32_t(u) : nch - 1) : zero16;
-    if (nch && is_short) ICS_CHECK16(q, bytes + a0, bytes + a0 + (uint64_t(nch) << 4));
-    v[u] = *q;
+  const uint64_t lmask = __ballot(valid && !is_short), smask = __ballot(valid && is_short);
+  uint32_t lbase = 0, sbase = 0;
+  if (lane == 0) {
+    lbase = atomicAdd(&cnt[0], uint32_t(__builtin_popcountll(lmask)));
+    sbase = atomicAdd(&cnt[1], uint32_t(__builtin_popcountll(smask)));
   }
-  // the long ones go to the wave's list, in lane order
-  const uint64_t lmask = __ballot(valid && !is_short);
-  const uint32_t rank = __builtin_amdgcn_mbcnt_hi(uint32_t(lmask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(lmask), 0u));
+  lbase = __builtin_amdgcn_readfirstlane(lbase);
+  sbase = __builtin_amdgcn_readfirstlane(sbase);
+  const uint32_t lr = __builtin_amdgcn_mbcnt_hi(uint32_t(lmask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(lmask), 0u));
+  const uint32_t sr = __builtin_amdgcn_mbcnt_hi(uint32_t(smask >> 32), __builtin_amdgcn_mbcnt_lo(uint32_t(smask), 0u));
   if (valid && !is_short) {
-    lst[wv][rank][0] = s;
-    lst[wv][rank][1] = e;
-    lseg[wv][rank] = uint32_t(seg);
+    lst[lbase + lr][0] = s;
+    lst[lbase + lr][1] = e;
+    lseg[lbase + lr] = uint32_t(seg);
   }
   if (valid && is_short) {
-    uint32_t ev = 0, od = 0;
-#pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      const uint64_t at = uint64_t(u) << 4;
-      const uint32_t lo = u == 0 ? uint32_t(s) & 15u : 0u;
-      const uint32_t hi = at >= span ? 0u : (span - at >= 16 ? 16u : uint32_t(span - at));
-      acc_chunk(v[u] & byte_range_mask(lo, hi), ev, od);
-    }
-    const uint32_t sw = (uint32_t(s) ^ uint32_t(odd[seg * odd_step])) & 1u;
-    const uint32_t sum = init[seg * init_step] + combine_roles(ev, od, sw);
-    if (OUT == 0)
-      static_cast<uint16_t*>(out)[seg] = fold_value(sum);
-    else
-      static_cast<uint32_t*>(out)[seg] = sum;
+    sst[sbase + sr][0] = s;
+    sst[sbase + sr][1] = e;
+    sseg[sbase + sr] = uint32_t(seg);
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  __syncthreads();
+  const uint32_t nlong = cnt[0], nshort = cnt[1];
+  auto store = [&](uint64_t sg, uint32_t sum) {
+    if (OUT == 0)
+      static_cast<uint16_t*>(out)[sg] = fold_value(sum);
+    else
+      static_cast<uint32_t*>(out)[sg] = sum;
+  };
+  if (wv == 0)
+    for (uint32_t r0 = 0; r0 < nshort; r0 += 64) {  // uniform
+      const uint32_t k = r0 + lane;
+      const bool mine = k < nshort;
+      const uint32_t kc = mine ? k : 0u;
+      const uint64_t ss = sst[kc][0], se = mine ? sst[kc][1] : ss;
+      const uint64_t sg = sseg[kc];
+      const uint64_t b0 = ss & ~uint64_t(15), span = se > ss ? se - b0 : 0;
+      const uint32_t nc = uint32_t((span + 15) >> 4);
+      const u32x4* __restrict__ p = reinterpret_cast<const u32x4*>(bytes + b0);
+      u32x4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {  // an empty slot loads the zero block
+        const u32x4* q = nc ? p + (uint32_t(u) < nc ? uint32_t(u) : nc - 1) : zero16;
+        if (nc) ICS_CHECK16(q, bytes + b0, bytes + b0 + (uint64_t(nc) << 4));
+        v[u] = *q;
+      }
+      const uint32_t i0 = init[sg * init_step];
+      const uint32_t sw = (uint32_t(ss) ^ uint32_t(odd[sg * odd_step])) & 1u;
+      uint32_t ev = 0, od = 0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint64_t at = uint64_t(u) << 4;
+        const uint32_t lo = u == 0 ? uint32_t(ss) & 15u : 0u;
+        const uint32_t hi = at >= span ? 0u : (span - at >= 16 ? 16u : uint32_t(span - at));
+        acc_chunk(v[u] & byte_range_mask(lo, hi), ev, od);
+      }
+      if (mine) store(sg, i0 + combine_roles(ev, od, sw));
+    }
   constexpr uint32_t kGroups = 64 / LONG_LPS;
-  const uint32_t nlong = uint32_t(__builtin_popcountll(lmask));
   const uint32_t g = lane / LONG_LPS, gl = lane & (LONG_LPS - 1);
-  for (uint32_t r0 = 0; r0 < nlong; r0 += kGroups) {  // uniform
+  for (;;) {
+    uint32_t r0 = 0;
+    if (lane == 0) r0 = atomicAdd(&cnt[2], kGroups);
+    r0 = __builtin_amdgcn_readfirstlane(r0);
+    if (r0 >= nlong) break;  // uniform
     const uint32_t k = r0 + g;
     const bool mine = k < nlong;
     const uint32_t kc = mine ? k : 0u;
-    const uint64_t ls = mine ? lst[wv][kc][0] : 0, le = mine ? lst[wv][kc][1] : 0;
-    const uint64_t lsg = lseg[wv][kc];
+    const uint64_t ls = mine ? lst[kc][0] : 0, le = mine ? lst[kc][1] : 0;
+    const uint64_t lsg = lseg[kc];
     const uint32_t i0 = init[lsg * init_step];
     const uint32_t sw = (uint32_t(ls) ^ uint32_t(odd[lsg * odd_step])) & 1u;
     uint32_t ev = 0, od = 0;
     range_sums_line_primed<LONG_LPS, 8, true>(bytes, ls, le, gl, ev, od);
     const uint32_t tot = group_sum<LONG_LPS>(combine_roles(ev, od, sw));
-    if (mine && gl == LONG_LPS - 1) {
-      const uint32_t sum = i0 + tot;
-      if (OUT == 0)
-        static_cast<uint16_t*>(out)[lsg] = fold_value(sum);
-      else
-        static_cast<uint32_t*>(out)[lsg] = sum;
-    }
+    if (mine && gl == LONG_LPS - 1) store(lsg, i0 + tot);
   }
 }
 

@@ -61,6 +61,14 @@ def cases_for(names, engines, dev):
             for tag, e in engines.items():
                 cases[f"{nm}_verify_{tag}"] = (lambda e, d, doff: lambda i: e.ipv4_tcp_batch(
                     d, 1, n=1 << 20, offsets=doff, ip_ck=o[0], tcp_ck=o[1], status=o[2]))(e, d, doff)
+    for nm, af in (("plain_mix50", 0.5), ("plain_mix75", 0.75), ("plain_mix88", 0.875)):  # receive mixes, AUTO
+        if nm in names:
+            d, doff, _ = batch(new, 1 << 20, af, 7)
+            keep.append((d, doff))
+            out_m = torch.empty(1 << 20, dtype=torch.int16, device=dev)
+            for tag, e in engines.items():
+                cases[f"{nm}_{tag}"] = (lambda e, d, doff: lambda i: e.checksum_batch(
+                    d, offsets=doff, out=out_m))(e, d, doff)
     for nm, L in (("dense32", 32), ("tcp64", 64), ("dense128", 128)):  # fixed-stride short segments + inits
         if nm in names:
             n, R = (64 << 20) // L, 6
