@@ -128,9 +128,12 @@ struct ics_ctx {
   static constexpr uint32_t kIpv4TwoClassWide16 = 11;
   // the plain checksum's short-mix threshold (short_mix: the two-class
   // launch); raw-datagram ACK shares, AUTO vs two-class at 16 per wave
-  // (tools/ab_ipv4_mix.py plain rows): 3/8 156.1 vs 144.1 us, 5/16 163.6 vs
-  // 157.8, 1/4 169.6 vs 169.0, 3/16 178.3 vs 181.4
-  static constexpr uint32_t kShortMix16 = 5;
+  // (round 2, tools/ab_ipv4_mix.py plain rows): 3/8 156.1 vs 144.1 us, 5/16
+  // 163.6 vs 157.8, 1/4 169.6 vs 169.0, 3/16 178.3 vs 181.4; with the block
+  // lists (round 3, tools/ab_plain_mix_threshold.py,
+  // profiles/r3_plain_mix_threshold.jsonl): 1/4 169.0 vs 166.1, 3/16 177.3
+  // vs 178.9, 1/8 186.8 vs 190.8
+  static constexpr uint32_t kShortMix16 = 4;
   uint64_t* plan_host = nullptr;      // host view of the kPlanSlots words
   uint64_t* plan_host_dev = nullptr;  // the device's pointer to them
   std::mutex plan_mu;
