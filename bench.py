@@ -103,11 +103,26 @@ def launch_ranks(args):
     return subprocess.call(cmd, env=env)
 
 
+def init_gloo(dist):
+    """Join the gloo group.  Gloo prints "[Gloo] Rank r is connected to ..."
+    on fd 1 while the group forms; that goes to stderr, so stdout holds only
+    rank 0's one JSON line."""
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        dist.init_process_group("gloo")
+        dist.barrier()
+    finally:
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def launch_check(rank, world):
     """Every rank joins a gloo group and rank 0 prints what each one saw."""
     import torch.distributed as dist
 
-    dist.init_process_group("gloo")
+    init_gloo(dist)
     seen = [None] * world
     dist.all_gather_object(seen, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "-1")),
                                   "world_size": dist.get_world_size(),
@@ -309,7 +324,7 @@ def main():
         # host-side group for the timing barrier and the max over ranks only:
         # every rank synchronises its device before either, so a host
         # collective brackets exactly the same work an RCCL one would
-        dist.init_process_group("gloo")
+        init_gloo(dist)
     eng = Engine(local)
     stream = torch.cuda.current_stream(dev)
 

@@ -26,8 +26,9 @@ def test_gpus_n_starts_n_ranks(n):
     r = subprocess.run([sys.executable, BENCH, "--gpus", str(n), "--launch-check"], env=_env(),
                        capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout  # rank 0 only
+    out = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(out) == 1, r.stdout  # rank 0's line only (gloo's connection lines go to stderr)
+    lines = [json.loads(out[0])]
     seen = lines[0]["launch_check"]
     assert sorted(s["rank"] for s in seen) == list(range(n))
     assert sorted(s["local_rank"] for s in seen) == list(range(n))
@@ -49,9 +50,9 @@ def test_driver_style_outer_launcher():
                         "--master-addr", "127.0.0.1", "--master-port", str(port), BENCH, "--gpus", str(n),
                         "--launch-check"], env=_env(), capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-2000:]
-    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
-    assert len(lines) == 1, r.stdout
-    seen = lines[0]["launch_check"]
+    out = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(out) == 1, r.stdout  # the driver reads exactly one line
+    seen = json.loads(out[0])["launch_check"]
     assert sorted(s["rank"] for s in seen) == list(range(n)) and {s["world_size"] for s in seen} == {n}
     assert len({s["pid"] for s in seen}) == n
 
