@@ -230,5 +230,8 @@ def test_auto_reaches_twoclass_from_cached_plan(engine, orc):
         ip, tcp, st = engine.ipv4_tcp_batch(d, 1, offsets=do)
         assert (_u16(ip) == want_v[0]).all() and (_u16(tcp) == want_v[1]).all(), call
         assert (st.cpu().numpy() == want_v[2]).all(), call
-        kinds.append(engine.dispatch_info()["kernel"])
+        info = engine.dispatch_info()
+        kinds.append(info["kernel"])
+        if call:  # 3/4 short datagrams: the wide block lists, 32 per wave (kIpv4TwoClassWide16)
+            assert info["unroll"] == 32, info
     assert kinds[2:] == ["twoclass", "ipv4_twoclass"] * 2, kinds
