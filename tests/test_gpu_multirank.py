@@ -64,3 +64,25 @@ def test_engine_shards_concatenate_to_reference_digest(config, world):
         nb = [s[2] for s in shards]
         ideal = sum(nb) / world
         assert all(abs(b - ideal) < 65536 for b in nb), nb  # each within one segment (< 64 KiB) of an equal share
+
+
+@pytest.mark.gpu
+def test_bench_two_ranks_one_line():
+    """The driver's N > 1 bench as a one-card rehearsal: `bench.py --gpus 2`
+    starts its two ranks itself (torch.distributed.run on 127.0.0.1, gloo for
+    the timing barrier and the max over ranks), and stdout is exactly ONE
+    JSON line — gloo's connection messages kept off it — carrying the NS
+    weak-scaling value over 2 x 1 M segments and the config-5 strong-scaling
+    view (8 M x 9000 B, 4 M segments per rank)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                        "--settle-ms", "10", "--config5-steps", "2", "--no-pmc", "--cpu-seconds", "0"],
+                       capture_output=True, text=True, timeout=400)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(out) == 1, r.stdout
+    d = json.loads(out[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == "weak" and d["value"] > 0
+    assert d["config"]["segments_total"] == 2 << 20 and d["config"]["segments_per_gpu"] == 1 << 20
+    c5 = d["config5"]
+    assert c5["segments_total"] == 8 << 20 and c5["segments_per_gpu"] == 4 << 20 and c5["value"] > 0
+    assert d["cpu_baseline"] is None and d["host_inclusive"] is None  # N = 1 only
