@@ -138,9 +138,9 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, const PlanReq& 
 bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
 
 // a short-heavy mix's single launch: the two-class launch (ACK-sized segments
-// one per lane, the rest 16 lanes each), 32 segments per wave from 3/4 short
-// segments up and 16 below (fewer long segments per wave: shorter-lived
-// waves).  2 M x 40 / 1460 B: 8-lane groups 279.5, two-class 64 / 32 / 16 per
+// one per lane, the rest 16 lanes each; block lists since round 3), 32
+// segments per wave from 3/4 short segments up and 16 below (round 2, the
+// per-wave version: fewer long segments per wave, shorter-lived waves).  2 M x 40 / 1460 B: 8-lane groups 279.5, two-class 64 / 32 / 16 per
 // wave 255.7 / 234.9 / 231.1 us; raw-datagram mixes (tools/ab_ipv4_mix.py
 // plain rows, 64 / 32 / 16): 7/8 ACKs 43.5 / 42.2 / 54.5, 3/4 74.8 / 68.5 /
 // 74.5, 1/2 132.4 / 122.5 / 119.0, 7/16 145.0 / 139.3 / 131.9 us

@@ -95,8 +95,10 @@ SegSpec bin_spec(const SegSpec& whole, const void* list, const uint32_t* meta, i
 // out_kind 0: u16 value(), 1: u32 raw sum
 hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                            int out_kind, Geometry g, uint32_t max_blocks, hipStream_t st);
-// Two-class launch (k_checksum_twoclass): short segments (<= 4 chunks) one
-// per lane, long ones 16 lanes each; spw (16 or 32) segments per wave
+// Two-class launch (k_checksum_twoclass, block lists): each block's short
+// segments (<= 4 chunks) one per lane on one wave, its long ones 16 lanes
+// each claimed by every wave; spw (16 or 32) segments per wave in the
+// bounds pass
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
                                     int out_kind, int spw, hipStream_t st);
 // Dense fixed-stride batches (stride == seg_len in {32, 64, 128}, 16-byte
