@@ -90,7 +90,7 @@ int main(int argc, char** argv) {
   }
   std::vector<Lib> libs;
   for (int i = 1; i < argc; ++i) libs.push_back(open_lib(argv[i]));
-  constexpr uint64_t kL = 1500, kMaxN = 4096;
+  constexpr uint64_t kL = 1500, kMaxN = 8192;
   std::vector<uint8_t> pageable(kMaxN * kL);
   std::mt19937_64 rng(7);
   for (auto& b : pageable) b = uint8_t(rng());
@@ -102,13 +102,15 @@ int main(int argc, char** argv) {
     msgs[i] = ics_tcp_msg{0x0a000001u, 0x0a000002u, uint32_t(rng()), uint32_t(rng()), 40000, 80, 64000, 0x10, 128,
                           0, 0};
   }
-  const uint64_t sizes[] = {1, 4, 16, 64, 256, 512, 1024, 4096};
+  const uint64_t sizes[] = {1, 4, 16, 64, 256, 512, 1024, 4096, 8192};
   const char* ops[] = {"verify", "verify_off", "checksum", "wrap"};
+  const char* only = getenv("TICK_OPS");  // comma list of ops to run (default: all)
   std::vector<uint64_t> offs(kMaxN + 1);
   for (uint64_t i = 0; i <= kMaxN; ++i) offs[i] = i * kL;
   const int rounds = 5, calls = 200;
   for (const char* op : ops)
-    for (int mem = 0; mem < 2; ++mem)
+    for (int mem = 0; mem < 2; ++mem) {
+      if (only && !strstr(only, op)) continue;
       for (uint64_t n : sizes) {
         uint8_t* src = mem ? pinned : pageable.data();
         std::vector<std::vector<double>> t(libs.size());
@@ -142,6 +144,7 @@ int main(int argc, char** argv) {
           fflush(stdout);
         }
       }
+    }
   for (auto& l : libs) l.destroy(l.ctx);
   return 0;
 }
