@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define ICS_ABI_VERSION 1
+#define ICS_ABI_VERSION 2 /* 2: ics_dispatch_info_t gained the host-pipeline counters */
 
 /* ---- status codes ------------------------------------------------------ */
 #define ICS_OK 0
@@ -292,6 +292,8 @@ typedef struct ics_dispatch_info_t {
   int32_t last_lps;        /* its lanes per segment (two-class: long-segment lanes) */
   int32_t last_unroll;     /* its loads in flight per lane (two-class: segments per wave) */
   int32_t last_plan;       /* the cached plan it followed (k_bin_plan ids 0-3), -1 none */
+  uint64_t host_zero_copy; /* *_host calls whose batch the kernel read in place (one chunk, no DMA) */
+  uint64_t host_dma_chunks; /* staged chunks (and long-segment pieces) the *_host calls DMA'd */
 } ics_dispatch_info_t;
 int ics_dispatch_info(const ics_ctx* ctx, ics_dispatch_info_t* info);
 

@@ -38,7 +38,8 @@ class DispatchInfo(ctypes.Structure):
     the plan cache's counters."""
     _fields_ = [("plan_hits", ctypes.c_uint64), ("plan_misses", ctypes.c_uint64),
                 ("plan_requests", ctypes.c_uint64), ("last_kernel", ctypes.c_int32),
-                ("last_lps", ctypes.c_int32), ("last_unroll", ctypes.c_int32), ("last_plan", ctypes.c_int32)]
+                ("last_lps", ctypes.c_int32), ("last_unroll", ctypes.c_int32), ("last_plan", ctypes.c_int32),
+                ("host_zero_copy", ctypes.c_uint64), ("host_dma_chunks", ctypes.c_uint64)]
 
 
 class SegBatch(ctypes.Structure):

@@ -151,6 +151,8 @@ int ics_dispatch_info(const ics_ctx* ctx, ics_dispatch_info_t* info) {
   info->last_lps = ctx->last_lps.load(std::memory_order_relaxed);
   info->last_unroll = ctx->last_unroll.load(std::memory_order_relaxed);
   info->last_plan = ctx->last_plan.load(std::memory_order_relaxed);
+  info->host_zero_copy = ctx->n_host_zc.load(std::memory_order_relaxed);
+  info->host_dma_chunks = ctx->n_host_dma.load(std::memory_order_relaxed);
   return ICS_OK;
 }
 

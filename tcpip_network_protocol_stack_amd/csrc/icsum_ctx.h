@@ -139,6 +139,7 @@ struct ics_ctx {
   std::mutex plan_mu;
   // diagnostics (ics_dispatch_info)
   std::atomic<uint64_t> n_hits{0}, n_misses{0}, n_replans{0};
+  std::atomic<uint64_t> n_host_zc{0}, n_host_dma{0};  // host pipeline: zero-copy calls, DMA'd chunks
   std::atomic<int32_t> last_kernel{0}, last_lps{0}, last_unroll{0}, last_plan{-1};
   // device scratch of the binned dispatch and the two-pass wrap (a binned
   // batch of n segments: 80 n bytes + 16 KiB; a two-pass wrap: 4 n)

@@ -300,6 +300,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
     if (int rc = retire(slot)) return rc;
     const uint64_t m = c.i1 - c.i0, nb = c.b1 - c.b0;
     const bool zc = !c.piece && c.i0 == 0 && c.i1 == n && nb <= ctx->zero_copy_max;
+    (zc ? ctx->n_host_zc : ctx->n_host_dma).fetch_add(1, std::memory_order_relaxed);
     uint8_t* src = static_cast<uint8_t*>(h_bytes) + c.b0;
     if (zc ? !pin.kernel : !direct) {
       par_memcpy(ctx, ctx->h_in[slot], src, nb);

@@ -61,12 +61,13 @@ class Engine:
 
     def dispatch_info(self):
         """ics_dispatch_info: {'plan_hits', 'plan_misses', 'plan_requests',
-        'kernel' (name of the last call's main launch), 'lps', 'unroll', 'plan'}."""
+        'kernel' (name of the last call's main launch), 'lps', 'unroll', 'plan',
+        'host_zero_copy', 'host_dma_chunks' (the *_host pipeline's counters)}."""
         d = _lib.DispatchInfo()
         self._check(self.lib.ics_dispatch_info(self.ctx, ctypes.byref(d)))
         return {"plan_hits": d.plan_hits, "plan_misses": d.plan_misses, "plan_requests": d.plan_requests,
                 "kernel": _lib.KERNELS.get(d.last_kernel), "lps": d.last_lps, "unroll": d.last_unroll,
-                "plan": d.last_plan}
+                "plan": d.last_plan, "host_zero_copy": d.host_zero_copy, "host_dma_chunks": d.host_dma_chunks}
 
     def close(self):
         if self.ctx:

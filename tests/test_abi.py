@@ -42,8 +42,34 @@ def test_version_and_abi():
     from tcpip_network_protocol_stack_amd import _lib
 
     lib = _lib.load()
-    assert lib.ics_abi_version() == 1
+    assert lib.ics_abi_version() == 2
     assert b"gfx950" in lib.ics_version()
+
+
+def test_struct_layouts_match_the_header(tmp_path):
+    """The ctypes mirrors of include/icsum.h's structs have the C compiler's
+    size and field offsets (a field added on one side only would make the
+    library write past the caller's struct)."""
+    from tcpip_network_protocol_stack_amd import _lib
+
+    structs = {"ics_dispatch_info_t": _lib.DispatchInfo, "ics_seg_batch": _lib.SegBatch,
+               "ics_dgram_batch": _lib.DgramBatch}
+    lines = ['#include <stddef.h>', '#include <stdio.h>', '#include "icsum.h"', "int main(void) {"]
+    for c, py in structs.items():
+        t = c if c.endswith("_t") else "struct " + c
+        lines.append(f'  printf("{c} size %zu\\n", sizeof({t}));')
+        for f, _ in py._fields_:
+            lines.append(f'  printf("{c} {f} %zu\\n", offsetof({t}, {f}));')
+    lines += ["  return 0;", "}"]
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines) + "\n")
+    exe = tmp_path / "layout"
+    subprocess.check_call(["gcc", "-std=c11", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)])
+    got = dict(l.rsplit(" ", 1) for l in subprocess.check_output([str(exe)], text=True).splitlines())
+    for c, py in structs.items():
+        assert int(got[f"{c} size"]) == ctypes.sizeof(py), c
+        for f, _ in py._fields_:
+            assert int(got[f"{c} {f}"]) == getattr(py, f).offset, (c, f)
 
 
 def test_no_gpu_fails_loudly():

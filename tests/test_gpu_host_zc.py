@@ -118,3 +118,21 @@ def test_zc_interleaved_calls_no_stale_results(zeng, orc):
             ip, tcp, st = zeng.ipv4_tcp_batch_host(buf.copy(), n, mode, offsets=off)
             w = orc.ipv4_tcp_batch(buf.copy(), n, mode, offsets=off)
             assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), r
+
+
+def test_zc_path_taken_per_threshold(zeng, orc, request):
+    """ics_dispatch_info's host counters show which path each engine took, so
+    a zero-copy path that silently stopped running (equal results either way)
+    fails here: a 6 KB batch is read in place unless zero_copy_max=0; a 3 MB
+    batch (above the default 2 MiB) is DMA'd unless the threshold is 2^30."""
+    param = request.node.callspec.params["zeng"]
+    rng = np.random.default_rng(17)
+    for n, zc_expected in ((4, param != "0"), (2048, param == str(1 << 30))):
+        buf = rng.integers(0, 256, n * 1500, dtype=np.uint8)
+        a = zeng.dispatch_info()
+        got = zeng.checksum_batch_host(buf, n, stride=1500, seg_len=1500)
+        b = zeng.dispatch_info()
+        assert (got == orc.checksum_batch(buf, n, stride=1500, seg_len=1500)).all(), n
+        zc = b["host_zero_copy"] - a["host_zero_copy"]
+        dma = b["host_dma_chunks"] - a["host_dma_chunks"]
+        assert (zc, dma) == ((1, 0) if zc_expected else (0, 1)), (param, n, zc, dma)
