@@ -17,6 +17,14 @@ sharded over the N GPUs — strong scaling, its own timed region after the NS
 one — so a 1/2/4/8 run measures both the north-star weak-scaling value and the
 config-5 curve.
 
+Every timed leg checks its own outputs against the reference's digests
+(tests/golden/configs.json, made by the reference's InternetChecksum,
+util/tools/checksum.h:20-41): `bit_exact` = rank 0's NS shard (the whole
+config-0 batch at any N) and `config5.bit_exact` = all ranks' config-5
+outputs gathered over gloo (the whole 8 M-segment batch).  `per_rank` lists
+each rank's kernel time, wall time, rate and output digest, so an N > 1 line
+can be read rank by rank.
+
 `--gpus N` without an outer launcher starts the N ranks itself (one process
 per GPU via torch.distributed.run on 127.0.0.1; this parent never touches the
 GPU); under a launcher, WORLD_SIZE must equal --gpus.
@@ -49,6 +57,13 @@ sys.path.insert(0, ROOT)
 METRIC = "device-resident GiB/s, Internet checksum over segment batch, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md §Chip-level parameters)
 KERNEL_PREFIX = "k_checksum"
+
+# reference digests (tests/golden/configs.json, computed by the reference's own
+# InternetChecksum, util/tools/checksum.h:20-41, over the whole BASELINE batch):
+# a weak-scaling workload's rank-0 shard IS that batch at any N (rank 0 owns
+# global segments [0, n) of the spec stream); a strong one gathered over the
+# ranks is the whole batch
+GOLDEN_KEY = {"ns_1Mx1500": "0", "tcp_1Mx64": "3", "jumbo_8Mx9000": "5"}
 
 WORKLOADS = {
     # name: (segments, segment bytes, seed, scaling) — DESIGN.md §Workload spec.
@@ -93,7 +108,15 @@ def _free_port():
 
 
 def launch_ranks(args):
-    """`--gpus N` without an outer launcher: start N ranks, one process per GPU,
+    """Every timed leg checks its own outputs against the reference's digests
+(tests/golden/configs.json, made by the reference's InternetChecksum,
+util/tools/checksum.h:20-41): `bit_exact` = rank 0's NS shard (the whole
+config-0 batch at any N) and `config5.bit_exact` = all ranks' config-5
+outputs gathered over gloo (the whole 8 M-segment batch).  `per_rank` lists
+each rank's kernel time, wall time, rate and output digest, so an N > 1 line
+can be read rank by rank.
+
+`--gpus N` without an outer launcher: start N ranks, one process per GPU,
     through torch.distributed.run on 127.0.0.1.  This parent never touches the
     GPU (nothing here imports torch), and the ranks are children, not an exec."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
@@ -101,6 +124,49 @@ def launch_ranks(args):
            f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
     env = dict(os.environ, OMP_NUM_THREADS=os.environ.get("OMP_NUM_THREADS", "1"))
     return subprocess.call(cmd, env=env)
+
+
+def golden_configs():
+    with open(os.path.join(ROOT, "tests", "golden", "configs.json")) as f:
+        return json.load(f)
+
+
+def u16_host(t):
+    import numpy as np
+
+    return t.cpu().numpy().view(np.uint16)
+
+
+def sha256_u16(a):
+    import hashlib
+
+    import numpy as np
+
+    return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def gather_u16(out, dist):
+    """The ranks' u16 outputs in rank order, concatenated on rank 0 (None on
+    the others): one gloo gather of host copies, after the timed region."""
+    import numpy as np
+
+    mine = u16_host(out)
+    if dist is None:
+        return mine
+    parts = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
+    dist.gather_object(mine.tobytes(), parts, dst=0)
+    if parts is None:
+        return None
+    return np.frombuffer(b"".join(parts), dtype=np.uint16)
+
+
+def gather_rows(row, dist):
+    """Every rank's row (a dict) on rank 0, in rank order (None elsewhere)."""
+    if dist is None:
+        return [row]
+    rows = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
+    dist.gather_object(row, rows, dst=0)
+    return rows
 
 
 def init_gloo(dist):
@@ -145,9 +211,15 @@ def pmc_traffic(args):
     cmd = [rocprof, "--pmc", "FETCH_SIZE", "--output-format", "csv", "-d", out, "-o", "pmc", "--",
            sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--warmup", "1",
            "--workload", args.workload, "--cpu-seconds", "0", "--no-pmc"]
+    # a one-rank child on this rank's GPU, also when this process is a rank
+    # of an N > 1 run (it runs before the rank joins its group)
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "ROLE_RANK", "MASTER_ADDR",
+                        "MASTER_PORT", "TORCHELASTIC_RUN_ID")}
+    env["LOCAL_RANK"] = os.environ.get("LOCAL_RANK", "0")
     try:
         subprocess.run(cmd, check=True, timeout=300, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                       cwd=out)
+                       cwd=out, env=env)
         rows = []
         for f in glob.glob(os.path.join(out, "**", "*counter_collection*.csv"), recursive=True):
             with open(f) as fh:
@@ -304,7 +376,9 @@ def main():
 
     # the PMC child pass runs before this process touches the GPU
     traffic, traffic_src = (None, "skipped")
-    if not args.pmc_child and not args.no_pmc and world == 1:
+    if not args.pmc_child and not args.no_pmc and rank == 0:
+        # rank 0's launches (every rank runs the same per-GPU workload); at
+        # N > 1 the other ranks wait in the group rendezvous meanwhile
         traffic, traffic_src = pmc_traffic(args)
 
     import torch
@@ -348,7 +422,7 @@ def main():
         elapsed = time.perf_counter() - t0
         if dist:
             dist.barrier()
-        return shard.max_over_ranks(elapsed, dist), ev0.elapsed_time(ev1) / 1e3 / steps
+        return shard.max_over_ranks(elapsed, dist), ev0.elapsed_time(ev1) / 1e3 / steps, elapsed
 
     def settle(step):
         for _ in range(args.warmup):
@@ -385,10 +459,30 @@ def main():
     # kernel time: HIP events on the stream the kernel runs on, bracketing the
     # K back-to-back launches of the timed region (per-launch event pairs
     # would insert markers between dispatches and measure their gaps too)
-    elapsed, kern_s = timed(step, args.steps)
+    elapsed, kern_s, own_s = timed(step, args.steps)
     bytes_step = n * seg  # algorithmic bytes per rank per step (each byte read once)
     value = n_total * seg * args.steps / elapsed / 2**30  # all ranks' bytes / max-over-ranks time
     achieved = bytes_step / kern_s / 1e9  # GB/s, decimal like the 8 TB/s peak
+
+    # the timed steps' outputs, checked against the reference's digest: rank
+    # 0's shard of a weak-scaling workload is the whole BASELINE batch the
+    # digest covers (its other ranks' shards lie past it in the same spec
+    # stream and are covered by config 5 below, which every rank computes)
+    gold = golden_configs()
+    ns_sha = sha256_u16(u16_host(out))
+    per_rank = gather_rows({"rank": rank, "device": local, "segments": n, "kernel_ms": round(kern_s * 1e3, 4),
+                            "wall_ms_per_step": round(own_s / args.steps * 1e3, 4),
+                            "GiB_s": round(bytes_step * args.steps / own_s / 2**30, 2),
+                            "roofline_frac": round(achieved / HBM_PEAK_GBS, 4), "out_sha256": ns_sha}, dist)
+    key = GOLDEN_KEY.get(args.workload)
+    bit_exact, checked = None, "no reference digest for this workload"
+    if key and scaling == "weak":
+        bit_exact = ns_sha == gold[key]["out_sha256"] if rank == 0 else None
+        checked = f"rank 0's {n} outputs vs tests/golden/configs.json[{key!r}].out_sha256"
+    elif key:
+        whole = gather_u16(out, dist)
+        bit_exact = sha256_u16(whole) == gold[key]["out_sha256"] if rank == 0 else None
+        checked = f"all ranks' {n_total} outputs vs tests/golden/configs.json[{key!r}].out_sha256"
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
@@ -414,13 +508,22 @@ def main():
 
         settle(step5)
         k5 = args.config5_steps or args.steps
-        el5, kern5 = timed(step5, k5)
+        el5, kern5, own5 = timed(step5, k5)
+        # the timed steps' outputs of every rank, gathered in rank order: the
+        # whole 8 M-segment batch, against the reference's digest
+        whole5 = gather_u16(o5, dist)
+        rows5 = gather_rows({"rank": rank, "segments": sh5.n, "kernel_ms": round(kern5 * 1e3, 4),
+                             "wall_ms_per_step": round(own5 / k5 * 1e3, 4),
+                             "roofline_frac": round(sh5.n * seg5 / kern5 / 1e9 / HBM_PEAK_GBS, 4)}, dist)
         config5 = {"workload": "jumbo_8Mx9000", "scaling": "strong", "segments_total": n5,
                    "segments_per_gpu": sh5.n, "segment_bytes": seg5, "steps": k5,
                    "ms_per_step": round(el5 / k5 * 1e3, 4),
                    "value": round(n5 * seg5 * k5 / el5 / 2**30, 2), "unit": "GiB/s",
                    "kernel_ms": round(kern5 * 1e3, 4),
-                   "roofline_frac": round(sh5.n * seg5 / kern5 / 1e9 / HBM_PEAK_GBS, 4)}
+                   "roofline_frac": round(sh5.n * seg5 / kern5 / 1e9 / HBM_PEAK_GBS, 4),
+                   "bit_exact": None if whole5 is None else sha256_u16(whole5) == gold["5"]["out_sha256"],
+                   "checked": f"all ranks' {n5} outputs (gathered) vs tests/golden/configs.json['5'].out_sha256",
+                   "per_rank": rows5}
         del d5, i5, o5
         torch.cuda.empty_cache()
 
@@ -448,6 +551,9 @@ def main():
                          "traffic": None if traffic is None else round(traffic),
                          "kernel_ms": round(kern_s * 1e3, 4),
                          "traffic_source": traffic_src},
+            "bit_exact": bit_exact,
+            "checked": checked,
+            "per_rank": per_rank,
             "cpu_baseline": cpu,
             "config5": config5,
             "host_inclusive": host,

@@ -284,13 +284,30 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 #define ICS_K_WRAP_2PASS 10      /* k_tcp_wrap (payload sums) + k_tcp_hdr */
 #define ICS_K_ROUTER 11          /* k_router_ttl */
 #define ICS_K_BATCHV 12          /* several batches in one launch (ics_*_batchv) */
+#define ICS_K_TILE 13            /* k_tile: an offsets batch as one packed stream, T segments per block */
+/* last_lps / last_unroll by kernel:
+ *   ICS_K_CHECKSUM .. ICS_K_WRAP_2PASS  lanes per segment / loads in flight per lane
+ *   ICS_K_TWOCLASS, ICS_K_IPV4_TWOCLASS  long-segment lanes (16) / segments per wave (16 or 32)
+ *   ICS_K_BATCHV  the ICS_BV_* shape of the last launch group / batches in the call
+ *   ICS_K_TILE    segments per tile (T) / ICS_TILE_* operation
+ *   ICS_K_ROUTER  0 / 0 */
+#define ICS_BV_DENSE64 0 /* fixed stride == length == 64 B, 16-byte aligned */
+#define ICS_BV_TINY 1    /* one lane per segment (ACK-sized fixed lengths) */
+#define ICS_BV_SMALL 2   /* 4-lane groups, two segments in flight */
+#define ICS_BV_LINE16 3  /* 16-lane line grid */
+#define ICS_BV_LINE64 4  /* 64-lane line grid */
+#define ICS_BV_LANE1 5   /* fused IPv4 kernel, one lane per ACK-sized datagram */
+#define ICS_TILE_CHECKSUM 0
+#define ICS_TILE_IPV4 1
+#define ICS_TILE_WRAP 2
+#define ICS_TILE_WRAP_APART 3
 typedef struct ics_dispatch_info_t {
   uint64_t plan_hits;      /* lookups that found this batch's landed plan */
   uint64_t plan_misses;    /* lookups that did not (first call, plan still in flight) */
   uint64_t plan_requests;  /* plan kernels queued behind launches */
   int32_t last_kernel;     /* ICS_K_* of the last call's main launch (0: none yet) */
-  int32_t last_lps;        /* its lanes per segment (two-class: long-segment lanes) */
-  int32_t last_unroll;     /* its loads in flight per lane (two-class: segments per wave) */
+  int32_t last_lps;        /* its lanes per segment (other kernels: see the table above) */
+  int32_t last_unroll;     /* its loads in flight per lane (other kernels: see the table above) */
   int32_t last_plan;       /* the cached plan it followed (k_bin_plan ids 0-3), -1 none */
   uint64_t host_zero_copy; /* *_host calls whose batch the kernel read in place (one chunk, no DMA) */
   uint64_t host_dma_chunks; /* staged chunks (and long-segment pieces) the *_host calls DMA'd */

@@ -83,6 +83,12 @@ struct ics_ctx {
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off)
   int bin_plan = -1;  // -1: decided on the device per batch; forced: 0 whole, 1 split, 2 whole16, 3 wholeS
   int twoclass = 0;   // 0: auto; 16 / 32: every offsets batch through the two-class launch (that many per wave)
+  // tile launches of offsets batches (k_tile): -1 auto, 0 never, 1 every
+  // offsets batch (checksum, fused IPv4, in-place wrap); tile_segs = T
+  // segments per tile (0: tile_segs_for), tile_blocks = grid cap (0: one block per tile)
+  int tile = -1;
+  uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order
+  uint32_t tile_segs = 0, tile_blocks = 0;
   // device wrap: 0 = two passes (payload sums, then a header launch) when
   // the headers go to an array of their own and the batch has at least
   // kWrapTwoPassMin datagrams, otherwise one pass (headers stored inside the

@@ -11,6 +11,20 @@
 
 namespace icsum::detail {
 
+static_assert(icsum::kBvDense64 == ICS_BV_DENSE64 && icsum::kBvTiny == ICS_BV_TINY && icsum::kBvSmall == ICS_BV_SMALL &&
+                  icsum::kBvLine16 == ICS_BV_LINE16 && icsum::kBvLine64 == ICS_BV_LINE64 &&
+                  icsum::kBvLane1 == ICS_BV_LANE1,
+              "multi-batch shapes are reported as ICS_BV_*");
+
+// Segments per tile of a tile launch (k_tile): the forced value, else as
+// many as keep >= 1024 tiles (four per CU) up to 128, at least 16 (128 was
+// the fastest of 32-256 on every mix at 256 Ki and 1 M segments,
+// tools/ab_tile.py)
+uint32_t tile_segs_for(const ics_ctx* ctx, uint64_t n) {
+  if (ctx->tile_segs) return std::min<uint32_t>(ctx->tile_segs, 256);
+  return uint32_t(std::clamp<uint64_t>(n / 1024, 16, 128));
+}
+
 bool wrap_two_pass(const ics_ctx* ctx, bool headers_apart, uint64_t n) {
   return ctx->wrap_passes == 2 || (ctx->wrap_passes == 0 && headers_apart && n >= ics_ctx::kWrapTwoPassMin);
 }
@@ -149,7 +163,7 @@ bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m
 hipError_t launch_mix(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                       void* d_out, int out_kind, const PlanMix& mix, hipStream_t st) {
   const int spw = mix.short16 >= 12 ? 32 : 16;
-  const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, spw, st);
+  const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, spw, ctx->twoclass_remap, st);
   if (e != hipErrorInvalidValue) {
     note(ctx, ICS_K_TWOCLASS, {16, spw, true, 3, 1});
     return e;
@@ -170,8 +184,14 @@ icsum::Geometry small_plan_geometry(const PlanMix& m) {
 int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                     void* d_out, int out_kind, hipStream_t st) {
   if (sp.offsets && ctx->twoclass) {  // test hook: the two-class launch on every offsets batch
-    ICS_HIP(icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, ctx->twoclass, st));
+    ICS_HIP(icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, ctx->twoclass, ctx->twoclass_remap, st));
     note(ctx, ICS_K_TWOCLASS, {16, ctx->twoclass, true, 3, 1});
+    return ICS_OK;
+  }
+  if (sp.offsets && ctx->tile == 1) {  // test hook: the tile launch on every offsets batch
+    const uint32_t T = tile_segs_for(ctx, sp.n);
+    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st));
+    note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM, true, 0, 1});
     return ICS_OK;
   }
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
@@ -320,9 +340,15 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
     two = true;
     spw = ctx->twoclass;
   }
+  if (d_offsets && ctx->tile == 1) {  // test hook
+    const uint32_t T = tile_segs_for(ctx, n);
+    ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, T, ctx->tile_blocks, st));
+    note(ctx, ICS_K_TILE, {int(T), ICS_TILE_IPV4, true, 0, 1}, plan_used);
+    return replan(ctx, sp, 64, req, st);
+  }
   hipError_t le = hipErrorInvalidValue;
   if (two) {
-    le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, spw, st);
+    le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, spw, ctx->twoclass_remap, st);
     if (le != hipErrorInvalidValue) note(ctx, ICS_K_IPV4_TWOCLASS, {16, spw, true, 3, 1}, plan_used);
   }
   if (le == hipErrorInvalidValue) {
@@ -381,6 +407,13 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
   PlanReq req;
   int plan = -1;
   const icsum::Geometry g = wrap_geometry(ctx, sp, hint, &req, &plan);
+  if (sp.offsets && ctx->tile == 1) {  // test hook: the wrap (in place or headers apart) as a tile launch
+    const uint32_t T = tile_segs_for(ctx, sp.n);
+    ICS_HIP(icsum::launch_tile_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), hdr_out, d_ip_ck, d_tcp_ck,
+                                    T, ctx->tile_blocks, st));
+    note(ctx, ICS_K_TILE, {int(T), hdr_out ? ICS_TILE_WRAP_APART : ICS_TILE_WRAP, true, 0, 1}, plan);
+    return replan(ctx, sp, 64, req, st);
+  }
   ICS_HIP(device_wrap(ctx, sp, d_msgs, hdr_out, d_ip_ck, d_tcp_ck, payload_only, g, plan, st));
   return replan(ctx, sp, 64, req, st);
 }
@@ -513,7 +546,11 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "twoclass" && (v == 0 || v == 16 || v == 32)) ctx->twoclass = int(v);
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
+    else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);
+    else if (k == "tile" && v >= -1 && v <= 1) ctx->tile = int(v);
+    else if (k == "tile_segs" && v >= 0 && v <= 256) ctx->tile_segs = uint32_t(v);
+    else if (k == "tile_blocks" && v >= 0) ctx->tile_blocks = uint32_t(v);
     else return fail(ICS_ERR_INVALID, "ICSUM_FORCE: unknown or out-of-range '%s'", item.c_str());
   }
   return ICS_OK;

@@ -16,6 +16,8 @@
 // so there is no inter-workgroup communication and no XCD dependence.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "icsum_device.h"
 #include "icsum_launch.h"
 
@@ -624,7 +626,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
                                                               const uint32_t* __restrict__ init, uint32_t init_step,
                                                               const uint8_t* __restrict__ odd, uint32_t odd_step,
                                                               const u32x4* __restrict__ zero16,
-                                                              void* __restrict__ out, uint64_t n) {
+                                                              void* __restrict__ out, uint64_t n, uint32_t remap) {
   constexpr uint32_t kPer = (kBlock / 64) * SPW;
   __shared__ uint64_t lst[kPer][2], sst[kPer][2];  // the block's long / short segments' {start, end}
   __shared__ uint32_t lseg[kPer], sseg[kPer];
@@ -633,7 +635,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
   if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
   __syncthreads();
   const Work w{n, nullptr};
-  const uint64_t gi = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
+  const uint64_t gi = (uint64_t(block_order(remap)) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
   uint64_t seg, s, e;
   src_locate(src, w, gi, n, seg, s, e);
   const bool valid = gi < n && lane < SPW;
@@ -976,6 +978,51 @@ __device__ __forceinline__ uint32_t ipv4_pseudo(const Hdr& h) {
   return (src >> 16) + (src & 0xffffu) + (dst >> 16) + (dst & 0xffffu) + h.byte(9) + plen;
 }
 
+// The per-datagram results of the fused kernels from its header fields, the
+// TCP bytes 12..19 (tf0 / tf1, read at t0 + 12) and tot = the sum of the TCP
+// part [t0, e) with roles relative to t0: IPv4Header::compute_checksum and
+// the parse checks (ipv4_header.cpp:9-59, 113-123), pseudo_checksum
+// (:103-110), TCPSegment::parse's verify (tcp_segment.cpp:11-18) or
+// compute_checksum with the checksum field counted as 0 (:109-118), the
+// status bits of include/icsum.h, and PATCH's two big-endian stores.
+// hdr false (a datagram under 20 bytes): zeros.
+__device__ __forceinline__ void ipv4_result(uint8_t* __restrict__ dg, uint64_t s, uint64_t e, uint64_t t0, bool hdr,
+                                            const Hdr& h, uint32_t tf0, uint32_t tf1, uint32_t tot, int mode,
+                                            uint64_t seg, uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
+                                            uint8_t* __restrict__ status) {
+  uint16_t ipc = 0, tcv = 0;
+  uint8_t st = 0;
+  if (hdr) {
+    const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu;
+    const bool hdr_ok = ver == 4 && hlen >= 5;  // ipv4_header.cpp:32-41
+    ipc = fold_value(ipv4_header_sum(h));
+    const uint32_t pseudo = ipv4_pseudo(h);
+    const uint64_t rem = e - t0;
+    if (h.byte(9) == 6) st |= 0x08;  // proto TCP
+    if (rem >= 20 && ((tf0 & 0xffu) >> 4) >= 5) st |= 0x04;  // tcp_segment.cpp:25-65
+    if (mode == 1) {
+      tcv = fold_value(pseudo + tot);  // tcp_segment.cpp:11-18
+      if (hdr_ok && ipc == h.be16(10)) st |= 0x01;  // ipv4_header.cpp:53-58
+      if (tcv == 0) st |= 0x02;
+    } else {
+      // tcp_segment.cpp:143: the checksum field counts as 0
+      uint32_t sum = pseudo + tot;
+      if (rem > 16) sum -= (rem >= 18 ? tf1 & 0xffu : uint32_t(dg[t0 + 16])) << 8;
+      if (rem > 17) sum -= (tf1 >> 8) & 0xffu;
+      tcv = fold_value(sum);
+      if (hdr_ok) st |= 0x01;
+      if (rem >= 18) st |= 0x02;
+      if (mode == 2) {
+        store_be16(dg + s + 10, ipc);
+        if (rem >= 18) store_be16(dg + t0 + 16, tcv);
+      }
+    }
+  }
+  if (ip_ck) ip_ck[seg] = ipc;
+  if (tcp_ck) tcp_ck[seg] = tcv;
+  if (status) status[seg] = st;
+}
+
 // --------------------------------------------- fused IPv4 + TCP ----------
 // One datagram [s, e) per group of LPS lanes (every lane of the wave calls it:
 // group sums and the wave-uniform re-sum below); `valid` false: an idle group.
@@ -1030,39 +1077,7 @@ __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, 
     od -= oo;
   }
   const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(t0) & 1u));
-  if (valid && lane == LPS - 1) {
-    uint16_t ipc = 0, tcv = 0;
-    uint8_t st = 0;
-    if (hdr) {
-      const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu;
-      const bool hdr_ok = ver == 4 && hlen >= 5;  // ipv4_header.cpp:32-41
-      ipc = fold_value(ipv4_header_sum(h));
-      const uint32_t pseudo = ipv4_pseudo(h);
-      const uint64_t rem = e - t0;
-      if (h.byte(9) == 6) st |= 0x08;  // proto TCP
-      if (rem >= 20 && ((tf0 & 0xffu) >> 4) >= 5) st |= 0x04;  // tcp_segment.cpp:25-65
-      if (mode == 1) {
-        tcv = fold_value(pseudo + tot);  // tcp_segment.cpp:11-18
-        if (hdr_ok && ipc == h.be16(10)) st |= 0x01;  // ipv4_header.cpp:53-58
-        if (tcv == 0) st |= 0x02;
-      } else {
-        // tcp_segment.cpp:143: the checksum field counts as 0
-        uint32_t sum = pseudo + tot;
-        if (rem > 16) sum -= (rem >= 18 ? tf1 & 0xffu : uint32_t(dg[t0 + 16])) << 8;
-        if (rem > 17) sum -= (tf1 >> 8) & 0xffu;
-        tcv = fold_value(sum);
-        if (hdr_ok) st |= 0x01;
-        if (rem >= 18) st |= 0x02;
-        if (mode == 2) {
-          store_be16(dg + s + 10, ipc);
-          if (rem >= 18) store_be16(dg + t0 + 16, tcv);
-        }
-      }
-    }
-    if (ip_ck) ip_ck[seg] = ipc;
-    if (tcp_ck) tcp_ck[seg] = tcv;
-    if (status) status[seg] = st;
-  }
+  if (valid && lane == LPS - 1) ipv4_result(dg, s, e, t0, hdr, h, tf0, tf1, tot, mode, seg, ip_ck, tcp_ck, status);
 }
 
 // datagrams [blk * groups, ...) striding by nblk blocks (block blk of nblk:
@@ -1116,7 +1131,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
                                                           uint64_t stride, uint64_t dlen, uint64_t n, int mode,
                                                           uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
                                                           uint8_t* __restrict__ status,
-                                                          const uint8_t* __restrict__ zpad) {
+                                                          const uint8_t* __restrict__ zpad, uint32_t remap) {
   constexpr uint32_t kPer = (kBlock / 64) * SPW;
   __shared__ uint64_t lst[kPer][2], sst[kPer][2];  // the block's long / short datagrams' {start, end}
   __shared__ uint32_t lseg[kPer], sseg[kPer];
@@ -1125,7 +1140,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
   if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t seg = (uint64_t(blockIdx.x) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
+  const uint64_t seg = (uint64_t(block_order(remap)) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
   const bool valid = seg < n && lane < SPW;
   uint64_t s, e;
   seg_bounds(offsets, stride, dlen, seg < n ? seg : n - 1, s, e);
@@ -1329,6 +1344,38 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
   }
 }
 
+// The 40 wire bytes wrap_tcp_in_ip puts in front of a payload of plen bytes
+// whose sum (roles relative to the payload start) is tot, from the message
+// record (ics_tcp_msg as dwords: a = src, dst, seqno, ackno; r4 = sport |
+// dport << 16; r5 = window | flags << 16 | ttl << 24; r6 = id): the IPv4
+// header (ipv4_header.cpp:62-86) and TCP header (tcp_segment.cpp:76-106) as
+// 10 little-endian dwords into w, with both checksums —
+// TCPSegment::compute_checksum seeded with the pseudo sum, then
+// IPv4Header::compute_checksum (tcp_over_ip.cpp:83-84) — also into ipc / tcv.
+__device__ __forceinline__ void wrap_header(const u32x4& a, uint32_t r4, uint32_t r5, uint32_t r6, uint64_t plen,
+                                            uint32_t tot, uint32_t* w, uint32_t& ipc, uint32_t& tcv) {
+  auto be16 = [](uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); };
+  const uint32_t sport = r4 & 0xffffu, dport = r4 >> 16, window = r5 & 0xffffu;
+  const uint32_t flags = (r5 >> 16) & 0xffu, ttl = r5 >> 24;
+  const uint32_t len = uint32_t(plen + 40) & 0xffffu;  // IPv4Header::len is uint16
+  const uint32_t addr = (a.x >> 16) + (a.x & 0xffffu) + (a.y >> 16) + (a.y & 0xffffu);
+  ipc = fold_value(0x4500u + len + r6 + 0x4000u + ((ttl << 8) | 6u) + addr);
+  const uint32_t pseudo = addr + 6u + ((len - 20u) & 0xffffu);  // ipv4_header.cpp:103-110
+  const uint32_t thdr = sport + dport + (a.z >> 16) + (a.z & 0xffffu) + (a.w >> 16) + (a.w & 0xffffu) +
+                        (0x5000u | flags) + window;
+  tcv = fold_value(pseudo + thdr + tot);
+  w[0] = 0x45u | (be16(len) << 16);
+  w[1] = be16(r6) | (0x40u << 16);                     // id, DF
+  w[2] = ttl | (6u << 8) | (be16(ipc) << 16);          // ttl, proto, checksum
+  w[3] = bswap32(a.x);
+  w[4] = bswap32(a.y);
+  w[5] = be16(sport) | (be16(dport) << 16);
+  w[6] = bswap32(a.z);
+  w[7] = bswap32(a.w);
+  w[8] = 0x50u | (flags << 8) | (be16(window) << 16);  // data offset 5, flags, window
+  w[9] = be16(tcv);                                    // checksum, urgent pointer 0
+}
+
 // Pass 2 of the device wrap when the headers go to an array of their own and
 // the batch is large (in place, and for short batches, the one-pass k_tcp_wrap
 // above is faster): the headers of 64 datagrams per wave from their 28-byte
@@ -1349,7 +1396,6 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
   __shared__ uint32_t stage[kBlock / 64][64 * 10];  // 10 KiB: each wave's 640 header dwords
   const uint32_t lane64 = threadIdx.x & 63u;
   uint32_t* const sw = stage[threadIdx.x >> 6];
-  auto be16 = [](uint32_t v) { return ((v & 0xffu) << 8) | ((v >> 8) & 0xffu); };
   for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock; b0 < n; b0 += uint64_t(gridDim.x) * kBlock) {
     const uint64_t base = b0 + (threadIdx.x & ~63u);  // the wave's first datagram
     if (base >= n) continue;                          // wave-uniform
@@ -1366,27 +1412,9 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
     __builtin_memcpy(&a, r, 16);
     const uint32_t r4 = r[4], r5 = r[5], r6 = r[6] & 0xffffu;
     const uint32_t tot = sums[idx];
-    const uint32_t sport = r4 & 0xffffu, dport = r4 >> 16, window = r5 & 0xffffu;
-    const uint32_t flags = (r5 >> 16) & 0xffu, ttl = r5 >> 24;
     const uint64_t p0 = payload_only ? s : s + 40;
-    const uint32_t len = uint32_t(e - p0 + 40) & 0xffffu;  // IPv4Header::len is uint16
-    const uint32_t addr = (a.x >> 16) + (a.x & 0xffffu) + (a.y >> 16) + (a.y & 0xffffu);
-    const uint32_t ipc = fold_value(0x4500u + len + r6 + 0x4000u + ((ttl << 8) | 6u) + addr);
-    const uint32_t pseudo = addr + 6u + ((len - 20u) & 0xffffu);  // ipv4_header.cpp:103-110
-    const uint32_t thdr = sport + dport + (a.z >> 16) + (a.z & 0xffffu) + (a.w >> 16) + (a.w & 0xffffu) +
-                          (0x5000u | flags) + window;
-    const uint32_t tcv = fold_value(pseudo + thdr + tot);
-    uint32_t* const my = sw + lane64 * 10;
-    my[0] = 0x45u | (be16(len) << 16);
-    my[1] = be16(r6) | (0x40u << 16);                     // id, DF
-    my[2] = ttl | (6u << 8) | (be16(ipc) << 16);          // ttl, proto, checksum
-    my[3] = bswap32(a.x);
-    my[4] = bswap32(a.y);
-    my[5] = be16(sport) | (be16(dport) << 16);
-    my[6] = bswap32(a.z);
-    my[7] = bswap32(a.w);
-    my[8] = 0x50u | (flags << 8) | (be16(window) << 16);  // data offset 5, flags, window
-    my[9] = be16(tcv);                                    // checksum, urgent pointer 0
+    uint32_t ipc, tcv;
+    wrap_header(a, r4, r5, r6, e - p0, tot, sw + lane64 * 10, ipc, tcv);
     if (valid) {
       if (ip_ck) ip_ck[i] = ok ? uint16_t(ipc) : uint16_t(0);
       if (tcp_ck) tcp_ck[i] = ok ? uint16_t(tcv) : uint16_t(0);
@@ -1495,6 +1523,403 @@ __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
       }
       status[i] = st;
     }
+  }
+}
+
+// ------------------------------------------ tile launches (offsets) -------
+// An offsets batch is one packed byte stream: segment i = [off[i], off[i+1]).
+// A tile = T consecutive segments (T <= 256: one per thread of the block),
+// and the block streams the tile's bytes [off[i0] & ~15, off[i0 + T]) whole,
+// whatever the segment lengths: no lane idles on an ACK-sized segment and no
+// lane group waits on an MTU-sized one (the per-segment launches above map
+// one segment to a lane group).  Each wave takes a contiguous quarter of the
+// tile's 16-byte chunks and streams it on its own — windows of 256 chunks,
+// four coalesced dwordx4 loads per lane, two windows' loads in flight while
+// one is summed, no block barrier — keeping the exclusive prefix of its
+// chunks' even / odd byte sums (a DPP scan per wave instruction).  The
+// segments' points (thread t: lo_t <= hi_t, sorted over the tile) are read
+// off by the wave whose window holds them: F(x), the sums of the wave's bytes
+// below x, is the prefix at x's chunk plus that chunk masked below x.  After
+// one barrier, F(x) gains the earlier waves' totals and segment t's sums over
+// [lo_t, hi_t) are F(hi_t) - F(lo_t): exact in uint32 (addition mod 2^32),
+// roles by address parity.
+//   checksum  lo = start                        (checksum.h:20-41)
+//   IPv4/TCP  lo = start + 4 hlen (TCP part)    (ipv4_header.cpp:50, tcp_segment.cpp:11-18)
+//   wrap      lo = start + 40 (the payload)     (tcp_over_ip.cpp:69-88)
+//   wrap, headers apart: lo = start (segments are payloads), the headers go
+//             to an array of their own, 40 * T contiguous bytes per tile
+// Bytes below the tile's first segment in its first chunk are masked off in
+// every sum that can see them, so a neighbouring tile's in-place stores
+// (PATCH, wrap) never reach one; this tile's own stores follow its stream.
+constexpr uint32_t kTileMax = kBlock;          // segments per tile
+constexpr uint32_t kWinChunks = 256;          // one wave window: 4 KiB, four loads per lane
+constexpr int kTileSum = 0, kTileIpv4 = 1, kTileWrap = 2, kTileWrapApart = 3;
+
+// inclusive prefix sum over the 64 lanes of a wave: row shifts 1, 2, 4, 8,
+// then row 0's total into row 1 and row 2's into row 3, then rows 0-1's into
+// rows 2-3
+__device__ __forceinline__ uint32_t wave_prefix_incl(uint32_t x) {
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, false);  // row_shr:1
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, false);  // row_shr:2
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, false);  // row_shr:4
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, false);  // row_shr:8
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+  x += __builtin_amdgcn_update_dpp(0u, x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+  return x;
+}
+
+struct TileArgs {
+  // checksum: per-segment initial sums and parities (zero16 + step 0 when absent), u16 or u32 out
+  const uint32_t* init;
+  const uint8_t* odd;
+  uint32_t init_step, odd_step;
+  void* out;
+  // IPv4 / TCP: mode and the three outputs (each nullable)
+  int mode;
+  uint16_t* ip_ck;
+  uint16_t* tcp_ck;
+  uint8_t* status;
+  // wrap: the message records; headers apart: the 40-byte headers' array
+  const TcpMsg* msgs;
+  uint32_t* hdr_out;
+};
+
+// One segment's inputs besides its bytes, loaded a tile ahead: its offsets and
+// the operation's per-segment words (checksum: initial sum and parity; IPv4:
+// the header dwords and the TCP fields at start + 20; wrap: the message record)
+struct TileSeg {
+  uint64_t s, e;
+  uint32_t w[9];
+};
+
+template <int OP>
+__device__ __forceinline__ TileSeg tile_seg_load(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                 uint64_t i, bool valid, uint64_t tend, const TileArgs& a,
+                                                 const uint8_t* zpad, const uint32_t* zlast) {
+  TileSeg g{};
+  g.s = valid ? off[i] : tend;
+  g.e = valid ? off[i + 1] : tend;
+  if constexpr (OP == kTileSum) {
+    g.w[0] = a.init[i * a.init_step];
+    g.w[1] = a.odd[i * a.odd_step];
+  } else if constexpr (OP == kTileIpv4) {
+    // the raw dwords of load_hdr and load_tcp_fields (start + 20): aligned on the host side of alignbyte
+    const bool hdr = valid && g.e - g.s >= 20;
+    const uint32_t* last = hdr ? last_dword(bytes + g.e) : zlast;
+    const uint8_t* hp = hdr ? bytes + g.s : zpad;
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(hp - (reinterpret_cast<uintptr_t>(hp) & 3u));
+#pragma unroll
+    for (int k = 0; k < 5; ++k) g.w[k] = q[k];
+    g.w[5] = *(q + 5 < last ? q + 5 : last);
+    const bool tcpf = hdr && g.e - (g.s + 20) >= 18;
+    const uint8_t* tp = tcpf ? bytes + g.s + 32 : zpad;
+    const uint32_t* tq = reinterpret_cast<const uint32_t*>(tp - (reinterpret_cast<uintptr_t>(tp) & 3u));
+    const uint32_t* tlast = tcpf ? last : zlast;
+    g.w[6] = tq[0];
+    g.w[7] = tq[1];
+    g.w[8] = *(tq + 2 < tlast ? tq + 2 : tlast);
+  } else {  // both wraps: the message record
+    const uint32_t* r = reinterpret_cast<const uint32_t*>(a.msgs + i);
+#pragma unroll
+    for (int k = 0; k < 7; ++k) g.w[k] = r[k];
+  }
+  return g;
+}
+
+template <int OP, int OUT>
+__global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                 uint64_t n, uint32_t T, TileArgs a, uint32_t remap,
+                                                 const u32x4* __restrict__ zero16) {
+  constexpr uint32_t kWaves = kBlock / 64;
+  __shared__ uint64_t s_pt[2 * kTileMax];    // the tile's points, sorted: lo_0, hi_0, lo_1, hi_1, ...
+  __shared__ uint32_t s_f[2 * kTileMax][2];  // F of each point over its wave's range (even, odd sums)
+  __shared__ uint32_t s_pre[kWaves][kWinChunks][2];  // each wave's window: exclusive prefix per chunk
+  // ... and its chunks (masked to the tile); the wrap's staged headers once the stream is done
+  __shared__ u32x4 s_raw[kWaves][kWinChunks];
+  __shared__ uint32_t s_tot[kWaves][2];
+  static_assert(sizeof(s_raw) >= 10 * kTileMax * 4, "the wraps stage their headers in s_raw");
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, in a scalar register
+  const uint64_t ntiles = (n + T - 1) / T;
+  const uint8_t* const zpad = reinterpret_cast<const uint8_t*>(zero16);
+  const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zero16) + 7;
+  // A tile's geometry (block-uniform, scalar loads): its segments, bytes,
+  // 16-byte chunks and this wave's quarter of them in windows of kWinChunks
+  // (counted up to a multiple of 4: the window loop below is unrolled by 4)
+  struct Geo {
+    uint64_t i0, first, a0, nch, quarter, wc0, wc1, nwin4;
+    uint32_t m;
+  };
+  auto geo_of = [&](uint64_t t) {
+    Geo g{};
+    if (t >= ntiles) return g;  // no tile: every range empty
+    g.i0 = t * T;
+    g.m = uint32_t(n - g.i0 < T ? n - g.i0 : T);
+    g.first = off[g.i0];
+    const uint64_t tend = off[g.i0 + g.m];
+    g.a0 = g.first & ~uint64_t(15);
+    g.nch = tend > g.a0 ? (tend - g.a0 + 15) >> 4 : 0;
+    const uint64_t q = (((g.nch + kWaves - 1) / kWaves) + 63) & ~uint64_t(63);
+    g.quarter = q ? q : 64;
+    g.wc0 = g.quarter * wv < g.nch ? g.quarter * wv : g.nch;
+    g.wc1 = g.wc0 + g.quarter < g.nch ? g.wc0 + g.quarter : g.nch;
+    g.nwin4 = ((g.wc1 - g.wc0 + kWinChunks - 1) / kWinChunks + 3) & ~uint64_t(3);
+    return g;
+  };
+  // window k of a tile: chunks [c0, c0 + len) (wave-uniform), read with
+  // buffer loads through a scalar resource spanning exactly those chunks: the
+  // lane offset is one 32-bit register for every window, instruction u adds u
+  // KiB as an immediate, and chunks past the range (a short last window, a
+  // window past the end, no tile at all) read as zeros without touching memory
+  const uint32_t voff = lane * 16u;
+  auto load_win = [&](const Geo& g, uint64_t k, u32x4 (&v)[4]) {
+    const uint64_t c0 = g.wc0 + k * kWinChunks;
+    const uint64_t left = g.wc1 > c0 ? g.wc1 - c0 : 0;
+    const uint32_t len = uint32_t(left < kWinChunks ? left : kWinChunks);
+    const u32x4* pw = reinterpret_cast<const u32x4*>(bytes + g.a0) + c0;
+#ifdef ICSUM_BOUNDS_CHECK
+    if (len) {  // the window's first and last chunk inside the tile's envelope
+      const uint8_t* lo8 = bytes + g.a0;
+      ICS_CHECK16(pw, lo8, lo8 + (g.nch << 4));
+      ICS_CHECK16(pw + len - 1, lo8, lo8 + (g.nch << 4));
+    }
+#endif
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4*>(pw), 0, int(len * 16u), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)  // aux 2: non-temporal
+      v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 1024, 2));
+  };
+  uint64_t tile = block_order(remap);
+  Geo g = geo_of(tile);
+  // this thread's segment of the first tile, then the tile's first three windows
+  TileSeg sg_a = tile_seg_load<OP>(bytes, off, g.i0 + (tid < g.m ? tid : 0u), tid < g.m, off[g.i0 + g.m], a, zpad,
+                                   zlast);
+  TileSeg sg_b{};
+  u32x4 b0[4], b1[4], b2[4], b3[4];
+  load_win(g, 0, b0);
+  load_win(g, 1, b1);
+  load_win(g, 2, b2);
+  // One tile: g, its segments' words in cur_sg; the next tile of this block
+  // is gn, whose words go to nxt_sg and whose first three windows are loaded
+  // by this tile's last window group.  The two TileSeg sets alternate between
+  // the loop's two calls (no register copy of a load still in flight, which
+  // would drain every outstanding load at the tile boundary).
+  auto run_tile = [&](const Geo& gn, const TileSeg& cur_sg, TileSeg& nxt_sg) {
+    const bool valid = tid < g.m;
+    const uint64_t i = g.i0 + (valid ? tid : 0u);
+    const uint64_t s = cur_sg.s, e = cur_sg.e;
+#ifdef ICSUM_BOUNDS_CHECK
+    if (valid && e < s) bounds_fail(kBoundsOffsets, i);
+#endif
+    // ---- this tile's points; the per-segment words of the next tile requested
+    Hdr h{};
+    uint32_t tf0 = 0, tf1 = 0;
+    bool hdr = false;
+    uint64_t lo = s;
+    if constexpr (OP == kTileIpv4) {
+      hdr = valid && e - s >= 20;
+      const uint32_t sh = uint32_t(s) & 3u, tsh = uint32_t(s + 32) & 3u;
+#pragma unroll
+      for (int k = 0; k < 5; ++k) h.w[k] = __builtin_amdgcn_alignbyte(cur_sg.w[k + 1], cur_sg.w[k], sh);
+      tf0 = __builtin_amdgcn_alignbyte(cur_sg.w[7], cur_sg.w[6], tsh);
+      tf1 = __builtin_amdgcn_alignbyte(cur_sg.w[8], cur_sg.w[7], tsh);
+      if (hdr) {
+        uint64_t o = 4u * (h.byte(0) & 0x0fu);  // options skipped (ipv4_header.cpp:50)
+        if (o < 20) o = 20;
+        if (o > e - s) o = e - s;
+        lo = s + o;
+      } else {
+        lo = e;
+      }
+    } else if constexpr (OP == kTileWrap) {
+      lo = e - s >= 40 ? s + 40 : e;
+    }
+    nxt_sg = tile_seg_load<OP>(bytes, off, gn.i0 + (tid < gn.m ? tid : 0u), tid < gn.m,
+                               gn.m ? off[gn.i0 + gn.m] : 0, a, zpad, zlast);
+    if (valid) {
+      s_pt[2 * tid] = lo;
+      s_pt[2 * tid + 1] = e;
+    }
+    __syncthreads();
+    const uint32_t npt = 2 * g.m;
+    const uint64_t a0c = g.a0 >> 4;
+    auto chunk_of = [&](uint64_t x) { return (x >> 4) - a0c; };
+    const u32x4 m0 = byte_range_mask(uint32_t(g.first) & 15u, 16u);  // chunk 0: the tile's bytes only
+    // this wave's first point: the first whose chunk is >= wc0 (uniform binary search)
+    uint32_t cur = 0;
+    {
+      uint32_t lo_i = 0, hi_i = npt;
+      while (lo_i < hi_i) {
+        const uint32_t mid = (lo_i + hi_i) >> 1;
+        if (chunk_of(s_pt[mid]) < g.wc0) lo_i = mid + 1;
+        else hi_i = mid;
+      }
+      cur = __builtin_amdgcn_readfirstlane(lo_i);
+    }
+    uint32_t ce = 0, co = 0;  // this wave's sums so far
+    auto window = [&](uint64_t k, const u32x4 (&v)[4]) {
+      const uint64_t c0 = g.wc0 + k * kWinChunks;
+      if (c0 >= g.wc1) return;  // uniform
+      const uint32_t len = uint32_t(g.wc1 - c0 < kWinChunks ? g.wc1 - c0 : kWinChunks);
+      const uint64_t c1 = c0 + len;
+      uint32_t be = ce, bo = co;
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t r = uint32_t(u) * 64u + lane;
+        u32x4 x = v[u];  // zeros past the range
+        if (c0 == 0 && r == 0) x &= m0;
+        uint32_t ev = 0, od = 0;
+        acc_chunk(x, ev, od);
+        const uint32_t ie = wave_prefix_incl(ev), io = wave_prefix_incl(od);
+        s_pre[wv][r][0] = be + ie - ev;
+        s_pre[wv][r][1] = bo + io - od;
+        s_raw[wv][r] = x;
+        be += __builtin_amdgcn_readlane(ie, 63);
+        bo += __builtin_amdgcn_readlane(io, 63);
+      }
+      ce = be;
+      co = bo;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the points in this window, 64 per round (sorted: a prefix of the lanes)
+      for (;;) {  // uniform
+        const uint32_t pi = cur + lane;
+        const uint64_t x = pi < npt ? s_pt[pi] : ~uint64_t(0);
+        const uint64_t c = pi < npt ? chunk_of(x) : ~uint64_t(0);
+        const bool in = c < c1;
+        if (in) {
+          const uint32_t k2 = uint32_t(c - c0);
+          uint32_t pe = s_pre[wv][k2][0], po = s_pre[wv][k2][1];
+          acc_chunk(s_raw[wv][k2] & byte_range_mask(0u, uint32_t(x) & 15u), pe, po);
+          s_f[pi][0] = pe;
+          s_f[pi][1] = po;
+        }
+        const uint32_t cnt = uint32_t(__builtin_popcountll(__ballot(in)));
+        cur += cnt;
+        if (cnt < 64) break;
+      }
+      __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
+    };
+    // Four register sets in turn: three windows' loads in flight while one is
+    // summed.  Loads past this tile's windows fetch the next tile's first
+    // three (a window past any range returns at once: a uniform branch), so
+    // the stream does not pause at the tile boundary.
+    auto load_any = [&](uint64_t k, u32x4 (&v)[4]) {
+      if (k < g.nwin4) load_win(g, k, v);
+      else load_win(gn, k - g.nwin4, v);
+    };
+    for (uint64_t k = 0; k < g.nwin4; k += 4) {  // wave-uniform
+      load_any(k + 3, b3);
+      window(k, b0);
+      load_any(k + 4, b0);
+      window(k + 1, b1);
+      load_any(k + 5, b1);
+      window(k + 2, b2);
+      load_any(k + 6, b2);
+      window(k + 3, b3);
+    }
+    if (g.nwin4 == 0) {  // an empty quarter: the next tile's windows still go out now
+      load_win(gn, 0, b0);
+      load_win(gn, 1, b1);
+      load_win(gn, 2, b2);
+    }
+    if (lane == 0) {
+      s_tot[wv][0] = ce;
+      s_tot[wv][1] = co;
+    }
+    __syncthreads();
+    // F(x) = x's sums within its wave's range + the earlier waves' totals; a
+    // point at the aligned end of the last chunk: every chunk is below it
+    auto F = [&](uint32_t pi, uint64_t x, uint32_t& fe, uint32_t& fo) {
+      const uint64_t c = chunk_of(x);
+      const uint32_t owner = c >= g.nch ? kWaves : uint32_t(c / g.quarter);
+      fe = c >= g.nch ? 0u : s_f[pi][0];
+      fo = c >= g.nch ? 0u : s_f[pi][1];
+#pragma unroll
+      for (uint32_t w = 0; w < kWaves; ++w) {
+        fe += w < owner ? s_tot[w][0] : 0u;
+        fo += w < owner ? s_tot[w][1] : 0u;
+      }
+    };
+    uint32_t fle = 0, flo = 0, fhe = 0, fho = 0;
+    if (valid) {
+      F(2 * tid, lo, fle, flo);
+      F(2 * tid + 1, e, fhe, fho);
+    }
+    const uint32_t se = fhe - fle, so = fho - flo;  // sums of [lo, e)
+    if constexpr (OP == kTileSum) {
+      if (valid) {
+        const uint32_t sum = cur_sg.w[0] + combine_roles(se, so, (uint32_t(lo) ^ cur_sg.w[1]) & 1u);
+        if (OUT == 0)
+          static_cast<uint16_t*>(a.out)[i] = fold_value(sum);
+        else
+          static_cast<uint32_t*>(a.out)[i] = sum;
+      }
+    } else if constexpr (OP == kTileIpv4) {
+      if (valid) {
+        if (hdr && lo != s + 20) {  // options: the TCP fields at the real start
+          tf0 = tf1 = 0;
+          if (e - lo >= 18) load_tcp_fields(bytes + lo, last_dword(bytes + e), tf0, tf1);
+        }
+        ipv4_result(bytes, s, e, lo, hdr, h, tf0, tf1, combine_roles(se, so, uint32_t(lo) & 1u), a.mode, i,
+                    a.ip_ck, a.tcp_ck, a.status);
+      }
+    } else {
+      uint32_t* const stage = reinterpret_cast<uint32_t*>(&s_raw[0][0]);  // the stream is done with it
+      const bool ok = valid && (OP == kTileWrapApart || e - s >= 40);
+      uint32_t ipc = 0, tcv = 0;
+      const u32x4 ra = {cur_sg.w[0], cur_sg.w[1], cur_sg.w[2], cur_sg.w[3]};
+      if (valid) wrap_header(ra, cur_sg.w[4], cur_sg.w[5], cur_sg.w[6] & 0xffffu, e - lo,
+                             combine_roles(se, so, uint32_t(lo) & 1u), stage + tid * 10, ipc, tcv);
+      if (valid) {
+        if (a.ip_ck) a.ip_ck[i] = ok ? uint16_t(ipc) : uint16_t(0);
+        if (a.tcp_ck) a.tcp_ck[i] = ok ? uint16_t(tcv) : uint16_t(0);
+      }
+      __syncthreads();
+      if constexpr (OP == kTileWrapApart) {
+        // the tile's headers are 10 * m consecutive dwords of the array: plain coalesced stores
+        uint32_t* const dst = a.hdr_out + g.i0 * 10;
+#pragma unroll 2
+        for (uint32_t j = 0; j < 10; ++j) {
+          const uint32_t t = j * kBlock + tid;
+          if (t < 10 * g.m) dst[t] = stage[t];
+        }
+      } else {
+        // in place: dword t of the tile = dword t % 10 of datagram t / 10
+        // (neighbouring lanes, neighbouring bytes), 256 per store round
+#pragma unroll 2
+        for (uint32_t j = 0; j < 10; ++j) {
+          const uint32_t t = j * kBlock + tid, d = t / 10, k = t - d * 10;
+          if (d < g.m) {
+            const uint64_t ds = d ? s_pt[2 * d - 1] : g.first, de = s_pt[2 * d + 1];
+            if (de - ds >= 40) {
+              const uint32_t v = stage[t];
+              uint8_t* q8 = bytes + ds + 4 * k;
+              if ((reinterpret_cast<uintptr_t>(q8) & 3u) == 0) {
+                *reinterpret_cast<uint32_t*>(q8) = v;
+              } else {
+#pragma unroll
+                for (int b = 0; b < 4; ++b) q8[b] = uint8_t(v >> (8 * b));
+              }
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();  // the shared arrays are the next tile's
+  };
+  while (tile < ntiles) {  // block-uniform; two tiles per pass, the TileSeg sets in turn
+    Geo gn = geo_of(tile + gridDim.x);
+    run_tile(gn, sg_a, sg_b);
+    tile += gridDim.x;
+    g = gn;
+    if (tile >= ntiles) break;
+    gn = geo_of(tile + gridDim.x);
+    run_tile(gn, sg_b, sg_a);
+    tile += gridDim.x;
+    g = gn;
   }
 }
 
@@ -1677,6 +2102,24 @@ __global__ __launch_bounds__(kBlock) void k_bin_scatter(const uint64_t* __restri
   }
 }
 
+// The most 256-thread blocks one dispatch holds: HSA packets carry the grid
+// in work-items as a uint32, so 2^24 blocks would be one work-item too many.
+// The two-class launches (one block per 64 or 128 segments) refuse batches
+// past it with hipErrorInvalidValue, and the dispatch falls back to a
+// grid-stride launch (8-lane groups / the fused kernel).
+constexpr uint64_t kMaxGridBlocks = (uint64_t(1) << 24) - 1;
+constexpr uint64_t twoclass_blocks(uint64_t n, uint64_t spw) {  // 4 waves x spw segments per block
+  return (n + (kBlock / 64) * spw - 1) / ((kBlock / 64) * spw);
+}
+static_assert(uint64_t(kBlock) * kMaxGridBlocks <= 0xFFFFFFFFull, "grid work-items fit a uint32");
+// the boundary ADVICE r3 found: n in (2^31 - 128, 2^31] at 32 per wave (or
+// (2^30 - 64, 2^30] at 16) needs 2^24 blocks and must be refused
+static_assert(twoclass_blocks((uint64_t(1) << 31) - 127, 32) > kMaxGridBlocks &&
+                  twoclass_blocks((uint64_t(1) << 31) - 128, 32) == kMaxGridBlocks &&
+                  twoclass_blocks((uint64_t(1) << 30) - 63, 16) > kMaxGridBlocks &&
+                  twoclass_blocks((uint64_t(1) << 30) - 64, 16) == kMaxGridBlocks,
+              "two-class grids: the largest batches that still fit");
+
 // element-wise grid: at most 64K blocks (16M work-items), grid-stride beyond
 inline uint32_t ew_blocks(uint64_t n) {
   const uint64_t b = (n + kBlock - 1) / kBlock;
@@ -1733,20 +2176,19 @@ hipError_t launch_checksum_small_t(const SegSpec& sp, const uint32_t* init, cons
 
 template <int LONG_LPS, int SPW>
 hipError_t launch_twoclass_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                             hipStream_t st) {
-  const uint64_t per_block = uint64_t(kBlock / 64) * SPW;
-  const uint64_t blocks = (sp.n + per_block - 1) / per_block;
-  if (blocks == 0 || blocks > (uint64_t(1) << 24)) return hipErrorInvalidValue;
+                             uint32_t remap, hipStream_t st) {
+  const uint64_t blocks = twoclass_blocks(sp.n, SPW);
+  if (blocks == 0 || blocks > kMaxGridBlocks) return hipErrorInvalidValue;
   const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
   const uint8_t* op = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
   const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
   const u32x4* z = static_cast<const u32x4*>(sp.zero16);
   if (out_kind == 0)
     hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, SPW, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st,
-                       sp.bytes, src_of(sp), ip, is, op, os, z, out, sp.n);
+                       sp.bytes, src_of(sp), ip, is, op, os, z, out, sp.n, remap);
   else
     hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, SPW, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st,
-                       sp.bytes, src_of(sp), ip, is, op, os, z, out, sp.n);
+                       sp.bytes, src_of(sp), ip, is, op, os, z, out, sp.n, remap);
   return hipGetLastError();
 }
 
@@ -1804,6 +2246,20 @@ hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_ou
     hipLaunchKernelGGL((k_tcp_wrap<LPS, UNROLL, NT, MODE, false>), dim3(blocks), dim3(kBlock), 0, st,
                        const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, msgs, hdr_out,
                        ip_ck, tcp_ck, g_xcd_remap, int(payload_only), sums);
+  return hipGetLastError();
+}
+
+template <int OP, int OUT>
+hipError_t launch_tile_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint32_t max_blocks, hipStream_t st) {
+  if (!sp.offsets || sp.list || sp.n == 0 || T == 0 || T > kTileMax) return hipErrorInvalidValue;
+  const uint64_t tiles = (sp.n + T - 1) / T;
+  // one block per tile by default (measured faster than a persistent grid of
+  // the resident blocks, tools/ab_tile.py); a capped grid (max_blocks) takes
+  // every gridDim-th tile with the next one's loads overlapping its own
+  const uint64_t cap = max_blocks ? max_blocks : kMaxGridBlocks;
+  const uint32_t blocks = uint32_t(tiles < cap ? tiles : cap);
+  hipLaunchKernelGGL((k_tile<OP, OUT>), dim3(blocks), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes),
+                     sp.offsets, sp.n, T, a, g_xcd_remap, static_cast<const u32x4*>(sp.zero16));
   return hipGetLastError();
 }
 
@@ -1875,10 +2331,10 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
 }
 
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
-                                    int out_kind, int spw, hipStream_t st) {
+                                    int out_kind, int spw, uint32_t remap, hipStream_t st) {
   if (sp.list) return hipErrorInvalidValue;
-  if (spw == 32) return launch_twoclass_t<16, 32>(sp, init, odd, out, out_kind, st);
-  if (spw == 16) return launch_twoclass_t<16, 16>(sp, init, odd, out, out_kind, st);
+  if (spw == 32) return launch_twoclass_t<16, 32>(sp, init, odd, out, out_kind, remap, st);
+  if (spw == 16) return launch_twoclass_t<16, 16>(sp, init, odd, out, out_kind, remap, st);
   return hipErrorInvalidValue;
 }
 
@@ -2013,19 +2469,18 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 }
 
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                int spw, hipStream_t st) {
+                                int spw, uint32_t remap, hipStream_t st) {
   if (spw != 16 && spw != 32) return hipErrorInvalidValue;
-  const uint64_t per_block = uint64_t(kBlock / 64) * uint64_t(spw);
-  const uint64_t blocks = (sp.n + per_block - 1) / per_block;
-  if (sp.list || blocks == 0 || blocks > (uint64_t(1) << 24)) return hipErrorInvalidValue;
+  const uint64_t blocks = twoclass_blocks(sp.n, uint64_t(spw));
+  if (sp.list || blocks == 0 || blocks > kMaxGridBlocks) return hipErrorInvalidValue;
   uint8_t* const dg = const_cast<uint8_t*>(sp.bytes);
   const uint8_t* const z = static_cast<const uint8_t*>(sp.zero16);
   if (spw == 16)
     hipLaunchKernelGGL(k_ipv4_twoclass<16>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, dg, sp.offsets, sp.stride,
-                       sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z);
+                       sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z, remap);
   else
     hipLaunchKernelGGL(k_ipv4_twoclass<32>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, dg, sp.offsets, sp.stride,
-                       sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z);
+                       sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z, remap);
   return hipGetLastError();
 }
 
@@ -2041,11 +2496,50 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
   ICS_GEOMETRIES(ICS_CASE)
 #undef ICS_CASE
   if (e != hipSuccess || !sums) return e;
+  return launch_tcp_hdr(sp, msgs, sums, hdr_out, ip_ck, tcp_ck, payload_only, st);
+}
+
+hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t* sums, uint32_t* hdr_out,
+                          uint16_t* ip_ck, uint16_t* tcp_ck, bool payload_only, hipStream_t st) {
+  if (sp.n == 0) return hipSuccess;
   const uint64_t blocks = (sp.n + kBlock - 1) / kBlock;  // one datagram per lane
   hipLaunchKernelGGL(k_tcp_hdr, dim3(uint32_t(blocks < (uint64_t(1) << 22) ? blocks : (uint64_t(1) << 22))),
                      dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n,
                      msgs, sums, hdr_out, ip_ck, tcp_ck, int(payload_only));
   return hipGetLastError();
+}
+
+hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
+                                uint32_t T, uint32_t max_blocks, hipStream_t st) {
+  TileArgs a{};
+  a.init = init ? init : static_cast<const uint32_t*>(sp.zero16);
+  a.odd = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
+  a.init_step = init ? 1u : 0u;
+  a.odd_step = odd ? 1u : 0u;
+  a.out = out;
+  return out_kind == 0 ? launch_tile_t<kTileSum, 0>(sp, a, T, max_blocks, st)
+                       : launch_tile_t<kTileSum, 1>(sp, a, T, max_blocks, st);
+}
+
+hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
+                            uint32_t T, uint32_t max_blocks, hipStream_t st) {
+  TileArgs a{};
+  a.mode = mode;
+  a.ip_ck = ip_ck;
+  a.tcp_ck = tcp_ck;
+  a.status = status;
+  return launch_tile_t<kTileIpv4, 0>(sp, a, T, max_blocks, st);
+}
+
+hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
+                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st) {
+  TileArgs a{};
+  a.msgs = msgs;
+  a.hdr_out = hdr_out;
+  a.ip_ck = ip_ck;
+  a.tcp_ck = tcp_ck;
+  return hdr_out ? launch_tile_t<kTileWrapApart, 0>(sp, a, T, max_blocks, st)
+                 : launch_tile_t<kTileWrap, 0>(sp, a, T, max_blocks, st);
 }
 
 uint64_t batchv_blocks(int cls, uint64_t n) {

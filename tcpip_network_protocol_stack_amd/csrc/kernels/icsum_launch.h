@@ -99,8 +99,9 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
 // segments (<= 4 chunks) one per lane on one wave, its long ones 16 lanes
 // each claimed by every wave; spw (16 or 32) segments per wave in the
 // bounds pass
+// (remap: block_order's log2 XCD run length, 0 = hardware order)
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
-                                    int out_kind, int spw, hipStream_t st);
+                                    int out_kind, int spw, uint32_t remap, hipStream_t st);
 // Dense fixed-stride batches (stride == seg_len in {32, 64, 128}, 16-byte
 // aligned bytes, no parity array): k_checksum_dense, SEGS segments per lane
 // group in flight (segs in {1, 2, 4, 8}; not every (seg_len, segs) pair exists)
@@ -137,6 +138,7 @@ static_assert(sizeof(BvSeg) == 64 && sizeof(BvDgram) == 64, "multi-batch descrip
 // lengths), 4-lane groups with two segments in flight (short fixed lengths),
 // the 16- and 64-lane line grids (MTU-sized / long or unknown mixes), and the
 // fused kernel's one lane per ACK-sized datagram
+// (the ICS_BV_* values ics_dispatch_info reports)
 enum BvClass : int { kBvDense64 = 0, kBvTiny = 1, kBvSmall = 2, kBvLine16 = 3, kBvLine64 = 4, kBvLane1 = 5 };
 // blocks one batch of n segments takes in a launch of class cls
 uint64_t batchv_blocks(int cls, uint64_t n);
@@ -146,7 +148,8 @@ hipError_t launch_checksum_batchv(const BvSeg* b, int k, int cls, const void* ze
 hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const void* zero16, hipStream_t st);
 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
-void set_xcd_remap(uint32_t run_log2);  // log2 XCD run length (default 10 = 1024 blocks), 0: hardware order
+void set_xcd_remap(uint32_t run_log2);
+void set_twoclass_remap(uint32_t run_log2);  // the two-class launches' (default 0: hardware order)  // log2 XCD run length (default 10 = 1024 blocks), 0: hardware order
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
 // one thread stores v into *flag (page-locked, coherent host memory) with
 // system-scope release, behind the stream's earlier work
@@ -158,8 +161,18 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 // (k_ipv4_twoclass); spw (16 or 32) datagrams per wave in the bounds pass,
 // i.e. 64 or 128 per block
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                int spw, hipStream_t st);
+                                int spw, uint32_t remap, hipStream_t st);
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
+
+// Tile launches of offsets batches (k_tile): T (1..256) consecutive segments
+// per block, the tile's bytes streamed whole in 16 KiB windows whatever the
+// lengths; max_blocks 0: one block per tile (capped, grid-stride beyond).
+// Checksum (out_kind as launch_checksum), the fused IPv4/TCP kernel (mode as
+// launch_ipv4_tcp) and the in-place wrap (as launch_tcp_wrap in place).
+hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
+                                uint32_t T, uint32_t max_blocks, hipStream_t st);
+hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
+                            uint32_t T, uint32_t max_blocks, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg
 // (include/icsum.h), 28 bytes.
@@ -179,6 +192,14 @@ static_assert(sizeof(TcpMsg) == 28, "ics_tcp_msg layout");
 hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
                            uint16_t* tcp_ck, bool payload_only, uint32_t* sums, Geometry g, uint32_t max_blocks,
                            hipStream_t st);
+// the wrap as a tile launch: in place (hdr_out null) or, with hdr_out, the
+// payload-only batch of ics_tcp_wrap_headers with its headers to hdr_out
+hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
+                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st);
+// pass 2 of the two-pass wrap alone (k_tcp_hdr): headers from the records and
+// the payload sums pass 1 left in `sums` (roles from each payload's start)
+hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t* sums, uint32_t* hdr_out,
+                          uint16_t* ip_ck, uint16_t* tcp_ck, bool payload_only, hipStream_t st);
 
 // bounds-checked build (libicsum_debug.so): synchronise `st` and take (read
 // and clear) the device's violation record; flags 0 = clean.  No-op returning

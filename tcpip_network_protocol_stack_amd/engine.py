@@ -40,6 +40,19 @@ def _stream(stream, device):
     return ctypes.c_void_p(s.cuda_stream)
 
 
+def _count(n, offsets, data, stride):
+    """Segments of a batch: n when given, else from the offsets (n + 1
+    entries), else from a positive fixed stride; a fixed-stride batch with no
+    stride and no n is an error (not one segment per byte)."""
+    if n is not None:
+        return int(n)
+    if offsets is not None:
+        return offsets.numel() - 1
+    if not stride or stride <= 0:
+        raise ValueError("batch without n, offsets or a positive stride")
+    return data.numel() // stride
+
+
 class Engine:
     """One engine context bound to one GPU (ics_create / ics_destroy)."""
 
@@ -84,8 +97,7 @@ class Engine:
     def checksum_batch(self, data, n=None, offsets=None, stride=0, seg_len=0, init=None, out=None,
                        stream=None):
         """u16 InternetChecksum{init_i}.add(segment_i).value() for every segment."""
-        if n is None:
-            n = offsets.numel() - 1 if offsets is not None else data.numel() // max(stride, 1)
+        n = _count(n, offsets, data, stride)
         if out is None:
             out = torch.empty(n, dtype=torch.int16, device=self.device)
         self._check(self.lib.ics_checksum_batch(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len,
@@ -95,8 +107,7 @@ class Engine:
     def sum_batch(self, data, n=None, offsets=None, stride=0, seg_len=0, init=None, odd=None,
                   out=None, stream=None):
         """Unfolded uint32 sum_ after add(segment_i) with parity odd_i (add() chains)."""
-        if n is None:
-            n = offsets.numel() - 1 if offsets is not None else data.numel() // max(stride, 1)
+        n = _count(n, offsets, data, stride)
         if out is None:
             out = torch.empty(n, dtype=torch.int32, device=self.device)
         self._check(self.lib.ics_sum_batch(self.ctx, _ptr(data), _ptr(offsets), stride, seg_len, _ptr(init),
@@ -118,9 +129,7 @@ class Engine:
         outs = []
         for j, b in enumerate(batches):
             offsets = b.get("offsets")
-            n = b.get("n")
-            if n is None:
-                n = offsets.numel() - 1 if offsets is not None else b["data"].numel() // max(b.get("stride", 1), 1)
+            n = _count(b.get("n"), offsets, b["data"], b.get("stride", 0))
             out = b.get("out")
             if out is None:
                 out = torch.empty(n, dtype=torch.int16, device=self.device)
@@ -138,9 +147,7 @@ class Engine:
         outs = []
         for j, b in enumerate(batches):
             offsets = b.get("offsets")
-            n = b.get("n")
-            if n is None:
-                n = offsets.numel() - 1 if offsets is not None else b["dgrams"].numel() // max(b.get("stride", 1), 1)
+            n = _count(b.get("n"), offsets, b["dgrams"], b.get("stride", 0))
             mk = lambda dt: torch.empty(n, dtype=dt, device=self.device)  # noqa: E731
             o = tuple(b.get(k) if b.get(k) is not None else mk(dt)
                       for k, dt in (("ip_ck", torch.int16), ("tcp_ck", torch.int16), ("status", torch.uint8)))
@@ -153,8 +160,7 @@ class Engine:
     # ---- fused IPv4 + TCP --------------------------------------------------
     def ipv4_tcp_batch(self, dgrams, mode, n=None, offsets=None, stride=0, dgram_len=0,
                        ip_ck=None, tcp_ck=None, status=None, stream=None):
-        if n is None:
-            n = offsets.numel() - 1 if offsets is not None else dgrams.numel() // max(stride, 1)
+        n = _count(n, offsets, dgrams, stride)
         mk = lambda dt: torch.empty(n, dtype=dt, device=self.device)  # noqa: E731
         ip_ck = mk(torch.int16) if ip_ck is None else ip_ck
         tcp_ck = mk(torch.int16) if tcp_ck is None else tcp_ck
@@ -169,8 +175,7 @@ class Engine:
                        tcp_ck=None, stream=None):
         """Headers + both checksums of every datagram written in place on the
         device; `msgs` is a device tensor holding n ics_tcp_msg records."""
-        if n is None:
-            n = offsets.numel() - 1 if offsets is not None else dgrams.numel() // max(stride, 1)
+        n = _count(n, offsets, dgrams, stride)
         self._check(self.lib.ics_tcp_wrap_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
                                           _ptr(msgs), _ptr(ip_ck), _ptr(tcp_ck), _stream(stream, self.device)))
         return dgrams
@@ -178,8 +183,7 @@ class Engine:
     def tcp_wrap_headers(self, payloads, msgs, hdrs, n=None, offsets=None, stride=0, payload_len=0, ip_ck=None,
                          tcp_ck=None, stream=None):
         """Payload-only batch; the 40 header bytes of datagram i go to hdrs[40 i:]."""
-        if n is None:
-            n = offsets.numel() - 1 if offsets is not None else payloads.numel() // max(stride, 1)
+        n = _count(n, offsets, payloads, stride)
         self._check(self.lib.ics_tcp_wrap_headers(self.ctx, _ptr(payloads), _ptr(offsets), stride, payload_len, n,
                                                   _ptr(msgs), _ptr(hdrs), _ptr(ip_ck), _ptr(tcp_ck),
                                                   _stream(stream, self.device)))
@@ -201,8 +205,7 @@ class Engine:
 
     def router_ttl_batch(self, dgrams, n=None, offsets=None, stride=0, dgram_len=0, status=None,
                          stream=None):
-        if n is None:
-            n = offsets.numel() - 1 if offsets is not None else dgrams.numel() // max(stride, 1)
+        n = _count(n, offsets, dgrams, stride)
         status = torch.empty(n, dtype=torch.uint8, device=self.device) if status is None else status
         self._check(self.lib.ics_router_ttl_batch(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
                                             _ptr(status), _stream(stream, self.device)))

@@ -53,8 +53,16 @@ def _worker(rank, port, q):
         parts4 = [None] * WORLD
         dist.all_gather_object(parts4, (ms.index0, o4.tolist(), ms.nbytes))
         t = shard.max_over_ranks(0.25 + rank, dist)
+        # bench.py's self-check at N > 1: the ranks' u16 outputs gathered in
+        # rank order over gloo, and one row per rank
+        import bench
+
+        whole = bench.gather_u16(torch.from_numpy(out.view(np.int16)), dist)
+        rows = bench.gather_rows({"rank": rank, "segments": sh.n}, dist)
         if rank == 0:
-            q.put((parts, parts4, t))
+            q.put((parts, parts4, t, bench.sha256_u16(whole), rows))
+        else:
+            assert whole is None and rows is None
     finally:
         dist.destroy_process_group()
 
@@ -66,7 +74,7 @@ def test_two_rank_shards_concatenate_to_single_gpu_result(orc):
     procs = [ctx.Process(target=_worker, args=(r, port, q)) for r in range(WORLD)]
     for p in procs:
         p.start()
-    parts, parts4, tmax = q.get(timeout=240)
+    parts, parts4, tmax, whole_sha, rows = q.get(timeout=240)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
@@ -76,6 +84,10 @@ def test_two_rank_shards_concatenate_to_single_gpu_result(orc):
                               init=orc.pseudo_inits(seed, n, length=L))
     got = [x for _, o in sorted(parts) for x in o]
     assert got == full.tolist()
+    import hashlib
+
+    assert whole_sha == hashlib.sha256(full.astype(np.uint16).tobytes()).hexdigest()
+    assert [r["rank"] for r in rows] == [0, 1] and sum(r["segments"] for r in rows) == n
     # mixed, byte balanced
     m, seed4 = 3000, 0x10710004
     lens = np.array([orc.mixed_len(seed4, i) for i in range(m)], dtype=np.uint64)

@@ -433,16 +433,31 @@ def main():
 
         n, seed = 1 << 18, 0x10710007
         rng = np.random.default_rng(seed)
-        rl = np.where(rng.random(n) < 0.5, 40, 1500)  # received: half pure ACKs, half MTU segments
+        # received: half pure ACKs (40 B), half MTU segments, back to back, with
+        # valid IPv4/TCP headers (ver 4, hlen 5, len, DF, ttl 64, TCP, data
+        # offset 5; both checksums set by a PATCH pass) — what a TUN read ring holds
+        rl = np.where(rng.random(n) < 0.5, 40, 1500)
         roff = np.zeros(n + 1, dtype=np.uint64)
         roff[1:] = np.cumsum(rl)
-        tl = 40 + rng.integers(0, 1001, n)  # transmitted: payloads of 0..1000 bytes behind 40 bytes of room
+        rbuf = rng.integers(0, 256, int(roff[-1]) + 16, dtype=np.uint8)
+        rs = roff[:-1].astype(np.int64)
+        rbuf[rs], rbuf[rs + 1], rbuf[rs + 2], rbuf[rs + 3] = 0x45, 0, (rl >> 8).astype(np.uint8), (rl & 255).astype(np.uint8)
+        rbuf[rs + 6], rbuf[rs + 7], rbuf[rs + 8], rbuf[rs + 9], rbuf[rs + 32] = 0x40, 0, 64, 6, 0x50
+        # transmitted: payloads of 0..1000 bytes (TCPConfig::MAX_PAYLOAD_SIZE) behind 40 bytes of room
+        pl = rng.integers(0, 1001, n)
+        tl = 40 + pl
         toff = np.zeros(n + 1, dtype=np.uint64)
         toff[1:] = np.cumsum(tl)
-        rx = eng.fill_bytes(torch.empty(int(roff[-1]) + 16, dtype=torch.uint8, device=dev), seed)
+        poff = np.zeros(n + 1, dtype=np.uint64)  # the same payloads alone (headers apart)
+        poff[1:] = np.cumsum(pl)
+        rx = torch.from_numpy(rbuf).to(dev)
         tx = eng.fill_bytes(torch.empty(int(toff[-1]) + 16, dtype=torch.uint8, device=dev), seed + 1)
+        px = eng.fill_bytes(torch.empty(int(poff[-1]) + 16, dtype=torch.uint8, device=dev), seed + 2)
+        hd = torch.empty(n * 40, dtype=torch.uint8, device=dev)
         drof = torch.from_numpy(roff.view(np.int64)).to(dev)
         dtof = torch.from_numpy(toff.view(np.int64)).to(dev)
+        dpof = torch.from_numpy(poff.view(np.int64)).to(dev)
+        eng.ipv4_tcp_batch(rx, 2, n=n, offsets=drof)  # PATCH: valid checksums
         m = np.zeros(n, dtype=TCP_MSG_DTYPE)
         for f, hi in (("src", 2**32), ("dst", 2**32), ("seqno", 2**32), ("ackno", 2**32), ("src_port", 2**16),
                       ("dst_port", 2**16), ("window", 2**16)):
@@ -459,6 +474,9 @@ def main():
         def wrap():
             eng.tcp_wrap_batch(tx, dm, n=n, offsets=dtof)
 
+        def wrap_apart():  # the iovec form: payload arena + the 40-byte headers in an array of their own
+            eng.tcp_wrap_headers(px, dm, hd, n=n, offsets=dpof)
+
         def per_call(fn, other, calls):
             """median of per-call HIP-event times of fn, each call alone or right after `other`"""
             st = torch.cuda.current_stream()
@@ -474,25 +492,38 @@ def main():
             torch.cuda.synchronize()
             return statistics.median(a.elapsed_time(b) / 1e3 for a, b in evs), eng.dispatch_info()
 
-        for _ in range(4):  # both keys miss once, then their plans land
+        for _ in range(4):  # every key misses once, then its plan lands
             verify()
             wrap()
+            wrap_apart()
         torch.cuda.synchronize()
         calls = args.iters * args.rounds
         rows = {}
+        entries = {verify: "ics_ipv4_tcp_batch VERIFY", wrap: "ics_tcp_wrap_batch",
+                   wrap_apart: "ics_tcp_wrap_headers"}
         for name, fn, other in (("verify_alone", verify, None), ("verify_after_wrap", verify, wrap),
-                                ("wrap_alone", wrap, None), ("wrap_after_verify", wrap, verify)):
+                                ("wrap_alone", wrap, None), ("wrap_after_verify", wrap, verify),
+                                ("wrap_apart_alone", wrap_apart, None), ("wrap_apart_after_verify", wrap_apart, verify)):
             before = eng.dispatch_info()
             t, info = per_call(fn, other, calls)
             rows[name] = t
-            nbytes = int(roff[-1]) if fn is verify else int(toff[-1])
+            nbytes = int(roff[-1]) if fn is verify else int(toff[-1])  # wrap: payloads + 40 header bytes each
             emit(f"stack_tick_{name}", nbytes, t, n * (5 if fn is verify else 28),
-                 entry="ics_ipv4_tcp_batch VERIFY" if fn is verify else "ics_tcp_wrap_batch",
+                 entry=entries[fn],
                  last_kernel=info["kernel"], last_plan=info["plan"],
                  plan_hits=info["plan_hits"] - before["plan_hits"],
                  plan_misses=info["plan_misses"] - before["plan_misses"],
                  note="median per-call HIP-event time; 256 Ki datagrams, packed offsets")
-        del rx, tx
+        # the same calls back to back (events around `iters` calls): no host
+        # gap between a call's first event and its launch
+        for name, fn in (("verify_b2b", verify), ("wrap_b2b", wrap), ("wrap_apart_b2b", wrap_apart)):
+            t = timed(lambda i=0, f=fn: f(), args.iters)
+            nbytes = int(roff[-1]) if fn is verify else int(toff[-1])
+            emit(f"stack_tick_{name}", nbytes, t, n * (5 if fn is verify else 28),
+                 entry=entries[fn],
+                 note="back-to-back calls, events around the run; 256 Ki datagrams, packed offsets")
+        assert (stt.cpu().numpy() == 0x0F).all(), "the receive batch must verify"
+        del rx, tx, px
     eng.close()
 
 
