@@ -345,7 +345,28 @@ def host_inclusive(eng, data, init, out, n, seg, passes=3, calls=300):
     del h
     return {"entry": "ics_checksum_batch_host", "memory": "page-locked", "bytes": n * seg, "passes": passes,
             "GB_s": round(n * seg * passes / el / 1e9, 2), "outputs_equal_device": same,
-            "tick_p50": tick, "tick_note": f"{seg}-byte segments, {calls} ctypes calls, preallocated outputs"}
+            "tick_p50": tick, "tick_note": f"{seg}-byte segments, {calls} ctypes calls, preallocated outputs",
+            "tick_p50_cpp": tick_cpp(calls),
+            "tick_cpp_note": "the same calls from C++ (tools/probe/tick_latency, dlopen of the in-tree libicsum.so, "
+                             "1500-byte segments with inits, page-locked), no interpreter in the loop"}
+
+
+def tick_cpp(calls):
+    """p50 of per-tick ics_checksum_batch_host calls timed in C++ (a child
+    process: the interpreter's ctypes overhead is not in these numbers)"""
+    exe = os.path.join(ROOT, "tools", "probe", "tick_latency")
+    lib = os.path.join(ROOT, "tcpip_network_protocol_stack_amd", "libicsum.so")
+    if not os.path.exists(exe):
+        return None
+    env = dict(os.environ, TICK_OPS="checksum", TICK_SIZES="1,16", TICK_MEM="pinned", TICK_CALLS=str(calls))
+    r = subprocess.run([exe, lib], env=env, capture_output=True, text=True, timeout=120)
+    if r.returncode:
+        raise RuntimeError(f"tick_latency: {r.returncode} {r.stderr.strip()[-300:]}")
+    out = {}
+    for line in r.stdout.splitlines():
+        d = json.loads(line)
+        out[f"segments_{d['n']}_us"] = d["p50_us"]
+    return out
 
 
 def _cpu_model():

@@ -150,6 +150,20 @@ int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets
                          uint64_t stride, uint64_t dgram_len, uint64_t n,
                          uint8_t* d_status, void* stream);
 
+/* The same router step with the forwarded headers apart: the datagrams are
+ * only read, and the 20 bytes Router::route's send_datagram serializes as the
+ * header piece (router.cpp:39-66 -> ipv4_header.cpp:62-86: ttl - 1, the
+ * recomputed checksum, the reserved flag bit dropped, no options) go to
+ * d_hdrs + 20 * i, 4-byte aligned, one coalesced array.  Datagram i on the
+ * wire = d_hdrs[20 i .. 20 i + 20) followed by its payload piece, the bytes
+ * after the parsed header: [start + 4 hlen, end) (ipv4_header.cpp:50).
+ * d_status[i] as ics_router_ttl_batch; a dropped or unparseable datagram's 20
+ * header bytes are zero.  A forwarded header equals the first 20 bytes the
+ * in-place call leaves. */
+int ics_router_ttl_headers(ics_ctx* ctx, const void* d_dgrams, const uint64_t* d_offsets,
+                           uint64_t stride, uint64_t dgram_len, uint64_t n, void* d_hdrs,
+                           uint8_t* d_status, void* stream);
+
 /* ---- a14 / §8(f) rank 2: device-side wrap_tcp_in_ip -------------------- */
 /* The fields of one TCPMessage as TCPOverIPv4Adapter::wrap_tcp_in_ip
  * (util/tcp_over_ip/tcp_over_ip.cpp:69-88) puts them on the wire.  28 bytes. */
@@ -285,12 +299,13 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 #define ICS_K_ROUTER 11          /* k_router_ttl */
 #define ICS_K_BATCHV 12          /* several batches in one launch (ics_*_batchv) */
 #define ICS_K_TILE 13            /* k_tile: an offsets batch as one packed stream, T segments per block */
+#define ICS_K_ROUTER_HDRS 14     /* k_router_hdrs: the router step, forwarded headers apart */
 /* last_lps / last_unroll by kernel:
  *   ICS_K_CHECKSUM .. ICS_K_WRAP_2PASS  lanes per segment / loads in flight per lane
  *   ICS_K_TWOCLASS, ICS_K_IPV4_TWOCLASS  long-segment lanes (16) / segments per wave (16 or 32)
  *   ICS_K_BATCHV  the ICS_BV_* shape of the last launch group / batches in the call
  *   ICS_K_TILE    segments per tile (T) / ICS_TILE_* operation
- *   ICS_K_ROUTER  0 / 0 */
+ *   ICS_K_ROUTER, ICS_K_ROUTER_HDRS  0 / 0 */
 #define ICS_BV_DENSE64 0 /* fixed stride == length == 64 B, 16-byte aligned */
 #define ICS_BV_TINY 1    /* one lane per segment (ACK-sized fixed lengths) */
 #define ICS_BV_SMALL 2   /* 4-lane groups, two segments in flight */

@@ -58,7 +58,8 @@ class DgramBatch(ctypes.Structure):
 
 # ICS_K_* kernel ids of ics_dispatch_info_t.last_kernel
 KERNELS = {1: "checksum", 2: "small", 3: "tiny", 4: "dense", 5: "twoclass", 6: "binned", 7: "ipv4",
-           8: "ipv4_twoclass", 9: "wrap", 10: "wrap_2pass", 11: "router", 12: "batchv", 13: "tile"}
+           8: "ipv4_twoclass", 9: "wrap", 10: "wrap_2pass", 11: "router", 12: "batchv", 13: "tile",
+           14: "router_hdrs"}
 
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -80,6 +81,7 @@ SIGNATURES = {
     "ics_fold_batch": (_int, [_p, _p, _p, _u64, _p]),
     "ics_ipv4_tcp_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p, _p]),
     "ics_router_ttl_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p]),
+    "ics_router_ttl_headers": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p, _p]),
     "ics_tcp_wrap_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p, _p, _p]),
     "ics_tcp_wrap_batch_host": (_int, [_p, _p, _p, _u64, _u64, _u64, _p]),
     "ics_tcp_wrap_headers": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p, _p, _p, _p]),

@@ -286,7 +286,19 @@ int ics_router_ttl_batch(ics_ctx* ctx, void* d_dgrams, const uint64_t* d_offsets
   if (!d_dgrams || !d_status) return fail(ICS_ERR_INVALID, "null device buffer");
   const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
   return bounds_verdict(static_cast<hipStream_t>(stream),
-                        router_device(ctx, sp, d_status, static_cast<hipStream_t>(stream)));
+                        router_device(ctx, sp, nullptr, d_status, static_cast<hipStream_t>(stream)));
+}
+
+int ics_router_ttl_headers(ics_ctx* ctx, const void* d_dgrams, const uint64_t* d_offsets, uint64_t stride,
+                           uint64_t dgram_len, uint64_t n, void* d_hdrs, uint8_t* d_status, void* stream) {
+  if (int rc = bind(ctx)) return rc;
+  if (n == 0) return ICS_OK;
+  if (!d_dgrams || !d_hdrs || !d_status) return fail(ICS_ERR_INVALID, "null device buffer");
+  if (reinterpret_cast<uintptr_t>(d_hdrs) & 3u) return fail(ICS_ERR_INVALID, "header array not 4-byte aligned");
+  const icsum::SegSpec sp{static_cast<const uint8_t*>(d_dgrams), d_offsets, stride, dgram_len, n, ctx->d_zero};
+  return bounds_verdict(static_cast<hipStream_t>(stream),
+                        router_device(ctx, sp, static_cast<uint32_t*>(d_hdrs), d_status,
+                                      static_cast<hipStream_t>(stream)));
 }
 
 int ics_checksum_batch_host(ics_ctx* ctx, const void* h_bytes, const uint64_t* h_offsets,

@@ -87,6 +87,9 @@ struct ics_ctx {
   // offsets batch (checksum, fused IPv4, in-place wrap); tile_segs = T
   // segments per tile (0: tile_segs_for), tile_blocks = grid cap (0: one block per tile)
   int tile = -1;
+  static constexpr uint64_t kTileMin = uint64_t(1) << 17;  // tile launches from this many segments (AUTO)
+  static constexpr uint32_t kTileMaxAvg = 1024;            // ... and up to this mean length (tile_wins)
+  static constexpr uint32_t kTileApartShort16 = 12;       // headers-apart wrap: below 12/16 empty-ish payloads
   uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order
   uint32_t tile_segs = 0, tile_blocks = 0;
   // device wrap: 0 = two passes (payload sums, then a header launch) when
@@ -179,11 +182,13 @@ struct ics_ctx {
   // what a per-tick TUN / socket batch pays for ("Per-tick host
   // batches"); ICSUM_FORCE zero_copy_max=0 turns it off (tests)
   uint64_t zero_copy_max = uint64_t(2) << 20;
-  // ... and it ends in a completion word its slot's stream writes after the
-  // kernel (k_host_flag), which the caller spins on: ~3.7 us less than
-  // waiting for the stream's completion signal (tools/probe/sync_probe.hip)
+  // ... and it ends in a completion word the launch's last block stores
+  // (icsum::Done, a block-count ticket in d_ticket), which the caller spins
+  // on: ~3.7 us less than waiting for the stream's completion signal
+  // (tools/probe/sync_probe.hip), and no second launch behind the kernel
   uint64_t* h_flag = nullptr;  // kMaxSlots words, 64 bytes apart, coherent page-locked
   uint64_t flag_ticket = 0;
+  uint32_t* d_ticket = nullptr;  // kMaxSlots block-count tickets, 64 bytes apart (icsum::Done)
   bool wrap_staged = false;
   uint8_t* h_msg[kMaxSlots] = {};
   uint8_t* d_msg[kMaxSlots] = {};
@@ -269,8 +274,9 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
 // hint = the mean length an offsets batch is assumed to have before its plan lands.
 int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msgs, uint32_t* hdr_out,
                 uint16_t* d_ip_ck, uint16_t* d_tcp_ck, bool payload_only, uint64_t hint, hipStream_t st);
-// c2: the router's TTL decrement + incremental checksum update.
-int router_device(ics_ctx* ctx, const icsum::SegSpec& sp, uint8_t* d_status, hipStream_t st);
+// c2: the router's TTL decrement + header checksum recompute, in place
+// (d_hdrs null) or with the forwarded headers to d_hdrs (20 bytes each).
+int router_device(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t* d_hdrs, uint8_t* d_status, hipStream_t st);
 // Multi-batch calls: batches grouped by kernel shape, one launch per group.
 int checksum_batchv_device(ics_ctx* ctx, const ics_seg_batch* batches, uint32_t k, hipStream_t st);
 int ipv4_batchv_device(ics_ctx* ctx, const ics_dgram_batch* batches, uint32_t k, int mode, hipStream_t st);

@@ -151,6 +151,23 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, const PlanReq& 
 // profiles/r2_csum_mix_sweep.jsonl), now the two-class launch (launch_mix)
 bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
 
+// The tile launch (k_tile) for an offsets batch whose device-reported mix
+// favours it: from kTileMin segments, a mean length of at most kTileMaxAvg
+// bytes (variable lengths leave per-segment lane groups idle), or — for the
+// fused IPv4 kernel and the wraps, which have no length binning — a sixteenth
+// or more of the bytes in segments over 1920 bytes.  Short-heavy mixes keep
+// the two-class launches (checked first by the callers), MTU-sized means the
+// 16-lane line grid.  tools/ab_dispatch.py, profiles/r4_ab_dispatch.jsonl
+// (256 Ki / 1 M segments, us, default vs tile): checksum 40..1040 B 37.1 /
+// 29.2 and 279.3 / 92.2, 770 B 40.0 / 35.7 and 153.4 / 122.6, MTU 56.7 /
+// 63.9; VERIFY 40..1040 B 40.0 / 34.5 and 150.0 / 116.9, config-4 mix 412.4 /
+// 387.1; headers-apart wrap 40..1040 B 39.6 / 32.0 and 138.7 / 109.0, MTU
+// 67.1 / 70.1; at 64 Ki the default wins or ties.
+bool tile_wins(const ics_ctx* ctx, const PlanMix& m, uint64_t n, bool fused) {
+  if (ctx->tile == 0 || n < ics_ctx::kTileMin) return false;
+  return m.avg <= ics_ctx::kTileMaxAvg || (fused && m.long16 >= 4);
+}
+
 // a short-heavy mix's single launch: the two-class launch (ACK-sized segments
 // one per lane, the rest 16 lanes each; block lists since round 3), 32
 // segments per wave from 3/4 short segments up and 16 below (round 2, the
@@ -245,6 +262,12 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     PlanMix mix;
     const bool hit = plan_lookup(ctx, sp, true, &hit_plan, &req, &mix);
     const bool mix8 = hit && hit_plan != icsum::kPlanWholeBatchSmall && short_mix(mix);
+    if (hit && !mix8 && hit_plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, sp.n, false)) {
+      const uint32_t T = tile_segs_for(ctx, sp.n);
+      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st));
+      note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM, true, 0, 1}, int(hit_plan));
+      return replan(ctx, sp, lps, req, st);
+    }
     if (hit && (hit_plan != icsum::kPlanSplitBins || mix8)) {
       // the whole-batch plan the device chose for this batch last time, as
       // its single launch: the last bin's geometry (whole), 16-lane groups
@@ -311,7 +334,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   // from 5/16 of <= 144-byte datagrams, 16 x 4 below that), the plan
   // kernels running behind the first and every 16th launch (DESIGN.md §4,
   // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
-  bool two = false;
+  bool two = false, tile = false;
   int spw = 16;
   PlanReq req;
   int plan_used = -1;
@@ -335,12 +358,13 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
     // pass carries more of them (3/4 ACKs 78.4 -> 75.4 us, mix_probe blk32)
     spw = mix.short16 >= ics_ctx::kIpv4TwoClassWide16 ? 32 : 16;
     plan_used = hit ? int(plan) : -1;
+    tile = hit && !two && plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, n, true);
   }
   if (d_offsets && ctx->twoclass) {  // test hook
     two = true;
     spw = ctx->twoclass;
   }
-  if (d_offsets && ctx->tile == 1) {  // test hook
+  if (d_offsets && (ctx->tile == 1 || tile)) {  // the test hook, or the cached mix favours the tile launch
     const uint32_t T = tile_segs_for(ctx, n);
     ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, T, ctx->tile_blocks, st));
     note(ctx, ICS_K_TILE, {int(T), ICS_TILE_IPV4, true, 0, 1}, plan_used);
@@ -385,7 +409,8 @@ hipError_t device_wrap(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg
 // hint.  The plan kernels run behind the launch as plan_lookup asks (the
 // wrap's transmit buffer keeps its own cache slot: a stack's receive-side
 // verify in between does not evict it).
-icsum::Geometry wrap_geometry(ics_ctx* ctx, const icsum::SegSpec& sp, uint64_t hint, PlanReq* req, int* plan_used) {
+icsum::Geometry wrap_geometry(ics_ctx* ctx, const icsum::SegSpec& sp, uint64_t hint, PlanReq* req, int* plan_used,
+                              PlanMix* mix_out) {
   const icsum::Geometry lane1{1, 4, false, 0, 1};
   const icsum::Geometry base = geometry_for(ctx, sp.offsets ? hint : sp.seg_len);
   icsum::Geometry g = base.mode == icsum::kModeTiny ? lane1 : ipv4_geometry(base);
@@ -396,7 +421,10 @@ icsum::Geometry wrap_geometry(ics_ctx* ctx, const icsum::SegSpec& sp, uint64_t h
     PlanMix mix;
     const bool hit = plan_lookup(ctx, sp, true, &plan, req, &mix);
     if (hit && plan == icsum::kPlanWholeBatchSmall && mix.avg <= icsum::kTinyMaxAvg) g = lane1;
-    if (hit) *plan_used = int(plan);
+    if (hit) {
+      *plan_used = int(plan);
+      *mix_out = mix;
+    }
   }
   return g;
 }
@@ -406,8 +434,21 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
                 uint16_t* d_ip_ck, uint16_t* d_tcp_ck, bool payload_only, uint64_t hint, hipStream_t st) {
   PlanReq req;
   int plan = -1;
-  const icsum::Geometry g = wrap_geometry(ctx, sp, hint, &req, &plan);
-  if (sp.offsets && ctx->tile == 1) {  // test hook: the wrap (in place or headers apart) as a tile launch
+  PlanMix mix;
+  const icsum::Geometry g = wrap_geometry(ctx, sp, hint, &req, &plan, &mix);
+  // the tile launch: the test hook; headers apart when the cached mix favours
+  // it; in place only for long-segment mixes (its header stores cost the
+  // same scattered write per datagram either way, and the per-segment wrap
+  // is faster on short ones: 40..1040 B, 256 Ki: 40.3 / 44.7 us; config-4 mix
+  // 499.3 / 464.2 us, tools/ab_dispatch.py).  Headers apart, the receive-side
+  // mix of empty and MTU payloads tiles too (256 Ki / 1 M: 48.8 / 40.5 and
+  // 169.3 / 150.8 us), payloads nearly all empty (pure ACKs) do not (1 M:
+  // 24.2 / 41.0 us; profiles/r4_ab_dispatch_tile.jsonl)
+  const bool tile_pick = plan >= 0 && plan != int(icsum::kPlanWholeBatchSmall) &&
+                         (payload_only ? mix.short16 < ics_ctx::kTileApartShort16 && tile_wins(ctx, mix, sp.n, true)
+                                       : !short_mix(mix) && ctx->tile != 0 && sp.n >= ics_ctx::kTileMin &&
+                                             mix.long16 >= 4);
+  if (sp.offsets && (ctx->tile == 1 || tile_pick)) {  // the wrap (in place or headers apart) as a tile launch
     const uint32_t T = tile_segs_for(ctx, sp.n);
     ICS_HIP(icsum::launch_tile_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), hdr_out, d_ip_ck, d_tcp_ck,
                                     T, ctx->tile_blocks, st));
@@ -418,9 +459,14 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
   return replan(ctx, sp, 64, req, st);
 }
 
-int router_device(ics_ctx* ctx, const icsum::SegSpec& sp, uint8_t* d_status, hipStream_t st) {
-  ICS_HIP(icsum::launch_router_ttl(sp, d_status, st));
-  note(ctx, ICS_K_ROUTER);
+int router_device(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t* d_hdrs, uint8_t* d_status, hipStream_t st) {
+  if (d_hdrs) {
+    ICS_HIP(icsum::launch_router_hdrs(sp, d_hdrs, d_status, st));
+    note(ctx, ICS_K_ROUTER_HDRS);
+  } else {
+    ICS_HIP(icsum::launch_router_ttl(sp, d_status, st));
+    note(ctx, ICS_K_ROUTER);
+  }
   return ICS_OK;
 }
 

@@ -51,6 +51,8 @@ int ensure_staging(ics_ctx* ctx) {
   ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_flag), ics_ctx::kMaxSlots * 64, hipHostMallocCoherent));
   std::memset(ctx->h_flag, 0, ics_ctx::kMaxSlots * 64);
   if (!host_pinned(ctx->h_flag).kernel) ctx->zero_copy_max = 0;
+  ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_ticket), ics_ctx::kMaxSlots * 64));
+  ICS_HIP(hipMemset(ctx->d_ticket, 0, ics_ctx::kMaxSlots * 64));
   ctx->staged = true;
   return ICS_OK;
 }
@@ -179,7 +181,8 @@ void host_patch_fields(uint8_t* bytes, const uint64_t* offsets, uint64_t stride,
   }
 }
 
-// Wait for a zero-copy chunk: spin on its completion word (k_host_flag) for
+// Wait for a zero-copy chunk: spin on its completion word (written by the
+// launch's last block, icsum_kernels.hip signal_done) for
 // up to a millisecond — a zero-copy chunk is at most zero_copy_max bytes, tens
 // of microseconds over PCIe — then block on the slot's stream, which also
 // surfaces a kernel fault as a HIP error instead of a hang.
@@ -218,6 +221,8 @@ void free_staging(ics_ctx* ctx) {
   }
   if (ctx->h_flag) (void)hipHostFree(ctx->h_flag);
   ctx->h_flag = nullptr;
+  if (ctx->d_ticket) (void)hipFree(ctx->d_ticket);
+  ctx->d_ticket = nullptr;
   ctx->staged = false;
   ctx->wrap_staged = false;
 }
@@ -231,10 +236,11 @@ void free_staging(ics_ctx* ctx) {
 // all: the kernel reads the pinned bytes, offsets, inits and messages over
 // PCIe and writes its results into the pinned result area (one launch, one
 // synchronisation).
-int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets,
-                  uint64_t stride, uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode,
-                  uint16_t* out_a, uint16_t* out_b, uint8_t* out_c, const ics_tcp_msg* h_msgs) {
-  std::lock_guard<std::mutex> lock(ctx->mu);
+namespace {
+
+int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets, uint64_t stride,
+                 uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode, uint16_t* out_a, uint16_t* out_b,
+                 uint8_t* out_c, const ics_tcp_msg* h_msgs) {
   if (int rc = ensure_staging(ctx)) return rc;
   if (kind == 2)
     if (int rc = ensure_wrap_staging(ctx)) return rc;
@@ -351,7 +357,11 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       ICS_HIP(h2d(ctx->d_off[slot], ctx->h_off[slot], (m + 1) * 8, &w));
       d_off = static_cast<const uint64_t*>(w);
     }
-    const icsum::SegSpec sp{in, d_off, stride, seg_len, m, ctx->d_zero};
+    icsum::SegSpec sp{in, d_off, stride, seg_len, m, ctx->d_zero};
+    // zero-copy: the launch itself stores the completion word (one launch per
+    // call, DESIGN.md §6 "Per-tick host batches"); staged: an event
+    flag_of[slot] = zc ? ++ctx->flag_ticket : 0;
+    if (zc) sp.done = icsum::Done{ctx->d_ticket + 16 * slot, ctx->h_flag + 8 * slot, flag_of[slot]};
     const uint64_t avg = h_offsets ? nb / m : seg_len;
     const icsum::Geometry g = geometry_for(ctx, avg);
     if (kind == 2) {
@@ -386,13 +396,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
       ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, ipv4_geometry(g), 0, st));
       ICS_HIP(d2h(ctx->h_out[slot], ctx->d_out[slot], m * 5));
     }
-    if (zc) {
-      flag_of[slot] = ++ctx->flag_ticket;
-      ICS_HIP(icsum::launch_host_flag(ctx->h_flag + 8 * slot, flag_of[slot], st));
-    } else {
-      flag_of[slot] = 0;
-      ICS_HIP(hipEventRecord(ctx->ev[slot], st));
-    }
+    if (!zc) ICS_HIP(hipEventRecord(ctx->ev[slot], st));
     pending[slot] = c;
     busy[slot] = true;
     i0 = c.i1;
@@ -401,6 +405,24 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
   for (int k = 0; k < ctx->nslots; ++k)  // oldest first
     if (int rc = retire((slot + k) % ctx->nslots)) return rc;
   return bounds_verdict(ctx->st[0], ICS_OK);
+}
+
+}  // namespace
+
+int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets,
+                  uint64_t stride, uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode,
+                  uint16_t* out_a, uint16_t* out_b, uint8_t* out_c, const ics_tcp_msg* h_msgs) {
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  const int rc = run_pipeline(ctx, kind, h_bytes, h_offsets, stride, seg_len, h_init, n, mode, out_a, out_b, out_c,
+                              h_msgs);
+  // an error after chunks were enqueued (a later datagram larger than a slot,
+  // a failed launch or copy) leaves copies — or zero-copy kernels reading the
+  // caller's page-locked bytes — in flight: drain every slot before the
+  // caller sees the error and frees or reuses its buffers
+  if (rc != ICS_OK && ctx->staged)
+    for (int k = 0; k < ctx->nslots; ++k)
+      if (ctx->st[k]) (void)hipStreamSynchronize(ctx->st[k]);
+  return rc;
 }
 
 }  // namespace icsum::detail

@@ -383,6 +383,27 @@ __device__ __forceinline__ uint32_t block_order(uint32_t run_log2) {
   return ((k >> lc) << (lc + 3)) + (x << lc) + (k & ((1u << lc) - 1u));
 }
 
+// End of a launch that completes a zero-copy host call (Done): the block's
+// barrier orders every wave's result stores before lane 0, whose
+// system-scope release (cumulative: one L2 write-back per block, not per
+// wave) puts them where the host reads them before it takes a ticket; the
+// block with the last ticket resets the ticket word and releases the
+// completion value into the host word.  A no-op (one uniform branch) for
+// every device-path launch.  Every thread of the block must reach it:
+// kernels call their body first.
+__device__ __forceinline__ void signal_done(const Done& d) {
+  if (d.flag == nullptr) return;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    const uint32_t t = __hip_atomic_fetch_add(d.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == gridDim.x - 1) {
+      __hip_atomic_store(d.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(d.flag, d.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 template <int LPS, int UNROLL, int SEGS, int OUT>
 __device__ __forceinline__ void checksum_small_body(const uint8_t* __restrict__ bytes, const SegSrc& src,
                                                     const uint32_t* __restrict__ init, uint32_t init_step,
@@ -398,13 +419,11 @@ __device__ __forceinline__ void checksum_tiny_body(const uint8_t* __restrict__ b
                                                    uint64_t n, uint32_t blk, uint32_t nblk);  // below
 
 template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
-__global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes, SegSrc src,
-                                                     const uint32_t* __restrict__ init,
-                                                     uint32_t init_step,
-                                                     const uint8_t* __restrict__ odd,
-                                                     uint32_t odd_step,
-                                                     void* __restrict__ out, uint64_t n, uint32_t remap,
-                                                     const u32x4* __restrict__ zero16) {
+__device__ __forceinline__ void checksum_entry(const uint8_t* __restrict__ bytes, const SegSrc& src,
+                                               const uint32_t* __restrict__ init, uint32_t init_step,
+                                               const uint8_t* __restrict__ odd, uint32_t odd_step,
+                                               void* __restrict__ out, uint64_t n, uint32_t remap,
+                                               const u32x4* __restrict__ zero16) {
   const uint32_t blk = block_order(remap);
   if constexpr (MODE == 3 && NT && UNROLL == 8 && (LPS == 32 || LPS == 64)) {
     // the last bin's launch under kPlanWhole16: every segment of the batch,
@@ -450,6 +469,18 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
   if (src.list && resolve(src, n).items == 0) return;
   checksum_body<LPS, UNROLL, NT, MODE, OUT>(bytes, src, init, init_step, odd, odd_step, out, n, blk,
                                             gridDim.x);
+}
+
+template <int LPS, int UNROLL, bool NT, int MODE, int OUT>
+__global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__ bytes, SegSrc src,
+                                                     const uint32_t* __restrict__ init,
+                                                     uint32_t init_step,
+                                                     const uint8_t* __restrict__ odd,
+                                                     uint32_t odd_step,
+                                                     void* __restrict__ out, uint64_t n, uint32_t remap,
+                                                     const u32x4* __restrict__ zero16, Done done) {
+  checksum_entry<LPS, UNROLL, NT, MODE, OUT>(bytes, src, init, init_step, odd, odd_step, out, n, remap, zero16);
+  signal_done(done);
 }
 
 // Small segments (a few 16-byte chunks): a lane group owns SEGS segments per
@@ -540,9 +571,10 @@ __global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __rest
                                                            const uint8_t* __restrict__ odd,
                                                            uint32_t odd_step,
                                                            const u32x4* __restrict__ zero16,
-                                                           void* __restrict__ out, uint64_t n) {
+                                                           void* __restrict__ out, uint64_t n, Done done) {
   checksum_small_body<LPS, UNROLL, SEGS, OUT>(bytes, src, init, init_step, odd, odd_step, zero16, out, n,
                                               blockIdx.x, gridDim.x);
+  signal_done(done);
 }
 
 // Tiny segments (ACK-sized TCP segments, <= 4 chunks): ONE lane per segment.
@@ -608,8 +640,9 @@ __global__ __launch_bounds__(kBlock) void k_checksum_tiny(const uint8_t* __restr
                                                           const uint32_t* __restrict__ init, uint32_t init_step,
                                                           const uint8_t* __restrict__ odd, uint32_t odd_step,
                                                           const u32x4* __restrict__ zero16, void* __restrict__ out,
-                                                          uint64_t n) {
+                                                          uint64_t n, Done done) {
   checksum_tiny_body<OUT>(bytes, src, init, init_step, odd, odd_step, zero16, out, n, blockIdx.x, gridDim.x);
+  signal_done(done);
 }
 
 // Two-class launch for receive mixes (ACKs among MTU segments), no binning
@@ -808,14 +841,6 @@ __global__ __launch_bounds__(kBlock) void k_checksum_bins(const uint8_t* __restr
 // element-wise kernels use a capped grid and stride over the rest.
 #define ICS_GRID_STRIDE(i, n) \
   for (uint64_t i = uint64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < (n); i += uint64_t(gridDim.x) * blockDim.x)
-
-// Completion word of a host-memory call: stream order puts it behind the
-// call's kernels (whose results a kernel boundary has already made visible),
-// and the host spins on the page-locked word instead of waiting for the
-// stream's completion signal ("Per-tick host batches").
-__global__ void k_host_flag(uint64_t* flag, uint64_t v) {
-  __hip_atomic_store(flag, v, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
 
 __global__ void k_fold(const uint32_t* __restrict__ sum, uint16_t* __restrict__ out, uint64_t n) {
   ICS_GRID_STRIDE(i, n) out[i] = fold_value(sum[i]);
@@ -1111,9 +1136,10 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
                                                      int mode, uint16_t* __restrict__ ip_ck,
                                                      uint16_t* __restrict__ tcp_ck,
                                                      uint8_t* __restrict__ status, uint32_t remap,
-                                                     const uint8_t* __restrict__ zpad) {
+                                                     const uint8_t* __restrict__ zpad, Done done) {
   ipv4_body<LPS, UNROLL, NT, MODE>(dg, offsets, stride, dlen, n, mode, ip_ck, tcp_ck, status, zpad,
                                    block_order(remap), gridDim.x);
+  signal_done(done);
 }
 
 // Two-class launch for receive mixes (ACKs among MTU datagrams): block b
@@ -1276,7 +1302,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
                                                      uint32_t* __restrict__ hdr_out,
                                                      uint16_t* __restrict__ ip_ck,
                                                      uint16_t* __restrict__ tcp_ck, uint32_t remap,
-                                                     int payload_only, uint32_t* __restrict__ sums) {
+                                                     int payload_only, uint32_t* __restrict__ sums, Done done) {
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
@@ -1342,6 +1368,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
       if (tcp_ck) tcp_ck[seg] = ok ? uint16_t(tcv) : uint16_t(0);
     }
   }
+  signal_done(done);
 }
 
 // The 40 wire bytes wrap_tcp_in_ip puts in front of a payload of plen bytes
@@ -1392,7 +1419,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
                                                     uint64_t dlen, uint64_t n, const TcpMsg* __restrict__ msgs,
                                                     const uint32_t* __restrict__ sums,
                                                     uint32_t* __restrict__ hdr_out, uint16_t* __restrict__ ip_ck,
-                                                    uint16_t* __restrict__ tcp_ck, int payload_only) {
+                                                    uint16_t* __restrict__ tcp_ck, int payload_only, Done done) {
   __shared__ uint32_t stage[kBlock / 64][64 * 10];  // 10 KiB: each wave's 640 header dwords
   const uint32_t lane64 = threadIdx.x & 63u;
   uint32_t* const sw = stage[threadIdx.x >> 6];
@@ -1446,6 +1473,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
     }
     __builtin_amdgcn_wave_barrier();  // the next step rewrites sw
   }
+  signal_done(done);
 }
 
 // --------------------------------------------------- router batch -------
@@ -1523,6 +1551,84 @@ __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
       }
       status[i] = st;
     }
+  }
+}
+
+// Router batch with the forwarded headers apart.  Router::route decrements
+// the ttl, recomputes the header checksum and hands send_datagram the
+// datagram (router.cpp:39-66), which serialize() turns into two pieces: the
+// 20 serialized header bytes (ipv4_header.cpp:62-86: options never written,
+// the reserved flag bit dropped) and the payload after the parsed header
+// (4 hlen bytes in, ipv4_header.cpp:50).  Here the payloads stay where they
+// are (read-only batch) and the forwarded headers go to one coalesced array,
+// 20 bytes per datagram: a forwarded datagram's header there is byte for
+// byte what the in-place k_router_ttl leaves in its first 20 bytes; a
+// dropped or unparseable one gets 20 zero bytes.  Headers are read as in
+// k_router_ttl (two lanes per datagram, three dwords each); each wave stages
+// its 32 headers in LDS and stores them as 160 consecutive dwords.
+__global__ __launch_bounds__(kBlock) void k_router_hdrs(const uint8_t* __restrict__ dg,
+                                                        const uint64_t* __restrict__ offsets, uint64_t stride,
+                                                        uint64_t dlen, uint64_t n, uint32_t* __restrict__ hdr_out,
+                                                        uint8_t* __restrict__ status,
+                                                        const uint32_t* __restrict__ zpad) {
+  constexpr uint32_t kG = kBlock / 2, kPerWave = 32;
+  __shared__ uint32_t stage[kBlock / 64][kPerWave * 5];
+  const uint32_t lane = threadIdx.x & 1u, lane64 = threadIdx.x & 63u;
+  uint32_t* const sw = stage[threadIdx.x >> 6];
+  const uint64_t step = uint64_t(gridDim.x) * kG;
+  for (uint64_t g0 = uint64_t(blockIdx.x) * kG; g0 < n; g0 += step) {  // uniform per block
+    const uint64_t i = g0 + threadIdx.x / 2;
+    const bool valid = i < n;
+    uint64_t s, e;
+    seg_bounds(offsets, stride, dlen, valid ? i : n - 1, s, e);
+    const bool hdr = valid && e - s >= 20;
+    const uint8_t* p = dg + s;
+    const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+    const uint32_t* q = hdr ? reinterpret_cast<const uint32_t*>(p - sh) : zpad;
+    const uint32_t* last = hdr ? last_dword(dg + e) : zpad + 7;
+    uint32_t mine[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint32_t* a = q + (lane + 2u * k);
+#ifdef ICSUM_BOUNDS_CHECK
+      if (hdr && k < 2 && a > last) bounds_fail(kBoundsHeader, reinterpret_cast<unsigned long long>(a));
+#endif
+      mine[k] = *(a < last ? a : last);
+    }
+    const int pair = int(lane64 & ~1u);
+    uint32_t d[6];
+#pragma unroll
+    for (int w = 0; w < 6; ++w) d[w] = uint32_t(__shfl(int(mine[w / 2]), pair + (w & 1), 64));
+    Hdr h;
+#pragma unroll
+    for (int k = 0; k < 5; ++k) h.w[k] = __builtin_amdgcn_alignbyte(d[k + 1], d[k], sh);
+    const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu, ttl = h.byte(8);
+    // NetworkInterface::recv_frame parse (network_interface.cpp:51), then
+    // Router::route: ttl <= 1 dropped, else ttl-- and compute_checksum()
+    const bool fwd = hdr && ver == 4 && hlen >= 5 && fold_value(ipv4_header_sum(h)) == h.be16(10) && ttl > 1;
+    h.w[2] = (h.w[2] & ~0xffu) | ((ttl - 1) & 0xffu);
+    const uint32_t c = fold_value(ipv4_header_sum(h));
+    uint32_t o[5];
+    o[0] = h.w[0];
+    o[1] = h.w[1] & ~0x00800000u;  // the flags word re-serialized: reserved bit dropped
+    o[2] = (h.w[2] & 0x0000ffffu) | ((c >> 8) << 16) | ((c & 0xffu) << 24);
+    o[3] = h.w[3];
+    o[4] = h.w[4];
+    const uint32_t slot = (lane64 >> 1) * 5;
+    for (uint32_t k = lane; k < 5; k += 2) sw[slot + k] = fwd ? o[k] : 0u;
+    if (valid && lane == 0) status[i] = fwd ? 1 : 0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the wave's datagrams [wbase, wbase + 32): 160 consecutive dwords of the array
+    const uint64_t wbase = g0 + (threadIdx.x >> 6) * kPerWave;
+    const uint64_t cnt = wbase < n ? (n - wbase < kPerWave ? n - wbase : kPerWave) : 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 3; ++j) {
+      const uint32_t t = j * 64u + lane64;
+      if (t < cnt * 5) hdr_out[wbase * 5 + t] = sw[t];
+    }
+    __builtin_amdgcn_wave_barrier();  // the next pass rewrites sw
   }
 }
 
@@ -2150,10 +2256,10 @@ hipError_t launch_checksum_t(const SegSpec& sp, const uint32_t* init, const uint
   const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
   if (out_kind == 0)
     hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap, static_cast<const u32x4*>(sp.zero16));
+                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap, static_cast<const u32x4*>(sp.zero16), sp.done);
   else
     hipLaunchKernelGGL((k_checksum<LPS, UNROLL, NT, MODE, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap, static_cast<const u32x4*>(sp.zero16));
+                       src_of(sp), ip, is, op, os, out, sp.n, g_xcd_remap, static_cast<const u32x4*>(sp.zero16), sp.done);
   return hipGetLastError();
 }
 
@@ -2167,10 +2273,10 @@ hipError_t launch_checksum_small_t(const SegSpec& sp, const uint32_t* init, cons
   const u32x4* z = static_cast<const u32x4*>(sp.zero16);
   if (out_kind == 0)
     hipLaunchKernelGGL((k_checksum_small<LPS, UNROLL, SEGS, 0>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, z, out, sp.n);
+                       src_of(sp), ip, is, op, os, z, out, sp.n, sp.done);
   else
     hipLaunchKernelGGL((k_checksum_small<LPS, UNROLL, SEGS, 1>), dim3(blocks), dim3(kBlock), 0, st, sp.bytes,
-                       src_of(sp), ip, is, op, os, z, out, sp.n);
+                       src_of(sp), ip, is, op, os, z, out, sp.n, sp.done);
   return hipGetLastError();
 }
 
@@ -2201,10 +2307,10 @@ hipError_t launch_checksum_tiny_t(const SegSpec& sp, const uint32_t* init, const
   const u32x4* z = static_cast<const u32x4*>(sp.zero16);
   if (out_kind == 0)
     hipLaunchKernelGGL(k_checksum_tiny<0>, dim3(blocks), dim3(kBlock), 0, st, sp.bytes, src_of(sp), ip, is, op, os,
-                       z, out, sp.n);
+                       z, out, sp.n, sp.done);
   else
     hipLaunchKernelGGL(k_checksum_tiny<1>, dim3(blocks), dim3(kBlock), 0, st, sp.bytes, src_of(sp), ip, is, op, os,
-                       z, out, sp.n);
+                       z, out, sp.n, sp.done);
   return hipGetLastError();
 }
 
@@ -2230,7 +2336,7 @@ hipError_t launch_ipv4_t(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t*
   const uint32_t blocks = blocks_for(sp.n, kBlock / LPS, max_blocks);
   hipLaunchKernelGGL((k_ipv4_tcp<LPS, UNROLL, NT, MODE>), dim3(blocks), dim3(kBlock), 0, st,
                      const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, mode,
-                     ip_ck, tcp_ck, status, g_xcd_remap, static_cast<const uint8_t*>(sp.zero16));
+                     ip_ck, tcp_ck, status, g_xcd_remap, static_cast<const uint8_t*>(sp.zero16), sp.done);
   return hipGetLastError();
 }
 
@@ -2241,11 +2347,11 @@ hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_ou
   if (sums)
     hipLaunchKernelGGL((k_tcp_wrap<LPS, UNROLL, NT, MODE, true>), dim3(blocks), dim3(kBlock), 0, st,
                        const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, msgs, hdr_out,
-                       ip_ck, tcp_ck, g_xcd_remap, int(payload_only), sums);
+                       ip_ck, tcp_ck, g_xcd_remap, int(payload_only), sums, Done{});  // k_tcp_hdr completes
   else
     hipLaunchKernelGGL((k_tcp_wrap<LPS, UNROLL, NT, MODE, false>), dim3(blocks), dim3(kBlock), 0, st,
                        const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n, msgs, hdr_out,
-                       ip_ck, tcp_ck, g_xcd_remap, int(payload_only), sums);
+                       ip_ck, tcp_ck, g_xcd_remap, int(payload_only), sums, sp.done);
   return hipGetLastError();
 }
 
@@ -2505,7 +2611,7 @@ hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t*
   const uint64_t blocks = (sp.n + kBlock - 1) / kBlock;  // one datagram per lane
   hipLaunchKernelGGL(k_tcp_hdr, dim3(uint32_t(blocks < (uint64_t(1) << 22) ? blocks : (uint64_t(1) << 22))),
                      dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes), sp.offsets, sp.stride, sp.seg_len, sp.n,
-                     msgs, sums, hdr_out, ip_ck, tcp_ck, int(payload_only));
+                     msgs, sums, hdr_out, ip_ck, tcp_ck, int(payload_only), sp.done);
   return hipGetLastError();
 }
 
@@ -2618,13 +2724,14 @@ bool geometry_supported(Geometry g) {
   return false;
 }
 
-hipError_t launch_host_flag(uint64_t* flag, uint64_t v, hipStream_t st) {
-  hipLaunchKernelGGL(k_host_flag, dim3(1), dim3(1), 0, st, flag, v);
+hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st) {
+  hipLaunchKernelGGL(k_fold, dim3(ew_blocks(n)), dim3(kBlock), 0, st, sum, out, n);
   return hipGetLastError();
 }
 
-hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st) {
-  hipLaunchKernelGGL(k_fold, dim3(ew_blocks(n)), dim3(kBlock), 0, st, sum, out, n);
+hipError_t launch_router_hdrs(const SegSpec& sp, uint32_t* hdr_out, uint8_t* status, hipStream_t st) {
+  hipLaunchKernelGGL(k_router_hdrs, dim3(ew_blocks(sp.n * 2)), dim3(kBlock), 0, st, sp.bytes, sp.offsets, sp.stride,
+                     sp.seg_len, sp.n, hdr_out, status, static_cast<const uint32_t*>(sp.zero16));
   return hipGetLastError();
 }
 

@@ -29,6 +29,19 @@ constexpr uint32_t kTinyMaxAvg = 56;
 Geometry pick_geometry(uint64_t avg_len);
 bool geometry_supported(Geometry g);
 
+// In-kernel completion of a zero-copy host call: every block makes its
+// results visible at system scope and takes a ticket; the block that takes
+// the last one resets the ticket word and stores `value` into the host word
+// `flag` with a system-scope release (the host spins on it).  flag == nullptr:
+// nothing (every device-path launch).  Honoured by the kernels the host path
+// launches: checksum (tiny, small, per-group), the fused IPv4 kernel, the
+// one-pass wrap and the two-pass wrap's header pass.
+struct Done {
+  uint32_t* ticket = nullptr;  // device word, 0 between launches
+  uint64_t* flag = nullptr;    // coherent page-locked host word
+  uint64_t value = 0;
+};
+
 struct SegSpec {
   const uint8_t* bytes;
   const uint64_t* offsets;  // n+1 or nullptr
@@ -42,6 +55,7 @@ struct SegSpec {
   const void* list = nullptr;
   const uint32_t* meta = nullptr;
   int bin = -1;
+  Done done{};  // see Done
 };
 
 // Length binning of an offsets batch (mixed segment sizes): every segment
@@ -153,7 +167,6 @@ void set_twoclass_remap(uint32_t run_log2);  // the two-class launches' (default
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
 // one thread stores v into *flag (page-locked, coherent host memory) with
 // system-scope release, behind the stream's earlier work
-hipError_t launch_host_flag(uint64_t* flag, uint64_t v, hipStream_t st);
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
 // fused IPv4 + TCP for receive mixes: each block's datagrams of <= 64 bytes
@@ -163,6 +176,9 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
                                 int spw, uint32_t remap, hipStream_t st);
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
+// the router step with the forwarded 20-byte headers to hdr_out (coalesced),
+// the datagrams read only (k_router_hdrs)
+hipError_t launch_router_hdrs(const SegSpec& sp, uint32_t* hdr_out, uint8_t* status, hipStream_t st);
 
 // Tile launches of offsets batches (k_tile): T (1..256) consecutive segments
 // per block, the tile's bytes streamed whole in 16 KiB windows whatever the

@@ -211,6 +211,18 @@ class Engine:
                                             _ptr(status), _stream(stream, self.device)))
         return status
 
+    def router_ttl_headers(self, dgrams, n=None, offsets=None, stride=0, dgram_len=0, hdrs=None, status=None,
+                           stream=None):
+        """The router step with the forwarded 20-byte headers into `hdrs`
+        (allocated when absent); the datagrams are only read.  Returns
+        (hdrs, status)."""
+        n = _count(n, offsets, dgrams, stride)
+        hdrs = torch.empty(n * 20, dtype=torch.uint8, device=self.device) if hdrs is None else hdrs
+        status = torch.empty(n, dtype=torch.uint8, device=self.device) if status is None else status
+        self._check(self.lib.ics_router_ttl_headers(self.ctx, _ptr(dgrams), _ptr(offsets), stride, dgram_len, n,
+                                                    _ptr(hdrs), _ptr(status), _stream(stream, self.device)))
+        return hdrs, status
+
     # ---- host-memory (PCIe-inclusive) variants -----------------------------
     def checksum_batch_host(self, data, n, offsets=None, stride=0, seg_len=0, init=None):
         out = np.empty(n, dtype=np.uint16)

@@ -136,3 +136,76 @@ def test_zc_path_taken_per_threshold(zeng, orc, request):
         zc = b["host_zero_copy"] - a["host_zero_copy"]
         dma = b["host_dma_chunks"] - a["host_dma_chunks"]
         assert (zc, dma) == ((1, 0) if zc_expected else (0, 1)), (param, n, zc, dma)
+
+
+def test_zc_completion_over_many_blocks_and_two_pass_wrap(orc):
+    """The completion word comes from the launch's last block (a block-count
+    ticket, icsum_kernels.hip signal_done): zero-copy launches of hundreds of
+    blocks, back to back on every slot (the ticket word must be back at 0
+    after each), and the two-pass wrap, whose header pass completes the call."""
+    from conftest import engine_with
+    from test_gpu_wrap import _oracle_wire, _random_batch
+
+    rng = np.random.default_rng(0xD0E)
+    for eng in engine_with({"zero_copy_max": str(1 << 30), "wrap_passes": "2"}):
+        for r in range(8):
+            n = int(rng.integers(1, 20000))
+            L = int(rng.choice([64, 576, 1500]))
+            buf = rng.integers(0, 256, n * L, dtype=np.uint8)
+            a = eng.dispatch_info()["host_zero_copy"]
+            got = eng.checksum_batch_host(buf, n, stride=L, seg_len=L)
+            assert eng.dispatch_info()["host_zero_copy"] == a + 1, r
+            assert (got == orc.checksum_batch(buf, n, stride=L, seg_len=L)).all(), (r, n, L)
+            ip, tcp, st = eng.ipv4_tcp_batch_host(buf, n, 1, stride=L, dgram_len=L)
+            w = orc.ipv4_tcp_batch(buf.copy(), n, 1, stride=L, dgram_len=L)
+            assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), (r, n, L)
+        for n in (1, 700, 9000):
+            segs, m = _random_batch(rng, n)
+            want = _oracle_wire(orc, segs, m)
+            buf, off = pack_contiguous(segs, 1)
+            eng.tcp_wrap_batch_host(buf, m, n, offsets=off)
+            for i, w in enumerate(want):
+                assert buf[off[i]:off[i + 1]].tobytes() == w, (n, i)
+            pb, poff = pack_contiguous([s[40:] for s in segs], 0)
+            hdrs = eng.tcp_wrap_headers_host(pb, m, n, offsets=poff)
+            for i, w in enumerate(want):
+                assert hdrs[40 * i:40 * i + 40].tobytes() == w[:40], (n, i)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_error_after_chunks_in_flight_drains_slots(orc, pinned):
+    """A fused-IPv4 host batch (datagrams never split into pieces) whose last
+    datagram is larger than a staging slot fails with ICS_ERR_INVALID after
+    several 1 MiB chunks were enqueued; the call drains every slot before it
+    returns, so the caller's buffer can be freed at once, and the engine's
+    next calls are exact."""
+    import os
+
+    import torch
+
+    from conftest import engine_with
+    from tcpip_network_protocol_stack_amd._lib import IcsumError
+
+    os.environ["ICSUM_HOST_SLOT_MB"] = "1"
+    try:
+        gen = engine_with()
+        eng = next(gen)
+    finally:
+        os.environ.pop("ICSUM_HOST_SLOT_MB")
+    try:
+        rng = np.random.default_rng(8)
+        lens = [1500] * 4000 + [(1 << 20) + 8]
+        off = np.zeros(len(lens) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        h = torch.empty(int(off[-1]), dtype=torch.uint8, pin_memory=pinned)
+        h.numpy()[:] = rng.integers(0, 256, int(off[-1]), dtype=np.uint8)
+        with pytest.raises(IcsumError, match="exceeds"):
+            eng.ipv4_tcp_batch_host(h.numpy(), len(lens), 1, offsets=off)
+        del h  # freed right after the error
+        torch.cuda.synchronize()
+        buf = rng.integers(0, 256, 4000 * 1500, dtype=np.uint8)
+        ip, tcp, st = eng.ipv4_tcp_batch_host(buf, 4000, 1, stride=1500, dgram_len=1500)
+        w = orc.ipv4_tcp_batch(buf.copy(), 4000, 1, stride=1500, dgram_len=1500)
+        assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all()
+    finally:
+        next(gen, None)

@@ -270,3 +270,69 @@ def test_tile_wrap_headers_apart(tile_apart, orc, lead):
     h = hd.cpu().numpy()
     for i, w in enumerate(want):
         assert h[40 * i:40 * i + 40].tobytes() == w[:40], i
+
+
+def test_auto_reaches_tile_from_cached_plan(engine, orc):
+    """The default dispatch: an offsets batch of variable-length datagrams
+    (40..1040 bytes: 0..1000-byte payloads, the transmit side's mix) above
+    the tile threshold plans on its first call and runs the tile launch from
+    the cached plan on the next ones — checksum, VERIFY and the headers-apart
+    wrap — with the oracle's results every time; an MTU-only batch keeps the
+    per-segment launches."""
+    import torch
+
+    from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE
+
+    rng = np.random.default_rng(0x7A0)
+    n = 140_000
+    lens = 40 + rng.integers(0, 1001, n)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    s = off[:-1].astype(np.int64)
+    buf[s], buf[s + 2], buf[s + 3] = 0x45, (lens >> 8).astype(np.uint8), (lens & 255).astype(np.uint8)
+    buf[s + 6], buf[s + 8], buf[s + 9], buf[s + 32] = 0x40, 64, 6, 0x50
+    orc.ipv4_tcp_batch(buf, n, 2, offsets=off)  # valid checksums
+    d, do = _t(buf), _t(off)
+    want = orc.checksum_batch(buf, n, offsets=off)
+    want_v = orc.ipv4_tcp_batch(buf.copy(), n, 1, offsets=off)
+    kinds = []
+    for call in range(3):
+        assert (_u16(engine.checksum_batch(d, offsets=do)) == want).all(), call
+        kinds.append(engine.dispatch_info()["kernel"])
+        ip, tcp, st = engine.ipv4_tcp_batch(d, 1, offsets=do)
+        assert (_u16(ip) == want_v[0]).all() and (_u16(tcp) == want_v[1]).all(), call
+        assert (st.cpu().numpy() == want_v[2]).all(), call
+        kinds.append(engine.dispatch_info()["kernel"])
+    assert kinds[2:] == ["tile", "tile"] * 2, kinds
+    # headers apart: payloads of the same lengths minus 40
+    m = np.zeros(n, dtype=TCP_MSG_DTYPE)
+    for f, hi in (("src", 2**32), ("dst", 2**32), ("seqno", 2**32), ("ackno", 2**32), ("src_port", 2**16),
+                  ("dst_port", 2**16), ("window", 2**16)):
+        m[f] = rng.integers(0, hi, n, dtype=np.uint64)
+    m["flags"], m["ttl"] = 0x10, 128
+    pay = [buf[int(off[i]) + 40:int(off[i + 1])].tobytes() for i in range(n)]
+    pb, poff = pack_contiguous(pay, 0)
+    dm = torch.from_numpy(m.view(np.uint8).copy()).cuda()
+    got = []
+    for call in range(3):
+        hd = torch.empty(n * 40, dtype=torch.uint8, device="cuda")
+        engine.tcp_wrap_headers(_t(pb), dm, hd, n=n, offsets=_t(poff))
+        got.append((engine.dispatch_info()["kernel"], hd.cpu().numpy()))
+    assert got[2][0] == "tile" and got[0][0] != "tile", [g[0] for g in got]
+    assert (got[0][1] == got[1][1]).all() and (got[1][1] == got[2][1]).all()  # every path: the same headers
+    # ... and those are the reference's: a sample against the oracle's wrap
+    from test_gpu_wrap import _oracle_wire
+
+    idx = rng.choice(n, 300, replace=False)
+    want_w = _oracle_wire(orc, [b"\0" * 40 + pay[i] for i in idx], m[idx])
+    for k, i in enumerate(idx):
+        assert got[2][1][40 * i:40 * i + 40].tobytes() == want_w[k][:40], i
+    # MTU-sized datagrams: the per-segment launch stays
+    lm = np.full(n, 1500)
+    offm = np.zeros(n + 1, dtype=np.uint64)
+    offm[1:] = np.cumsum(lm)
+    bm = rng.integers(0, 256, int(offm[-1]) + 16, dtype=np.uint8)
+    for call in range(3):
+        engine.checksum_batch(_t(bm), offsets=_t(offm))
+    assert engine.dispatch_info()["kernel"] != "tile"

@@ -172,6 +172,17 @@ def main():
             ts.append(a.elapsed_time(b) / 1e3 / iters)
         assert (st.cpu().numpy() == 1).all(), "router batch stopped forwarding"
         t = statistics.median(ts)
+        # the same step with the forwarded headers apart (read-only batch, 20 B per datagram to one array)
+        hd = torch.empty(n * 20, dtype=torch.uint8, device=dev)
+        th = timed(lambda i=0: eng.router_ttl_headers(bufs[i % R], n=n, stride=L, dgram_len=L, hdrs=hd, status=st),
+                   args.iters)
+        assert (st.cpu().numpy() == 1).all()
+        print(json.dumps({"config": "router_ttl_headers_1Mx1500", "datagrams": n, "us": round(th * 1e6, 2),
+                          "Mdgram_s": round(n / th / 1e6, 1), "header_GB_s": round(n * 40 / th / 1e9, 1),
+                          "line_GB_s": round(n * 128 / th / 1e9, 1),
+                          "frac_hbm_peak_lines": round(n * 128 / th / 1e9 / PEAK, 4),
+                          "entry": "ics_router_ttl_headers", "rotation": R,
+                          "note": "20 header bytes read + 20 written per datagram; payloads untouched"}), flush=True)
         # algorithmic: 20 header bytes read + 4 written per datagram; the
         # memory system moves at least one 128-B line per datagram
         print(json.dumps({"config": "router_ttl_1Mx1500", "datagrams": n, "us": round(t * 1e6, 2),

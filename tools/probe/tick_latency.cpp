@@ -7,6 +7,12 @@
 // the same buffers; every build's outputs must equal the first's.
 //   g++ -O2 -std=c++17 -I../../include tick_latency.cpp -o tick_latency -ldl
 //   tick_latency libA.so [libB.so ...]
+// Environment: TICK_OPS (comma list of verify, verify_off, checksum, wrap;
+// default all), TICK_SIZES (comma list of batch sizes, default 1..8192),
+// TICK_MEM (pinned | pageable, default both), TICK_CALLS (timed calls per
+// round, default 200).  Checksum calls pass per-segment inits (the NS
+// workload's pseudo-header sums).  bench.py's host_inclusive runs it as
+// TICK_OPS=checksum TICK_SIZES=1,16 TICK_MEM=pinned (built by build()).
 #include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -102,15 +108,32 @@ int main(int argc, char** argv) {
     msgs[i] = ics_tcp_msg{0x0a000001u, 0x0a000002u, uint32_t(rng()), uint32_t(rng()), 40000, 80, 64000, 0x10, 128,
                           0, 0};
   }
-  const uint64_t sizes[] = {1, 4, 16, 64, 256, 512, 1024, 4096, 8192};
+  std::vector<uint64_t> sizes = {1, 4, 16, 64, 256, 512, 1024, 4096, 8192};
+  if (const char* e = getenv("TICK_SIZES")) {
+    sizes.clear();
+    for (const char* p = e; *p;) {
+      char* end = nullptr;
+      const unsigned long long v = strtoull(p, &end, 10);
+      if (end == p || v == 0 || v > kMaxN) {
+        fprintf(stderr, "TICK_SIZES: sizes 1..%llu, comma-separated\n", (unsigned long long)kMaxN);
+        return 2;
+      }
+      sizes.push_back(v);
+      p = *end == ',' ? end + 1 : end;
+    }
+  }
+  const char* mem_only = getenv("TICK_MEM");
+  std::vector<uint32_t> inits(kMaxN);
+  for (auto& v : inits) v = uint32_t(rng());
   const char* ops[] = {"verify", "verify_off", "checksum", "wrap"};
   const char* only = getenv("TICK_OPS");  // comma list of ops to run (default: all)
   std::vector<uint64_t> offs(kMaxN + 1);
   for (uint64_t i = 0; i <= kMaxN; ++i) offs[i] = i * kL;
-  const int rounds = 5, calls = 200;
+  const int rounds = 5, calls = getenv("TICK_CALLS") ? std::max(10, atoi(getenv("TICK_CALLS"))) : 200;
   for (const char* op : ops)
     for (int mem = 0; mem < 2; ++mem) {
       if (only && !strstr(only, op)) continue;
+      if (mem_only && strcmp(mem_only, mem ? "pinned" : "pageable")) continue;
       for (uint64_t n : sizes) {
         uint8_t* src = mem ? pinned : pageable.data();
         std::vector<std::vector<double>> t(libs.size());
@@ -128,7 +151,7 @@ int main(int argc, char** argv) {
               else if (op[0] == 'v')
                 check(l, l.ipv4_host(l.ctx, src, nullptr, kL, kL, n, ICS_MODE_VERIFY, a, b, st));
               else if (op[0] == 'c')
-                check(l, l.checksum_host(l.ctx, src, nullptr, kL, kL, nullptr, a, n));
+                check(l, l.checksum_host(l.ctx, src, nullptr, kL, kL, inits.data(), a, n));
               else
                 check(l, l.wrap_host(l.ctx, src, nullptr, kL, kL, n, msgs.data()));
               if (c >= 10) t[k].push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
