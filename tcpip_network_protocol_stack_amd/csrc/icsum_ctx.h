@@ -91,6 +91,7 @@ struct ics_ctx {
   static constexpr uint32_t kTileMaxAvg = 1024;            // ... and up to this mean length (tile_wins)
   static constexpr uint32_t kTileApartShort16 = 12;       // headers-apart wrap: below 12/16 empty-ish payloads
   uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order
+  uint32_t twoclass_lds = 0;    // dynamic LDS bytes per two-class block (residency cap; ICSUM_FORCE twoclass_lds)
   uint32_t tile_segs = 0, tile_blocks = 0;
   // device wrap: 0 = two passes (payload sums, then a header launch) when
   // the headers go to an array of their own and the batch has at least

@@ -180,7 +180,7 @@ bool tile_wins(const ics_ctx* ctx, const PlanMix& m, uint64_t n, bool fused) {
 hipError_t launch_mix(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                       void* d_out, int out_kind, const PlanMix& mix, hipStream_t st) {
   const int spw = mix.short16 >= 12 ? 32 : 16;
-  const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, spw, ctx->twoclass_remap, st);
+  const hipError_t e = icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, spw, ctx->twoclass_remap, st, ctx->twoclass_lds);
   if (e != hipErrorInvalidValue) {
     note(ctx, ICS_K_TWOCLASS, {16, spw, true, 3, 1});
     return e;
@@ -201,7 +201,7 @@ icsum::Geometry small_plan_geometry(const PlanMix& m) {
 int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_init, const uint8_t* d_odd,
                     void* d_out, int out_kind, hipStream_t st) {
   if (sp.offsets && ctx->twoclass) {  // test hook: the two-class launch on every offsets batch
-    ICS_HIP(icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, ctx->twoclass, ctx->twoclass_remap, st));
+    ICS_HIP(icsum::launch_checksum_twoclass(sp, d_init, d_odd, d_out, out_kind, ctx->twoclass, ctx->twoclass_remap, st, ctx->twoclass_lds));
     note(ctx, ICS_K_TWOCLASS, {16, ctx->twoclass, true, 3, 1});
     return ICS_OK;
   }
@@ -372,7 +372,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   }
   hipError_t le = hipErrorInvalidValue;
   if (two) {
-    le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, spw, ctx->twoclass_remap, st);
+    le = icsum::launch_ipv4_twoclass(sp, mode, d_ip_ck, d_tcp_ck, d_status, spw, ctx->twoclass_remap, st, ctx->twoclass_lds);
     if (le != hipErrorInvalidValue) note(ctx, ICS_K_IPV4_TWOCLASS, {16, spw, true, 3, 1}, plan_used);
   }
   if (le == hipErrorInvalidValue) {
@@ -593,6 +593,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
+    else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);
     else if (k == "tile" && v >= -1 && v <= 1) ctx->tile = int(v);
     else if (k == "tile_segs" && v >= 0 && v <= 256) ctx->tile_segs = uint32_t(v);

@@ -2282,7 +2282,7 @@ hipError_t launch_checksum_small_t(const SegSpec& sp, const uint32_t* init, cons
 
 template <int LONG_LPS, int SPW>
 hipError_t launch_twoclass_t(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                             uint32_t remap, hipStream_t st) {
+                             uint32_t remap, uint32_t lds_pad, hipStream_t st) {
   const uint64_t blocks = twoclass_blocks(sp.n, SPW);
   if (blocks == 0 || blocks > kMaxGridBlocks) return hipErrorInvalidValue;
   const uint32_t* ip = init ? init : static_cast<const uint32_t*>(sp.zero16);
@@ -2290,10 +2290,10 @@ hipError_t launch_twoclass_t(const SegSpec& sp, const uint32_t* init, const uint
   const uint32_t is = init ? 1u : 0u, os = odd ? 1u : 0u;
   const u32x4* z = static_cast<const u32x4*>(sp.zero16);
   if (out_kind == 0)
-    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, SPW, 0>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st,
+    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, SPW, 0>), dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st,
                        sp.bytes, src_of(sp), ip, is, op, os, z, out, sp.n, remap);
   else
-    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, SPW, 1>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st,
+    hipLaunchKernelGGL((k_checksum_twoclass<LONG_LPS, SPW, 1>), dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st,
                        sp.bytes, src_of(sp), ip, is, op, os, z, out, sp.n, remap);
   return hipGetLastError();
 }
@@ -2437,10 +2437,10 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
 }
 
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
-                                    int out_kind, int spw, uint32_t remap, hipStream_t st) {
+                                    int out_kind, int spw, uint32_t remap, hipStream_t st, uint32_t lds_pad) {
   if (sp.list) return hipErrorInvalidValue;
-  if (spw == 32) return launch_twoclass_t<16, 32>(sp, init, odd, out, out_kind, remap, st);
-  if (spw == 16) return launch_twoclass_t<16, 16>(sp, init, odd, out, out_kind, remap, st);
+  if (spw == 32) return launch_twoclass_t<16, 32>(sp, init, odd, out, out_kind, remap, lds_pad, st);
+  if (spw == 16) return launch_twoclass_t<16, 16>(sp, init, odd, out, out_kind, remap, lds_pad, st);
   return hipErrorInvalidValue;
 }
 
@@ -2575,17 +2575,17 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 }
 
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                int spw, uint32_t remap, hipStream_t st) {
+                                int spw, uint32_t remap, hipStream_t st, uint32_t lds_pad) {
   if (spw != 16 && spw != 32) return hipErrorInvalidValue;
   const uint64_t blocks = twoclass_blocks(sp.n, uint64_t(spw));
   if (sp.list || blocks == 0 || blocks > kMaxGridBlocks) return hipErrorInvalidValue;
   uint8_t* const dg = const_cast<uint8_t*>(sp.bytes);
   const uint8_t* const z = static_cast<const uint8_t*>(sp.zero16);
   if (spw == 16)
-    hipLaunchKernelGGL(k_ipv4_twoclass<16>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, dg, sp.offsets, sp.stride,
+    hipLaunchKernelGGL(k_ipv4_twoclass<16>, dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st, dg, sp.offsets, sp.stride,
                        sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z, remap);
   else
-    hipLaunchKernelGGL(k_ipv4_twoclass<32>, dim3(uint32_t(blocks)), dim3(kBlock), 0, st, dg, sp.offsets, sp.stride,
+    hipLaunchKernelGGL(k_ipv4_twoclass<32>, dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st, dg, sp.offsets, sp.stride,
                        sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z, remap);
   return hipGetLastError();
 }

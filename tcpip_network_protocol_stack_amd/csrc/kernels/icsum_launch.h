@@ -115,7 +115,7 @@ hipError_t launch_checksum(const SegSpec& sp, const uint32_t* init, const uint8_
 // bounds pass
 // (remap: block_order's log2 XCD run length, 0 = hardware order)
 hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out,
-                                    int out_kind, int spw, uint32_t remap, hipStream_t st);
+                                    int out_kind, int spw, uint32_t remap, hipStream_t st, uint32_t lds_pad = 0);
 // Dense fixed-stride batches (stride == seg_len in {32, 64, 128}, 16-byte
 // aligned bytes, no parity array): k_checksum_dense, SEGS segments per lane
 // group in flight (segs in {1, 2, 4, 8}; not every (seg_len, segs) pair exists)
@@ -163,18 +163,17 @@ hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const 
 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
 void set_xcd_remap(uint32_t run_log2);
-void set_twoclass_remap(uint32_t run_log2);  // the two-class launches' (default 0: hardware order)  // log2 XCD run length (default 10 = 1024 blocks), 0: hardware order
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
-// one thread stores v into *flag (page-locked, coherent host memory) with
-// system-scope release, behind the stream's earlier work
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
 // fused IPv4 + TCP for receive mixes: each block's datagrams of <= 64 bytes
 // one per lane on one wave, the rest 16 lanes each claimed by every wave
 // (k_ipv4_twoclass); spw (16 or 32) datagrams per wave in the bounds pass,
-// i.e. 64 or 128 per block
+// i.e. 64 or 128 per block; lds_pad: bytes of dynamic LDS per block on top
+// of the kernel's own (caps the blocks resident per CU; 0 in the default
+// dispatch, ICSUM_FORCE twoclass_lds)
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                                int spw, uint32_t remap, hipStream_t st);
+                                int spw, uint32_t remap, hipStream_t st, uint32_t lds_pad = 0);
 hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st);
 // the router step with the forwarded 20-byte headers to hdr_out (coalesced),
 // the datagrams read only (k_router_hdrs)
