@@ -107,10 +107,12 @@ struct ics_ctx {
   // whose key holds a whole-batch plan skips the binning passes (their 4
   // dispatches, ~25 us) and runs that plan's single launch; every
   // kPlanRefresh-th hit re-plans behind its launch, so a changed mix is
-  // noticed within kPlanRefresh calls.  Several slots: a stack alternates its
+  // noticed within kPlanRefresh calls (64: the stats + plan kernels cost
+  // ≈ 9.5 us behind a 256 Ki-datagram call, 0.6 us per call at every 16th,
+  // profiles/r4_stack_kernel_stats.csv).  Several slots: a stack alternates its
   // transmit buffer (wrap) with its receive buffer (verify / unwrap), and
   // neither may evict the other's plan (LRU over the slots).
-  static constexpr uint32_t kPlanRefresh = 16;
+  static constexpr uint32_t kPlanRefresh = 64;
   static constexpr int kPlanSlots = 4;
   struct PlanSlot {
     const uint64_t* key = nullptr;

@@ -332,7 +332,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   // follows the plan the device reported for the same offsets buffer last
   // time (4-lane groups when it was the small-segment plan, 8-lane groups
   // from 5/16 of <= 144-byte datagrams, 16 x 4 below that), the plan
-  // kernels running behind the first and every 16th launch (DESIGN.md §4,
+  // kernels running behind the first and every 64th launch (DESIGN.md §4,
   // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
   bool two = false, tile = false;
   int spw = 16;
@@ -589,7 +589,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "last_bin_lps") ctx->last_bin_lps = uint32_t(v);
     else if (k == "last_bin_blocks") ctx->last_bin_blocks = uint32_t(v);
     else if (k == "dense_segs") ctx->dense_segs = int(v);
-    else if (k == "twoclass" && (v == 0 || v == 16 || v == 32)) ctx->twoclass = int(v);
+    else if (k == "twoclass" && (v == 0 || v == 8 || v == 16 || v == 32)) ctx->twoclass = int(v);
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);

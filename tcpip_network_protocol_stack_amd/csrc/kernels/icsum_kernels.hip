@@ -2441,6 +2441,7 @@ hipError_t launch_checksum_twoclass(const SegSpec& sp, const uint32_t* init, con
   if (sp.list) return hipErrorInvalidValue;
   if (spw == 32) return launch_twoclass_t<16, 32>(sp, init, odd, out, out_kind, remap, lds_pad, st);
   if (spw == 16) return launch_twoclass_t<16, 16>(sp, init, odd, out, out_kind, remap, lds_pad, st);
+  if (spw == 8) return launch_twoclass_t<16, 8>(sp, init, odd, out, out_kind, remap, lds_pad, st);
   return hipErrorInvalidValue;
 }
 
@@ -2576,17 +2577,18 @@ hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_
 
 hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
                                 int spw, uint32_t remap, hipStream_t st, uint32_t lds_pad) {
-  if (spw != 16 && spw != 32) return hipErrorInvalidValue;
+  if (spw != 8 && spw != 16 && spw != 32) return hipErrorInvalidValue;
   const uint64_t blocks = twoclass_blocks(sp.n, uint64_t(spw));
   if (sp.list || blocks == 0 || blocks > kMaxGridBlocks) return hipErrorInvalidValue;
   uint8_t* const dg = const_cast<uint8_t*>(sp.bytes);
   const uint8_t* const z = static_cast<const uint8_t*>(sp.zero16);
-  if (spw == 16)
-    hipLaunchKernelGGL(k_ipv4_twoclass<16>, dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st, dg, sp.offsets, sp.stride,
-                       sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z, remap);
-  else
-    hipLaunchKernelGGL(k_ipv4_twoclass<32>, dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st, dg, sp.offsets, sp.stride,
-                       sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z, remap);
+#define ICS_TWO(W)                                                                                        \
+  hipLaunchKernelGGL(k_ipv4_twoclass<W>, dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st, dg, sp.offsets,    \
+                     sp.stride, sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z, remap)
+  if (spw == 8) ICS_TWO(8);
+  else if (spw == 16) ICS_TWO(16);
+  else ICS_TWO(32);
+#undef ICS_TWO
   return hipGetLastError();
 }
 

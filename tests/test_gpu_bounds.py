@@ -128,8 +128,8 @@ def test_non_monotone_offsets_are_reported(dbg, engine):
         dbg.ipv4_tcp_batch(d, 1, offsets=do)
 
 
-@pytest.mark.parametrize("force", [{"lps": 1, "unroll": 4, "mode": 4}, {"twoclass": 16}, {"twoclass": 32}],
-                         ids=["tiny", "twoclass16", "twoclass32"])
+@pytest.mark.parametrize("force", [{"lps": 1, "unroll": 4, "mode": 4}, {"twoclass": 8}, {"twoclass": 16}, {"twoclass": 32}],
+                         ids=["tiny", "twoclass8", "twoclass16", "twoclass32"])
 def test_round2_dispatches_clean_and_identical(engine, force):
     # the round-2 kernels (one lane per segment, the two-class launches)
     # under the bounds-checked build: clean, and equal to the release

@@ -14,7 +14,7 @@ from test_gpu_parity import _t, _u16, _u32
 
 pytestmark = pytest.mark.gpu
 
-TWO_FORCE = [{"twoclass": 16}, {"twoclass": 32}]
+TWO_FORCE = [{"twoclass": 8}, {"twoclass": 16}, {"twoclass": 32}]
 
 
 @pytest.fixture(scope="module", params=TWO_FORCE, ids=force_id)
@@ -163,7 +163,7 @@ def test_twoclass_config4_full_size(two_csum):
     assert hashlib.sha256(out.tobytes()).hexdigest() == g["out_sha256"]
 
 
-@pytest.fixture(scope="module", params=[{"twoclass": 32}, {"twoclass": 16}], ids=force_id)
+@pytest.fixture(scope="module", params=[{"twoclass": 32}, {"twoclass": 16}, {"twoclass": 8}], ids=force_id)
 def two_engine(request):
     yield from engine_with(request.param)
 

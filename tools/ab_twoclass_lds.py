@@ -2,9 +2,10 @@
 """Dev measurement: the two-class launches (checksum and fused VERIFY) on the
 receive mix (half 40-byte ACKs, half 1500-byte datagrams, valid headers,
 packed offsets) with the blocks resident per CU capped by dynamic LDS
-(ICSUM_FORCE twoclass_lds: bytes per block on top of the kernel's own), at
-256 Ki and 1 M datagrams.  Two copies rotate; HIP events around 20
-back-to-back calls, median of 5 rounds."""
+(ICSUM_FORCE twoclass_lds: bytes per block on top of the kernel's own) and
+with 8 / 16 / 32 datagrams per wave (twoclass=N), at 256 Ki and 1 M
+datagrams.  Two copies rotate; HIP events around 20 back-to-back calls,
+median of 5 rounds."""
 import json
 import os
 import sys
@@ -22,7 +23,9 @@ def main():
     sizes = [int(x) for x in sys.argv[1].split(",")] if len(sys.argv) > 1 else [1 << 18, 1 << 20]
     pads = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 8192, 16384, 24576, 32768, 49152]
     auto = engine()
-    engs = {p: (engine(twoclass_lds=p) if p else auto) for p in pads}
+    engs = {f"lds{p}": (engine(twoclass_lds=p) if p else auto) for p in pads}
+    engs.update({f"spw{w}": engine(twoclass=w) for w in (8, 16, 32)})
+    engs.update({f"spw8_lds{p}": engine(twoclass=8, twoclass_lds=p) for p in (16384, 32768)})
     for n in sizes:
         rx = [rx_batch(auto, n, 11 + r) for r in range(R)]
         nb = rx[0][2]
@@ -35,11 +38,11 @@ def main():
                                                       tcp_ck=tcp, status=st))
             assert (st.cpu().numpy() == 0x0F).all(), p
             k = e.dispatch_info()["kernel"]
-            print(json.dumps({"row": f"verify_{n}_lds{p}", "bytes": nb, "us": round(t * 1e6, 2),
+            print(json.dumps({"row": f"verify_{n}", "lib": p, "bytes": nb, "us": round(t * 1e6, 2),
                               "frac": round(nb / t / PEAK, 4), "kernel": k}), flush=True)
             t = timed(lambda i, e=e: e.checksum_batch(rx[i % R][0], n=n, offsets=rx[i % R][1], out=out))
             k = e.dispatch_info()["kernel"]
-            print(json.dumps({"row": f"checksum_{n}_lds{p}", "bytes": nb, "us": round(t * 1e6, 2),
+            print(json.dumps({"row": f"checksum_{n}", "lib": p, "bytes": nb, "us": round(t * 1e6, 2),
                               "frac": round(nb / t / PEAK, 4), "kernel": k}), flush=True)
         del rx
 
