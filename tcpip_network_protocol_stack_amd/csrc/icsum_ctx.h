@@ -90,6 +90,9 @@ struct ics_ctx {
   static constexpr uint64_t kTileMin = uint64_t(1) << 17;  // tile launches from this many segments (AUTO)
   static constexpr uint32_t kTileMaxAvg = 1024;            // ... and up to this mean length (tile_wins)
   static constexpr uint32_t kTileApartShort16 = 12;       // headers-apart wrap: below 12/16 empty-ish payloads
+  static constexpr uint64_t kTileBytes = 96 << 10;        // segment bytes per tile (tile_segs_for)
+  static constexpr uint64_t kTileResident = 1024;          // tile blocks resident at once: 4 per CU x 256 CUs
+  static constexpr uint64_t kTileRoundBytes = 160 << 10;   // largest tile taken to fit all tiles in one round
   uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order
   uint32_t twoclass_lds = 0;    // dynamic LDS bytes per two-class block (residency cap; ICSUM_FORCE twoclass_lds)
   uint32_t tile_segs = 0, tile_blocks = 0;

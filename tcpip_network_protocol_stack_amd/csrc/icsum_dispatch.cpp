@@ -16,13 +16,23 @@ static_assert(icsum::kBvDense64 == ICS_BV_DENSE64 && icsum::kBvTiny == ICS_BV_TI
                   icsum::kBvLane1 == ICS_BV_LANE1,
               "multi-batch shapes are reported as ICS_BV_*");
 
-// Segments per tile of a tile launch (k_tile): the forced value, else as
-// many as keep >= 1024 tiles (four per CU) up to 128, at least 16 (128 was
-// the fastest of 32-256 on every mix at 256 Ki and 1 M segments,
-// tools/ab_tile.py)
-uint32_t tile_segs_for(const ics_ctx* ctx, uint64_t n) {
+// Segments per tile of a tile launch (k_tile): the forced value; without a
+// mean length (the test hook on an unplanned batch) as many as keep >= 1024
+// tiles up to 128; with the cached plan's mean length, about kTileBytes of
+// segments per tile (128..256), and all the tiles in one round of resident
+// blocks (kTileResident: 4 per CU, LDS-bound) when a tile of up to
+// kTileRoundBytes does it.  Measured (tools/ab_tile_T.py,
+// profiles/r4_ab_tile_T.jsonl, us, T = 64..256): 0..1000-byte payloads best
+// at 192 from 192 Ki to 1 M datagrams except 256 at 256 Ki (one round:
+// headers-apart wrap 32.6 -> 30.5), 770-byte segments best at 128 except
+// 192 at 192 Ki (one round).
+uint32_t tile_segs_for(const ics_ctx* ctx, uint64_t n, uint32_t avg) {
   if (ctx->tile_segs) return std::min<uint32_t>(ctx->tile_segs, 256);
-  return uint32_t(std::clamp<uint64_t>(n / 1024, 16, 128));
+  if (avg == 0) return uint32_t(std::clamp<uint64_t>(n / 1024, 16, 128));
+  uint64_t T = std::clamp<uint64_t>((ics_ctx::kTileBytes / avg + 16) & ~uint64_t(31), 128, 256);
+  const uint64_t one = (n + ics_ctx::kTileResident - 1) / ics_ctx::kTileResident;  // T of a single round
+  if ((n + T - 1) / T > ics_ctx::kTileResident && one <= 256 && one * avg <= ics_ctx::kTileRoundBytes) T = one;
+  return uint32_t(T);
 }
 
 bool wrap_two_pass(const ics_ctx* ctx, bool headers_apart, uint64_t n) {
@@ -206,7 +216,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     return ICS_OK;
   }
   if (sp.offsets && ctx->tile == 1) {  // test hook: the tile launch on every offsets batch
-    const uint32_t T = tile_segs_for(ctx, sp.n);
+    const uint32_t T = tile_segs_for(ctx, sp.n, 0);
     ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st));
     note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM, true, 0, 1});
     return ICS_OK;
@@ -263,7 +273,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     const bool hit = plan_lookup(ctx, sp, true, &hit_plan, &req, &mix);
     const bool mix8 = hit && hit_plan != icsum::kPlanWholeBatchSmall && short_mix(mix);
     if (hit && !mix8 && hit_plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, sp.n, false)) {
-      const uint32_t T = tile_segs_for(ctx, sp.n);
+      const uint32_t T = tile_segs_for(ctx, sp.n, mix.avg);
       ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st));
       note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM, true, 0, 1}, int(hit_plan));
       return replan(ctx, sp, lps, req, st);
@@ -336,6 +346,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
   bool two = false, tile = false;
   int spw = 16;
+  uint32_t tile_avg = 0;  // the cached plan's mean length (tile_segs_for)
   PlanReq req;
   int plan_used = -1;
   if (d_offsets && !forced_geometry(ctx) && !ctx->twoclass && n >= ics_ctx::kSmallPlanMin && n <= 0xFFFFFFFFull) {
@@ -359,13 +370,14 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
     spw = mix.short16 >= ics_ctx::kIpv4TwoClassWide16 ? 32 : 16;
     plan_used = hit ? int(plan) : -1;
     tile = hit && !two && plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, n, true);
+    tile_avg = hit ? mix.avg : 0u;
   }
   if (d_offsets && ctx->twoclass) {  // test hook
     two = true;
     spw = ctx->twoclass;
   }
   if (d_offsets && (ctx->tile == 1 || tile)) {  // the test hook, or the cached mix favours the tile launch
-    const uint32_t T = tile_segs_for(ctx, n);
+    const uint32_t T = tile_segs_for(ctx, n, tile_avg);
     ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, T, ctx->tile_blocks, st));
     note(ctx, ICS_K_TILE, {int(T), ICS_TILE_IPV4, true, 0, 1}, plan_used);
     return replan(ctx, sp, 64, req, st);
@@ -449,7 +461,7 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
                                        : !short_mix(mix) && ctx->tile != 0 && sp.n >= ics_ctx::kTileMin &&
                                              mix.long16 >= 4);
   if (sp.offsets && (ctx->tile == 1 || tile_pick)) {  // the wrap (in place or headers apart) as a tile launch
-    const uint32_t T = tile_segs_for(ctx, sp.n);
+    const uint32_t T = tile_segs_for(ctx, sp.n, plan >= 0 ? mix.avg : 0u);
     ICS_HIP(icsum::launch_tile_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), hdr_out, d_ip_ck, d_tcp_ck,
                                     T, ctx->tile_blocks, st));
     note(ctx, ICS_K_TILE, {int(T), hdr_out ? ICS_TILE_WRAP_APART : ICS_TILE_WRAP, true, 0, 1}, plan);
