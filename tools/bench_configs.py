@@ -533,6 +533,32 @@ def main():
             emit(f"stack_tick_{name}", nbytes, t, n * (5 if fn is verify else 28),
                  entry=entries[fn],
                  note="back-to-back calls, events around the run; 256 Ki datagrams, packed offsets")
+        # one whole tick: the receive VERIFY and the transmit headers-apart wrap,
+        # on one stream in turn, and on two streams (forked from and joined
+        # back into the caller's stream every tick: the results of both are
+        # needed before the next tick, util/tcp_minnow_socket/tcp_minnow_socket.h:138-164)
+        s1, s2 = torch.cuda.current_stream(), torch.cuda.Stream(device=dev)
+        fork, join = torch.cuda.Event(), torch.cuda.Event()
+
+        def tick_one(i=0):
+            verify()
+            wrap_apart()
+
+        def tick_two(i=0):
+            fork.record(s1)
+            s2.wait_event(fork)
+            eng.tcp_wrap_headers(px, dm, hd, n=n, offsets=dpof, stream=s2)
+            verify()
+            join.record(s2)
+            s1.wait_event(join)
+
+        both = int(roff[-1]) + int(toff[-1])
+        for name, fn in (("both_one_stream", tick_one), ("both_two_streams", tick_two)):
+            t = timed(fn, args.iters)
+            emit(f"stack_tick_{name}", both, t, n * 33,
+                 entry="ics_ipv4_tcp_batch VERIFY + ics_tcp_wrap_headers",
+                 note="one tick per step: 256 Ki received datagrams VERIFYed and 256 Ki transmitted datagrams "
+                      "wrapped with the headers apart, back to back, events around the run")
         assert (stt.cpu().numpy() == 0x0F).all(), "the receive batch must verify"
         del rx, tx, px
     eng.close()
