@@ -1869,23 +1869,40 @@ __global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, co
       if (c0 >= g.wc1) return;  // uniform
       const uint32_t len = uint32_t(g.wc1 - c0 < kWinChunks ? g.wc1 - c0 : kWinChunks);
       const uint64_t c1 = c0 + len;
-      uint32_t be = ce, bo = co;
+      // the window's chunks to LDS as loaded (chunk r = 64 u + lane), then
+      // read back four consecutive ones per lane (chunks 4 lane .. 4 lane + 3):
+      // a lane's prefix over its own four is three adds, and ONE wave scan of
+      // the lane totals (per role) gives every chunk's exclusive prefix —
+      // instead of a wave scan per loaded row (four per role)
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const uint32_t r = uint32_t(u) * 64u + lane;
         u32x4 x = v[u];  // zeros past the range
         if (c0 == 0 && r == 0) x &= m0;
-        uint32_t ev = 0, od = 0;
-        acc_chunk(x, ev, od);
-        const uint32_t ie = wave_prefix_incl(ev), io = wave_prefix_incl(od);
-        s_pre[wv][r][0] = be + ie - ev;
-        s_pre[wv][r][1] = bo + io - od;
         s_raw[wv][r] = x;
-        be += __builtin_amdgcn_readlane(ie, 63);
-        bo += __builtin_amdgcn_readlane(io, 63);
       }
-      ce = be;
-      co = bo;
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint32_t pe[4], po[4], te = 0, to = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t ev = 0, od = 0;
+        acc_chunk(s_raw[wv][4u * lane + uint32_t(j)], ev, od);
+        pe[j] = te;
+        po[j] = to;
+        te += ev;
+        to += od;
+      }
+      const uint32_t ie = wave_prefix_incl(te), io = wave_prefix_incl(to);
+      const uint32_t xe = ce + ie - te, xo = co + io - to;  // sums of the window's chunks below 4 lane
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s_pre[wv][4u * lane + uint32_t(j)][0] = xe + pe[j];
+        s_pre[wv][4u * lane + uint32_t(j)][1] = xo + po[j];
+      }
+      ce += __builtin_amdgcn_readlane(ie, 63);
+      co += __builtin_amdgcn_readlane(io, 63);
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
