@@ -217,3 +217,66 @@ def test_batchv_clean_and_identical(dbg, engine):
                 assert (a.cpu().numpy() == c.cpu().numpy()).all(), mode
         for a, c in zip(d1, d2):
             assert (a["dgrams"].cpu().numpy() == c["dgrams"].cpu().numpy()).all(), mode
+
+
+@pytest.mark.parametrize("force", [{"tile": 1}, {"tile": 1, "tile_segs": 7}, {"tile": 1, "tile_segs": 256}],
+                         ids=["tile", "tile7", "tile256"])
+def test_tile_clean_and_identical(engine, orc, force):
+    """The tile launch (round 4) under the bounds-checked build — every window
+    and header load checked against the tile's envelope — on a variable-length
+    batch with empty, short and jumbo segments: clean, and equal to the
+    release library's default dispatch for the checksum, the unfolded sums,
+    the fused kernel in every mode and both wraps."""
+    import torch
+
+    from conftest import engine_with
+    from tcpip_network_protocol_stack_amd.engine import TCP_MSG_DTYPE
+
+    gen = engine_with(force, debug=True)
+    dbg = next(gen)
+    try:
+        rng = np.random.default_rng(0x711E)
+        n = 20_000
+        lens = 40 + rng.integers(0, 1001, n)
+        lens[::13] = rng.integers(0, 40, lens[::13].size)
+        lens[::997] = 9000
+        off = np.zeros(n + 1, dtype=np.uint64)
+        off[1:] = np.cumsum(lens)
+        off += 3
+        buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+        s, ln = off[:-1].astype(np.int64), np.diff(off).astype(np.int64)
+        ok = ln >= 40
+        buf[s[ok]], buf[s[ok] + 9], buf[s[ok] + 32] = 0x45, 6, 0x50
+        buf[s[ok] + 2], buf[s[ok] + 3] = (ln[ok] >> 8).astype(np.uint8), (ln[ok] & 255).astype(np.uint8)
+        d, do = _t(buf), _t(off)
+        odd = _t(rng.integers(0, 2, n).astype(np.uint8))
+        got = _u(dbg.checksum_batch(d, offsets=do), np.uint16)
+        assert dbg.dispatch_info()["kernel"] == "tile"
+        assert (got == _u(engine.checksum_batch(d, offsets=do), np.uint16)).all()
+        assert (got == orc.checksum_batch(buf, n, offsets=off)).all()
+        assert (_u(dbg.sum_batch(d, offsets=do, odd=odd), np.uint32) ==
+                _u(engine.sum_batch(d, offsets=do, odd=odd), np.uint32)).all()
+        for mode in (0, 1, 2):
+            d1, d2 = _t(buf), _t(buf)
+            r1 = dbg.ipv4_tcp_batch(d1, mode, offsets=do)
+            r2 = engine.ipv4_tcp_batch(d2, mode, offsets=do)
+            for x, y in zip(r1, r2):
+                assert (x.cpu().numpy() == y.cpu().numpy()).all(), mode
+            assert (d1.cpu().numpy() == d2.cpu().numpy()).all(), mode
+        m = np.zeros(n, dtype=TCP_MSG_DTYPE)
+        m["src"], m["dst"], m["seqno"] = rng.integers(0, 2**32, (3, n), dtype=np.uint64)
+        m["flags"], m["ttl"] = 0x10, 128
+        dm = torch.from_numpy(m.view(np.uint8).copy()).cuda()
+        d1, d2 = _t(buf), _t(buf)
+        dbg.tcp_wrap_batch(d1, dm, n=n, offsets=do)
+        engine.tcp_wrap_batch(d2, dm, n=n, offsets=do)
+        assert (d1.cpu().numpy() == d2.cpu().numpy()).all()
+        h1 = torch.empty(n * 40, dtype=torch.uint8, device="cuda")
+        h2 = torch.empty(n * 40, dtype=torch.uint8, device="cuda")
+        dbg.tcp_wrap_headers(d, dm, h1, n=n, offsets=do)
+        engine.tcp_wrap_headers(d, dm, h2, n=n, offsets=do)
+        assert dbg.dispatch_info()["kernel"] == "tile"
+        assert (h1.cpu().numpy() == h2.cpu().numpy()).all()
+        torch.cuda.synchronize()
+    finally:
+        dbg.close()
