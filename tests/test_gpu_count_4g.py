@@ -14,7 +14,8 @@ the unknown-mix geometry); this module pins that path too.
 * 2^32 + 1001 packed offsets (34 GiB), all segments empty except eight —
   placed at 0, 1, 2^31 - 1, 2^31, 2^32 - 1, 2^32, 2^32 + 1 and the last —
   holding real datagrams: the plain checksum (automatic, forced one lane,
-  forced 16-lane), IPv4/TCP VERIFY (automatic, one lane) and the router.
+  forced 16-lane, the tile launch), IPv4/TCP VERIFY (automatic, one lane,
+  the tile launch) and the router.
   Every empty segment must give the oracle's value for an empty segment, the
   eight the oracle's values for their bytes.
 
@@ -132,7 +133,7 @@ def _only_picks_differ(t, empty_value):
     return got
 
 
-OFF_FORCE = [None, {"lps": 1, "unroll": 4, "mode": 4}, {"lps": 16, "unroll": 8, "mode": 3}]
+OFF_FORCE = [None, {"lps": 1, "unroll": 4, "mode": 4}, {"lps": 16, "unroll": 8, "mode": 3}, {"tile": 1}]
 
 
 @pytest.fixture(scope="module", params=OFF_FORCE, ids=lambda f: force_id(f or {}))
@@ -154,7 +155,7 @@ def test_offsets_mostly_empty_past_2p32(oeng, orc, sparse):
     torch.cuda.empty_cache()
 
 
-IPV4_FORCE = [None, {"lps": 1, "unroll": 4, "mode": 4}]
+IPV4_FORCE = [None, {"lps": 1, "unroll": 4, "mode": 4}, {"tile": 1}]
 
 
 @pytest.fixture(scope="module", params=IPV4_FORCE, ids=lambda f: force_id(f or {}))
