@@ -1152,7 +1152,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
 // short phase for a fraction of a long round's bytes; with the classes
 // split over the block's waves only one wave does (½-ACK
 // VERIFY of 1 M datagrams 135.5 -> 129.1 us, ¼-ACK 189.7 -> 177.8 us).
-template <int SPW>
+template <int SPW, int MODE_OP>  // MODE_OP: the batch's mode as a constant (only its code is built)
 __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
                                                           uint64_t stride, uint64_t dlen, uint64_t n, int mode,
                                                           uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
@@ -1200,7 +1200,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
       const bool mine = k < nshort;
       const uint32_t kc = mine ? k : 0u;
       const uint64_t ss = sst[kc][0], se = mine ? sst[kc][1] : ss;
-      ipv4_item<1, 4, false, 0>(dg, ss, se, sseg[kc], mine, 0u, mode, ip_ck, tcp_ck, status, zpad, zlast);
+      ipv4_item<1, 4, false, 0>(dg, ss, se, sseg[kc], mine, 0u, MODE_OP, ip_ck, tcp_ck, status, zpad, zlast);
     }
   const uint32_t g = lane >> 4, gl = lane & 15u;
   for (;;) {
@@ -1212,7 +1212,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
     const bool mine = k < nlong;
     const uint32_t kc = mine ? k : 0u;
     const uint64_t ls = lst[kc][0], le = mine ? lst[kc][1] : ls;
-    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[kc], mine, gl, mode, ip_ck, tcp_ck, status, zpad, zlast);
+    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[kc], mine, gl, MODE_OP, ip_ck, tcp_ck, status, zpad, zlast);
   }
 }
 
@@ -2599,12 +2599,16 @@ hipError_t launch_ipv4_twoclass(const SegSpec& sp, int mode, uint16_t* ip_ck, ui
   if (sp.list || blocks == 0 || blocks > kMaxGridBlocks) return hipErrorInvalidValue;
   uint8_t* const dg = const_cast<uint8_t*>(sp.bytes);
   const uint8_t* const z = static_cast<const uint8_t*>(sp.zero16);
-#define ICS_TWO(W)                                                                                        \
-  hipLaunchKernelGGL(k_ipv4_twoclass<W>, dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st, dg, sp.offsets,    \
+  if (mode < 0 || mode > 2) return hipErrorInvalidValue;
+#define ICS_TWO(W, M)                                                                                        \
+  hipLaunchKernelGGL((k_ipv4_twoclass<W, M>), dim3(uint32_t(blocks)), dim3(kBlock), lds_pad, st, dg, sp.offsets, \
                      sp.stride, sp.seg_len, sp.n, mode, ip_ck, tcp_ck, status, z, remap)
-  if (spw == 8) ICS_TWO(8);
-  else if (spw == 16) ICS_TWO(16);
-  else ICS_TWO(32);
+#define ICS_TWO_M(W) \
+  if (mode == 0) ICS_TWO(W, 0); else if (mode == 1) ICS_TWO(W, 1); else ICS_TWO(W, 2)
+  if (spw == 8) { ICS_TWO_M(8); }
+  else if (spw == 16) { ICS_TWO_M(16); }
+  else { ICS_TWO_M(32); }
+#undef ICS_TWO_M
 #undef ICS_TWO
   return hipGetLastError();
 }
