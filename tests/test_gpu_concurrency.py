@@ -9,7 +9,9 @@ inside the library and touch its shared state together:
 * the plan cache: more batch keys than slots, so slots are re-keyed (LRU)
   while plan kernels queued by other threads for the old key are still in
   flight — their words carry the old generation and must not be trusted;
-* the multi-batch grouping and the diagnostics counters.
+* the multi-batch grouping and the diagnostics counters;
+* round 4: the router step with its headers apart and a variable-length
+  batch that reaches the tile launch from its cached plan.
 
 Every thread's outputs after every round (each round starts from sentinel
 outputs) must equal what the same calls gave one at a time on one stream.
@@ -75,6 +77,10 @@ class Job:
         off3 = _offsets(rng.integers(0, 2000, 2000), lead=1)
         self.bv_off = _t(off3)
         self.bv_buf3 = _t(rng.integers(0, 256, int(off3[-1]) + 16, dtype=np.uint8))
+        # a variable-length batch above the tile threshold (the tile launch once its plan is cached)
+        self.toff = _offsets(40 + rng.integers(0, 1001, 140_000), lead=2)
+        self.tbuf = rng.integers(0, 256, int(self.toff[-1]) + 16, dtype=np.uint8)
+        self.d_toff, self.d_tbuf = _t(self.toff), _t(self.tbuf)
         dev = "cuda:0"
         self.outs = [torch.empty(70000, dtype=torch.int16, device=dev),
                      torch.empty(self.ndg, dtype=torch.int16, device=dev),
@@ -85,7 +91,10 @@ class Job:
                      torch.empty(self.nw, dtype=torch.int16, device=dev),
                      torch.empty(3000, dtype=torch.int16, device=dev),
                      torch.empty(5000, dtype=torch.int16, device=dev),
-                     torch.empty(2000, dtype=torch.int16, device=dev)]
+                     torch.empty(2000, dtype=torch.int16, device=dev),
+                     torch.empty(self.ndg * 20, dtype=torch.uint8, device=dev),  # router: forwarded headers
+                     torch.empty(self.ndg, dtype=torch.uint8, device=dev),
+                     torch.empty(140_000, dtype=torch.int16, device=dev)]
         self.want = None
 
     def reset(self, stream):
@@ -105,6 +114,8 @@ class Job:
         e.checksum_batchv([dict(data=self.bv_bufs[0], n=3000, stride=1500, seg_len=1500, out=o[7]),
                            dict(data=self.bv_bufs[1], n=5000, stride=64, seg_len=64, init=self.bv_init, out=o[8]),
                            dict(data=self.bv_buf3, n=2000, offsets=self.bv_off, out=o[9])], stream=stream)
+        e.router_ttl_headers(self.d_dg, n=self.ndg, offsets=self.d_dgoff, hdrs=o[10], status=o[11], stream=stream)
+        e.checksum_batch(self.d_tbuf, offsets=self.d_toff, out=o[12], stream=stream)
 
 
 def test_one_context_many_threads_and_streams(ceng, orc):
@@ -136,6 +147,7 @@ def test_one_context_many_threads_and_streams(ceng, orc):
     for i in range(0, 20000, 487):
         wip, wtcp, wst, _ = orc.ipv4_tcp(segs[i], 1)
         assert (int(ip.view(np.uint16)[i]), int(tcp.view(np.uint16)[i]), int(st[i])) == (wip, wtcp, wst), i
+    assert np.array_equal(j.want[12].cpu().numpy().view(np.uint16), orc.checksum_batch(j.tbuf, 140_000, offsets=j.toff))
     hd = j.want[4].cpu().numpy()
     for i in range(0, 5000, 311):
         want = _oracle_wire(orc, [b"\0" * 40 + wrap_pay[100 * i:100 * i + 100].tobytes()], wmsgs[i:i + 1])[0]
