@@ -1160,13 +1160,18 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
                                                           const uint8_t* __restrict__ zpad, uint32_t remap) {
   constexpr uint32_t kPer = (kBlock / 64) * SPW;
   __shared__ uint64_t lst[kPer][2], sst[kPer][2];  // the block's long / short datagrams' {start, end}
-  __shared__ uint32_t lseg[kPer], sseg[kPer];
+  __shared__ uint32_t lseg[kPer], sseg[kPer];       // ... and their index within the block
   __shared__ uint32_t cnt[3];  // long, short, long claimed
+  // the verdicts land in the block's rows here and leave as three coalesced
+  // rows at the end, instead of three 1-2-byte stores per datagram in claim order
+  __shared__ uint16_t o_ip[kPer], o_tcp[kPer];
+  __shared__ uint8_t o_st[kPer];
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
   if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
   __syncthreads();
-  const uint64_t seg = (uint64_t(block_order(remap)) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
+  const uint64_t b0 = uint64_t(block_order(remap)) * kPer;  // the block's datagrams [b0, b0 + kPer)
+  const uint64_t seg = b0 + wv * SPW + (lane < SPW ? lane : 0u);
   const bool valid = seg < n && lane < SPW;
   uint64_t s, e;
   seg_bounds(offsets, stride, dlen, seg < n ? seg : n - 1, s, e);
@@ -1185,12 +1190,12 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
   if (valid && !is_short) {
     lst[lbase + lr][0] = s;
     lst[lbase + lr][1] = e;
-    lseg[lbase + lr] = uint32_t(seg);
+    lseg[lbase + lr] = uint32_t(seg - b0);
   }
   if (valid && is_short) {
     sst[sbase + sr][0] = s;
     sst[sbase + sr][1] = e;
-    sseg[sbase + sr] = uint32_t(seg);
+    sseg[sbase + sr] = uint32_t(seg - b0);
   }
   __syncthreads();
   const uint32_t nlong = cnt[0], nshort = cnt[1];
@@ -1200,7 +1205,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
       const bool mine = k < nshort;
       const uint32_t kc = mine ? k : 0u;
       const uint64_t ss = sst[kc][0], se = mine ? sst[kc][1] : ss;
-      ipv4_item<1, 4, false, 0>(dg, ss, se, sseg[kc], mine, 0u, MODE_OP, ip_ck, tcp_ck, status, zpad, zlast);
+      ipv4_item<1, 4, false, 0>(dg, ss, se, sseg[kc], mine, 0u, MODE_OP, o_ip, o_tcp, o_st, zpad, zlast);
     }
   const uint32_t g = lane >> 4, gl = lane & 15u;
   for (;;) {
@@ -1212,7 +1217,14 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
     const bool mine = k < nlong;
     const uint32_t kc = mine ? k : 0u;
     const uint64_t ls = lst[kc][0], le = mine ? lst[kc][1] : ls;
-    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[kc], mine, gl, MODE_OP, ip_ck, tcp_ck, status, zpad, zlast);
+    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[kc], mine, gl, MODE_OP, o_ip, o_tcp, o_st, zpad, zlast);
+  }
+  __syncthreads();
+  const uint64_t i = b0 + threadIdx.x;  // every datagram of the block was verified: its row is complete
+  if (threadIdx.x < kPer && i < n) {
+    if (ip_ck) ip_ck[i] = o_ip[threadIdx.x];
+    if (tcp_ck) tcp_ck[i] = o_tcp[threadIdx.x];
+    if (status) status[i] = o_st[threadIdx.x];
   }
 }
 
