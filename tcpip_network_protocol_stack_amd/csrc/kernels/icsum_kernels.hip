@@ -664,11 +664,13 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
   __shared__ uint64_t lst[kPer][2], sst[kPer][2];  // the block's long / short segments' {start, end}
   __shared__ uint32_t lseg[kPer], sseg[kPer];
   __shared__ uint32_t cnt[3];  // long, short, long claimed
+  __shared__ uint32_t o_sum[kPer];  // the block's sums, written out as one coalesced row at the end
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
   __syncthreads();
   const Work w{n, nullptr};
-  const uint64_t gi = (uint64_t(block_order(remap)) * (kBlock / 64) + wv) * SPW + (lane < SPW ? lane : 0u);
+  const uint64_t bb = uint64_t(block_order(remap)) * kPer;  // the block's segments [bb, bb + kPer) (no list)
+  const uint64_t gi = bb + wv * SPW + (lane < SPW ? lane : 0u);
   uint64_t seg, s, e;
   src_locate(src, w, gi, n, seg, s, e);
   const bool valid = gi < n && lane < SPW;
@@ -697,12 +699,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
   }
   __syncthreads();
   const uint32_t nlong = cnt[0], nshort = cnt[1];
-  auto store = [&](uint64_t sg, uint32_t sum) {
-    if (OUT == 0)
-      static_cast<uint16_t*>(out)[sg] = fold_value(sum);
-    else
-      static_cast<uint32_t*>(out)[sg] = sum;
-  };
+  auto store = [&](uint64_t sg, uint32_t sum) { o_sum[sg - bb] = sum; };
   if (wv == 0)
     for (uint32_t r0 = 0; r0 < nshort; r0 += 64) {  // uniform
       const uint32_t k = r0 + lane;
@@ -750,6 +747,14 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
     range_sums_line_primed<LONG_LPS, 8, true>(bytes, ls, le, gl, ev, od);
     const uint32_t tot = group_sum<LONG_LPS>(combine_roles(ev, od, sw));
     if (mine && gl == LONG_LPS - 1) store(lsg, i0 + tot);
+  }
+  __syncthreads();
+  const uint64_t i = bb + threadIdx.x;  // every segment of the block was summed: its row is complete
+  if (threadIdx.x < kPer && i < n) {
+    if (OUT == 0)
+      static_cast<uint16_t*>(out)[i] = fold_value(o_sum[threadIdx.x]);
+    else
+      static_cast<uint32_t*>(out)[i] = o_sum[threadIdx.x];
   }
 }
 
