@@ -922,6 +922,34 @@ __device__ __forceinline__ void load_tcp_fields(const uint8_t* t, const uint32_t
   tf1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
 }
 
+// The same dwords unaligned (the stashed form, VRec): the six aligned dwords
+// holding header bytes 0..19 at p and the three holding TCP bytes 12..19 at
+// t, with their byte shifts.
+__device__ __forceinline__ void load_hdr_raw(const uint8_t* p, const uint32_t* last, uint32_t* d, uint32_t& sh) {
+  sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(p - sh);
+#ifdef ICSUM_BOUNDS_CHECK
+  if (q + 4 > last) bounds_fail(kBoundsHeader, reinterpret_cast<unsigned long long>(q + 4));
+#endif
+#pragma unroll
+  for (int k = 0; k < 5; ++k) d[k] = q[k];
+  d[5] = *(q + 5 < last ? q + 5 : last);
+}
+
+__device__ __forceinline__ uint32_t tcp_shift(const uint8_t* t) {
+  return uint32_t(reinterpret_cast<uintptr_t>(t + 12) & 3u);
+}
+
+// dword k (0..2) of the TCP-field window of the segment at t (the third
+// clamped to `last`)
+__device__ __forceinline__ uint32_t load_tcp_raw(const uint8_t* t, const uint32_t* last, uint32_t k) {
+  const uint32_t* q = reinterpret_cast<const uint32_t*>(t + 12 - tcp_shift(t));
+#ifdef ICSUM_BOUNDS_CHECK
+  if (q + 1 > last) bounds_fail(kBoundsHeader, reinterpret_cast<unsigned long long>(q + 1));
+#endif
+  return *(q + k < last ? q + k : last);
+}
+
 // The header dwords and the TCP fields with ONE load instruction for a lane
 // group of >= 16 lanes: lane k (< 9) of the group loads header dword k (k <
 // 6: the aligned window at p, the sixth clamped to `last`) or TCP-field dword
@@ -1016,51 +1044,93 @@ __device__ __forceinline__ uint32_t ipv4_pseudo(const Hdr& h) {
 // compute_checksum with the checksum field counted as 0 (:109-118), the
 // status bits of include/icsum.h, and PATCH's two big-endian stores.
 // hdr false (a datagram under 20 bytes): zeros.
+// The verdict from the header, the TCP fields, the TCP part's sum and its
+// length rem = e - t0 (b16: the TCP part's byte 16 when rem == 17, the
+// checksum field's only byte there; COMPUTE / PATCH only).
+struct Verdict {
+  uint32_t ipc, tcv, st;
+};
+__device__ __forceinline__ Verdict ipv4_verdict(bool hdr, const Hdr& h, uint32_t tf0, uint32_t tf1, uint32_t tot,
+                                                uint64_t rem, uint32_t b16, int mode) {
+  Verdict v{0, 0, 0};
+  if (hdr) {
+    const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu;
+    const bool hdr_ok = ver == 4 && hlen >= 5;  // ipv4_header.cpp:32-41
+    v.ipc = fold_value(ipv4_header_sum(h));
+    const uint32_t pseudo = ipv4_pseudo(h);
+    if (h.byte(9) == 6) v.st |= 0x08;  // proto TCP
+    if (rem >= 20 && ((tf0 & 0xffu) >> 4) >= 5) v.st |= 0x04;  // tcp_segment.cpp:25-65
+    if (mode == 1) {
+      v.tcv = fold_value(pseudo + tot);  // tcp_segment.cpp:11-18
+      if (hdr_ok && v.ipc == h.be16(10)) v.st |= 0x01;  // ipv4_header.cpp:53-58
+      if (v.tcv == 0) v.st |= 0x02;
+    } else {
+      // tcp_segment.cpp:143: the checksum field counts as 0
+      uint32_t sum = pseudo + tot;
+      if (rem > 16) sum -= (rem >= 18 ? tf1 & 0xffu : b16) << 8;
+      if (rem > 17) sum -= (tf1 >> 8) & 0xffu;
+      v.tcv = fold_value(sum);
+      if (hdr_ok) v.st |= 0x01;
+      if (rem >= 18) v.st |= 0x02;
+    }
+  }
+  return v;
+}
+
 __device__ __forceinline__ void ipv4_result(uint8_t* __restrict__ dg, uint64_t s, uint64_t e, uint64_t t0, bool hdr,
                                             const Hdr& h, uint32_t tf0, uint32_t tf1, uint32_t tot, int mode,
                                             uint64_t seg, uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
                                             uint8_t* __restrict__ status) {
-  uint16_t ipc = 0, tcv = 0;
-  uint8_t st = 0;
-  if (hdr) {
-    const uint32_t ver = h.byte(0) >> 4, hlen = h.byte(0) & 0x0fu;
-    const bool hdr_ok = ver == 4 && hlen >= 5;  // ipv4_header.cpp:32-41
-    ipc = fold_value(ipv4_header_sum(h));
-    const uint32_t pseudo = ipv4_pseudo(h);
-    const uint64_t rem = e - t0;
-    if (h.byte(9) == 6) st |= 0x08;  // proto TCP
-    if (rem >= 20 && ((tf0 & 0xffu) >> 4) >= 5) st |= 0x04;  // tcp_segment.cpp:25-65
-    if (mode == 1) {
-      tcv = fold_value(pseudo + tot);  // tcp_segment.cpp:11-18
-      if (hdr_ok && ipc == h.be16(10)) st |= 0x01;  // ipv4_header.cpp:53-58
-      if (tcv == 0) st |= 0x02;
-    } else {
-      // tcp_segment.cpp:143: the checksum field counts as 0
-      uint32_t sum = pseudo + tot;
-      if (rem > 16) sum -= (rem >= 18 ? tf1 & 0xffu : uint32_t(dg[t0 + 16])) << 8;
-      if (rem > 17) sum -= (tf1 >> 8) & 0xffu;
-      tcv = fold_value(sum);
-      if (hdr_ok) st |= 0x01;
-      if (rem >= 18) st |= 0x02;
-      if (mode == 2) {
-        store_be16(dg + s + 10, ipc);
-        if (rem >= 18) store_be16(dg + t0 + 16, tcv);
-      }
-    }
+  const uint64_t rem = e - t0;
+  const uint32_t b16 = (hdr && mode != 1 && rem == 17) ? uint32_t(dg[t0 + 16]) : 0u;
+  const Verdict v = ipv4_verdict(hdr, h, tf0, tf1, tot, rem, b16, mode);
+  if (hdr && mode == 2) {
+    store_be16(dg + s + 10, v.ipc);
+    if (rem >= 18) store_be16(dg + t0 + 16, v.tcv);
   }
-  if (ip_ck) ip_ck[seg] = ipc;
-  if (tcp_ck) tcp_ck[seg] = tcv;
-  if (status) status[seg] = st;
+  if (ip_ck) ip_ck[seg] = uint16_t(v.ipc);
+  if (tcp_ck) tcp_ck[seg] = uint16_t(v.tcv);
+  if (status) status[seg] = uint8_t(v.st);
+}
+
+// What ipv4_result needs, kept per datagram by k_ipv4_twoclass COMPUTE /
+// VERIFY, which computes the block's verdicts at its end one datagram per
+// lane instead of in one lane of each group per claim: the nine dwords as
+// loaded (d[0..5]: the header window, shift sh; d[6..8]: the TCP-field window,
+// shift tsh; lane k < 9 of a 16-lane group writes d[k] — no broadcast, no
+// alignment in the claim), the TCP part's sum and the rest packed in meta:
+// hdr | sh << 2 | tsh << 4 | b16 << 8 | min(rem, 0xffff) << 16 (rem = e - t0;
+// the verdict only compares it with 16..20).  44 bytes: an odd dword stride,
+// conflict-free rows at the end.
+struct VRec {
+  uint32_t d[9], tot, meta;
+};
+
+__device__ __forceinline__ uint32_t vrec_meta(bool hdr, uint32_t sh, uint32_t tsh, uint32_t b16, uint64_t rem) {
+  return uint32_t(hdr) | (sh << 2) | (tsh << 4) | (b16 << 8) | (uint32_t(rem < 0xffffu ? rem : 0xffffu) << 16);
+}
+
+__device__ __forceinline__ Verdict vrec_verdict(const VRec& r, int mode) {
+  const uint32_t sh = (r.meta >> 2) & 3u, tsh = (r.meta >> 4) & 3u;
+  Hdr h;
+#pragma unroll
+  for (int j = 0; j < 5; ++j) h.w[j] = __builtin_amdgcn_alignbyte(r.d[j + 1], r.d[j], sh);
+  const uint32_t tf0 = __builtin_amdgcn_alignbyte(r.d[7], r.d[6], tsh);
+  const uint32_t tf1 = __builtin_amdgcn_alignbyte(r.d[8], r.d[7], tsh);
+  return ipv4_verdict((r.meta & 1u) != 0, h, tf0, tf1, r.tot, r.meta >> 16, (r.meta >> 8) & 0xffu, mode);
 }
 
 // --------------------------------------------- fused IPv4 + TCP ----------
 // One datagram [s, e) per group of LPS lanes (every lane of the wave calls it:
 // group sums and the wave-uniform re-sum below); `valid` false: an idle group.
-template <int LPS, int UNROLL, bool NT, int MODE>
+// STASH: the datagram's VRec goes to stash[seg] instead of its results to
+// the output rows (COMPUTE / VERIFY only).
+template <int LPS, int UNROLL, bool NT, int MODE, bool STASH = false>
 __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, uint64_t e, uint64_t seg, bool valid,
                                           uint32_t lane, int mode, uint16_t* __restrict__ ip_ck,
                                           uint16_t* __restrict__ tcp_ck, uint8_t* __restrict__ status,
-                                          const uint8_t* __restrict__ zpad, const uint32_t* zlast) {
+                                          const uint8_t* __restrict__ zpad, const uint32_t* zlast,
+                                          VRec* stash = nullptr) {
   const bool hdr = e - s >= 20;
   // Speculate the usual header length (hlen = 5): the IPv4 header dwords,
   // the TCP fields the verdict needs (data offset, checksum) and the TCP
@@ -1074,25 +1144,53 @@ __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, 
   uint32_t tf0 = 0, tf1 = 0;  // TCP bytes 12..15 and 16..19 (little-endian)
   const bool tcpf = hdr && e - t0 >= 18;
   GroupHdr gh{};
+  [[maybe_unused]] uint32_t raw[9], sh = 0;  // STASH, one lane per datagram
   if constexpr (LPS >= 16) {
     gh = group_hdr_load<LPS>(hdr ? dg + s : zpad, last, tcpf ? dg + t0 : zpad, tcpf ? last : zlast);
+  } else if constexpr (STASH) {
+    load_hdr_raw(hdr ? dg + s : zpad, last, raw, sh);
+    gh.tsh = tcp_shift(tcpf ? dg + t0 : zpad);
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) raw[6 + k] = load_tcp_raw(tcpf ? dg + t0 : zpad, tcpf ? last : zlast, k);
   } else {
     h = load_hdr(hdr ? dg + s : zpad, last);
     load_tcp_fields(tcpf ? dg + t0 : zpad, tcpf ? last : zlast, tf0, tf1);
   }
   uint32_t ev = 0, od = 0;
   seg_sums<LPS, UNROLL, NT, MODE>(dg, t0, e, lane, ev, od);
-  if constexpr (LPS >= 16) group_hdr_take<LPS>(gh, h, tf0, tf1);
+  uint32_t b0;  // header byte 0 (version, hlen)
+  if constexpr (STASH) {
+    if constexpr (LPS >= 16) {
+      sh = gh.sh;
+      b0 = (__builtin_amdgcn_update_dpp(0u, gh.v, 0x150, 0xF, 0xF, false) >> (8 * sh)) & 0xffu;  // row_newbcast:0
+    } else {
+      b0 = (raw[0] >> (8 * sh)) & 0xffu;
+    }
+  } else {
+    if constexpr (LPS >= 16) group_hdr_take<LPS>(gh, h, tf0, tf1);
+    b0 = h.byte(0);
+  }
   bool redo = false;
   if (hdr) {
-    uint64_t off = 4u * (h.byte(0) & 0x0fu);  // options skipped (ipv4_header.cpp:50)
+    uint64_t off = 4u * (b0 & 0x0fu);  // options skipped (ipv4_header.cpp:50)
     if (off < 20) off = 20;
     if (off > e - s) off = e - s;
     redo = s + off != t0;
     t0 = s + off;
     if (redo) {
-      tf0 = tf1 = 0;
-      if (e - t0 >= 18) load_tcp_fields(dg + t0, last, tf0, tf1);
+      const bool f = e - t0 >= 18;
+      if constexpr (STASH) {
+        gh.tsh = tcp_shift(dg + t0);
+        if constexpr (LPS >= 16) {
+          if (lane >= 6 && lane < 9) gh.v = f ? load_tcp_raw(dg + t0, last, lane - 6) : 0u;
+        } else {
+#pragma unroll
+          for (uint32_t k = 0; k < 3; ++k) raw[6 + k] = f ? load_tcp_raw(dg + t0, last, k) : 0u;
+        }
+      } else {
+        tf0 = tf1 = 0;
+        if (f) load_tcp_fields(dg + t0, last, tf0, tf1);
+      }
     }
   }
   if (__any(redo)) {  // wave-uniform
@@ -1107,7 +1205,25 @@ __device__ __forceinline__ void ipv4_item(uint8_t* __restrict__ dg, uint64_t s, 
     od -= oo;
   }
   const uint32_t tot = group_sum<LPS>(combine_roles(ev, od, uint32_t(t0) & 1u));
-  if (valid && lane == LPS - 1) ipv4_result(dg, s, e, t0, hdr, h, tf0, tf1, tot, mode, seg, ip_ck, tcp_ck, status);
+  if constexpr (STASH) {  // the verdict later, from stash[seg]
+    if (valid) {
+      VRec& r = stash[seg];
+      if constexpr (LPS >= 16) {
+        if (lane < 9) r.d[lane] = gh.v;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 9; ++k) r.d[k] = raw[k];
+      }
+      if (lane == LPS - 1) {
+        const uint64_t rem = e - t0;
+        const uint32_t b16 = (hdr && mode != 1 && rem == 17) ? uint32_t(dg[t0 + 16]) : 0u;
+        r.tot = tot;
+        r.meta = vrec_meta(hdr, sh, gh.tsh, b16, rem);
+      }
+    }
+  } else if (valid && lane == LPS - 1) {
+    ipv4_result(dg, s, e, t0, hdr, h, tf0, tf1, tot, mode, seg, ip_ck, tcp_ck, status);
+  }
 }
 
 // datagrams [blk * groups, ...) striding by nblk blocks (block blk of nblk:
@@ -1159,18 +1275,27 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_tcp(uint8_t* __restrict__ dg,
 // VERIFY of 1 M datagrams 135.5 -> 129.1 us, ¼-ACK 189.7 -> 177.8 us).
 template <int SPW, int MODE_OP>  // MODE_OP: the batch's mode as a constant (only its code is built)
 __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ dg, const uint64_t* __restrict__ offsets,
-                                                          uint64_t stride, uint64_t dlen, uint64_t n, int mode,
-                                                          uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
-                                                          uint8_t* __restrict__ status,
+                                                          uint64_t stride, uint64_t dlen, uint64_t n,
+                                                          int /*mode: MODE_OP*/, uint16_t* __restrict__ ip_ck,
+                                                          uint16_t* __restrict__ tcp_ck, uint8_t* __restrict__ status,
                                                           const uint8_t* __restrict__ zpad, uint32_t remap) {
   constexpr uint32_t kPer = (kBlock / 64) * SPW;
   __shared__ uint64_t lst[kPer][2], sst[kPer][2];  // the block's long / short datagrams' {start, end}
   __shared__ uint32_t lseg[kPer], sseg[kPer];       // ... and their index within the block
   __shared__ uint32_t cnt[3];  // long, short, long claimed
-  // the verdicts land in the block's rows here and leave as three coalesced
-  // rows at the end, instead of three 1-2-byte stores per datagram in claim order
-  __shared__ uint16_t o_ip[kPer], o_tcp[kPer];
-  __shared__ uint8_t o_st[kPer];
+  // COMPUTE / VERIFY: each datagram's header and TCP-field dwords as loaded
+  // and its sum land in the block's records (VRec), and the block computes the
+  // verdicts at its end, one datagram per lane, and writes them as three
+  // coalesced rows: no header broadcast, alignment or verdict in the claims,
+  // no 1-2-byte stores in claim order (stack VERIFY of 256 Ki datagrams
+  // 36.22 -> 35.72 us back to back; profiles/r4_ab_twoclass_block_verdicts.jsonl).
+  // PATCH stages the outputs only (its stores into the datagrams stay in the
+  // claim).
+  constexpr bool kStash = MODE_OP != 2;
+  __shared__ VRec recs[kStash ? kPer : 1];
+  __shared__ uint16_t o_ip[kStash ? 1 : kPer], o_tcp[kStash ? 1 : kPer];
+  __shared__ uint8_t o_st[kStash ? 1 : kPer];
+  VRec* const stash = kStash ? recs : nullptr;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
   if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
@@ -1210,7 +1335,7 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
       const bool mine = k < nshort;
       const uint32_t kc = mine ? k : 0u;
       const uint64_t ss = sst[kc][0], se = mine ? sst[kc][1] : ss;
-      ipv4_item<1, 4, false, 0>(dg, ss, se, sseg[kc], mine, 0u, MODE_OP, o_ip, o_tcp, o_st, zpad, zlast);
+      ipv4_item<1, 4, false, 0, kStash>(dg, ss, se, sseg[kc], mine, 0u, MODE_OP, o_ip, o_tcp, o_st, zpad, zlast, stash);
     }
   const uint32_t g = lane >> 4, gl = lane & 15u;
   for (;;) {
@@ -1222,14 +1347,21 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
     const bool mine = k < nlong;
     const uint32_t kc = mine ? k : 0u;
     const uint64_t ls = lst[kc][0], le = mine ? lst[kc][1] : ls;
-    ipv4_item<16, 8, true, 3>(dg, ls, le, lseg[kc], mine, gl, MODE_OP, o_ip, o_tcp, o_st, zpad, zlast);
+    ipv4_item<16, 8, true, 3, kStash>(dg, ls, le, lseg[kc], mine, gl, MODE_OP, o_ip, o_tcp, o_st, zpad, zlast, stash);
   }
   __syncthreads();
-  const uint64_t i = b0 + threadIdx.x;  // every datagram of the block was verified: its row is complete
+  const uint64_t i = b0 + threadIdx.x;  // every datagram of the block was summed: its row is complete
   if (threadIdx.x < kPer && i < n) {
-    if (ip_ck) ip_ck[i] = o_ip[threadIdx.x];
-    if (tcp_ck) tcp_ck[i] = o_tcp[threadIdx.x];
-    if (status) status[i] = o_st[threadIdx.x];
+    uint32_t ipc, tcv, st;
+    if constexpr (kStash) {
+      const Verdict v = vrec_verdict(recs[threadIdx.x], MODE_OP);
+      ipc = v.ipc, tcv = v.tcv, st = v.st;
+    } else {
+      ipc = o_ip[threadIdx.x], tcv = o_tcp[threadIdx.x], st = o_st[threadIdx.x];
+    }
+    if (ip_ck) ip_ck[i] = uint16_t(ipc);
+    if (tcp_ck) tcp_ck[i] = uint16_t(tcv);
+    if (status) status[i] = uint8_t(st);
   }
 }
 
