@@ -53,6 +53,11 @@ int ensure_staging(ics_ctx* ctx) {
   if (!host_pinned(ctx->h_flag).kernel) ctx->zero_copy_max = 0;
   ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_ticket), ics_ctx::kMaxSlots * 64));
   ICS_HIP(hipMemset(ctx->d_ticket, 0, ics_ctx::kMaxSlots * 64));
+  // The slots' streams are non-blocking: they do not wait for the null
+  // stream's memset, and a first launch that read the tickets before it landed
+  // (the allocation reusing freed, non-zero memory) would never reach its
+  // last-block count — the call failing with its completion word unwritten.
+  ICS_HIP(hipDeviceSynchronize());
   ctx->staged = true;
   return ICS_OK;
 }

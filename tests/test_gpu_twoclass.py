@@ -181,16 +181,18 @@ def test_ipv4_twoclass_vs_oracle(two_engine, orc, mix):
     n = 20_000
     ack = lambda p: np.where(rng.random(n) < p, 40, 1460) + rng.integers(0, 4, n)  # noqa: E731
     lens = {"bimodal": lambda: ack(0.5), "ackheavy": lambda: ack(0.75),
-            "tricky": lambda: rng.choice([0, 7, 19, 20, 39, 40, 41, 63, 64, 65, 100, 1460, 1500], n)}[mix]()
+            "tricky": lambda: rng.choice([0, 7, 19, 20, 36, 37, 38, 39, 40, 41, 42, 63, 64, 65, 100, 1460, 1500],
+                                         n)}[mix]()
     off = np.zeros(n + 1, dtype=np.uint64)
     off[1:] = np.cumsum(lens)
     off += 3
     buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
     s, ln = off[:-1].astype(np.int64), np.diff(off).astype(np.int64)
-    ok = ln >= 40
+    ok = ln >= (36 if mix == "tricky" else 40)  # 36..39: TCP parts of 16..19 bytes (the checksum field cut)
     s, ln = s[ok], ln[ok]
     buf[s], buf[s + 2], buf[s + 3] = 0x45, (ln >> 8).astype(np.uint8), (ln & 255).astype(np.uint8)
-    buf[s + 6], buf[s + 8], buf[s + 9], buf[s + 32] = 0x40, 64, 6, 0x50
+    buf[s + 6], buf[s + 8], buf[s + 9] = 0x40, 64, 6
+    buf[s[ln > 32] + 32] = 0x50
     if mix == "tricky":
         buf[s[::7]] = 0x46  # options (hlen 6)
         buf[s[::11] + 25] ^= 0x10  # corrupted TCP bytes
