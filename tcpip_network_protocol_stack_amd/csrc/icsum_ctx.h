@@ -268,6 +268,7 @@ int apply_force(ics_ctx* ctx, const char* spec);
 icsum::Geometry geometry_for(const ics_ctx* ctx, uint64_t avg_len);
 // The fused IPv4 kernels' variant of a checksum geometry.
 icsum::Geometry ipv4_geometry(icsum::Geometry g);
+icsum::Geometry ipv4_fixed_geometry(const ics_ctx* ctx, icsum::Geometry g, uint64_t len);
 // Does the device wrap use two passes for this call?
 bool wrap_two_pass(const ics_ctx* ctx, bool headers_apart, uint64_t n);
 // a1-a4: checksum (out_kind 0: folded u16) or raw sums (1: u32) of a batch.

@@ -58,6 +58,18 @@ icsum::Geometry ipv4_geometry(icsum::Geometry g) {
   return g;
 }
 
+// Fixed-length datagrams of at most 1664 bytes on the 16 x 8 line grid: 7
+// loads per lane still cover the span (<= 111 chunks with the line's head) in
+// one pass, and the fused kernel drops from 82 to 76 VGPRs (5 -> 6 waves /
+// SIMD): config 2 COMPUTE / PATCH / VERIFY 16.88 / 20.88 / 16.73 -> 16.74 /
+// 20.68 / 16.58 us (profiles/r4_ab_ipv4_unroll7.jsonl).  The plain checksum
+// keeps 8 (already 8 waves; 1 M x 1500 B 209.2 vs 211.2 us at 7).
+icsum::Geometry ipv4_fixed_geometry(const ics_ctx* ctx, icsum::Geometry g, uint64_t len) {
+  const bool forced = ctx->force_lps || ctx->force_unroll || ctx->force_mode >= 0 || ctx->force_segs;
+  if (!forced && g.lps == 16 && g.unroll == 8 && g.mode == 3 && len > 0 && len <= 1664) g.unroll = 7;
+  return g;
+}
+
 namespace {
 
 // average segment length for the geometry choice without reading d_offsets
@@ -337,6 +349,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   const icsum::Geometry lane1{1, 4, false, 0, 1};
   const icsum::Geometry base = geometry_for(ctx, d_offsets ? 1500 : sp.seg_len);
   icsum::Geometry g = base.mode == icsum::kModeTiny ? lane1 : ipv4_geometry(base);
+  if (!d_offsets) g = ipv4_fixed_geometry(ctx, g, sp.seg_len);
   // a receive batch of mostly short datagrams (pure ACKs: 40 bytes) leaves
   // most of a 16-lane group idle: from 16 Ki datagrams up the geometry
   // follows the plan the device reported for the same offsets buffer last

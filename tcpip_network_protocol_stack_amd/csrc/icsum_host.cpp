@@ -398,7 +398,8 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
       // fields are written into the caller's bytes on the host at retire,
       // instead of copying every patched byte back over PCIe
       const int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;
-      ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, ipv4_geometry(g), 0, st));
+      const icsum::Geometry gi = h_offsets ? ipv4_geometry(g) : ipv4_fixed_geometry(ctx, ipv4_geometry(g), seg_len);
+      ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, gi, 0, st));
       ICS_HIP(d2h(ctx->h_out[slot], ctx->d_out[slot], m * 5));
     }
     if (!zc) ICS_HIP(hipEventRecord(ctx->ev[slot], st));

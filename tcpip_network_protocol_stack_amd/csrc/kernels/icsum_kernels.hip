@@ -2580,8 +2580,8 @@ Geometry pick_geometry(uint64_t avg_len) {
 // (mode 0, default-policy loads) and the 8-lane groups of ACK + MTU mixes
 #define ICS_GEOMETRIES(X)                                                                     \
   X(1, 4, false, 0) X(4, 1, true, 2) X(4, 2, true, 2) X(8, 2, true, 2) X(8, 8, true, 3)      \
-  X(16, 4, true, 3) X(16, 5, true, 3) X(16, 6, true, 3) X(16, 8, true, 3) X(32, 8, true, 3) \
-  X(64, 8, true, 3)
+  X(16, 4, true, 3) X(16, 5, true, 3) X(16, 6, true, 3) X(16, 7, true, 3) X(16, 8, true, 3) \
+  X(32, 8, true, 3) X(64, 8, true, 3)
 
 // small-segment kernel instantiations (LPS, UNROLL, SEGS); Geometry::segs > 1
 #define ICS_SMALL_GEOMETRIES(X) X(4, 1, 2) X(4, 2, 2) X(8, 2, 2)

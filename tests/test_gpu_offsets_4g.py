@@ -215,8 +215,8 @@ def _place(t, buf, rel, bnd, how):
 
 IPV4_FORCE = [None, {"twoclass": 32}, {"lps": 1, "unroll": 4, "mode": 4}, {"lps": 4, "unroll": 1, "mode": 2},
               {"lps": 8, "unroll": 2, "mode": 2}, {"lps": 8, "unroll": 8, "mode": 3},
-              {"lps": 16, "unroll": 8, "mode": 3}, {"lps": 64, "unroll": 8, "mode": 3},
-              {"tile": 1}, {"tile": 1, "tile_segs": 7}]
+              {"lps": 16, "unroll": 7, "mode": 3}, {"lps": 16, "unroll": 8, "mode": 3},
+              {"lps": 64, "unroll": 8, "mode": 3}, {"tile": 1}, {"tile": 1, "tile_segs": 7}]
 IPV4_MIX = {"ack": [40, 41, 42, 43], "bimodal": [40, 41, 1460, 1500],
             "tricky": [0, 7, 19, 20, 39, 40, 41, 63, 64, 65, 100, 1460, 1500, 9000]}
 

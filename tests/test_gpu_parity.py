@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 # keep in sync with ICS_GEOMETRIES in icsum_kernels.hip (MODE 2: 16-byte grid
 # fully masked, 3: 128-byte-line grid with primed boundary loads) — plus MODE
 # 4, k_checksum_tiny (one lane per segment)
-GEOMETRIES = [(4, 1, 2), (4, 2, 2), (8, 2, 2), (8, 8, 3), (16, 4, 3), (16, 5, 3), (16, 6, 3), (16, 8, 3),
+GEOMETRIES = [(4, 1, 2), (4, 2, 2), (8, 2, 2), (8, 8, 3), (16, 4, 3), (16, 5, 3), (16, 6, 3), (16, 7, 3), (16, 8, 3),
               (32, 8, 3), (64, 8, 3), (1, 4, 4)]
 # small-segment kernel (k_checksum_small): (LPS, UNROLL, MODE unused, SEGS) — ICS_SMALL_GEOMETRIES
 SMALL_GEOMETRIES = [(4, 1, 0, 2), (4, 2, 0, 2), (8, 2, 0, 2)]
@@ -522,6 +522,8 @@ def test_config2_ipv4_full_size(engine):
     engine.ipv4_tcp_headers(d, n, L, L, seed)
     ip, tcp, st = engine.ipv4_tcp_batch(d, 0, n=n, stride=L, dgram_len=L)
     assert _sha(_u16(ip)) == g["ipck_sha256"] and _sha(_u16(tcp)) == g["tcpck_sha256"]
+    info = engine.dispatch_info()  # fixed-length MTU datagrams: 7 loads per lane (ipv4_fixed_geometry)
+    assert (info["kernel"], info["lps"], info["unroll"]) == ("ipv4", 16, 7), info
     engine.ipv4_tcp_batch(d, 2, n=n, stride=L, dgram_len=L)
     assert _sha(d.cpu().numpy()) == g["patched_sha256"]
     _, _, st = engine.ipv4_tcp_batch(d, 1, n=n, stride=L, dgram_len=L)
