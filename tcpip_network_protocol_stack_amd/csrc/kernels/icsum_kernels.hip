@@ -744,7 +744,10 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
     const uint32_t i0 = init[lsg * init_step];
     const uint32_t sw = (uint32_t(ls) ^ uint32_t(odd[lsg * odd_step])) & 1u;
     uint32_t ev = 0, od = 0;
-    range_sums_line_primed<LONG_LPS, 8, true>(bytes, ls, le, gl, ev, od);
+    // 7 loads per lane: an MSS segment's line-grid span (<= 100 chunks) in one
+    // pass of 112 chunks, fewer clamped slot loads than 8 (2 M bimodal
+    // 226.6 -> 221.1 us, profiles/r4_ab_csum_twoclass_unroll7.jsonl)
+    range_sums_line_primed<LONG_LPS, 7, true>(bytes, ls, le, gl, ev, od);
     const uint32_t tot = group_sum<LONG_LPS>(combine_roles(ev, od, sw));
     if (mine && gl == LONG_LPS - 1) store(lsg, i0 + tot);
   }
