@@ -1040,16 +1040,14 @@ __device__ __forceinline__ uint32_t ipv4_pseudo(const Hdr& h) {
 }
 
 // The per-datagram results of the fused kernels from its header fields, the
-// TCP bytes 12..19 (tf0 / tf1, read at t0 + 12) and tot = the sum of the TCP
-// part [t0, e) with roles relative to t0: IPv4Header::compute_checksum and
-// the parse checks (ipv4_header.cpp:9-59, 113-123), pseudo_checksum
-// (:103-110), TCPSegment::parse's verify (tcp_segment.cpp:11-18) or
-// compute_checksum with the checksum field counted as 0 (:109-118), the
-// status bits of include/icsum.h, and PATCH's two big-endian stores.
-// hdr false (a datagram under 20 bytes): zeros.
-// The verdict from the header, the TCP fields, the TCP part's sum and its
-// length rem = e - t0 (b16: the TCP part's byte 16 when rem == 17, the
-// checksum field's only byte there; COMPUTE / PATCH only).
+// TCP bytes 12..19 (tf0 / tf1, read at t0 + 12), tot = the sum of the TCP
+// part [t0, e) with roles relative to t0 and its length rem = e - t0 (b16:
+// the TCP part's byte 16 when rem == 17, the checksum field's only byte
+// there; COMPUTE / PATCH only): IPv4Header::compute_checksum and the parse
+// checks (ipv4_header.cpp:9-59, 113-123), pseudo_checksum (:103-110),
+// TCPSegment::parse's verify (tcp_segment.cpp:11-18) or compute_checksum with
+// the checksum field counted as 0 (:109-118), and the status bits of
+// include/icsum.h.  hdr false (a datagram under 20 bytes): zeros.
 struct Verdict {
   uint32_t ipc, tcv, st;
 };
@@ -1080,6 +1078,7 @@ __device__ __forceinline__ Verdict ipv4_verdict(bool hdr, const Hdr& h, uint32_t
   return v;
 }
 
+// ipv4_verdict in the claim, PATCH's two big-endian stores and the outputs
 __device__ __forceinline__ void ipv4_result(uint8_t* __restrict__ dg, uint64_t s, uint64_t e, uint64_t t0, bool hdr,
                                             const Hdr& h, uint32_t tf0, uint32_t tf1, uint32_t tot, int mode,
                                             uint64_t seg, uint16_t* __restrict__ ip_ck, uint16_t* __restrict__ tcp_ck,
