@@ -172,6 +172,41 @@ def test_zc_completion_over_many_blocks_and_two_pass_wrap(orc):
                 assert hdrs[40 * i:40 * i + 40].tobytes() == w[:40], (n, i)
 
 
+def test_zc_first_call_after_freed_device_memory(orc):
+    """A context's first zero-copy call right after device memory full of
+    0xFF bytes was freed (the C-ABI example's order: ics_malloc / ics_free,
+    then a host call): the completion tickets the call allocates may reuse
+    that memory, and the slots' non-blocking streams do not wait for the
+    null stream's memset — ensure_staging synchronises the device before the
+    first launch, so the ticket starts at 0 and the call completes (the
+    round-4 c_abi_example failure, 'completion word was not written')."""
+    import ctypes
+
+    from conftest import engine_with
+
+    rng = np.random.default_rng(0x71C)
+    for _ in range(3):
+        for eng in engine_with({"zero_copy_max": str(1 << 30)}):
+            ptrs = []
+            junk = np.full(1 << 20, 0xFF, dtype=np.uint8)
+            for _ in range(8):
+                p = ctypes.c_void_p()
+                assert eng.lib.ics_malloc(eng.ctx, ctypes.byref(p), junk.size) == 0
+                assert eng.lib.ics_memcpy_htod(eng.ctx, p, junk.ctypes.data, junk.size, None) == 0
+                ptrs.append(p)
+            assert eng.lib.ics_stream_synchronize(eng.ctx, None) == 0
+            for p in ptrs:
+                assert eng.lib.ics_free(eng.ctx, p) == 0
+            n, L = 64, 1500
+            buf = rng.integers(0, 256, n * L, dtype=np.uint8)
+            want = buf.copy()
+            w = orc.ipv4_tcp_batch(want, n, 2, stride=L, dgram_len=L)
+            ip, tcp, st = eng.ipv4_tcp_batch_host(buf, n, 2, stride=L, dgram_len=L)
+            assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all()
+            assert (buf == want).all()  # PATCH wrote what the oracle wrote
+            assert eng.dispatch_info()["host_zero_copy"] >= 1
+
+
 @pytest.mark.parametrize("pinned", [False, True])
 def test_error_after_chunks_in_flight_drains_slots(orc, pinned):
     """A fused-IPv4 host batch (datagrams never split into pieces) whose last
