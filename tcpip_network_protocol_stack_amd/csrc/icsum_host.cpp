@@ -52,12 +52,13 @@ int ensure_staging(ics_ctx* ctx) {
   std::memset(ctx->h_flag, 0, ics_ctx::kMaxSlots * 64);
   if (!host_pinned(ctx->h_flag).kernel) ctx->zero_copy_max = 0;
   ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_ticket), ics_ctx::kMaxSlots * 64));
-  ICS_HIP(hipMemset(ctx->d_ticket, 0, ics_ctx::kMaxSlots * 64));
-  // The slots' streams are non-blocking: they do not wait for the null
-  // stream's memset, and a first launch that read the tickets before it landed
-  // (the allocation reusing freed, non-zero memory) would never reach its
-  // last-block count — the call failing with its completion word unwritten.
-  ICS_HIP(hipDeviceSynchronize());
+  // Zeroed and waited for before any slot launches: the slots' streams are
+  // non-blocking (they would not wait for a null-stream memset), and a first
+  // launch that read the tickets before the zeros landed (the allocation
+  // reusing freed, non-zero memory) would never reach its last-block count —
+  // the call failing with its completion word unwritten.
+  ICS_HIP(hipMemsetAsync(ctx->d_ticket, 0, ics_ctx::kMaxSlots * 64, ctx->st[0]));
+  ICS_HIP(hipStreamSynchronize(ctx->st[0]));
   ctx->staged = true;
   return ICS_OK;
 }
