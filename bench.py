@@ -19,11 +19,14 @@ config-5 curve.
 
 Every timed leg checks its own outputs against the reference's digests
 (tests/golden/configs.json, made by the reference's InternetChecksum,
-util/tools/checksum.h:20-41): `bit_exact` = rank 0's NS shard (the whole
-config-0 batch at any N) and `config5.bit_exact` = all ranks' config-5
-outputs gathered over gloo (the whole 8 M-segment batch).  `per_rank` lists
-each rank's kernel time, wall time, rate and output digest, so an N > 1 line
-can be read rank by rank.
+util/tools/checksum.h:20-41): `bit_exact` = EVERY rank's NS shard against
+the reference's digest of that shard (`configs.json["0"].shard_sha256[r]`,
+global segments [r 2^20, (r+1) 2^20) of config 0's spec stream; shard 0 is the
+config-0 batch) and `config5.bit_exact` = all ranks' config-5 outputs gathered
+over gloo (the whole 8 M-segment batch).  `per_rank` lists each rank's device
+(PCI address and UUID), kernel time, wall time, rate, output digest and its
+match, so an N > 1 line can be read rank by rank; `ranks_per_gpu` counts the
+ranks per distinct device id gathered, not a device count.
 
 `--gpus N` without an outer launcher starts the N ranks itself (one process
 per GPU via torch.distributed.run on 127.0.0.1; this parent never touches the
@@ -108,15 +111,7 @@ def _free_port():
 
 
 def launch_ranks(args):
-    """Every timed leg checks its own outputs against the reference's digests
-(tests/golden/configs.json, made by the reference's InternetChecksum,
-util/tools/checksum.h:20-41): `bit_exact` = rank 0's NS shard (the whole
-config-0 batch at any N) and `config5.bit_exact` = all ranks' config-5
-outputs gathered over gloo (the whole 8 M-segment batch).  `per_rank` lists
-each rank's kernel time, wall time, rate and output digest, so an N > 1 line
-can be read rank by rank.
-
-`--gpus N` without an outer launcher: start N ranks, one process per GPU,
+    """`--gpus N` without an outer launcher: start N ranks, one process per GPU,
     through torch.distributed.run on 127.0.0.1.  This parent never touches the
     GPU (nothing here imports torch), and the ranks are children, not an exec."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
@@ -347,7 +342,7 @@ def host_inclusive(eng, data, init, out, n, seg, passes=3, calls=300):
     return {"entry": "ics_checksum_batch_host", "memory": "page-locked", "bytes": n * seg, "passes": passes,
             "GB_s": round(n * seg * passes / el / 1e9, 2), "outputs_equal_device": same,
             "tick_p50": tick, "tick_note": f"{seg}-byte segments, {calls} ctypes calls, preallocated outputs, buffer addresses taken once",
-            "tick_p50_cpp": tick_cpp(calls),
+            "tick_p50_cpp": tick_cpp_guarded(calls),
             "tick_cpp_note": "the same calls from C++ (tools/probe/tick_latency, dlopen of the in-tree libicsum.so, "
                              "1500-byte segments with inits, page-locked), no interpreter in the loop"}
 
@@ -368,6 +363,31 @@ def tick_cpp(calls):
         d = json.loads(line)
         out[f"segments_{d['n']}_us"] = d["p50_us"]
     return out
+
+
+def tick_cpp_guarded(calls):
+    """tick_cpp, reported and never fatal (like pmc_traffic): a failure of
+    this secondary figure must not cost the line its headline"""
+    try:
+        return tick_cpp(calls)
+    except Exception as e:
+        return {"error": f"{type(e).__name__}: {str(e)[-200:]}"}
+
+
+def device_id(local):
+    """(PCI address, UUID) of this rank's device: what identifies the card
+    across processes, whatever the launcher's device visibility"""
+    import torch
+
+    p = torch.cuda.get_device_properties(local)
+    return f"{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}", str(getattr(p, "uuid", ""))
+
+
+def ranks_per_gpu(rows):
+    """The most ranks that shared one device, from the gathered device ids"""
+    from collections import Counter
+
+    return max(Counter((r["pci"], r["uuid"]) for r in rows).values())
 
 
 def _cpu_model():
@@ -486,21 +506,35 @@ def main():
     value = n_total * seg * args.steps / elapsed / 2**30  # all ranks' bytes / max-over-ranks time
     achieved = bytes_step / kern_s / 1e9  # GB/s, decimal like the 8 TB/s peak
 
-    # the timed steps' outputs, checked against the reference's digest: rank
-    # 0's shard of a weak-scaling workload is the whole BASELINE batch the
-    # digest covers (its other ranks' shards lie past it in the same spec
-    # stream and are covered by config 5 below, which every rank computes)
+    # the timed steps' outputs, checked against the reference's digests: rank
+    # r's shard of a weak-scaling workload is global segments [r n, (r+1) n)
+    # of one spec stream, and the reference's outputs for each such slice
+    # are hashed in configs.json (shard 0 = the BASELINE batch itself)
     gold = golden_configs()
     ns_sha = sha256_u16(u16_host(out))
-    per_rank = gather_rows({"rank": rank, "device": local, "segments": n, "kernel_ms": round(kern_s * 1e3, 4),
+    key = GOLDEN_KEY.get(args.workload)
+    # this rank's shard digest: global segments [rank n, (rank+1) n) of the
+    # workload's spec stream (weak scaling: n per rank at any N)
+    want = None
+    if key and scaling == "weak":
+        shards = gold[key].get("shard_sha256") or [gold[key]["out_sha256"]]
+        want = shards[rank] if rank < len(shards) else None
+    pci, uuid = device_id(local)
+    per_rank = gather_rows({"rank": rank, "device": local, "pci": pci, "uuid": uuid, "segments": n,
+                            "index0": sh.index0, "kernel_ms": round(kern_s * 1e3, 4),
                             "wall_ms_per_step": round(own_s / args.steps * 1e3, 4),
                             "GiB_s": round(bytes_step * args.steps / own_s / 2**30, 2),
-                            "roofline_frac": round(achieved / HBM_PEAK_GBS, 4), "out_sha256": ns_sha}, dist)
-    key = GOLDEN_KEY.get(args.workload)
+                            "roofline_frac": round(achieved / HBM_PEAK_GBS, 4), "out_sha256": ns_sha,
+                            "bit_exact": None if want is None else ns_sha == want}, dist)
     bit_exact, checked = None, "no reference digest for this workload"
     if key and scaling == "weak":
-        bit_exact = ns_sha == gold[key]["out_sha256"] if rank == 0 else None
-        checked = f"rank 0's {n} outputs vs tests/golden/configs.json[{key!r}].out_sha256"
+        if rank == 0:
+            marks = [r["bit_exact"] for r in per_rank]
+            bit_exact = all(m is True for m in marks)
+            unchecked = sum(m is None for m in marks)
+            checked = (f"every rank's {n} outputs vs its reference shard digest "
+                       f"(tests/golden/configs.json[{key!r}].shard_sha256[rank])"
+                       + (f"; {unchecked} rank(s) have no shard digest, so not bit_exact" if unchecked else ""))
     elif key:
         whole = gather_u16(out, dist)
         bit_exact = sha256_u16(whole) == gold[key]["out_sha256"] if rank == 0 else None
@@ -567,7 +601,8 @@ def main():
                        "segment_bytes": seg,
                        "bytes_per_step_per_gpu": bytes_step, "inits": "IPv4 pseudo-header sums",
                        "entry": "ics_checksum_batch", "parallelism": f"shard{world}",
-                       "ranks_per_gpu": -(-world // max(1, torch.cuda.device_count()))},
+                       "ranks_per_gpu": ranks_per_gpu(per_rank),
+                       "devices": len({(r["pci"], r["uuid"]) for r in per_rank})},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                          "traffic": None if traffic is None else round(traffic),

@@ -302,7 +302,7 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 #define ICS_K_ROUTER_HDRS 14     /* k_router_hdrs: the router step, forwarded headers apart */
 /* last_lps / last_unroll by kernel:
  *   ICS_K_CHECKSUM .. ICS_K_WRAP_2PASS  lanes per segment / loads in flight per lane
- *   ICS_K_TWOCLASS, ICS_K_IPV4_TWOCLASS  long-segment lanes (16) / segments per wave (16 or 32)
+ *   ICS_K_TWOCLASS, ICS_K_IPV4_TWOCLASS  long-segment lanes (16) / segments per wave (16 or 32; 8 only under ICSUM_FORCE twoclass=8)
  *   ICS_K_BATCHV  the ICS_BV_* shape of the last launch group / batches in the call
  *   ICS_K_TILE    segments per tile (T) / ICS_TILE_* operation
  *   ICS_K_ROUTER, ICS_K_ROUTER_HDRS  0 / 0 */

@@ -419,8 +419,10 @@ void write_bin(const std::string& path, const void* p, size_t n) {
 }
 
 // fixed-stride / offset segment configs: out[i] = InternetChecksum{pseudo}.add(seg).value()
-void config_bytes(int k, uint64_t n, uint64_t stride, bool mixed, const std::string& dir) {
+// (`tag` names the output file; the spec seed is config k's)
+void config_bytes(int k, uint64_t n, uint64_t stride, bool mixed, const std::string& dir, int tag = -1) {
   const uint64_t seed = 0x10710000ull + uint64_t(k);
+  if (tag < 0) tag = k;
   std::vector<uint16_t> out(n);
   unsigned nt = std::max(1u, std::thread::hardware_concurrency());
   std::vector<std::thread> th;
@@ -444,9 +446,9 @@ void config_bytes(int k, uint64_t n, uint64_t stride, bool mixed, const std::str
       }
     });
   for (auto& x : th) x.join();
-  write_bin(dir + "/cfg" + std::to_string(k) + "_out.bin", out.data(), n * 2);
+  write_bin(dir + "/cfg" + std::to_string(tag) + "_out.bin", out.data(), n * 2);
   uint64_t total = mixed ? offs[n] : n * stride;
-  std::printf("config %d: n=%llu bytes=%llu\n", k, (unsigned long long)n, (unsigned long long)total);
+  std::printf("config %d: n=%llu bytes=%llu\n", tag, (unsigned long long)n, (unsigned long long)total);
 }
 
 // config 2: IPv4 datagrams — build each through the reference types exactly
@@ -623,9 +625,13 @@ int main(int argc, char** argv) {
       case 5: config_bytes(5, 8ull << 20, 9000, false, dir); return 0;
       case 6: config_wrap(dir); return 0;
       case 7: config_router(dir); return 0;
+      // the north-star spec stream continued to 8 M segments: bench.py's
+      // weak-scaling NS run gives rank r global segments [r 2^20, (r+1) 2^20)
+      // of it, so each 2^20-output slice is one rank's reference digest
+      case 8: config_bytes(0, 8ull << 20, 1500, false, dir, 8); return 0;
       default: break;
     }
   }
-  std::fprintf(stderr, "usage: golden_gen kat DIR | golden_gen config {0,2,3,4,5,6,7} DIR\n");
+  std::fprintf(stderr, "usage: golden_gen kat DIR | golden_gen config {0,2,3,4,5,6,7,8} DIR\n");
   return 1;
 }

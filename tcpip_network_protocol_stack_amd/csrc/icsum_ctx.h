@@ -195,6 +195,9 @@ struct ics_ctx {
   uint64_t* h_flag = nullptr;  // kMaxSlots words, 64 bytes apart, coherent page-locked
   uint64_t flag_ticket = 0;
   uint32_t* d_ticket = nullptr;  // kMaxSlots block-count tickets, 64 bytes apart (icsum::Done)
+  // test hook (ICSUM_FORCE poison_ticket=V): slot 0's ticket is set to V once
+  // staging exists, so a test can drive the recovery in wait_flag
+  uint32_t poison_ticket = 0;
   bool wrap_staged = false;
   uint8_t* h_msg[kMaxSlots] = {};
   uint8_t* d_msg[kMaxSlots] = {};

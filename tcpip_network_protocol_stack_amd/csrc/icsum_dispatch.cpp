@@ -620,6 +620,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);
+    else if (k == "poison_ticket" && v > 0 && v <= 0xFFFFFFFFll) ctx->poison_ticket = uint32_t(v);
     else if (k == "tile" && v >= -1 && v <= 1) ctx->tile = int(v);
     else if (k == "tile_segs" && v >= 0 && v <= 256) ctx->tile_segs = uint32_t(v);
     else if (k == "tile_blocks" && v >= 0) ctx->tile_blocks = uint32_t(v);

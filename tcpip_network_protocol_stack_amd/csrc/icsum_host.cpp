@@ -58,6 +58,8 @@ int ensure_staging(ics_ctx* ctx) {
   // reusing freed, non-zero memory) would never reach its last-block count —
   // the call failing with its completion word unwritten.
   ICS_HIP(hipMemsetAsync(ctx->d_ticket, 0, ics_ctx::kMaxSlots * 64, ctx->st[0]));
+  if (ctx->poison_ticket)  // test hook: a ticket left non-zero (wait_flag recovers it)
+    ICS_HIP(hipMemcpyAsync(ctx->d_ticket, &ctx->poison_ticket, 4, hipMemcpyHostToDevice, ctx->st[0]));
   ICS_HIP(hipStreamSynchronize(ctx->st[0]));
   ctx->staged = true;
   return ICS_OK;
@@ -191,7 +193,11 @@ void host_patch_fields(uint8_t* bytes, const uint64_t* offsets, uint64_t stride,
 // launch's last block, icsum_kernels.hip signal_done) for
 // up to a millisecond — a zero-copy chunk is at most zero_copy_max bytes, tens
 // of microseconds over PCIe — then block on the slot's stream, which also
-// surfaces a kernel fault as a HIP error instead of a hang.
+// surfaces a kernel fault as a HIP error instead of a hang.  A launch that
+// finished without writing the word found its block-count ticket non-zero at
+// the start (no block drew the last ticket): the call fails, but the ticket
+// is zeroed on the slot's stream first, so the next call on this slot counts
+// from zero again instead of failing the same way for the context's life.
 int wait_flag(ics_ctx* ctx, int k, uint64_t v) {
   const uint64_t* f = ctx->h_flag + 8 * k;
   const auto t0 = std::chrono::steady_clock::now();
@@ -201,7 +207,9 @@ int wait_flag(ics_ctx* ctx, int k, uint64_t v) {
   }
   ICS_HIP(hipStreamSynchronize(ctx->st[k]));
   if (__atomic_load_n(f, __ATOMIC_ACQUIRE) >= v) return ICS_OK;
-  return fail(ICS_ERR_HIP, "host path: slot %d's completion word was not written", k);
+  ICS_HIP(hipMemsetAsync(ctx->d_ticket + 16 * k, 0, 64, ctx->st[k]));
+  ICS_HIP(hipStreamSynchronize(ctx->st[k]));
+  return fail(ICS_ERR_HIP, "host path: slot %d's completion word was not written (its ticket was reset)", k);
 }
 
 }  // namespace

@@ -383,8 +383,11 @@ __device__ __forceinline__ uint32_t block_order(uint32_t run_log2) {
   return ((k >> lc) << (lc + 3)) + (x << lc) + (k & ((1u << lc) - 1u));
 }
 
-// End of a launch that completes a zero-copy host call (Done): the block's
-// barrier orders every wave's result stores before lane 0, whose
+// End of a launch that completes a zero-copy host call (Done): every wave
+// first waits for its own outstanding memory operations (s_waitcnt 0: on
+// gfx9 stores count in vmcnt, so its result stores have left the CU — made
+// explicit rather than relying on the barrier's workgroup-scope release to
+// emit that wait), then the block's barrier orders them before lane 0, whose
 // system-scope release (cumulative: one L2 write-back per block, not per
 // wave) puts them where the host reads them before it takes a ticket; the
 // block with the last ticket resets the ticket word and releases the
@@ -393,6 +396,7 @@ __device__ __forceinline__ uint32_t block_order(uint32_t run_log2) {
 // kernels call their body first.
 __device__ __forceinline__ void signal_done(const Done& d) {
   if (d.flag == nullptr) return;
+  __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope

@@ -177,9 +177,10 @@ def test_zc_first_call_after_freed_device_memory(orc):
     0xFF bytes was freed (the C-ABI example's order: ics_malloc / ics_free,
     then a host call): the completion tickets the call allocates may reuse
     that memory, and the slots' non-blocking streams do not wait for the
-    null stream's memset — ensure_staging synchronises the device before the
-    first launch, so the ticket starts at 0 and the call completes (the
-    round-4 c_abi_example failure, 'completion word was not written')."""
+    null stream's memset — ensure_staging zeroes the tickets on slot 0's
+    stream and waits for that stream before any slot launches, so the ticket
+    starts at 0 and the call completes (the round-4 c_abi_example failure,
+    'completion word was not written')."""
     import ctypes
 
     from conftest import engine_with
@@ -205,6 +206,31 @@ def test_zc_first_call_after_freed_device_memory(orc):
             assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all()
             assert (buf == want).all()  # PATCH wrote what the oracle wrote
             assert eng.dispatch_info()["host_zero_copy"] >= 1
+
+
+def test_poisoned_ticket_fails_once_then_recovers(orc):
+    """A slot whose block-count ticket is non-zero when a zero-copy launch
+    starts (ICSUM_FORCE poison_ticket: slot 0's ticket set to 2^30 once the
+    staging exists) never has a block draw the last ticket, so the call's
+    completion word stays unwritten: that call fails with ICS_ERR_HIP, and
+    wait_flag zeroes the slot's ticket before returning — the next call on
+    the same context and slot is exact, and so are the ones after it."""
+    from conftest import engine_with
+    from tcpip_network_protocol_stack_amd._lib import IcsumError
+
+    rng = np.random.default_rng(0x71D)
+    n, L = 48, 1500
+    buf = rng.integers(0, 256, n * L, dtype=np.uint8)
+    init = rng.integers(0, 1 << 32, n, dtype=np.uint32)
+    want = orc.checksum_batch(buf, n, stride=L, seg_len=L, init=init)
+    for eng in engine_with({"zero_copy_max": str(1 << 30), "poison_ticket": str(1 << 30)}):
+        with pytest.raises(IcsumError) as e:
+            eng.checksum_batch_host(buf, n, stride=L, seg_len=L, init=init)
+        assert "icsum error -2" in str(e.value) and "completion word was not written" in str(e.value)
+        for _ in range(3):  # recovered: slot 0 counts from zero again
+            got = eng.checksum_batch_host(buf, n, stride=L, seg_len=L, init=init)
+            assert (got == want).all()
+        assert eng.dispatch_info()["host_zero_copy"] == 4
 
 
 @pytest.mark.parametrize("pinned", [False, True])

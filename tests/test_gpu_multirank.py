@@ -86,8 +86,16 @@ def test_bench_two_ranks_one_line():
     c5 = d["config5"]
     assert c5["segments_total"] == 8 << 20 and c5["segments_per_gpu"] == 4 << 20 and c5["value"] > 0
     assert d["cpu_baseline"] is None and d["host_inclusive"] is None  # N = 1 only
-    # the timed outputs checked against the reference digests: rank 0's NS
-    # shard = config 0, both ranks' config-5 outputs gathered = config 5
+    # the timed outputs checked against the reference digests: EVERY rank's
+    # NS shard against its own shard digest (rank r = global segments
+    # [r 2^20, (r+1) 2^20)), both ranks' config-5 outputs gathered = config 5
     assert d["bit_exact"] is True and c5["bit_exact"] is True
     assert [r["rank"] for r in d["per_rank"]] == [0, 1] and [r["rank"] for r in c5["per_rank"]] == [0, 1]
+    assert all(r["bit_exact"] is True for r in d["per_rank"])
+    gold = json.load(open(os.path.join(ROOT, "tests", "golden", "configs.json")))["0"]["shard_sha256"]
+    assert [r["out_sha256"] for r in d["per_rank"]] == gold[:2]
+    assert [r["index0"] for r in d["per_rank"]] == [0, 1 << 20]
     assert all(r["kernel_ms"] > 0 for r in d["per_rank"] + c5["per_rank"])
+    # device identity measured, not inferred: both ranks on this box's one card
+    assert all(r["pci"] and ":" in r["pci"] for r in d["per_rank"])
+    assert d["config"]["devices"] == 1 and d["config"]["ranks_per_gpu"] == 2

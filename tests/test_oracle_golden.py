@@ -221,3 +221,19 @@ def _pseudo_inits_np(seed, n, length, lens=None, index0=0):
     L = (lens if lens is not None else np.full(n, length, dtype=np.uint64)) & np.uint64(0xFFFF)
     s = (src >> np.uint64(16)) + (src & np.uint64(0xFFFF)) + (dst >> np.uint64(16)) + (dst & np.uint64(0xFFFF))
     return (s + np.uint64(6) + L).astype(np.uint32)
+
+
+def test_ns_shard_digests(orc):
+    """configs.json["0"].shard_sha256: the reference's outputs for global
+    segments [r 2^20, (r+1) 2^20) of config 0's spec stream, one per rank of
+    bench.py's weak-scaling NS run (golden_gen config 8).  Shard 0 is the
+    config-0 batch; the oracle reproduces the last shard (index0 = 7 2^20,
+    byte 0 = 11 GB into the stream) from the spec alone."""
+    g = golden("configs.json")["0"]
+    shards = g["shard_sha256"]
+    assert len(shards) == 8 and len(set(shards)) == 8 and shards[0] == g["out_sha256"]
+    n, stride, seed, r = 1 << 20, g["stride"], g["seed"], 7
+    data = orc.fill_bytes(seed, r * n * stride, n * stride)
+    init = _pseudo_inits_np(seed, n, g["seg_len"], index0=r * n)
+    out = orc.checksum_batch(data, n, stride=stride, seg_len=g["seg_len"], init=init, threads=8)
+    assert _sha(out) == shards[r]
