@@ -96,10 +96,13 @@ struct ics_ctx {
   uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order
   uint32_t twoclass_lds = 0;    // dynamic LDS bytes per two-class block (residency cap; ICSUM_FORCE twoclass_lds)
   uint32_t tile_segs = 0, tile_blocks = 0;
+  // the checksum and headers-apart wrap tile launches on k_stream (a
+  // metadata wave per block, round 5) or, false, on k_tile (ICSUM_FORCE stream)
+  bool tile_stream = true;
   // device wrap: 0 = two passes (payload sums, then a header launch) when
   // the headers go to an array of their own and the batch has at least
   // kWrapTwoPassMin datagrams, otherwise one pass (headers stored inside the
-  // payload stream) — each the faster there (tools/ab_wrap_twopass.py,
+  // payload stream) — each the faster there (git 7692616:tools/ab_wrap_twopass.py,
   // DESIGN.md §6); 1 / 2 = always one / two (tests)
   static constexpr uint64_t kWrapTwoPassMin = uint64_t(1) << 18;
   uint32_t wrap_passes = 0;
@@ -135,7 +138,7 @@ struct ics_ctx {
   static constexpr uint32_t kIpv4ShortMix16 = 5;
   // ... and from this share up the two-class launch (k_ipv4_twoclass, block
   // lists, 16 datagrams per wave in the bounds pass), which beats 16 x 4
-  // groups from 3/16 ACKs up (1 M datagrams VERIFY, tools/ab_mix_split.py,
+  // groups from 3/16 ACKs up (1 M datagrams VERIFY, git 7692616:tools/ab_mix_split.py,
   // profiles/r3_mix_twoclass_ab.jsonl: 1/8 200.2 vs 198.5 us, 3/16 187.3 vs
   // 191.4, 1/4 176.0 vs 185.4, 5/16 164.3 vs 184.2)
   static constexpr uint32_t kIpv4TwoClass16 = 3;
@@ -143,9 +146,9 @@ struct ics_ctx {
   static constexpr uint32_t kIpv4TwoClassWide16 = 11;
   // the plain checksum's short-mix threshold (short_mix: the two-class
   // launch); raw-datagram ACK shares, AUTO vs two-class at 16 per wave
-  // (round 2, tools/ab_ipv4_mix.py plain rows): 3/8 156.1 vs 144.1 us, 5/16
+  // (round 2, git 7692616:tools/ab_ipv4_mix.py plain rows): 3/8 156.1 vs 144.1 us, 5/16
   // 163.6 vs 157.8, 1/4 169.6 vs 169.0, 3/16 178.3 vs 181.4; with the block
-  // lists (round 3, tools/ab_plain_mix_threshold.py,
+  // lists (round 3, git 7692616:tools/ab_plain_mix_threshold.py,
   // profiles/r3_plain_mix_threshold.jsonl): 1/4 169.0 vs 166.1, 3/16 177.3
   // vs 178.9, 1/8 186.8 vs 190.8
   static constexpr uint32_t kShortMix16 = 4;
@@ -164,7 +167,7 @@ struct ics_ctx {
   // (ICSUM_HOST_SLOT_MB), each with pinned in/out staging, device buffers and a stream
   static constexpr int kMaxSlots = 4;
   static constexpr size_t kSlotSegs = size_t(1) << 20;
-  int nslots = 3;  // 3 x 32 MiB: pageable 49.2 -> 51.4 GB/s over 2 x 64 MiB, pinned equal (tools/ab_host.py)
+  int nslots = 3;  // 3 x 32 MiB: pageable 49.2 -> 51.4 GB/s over 2 x 64 MiB, pinned equal (git 7692616:tools/ab_host.py)
   size_t slot_bytes = size_t(32) << 20;
   bool staged = false;
   hipStream_t st[kMaxSlots] = {};
@@ -191,7 +194,7 @@ struct ics_ctx {
   // ... and it ends in a completion word the launch's last block stores
   // (icsum::Done, a block-count ticket in d_ticket), which the caller spins
   // on: ~3.7 us less than waiting for the stream's completion signal
-  // (tools/probe/sync_probe.hip), and no second launch behind the kernel
+  // (git 7692616:tools/probe/sync_probe.hip), and no second launch behind the kernel
   uint64_t* h_flag = nullptr;  // kMaxSlots words, 64 bytes apart, coherent page-locked
   uint64_t flag_ticket = 0;
   uint32_t* d_ticket = nullptr;  // kMaxSlots block-count tickets, 64 bytes apart (icsum::Done)

@@ -179,7 +179,7 @@ bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m
 // fused IPv4 kernel and the wraps, which have no length binning — a sixteenth
 // or more of the bytes in segments over 1920 bytes.  Short-heavy mixes keep
 // the two-class launches (checked first by the callers), MTU-sized means the
-// 16-lane line grid.  tools/ab_dispatch.py, profiles/r4_ab_dispatch.jsonl
+// 16-lane line grid.  git 7692616:tools/ab_dispatch.py, profiles/r4_ab_dispatch.jsonl
 // (256 Ki / 1 M segments, us, default vs tile): checksum 40..1040 B 37.1 /
 // 29.2 and 279.3 / 92.2, 770 B 40.0 / 35.7 and 153.4 / 122.6, MTU 56.7 /
 // 63.9; VERIFY 40..1040 B 40.0 / 34.5 and 150.0 / 116.9, config-4 mix 412.4 /
@@ -194,7 +194,7 @@ bool tile_wins(const ics_ctx* ctx, const PlanMix& m, uint64_t n, bool fused) {
 // one per lane, the rest 16 lanes each; block lists since round 3), 32
 // segments per wave from 3/4 short segments up and 16 below (round 2, the
 // per-wave version: fewer long segments per wave, shorter-lived waves).  2 M x 40 / 1460 B: 8-lane groups 279.5, two-class 64 / 32 / 16 per
-// wave 255.7 / 234.9 / 231.1 us; raw-datagram mixes (tools/ab_ipv4_mix.py
+// wave 255.7 / 234.9 / 231.1 us; raw-datagram mixes (git 7692616:tools/ab_ipv4_mix.py
 // plain rows, 64 / 32 / 16): 7/8 ACKs 43.5 / 42.2 / 54.5, 3/4 74.8 / 68.5 /
 // 74.5, 1/2 132.4 / 122.5 / 119.0, 7/16 145.0 / 139.3 / 131.9 us
 // (profiles/r2_twoclass_spw*.jsonl).  Batches past the two-class grid's
@@ -229,8 +229,9 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   }
   if (sp.offsets && ctx->tile == 1) {  // test hook: the tile launch on every offsets batch
     const uint32_t T = tile_segs_for(ctx, sp.n, 0);
-    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st));
-    note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM, true, 0, 1});
+    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st,
+                                                ctx->tile_stream));
+    note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM | (ctx->tile_stream ? ICS_TILE_STREAM : 0), true, 0, 1});
     return ICS_OK;
   }
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
@@ -241,7 +242,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     // from the plan the device reported for this batch last time (16-lane
     // groups for MTU-sized mixes, the small-segment body for short ones);
     // on a miss the unknown-mix geometry, and the plan kernels run behind
-    // the launch for the next call (tools/ab_small_offsets.py)
+    // the launch for the next call (git 7692616:tools/ab_small_offsets.py)
     uint32_t plan = 0;
     PlanMix mix;
     PlanReq req;
@@ -286,8 +287,10 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     const bool mix8 = hit && hit_plan != icsum::kPlanWholeBatchSmall && short_mix(mix);
     if (hit && !mix8 && hit_plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, sp.n, false)) {
       const uint32_t T = tile_segs_for(ctx, sp.n, mix.avg);
-      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st));
-      note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM, true, 0, 1}, int(hit_plan));
+      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st,
+                                                ctx->tile_stream));
+      note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM | (ctx->tile_stream ? ICS_TILE_STREAM : 0), true, 0, 1},
+           int(hit_plan));
       return replan(ctx, sp, lps, req, st);
     }
     if (hit && (hit_plan != icsum::kPlanSplitBins || mix8)) {
@@ -342,10 +345,10 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   // an offsets batch of raw datagrams gives no length hint; datagrams are at
   // most 64 KiB and mostly MTU-sized, and the 16-lane line grid is the best
   // measured geometry for both 1500- and 9000-byte datagrams (64 Ki x 1500 B:
-  // 18.3 us vs 48.8 us with the 64-lane default; tools/ab_ipv4_offsets.py)
+  // 18.3 us vs 48.8 us with the 64-lane default; git 7692616:tools/ab_ipv4_offsets.py)
   // ACK-sized datagrams (a fixed length <= kTinyMaxAvg, or a cached plan
   // whose mean is) run one lane per datagram with default-policy loads
-  // (neighbours share lines): 1 M x 40 B VERIFY 30.3 -> 10.6 us (tools/ab_ipv4_mix.py, AB_LANE1)
+  // (neighbours share lines): 1 M x 40 B VERIFY 30.3 -> 10.6 us (git 7692616:tools/ab_ipv4_mix.py, AB_LANE1)
   const icsum::Geometry lane1{1, 4, false, 0, 1};
   const icsum::Geometry base = geometry_for(ctx, d_offsets ? 1500 : sp.seg_len);
   icsum::Geometry g = base.mode == icsum::kModeTiny ? lane1 : ipv4_geometry(base);
@@ -356,7 +359,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   // time (4-lane groups when it was the small-segment plan, 8-lane groups
   // from 5/16 of <= 144-byte datagrams, 16 x 4 below that), the plan
   // kernels running behind the first and every 64th launch (DESIGN.md §4,
-  // tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
+  // git 7692616:tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
   bool two = false, tile = false;
   int spw = 16;
   uint32_t tile_avg = 0;  // the cached plan's mean length (tile_segs_for)
@@ -376,7 +379,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
       g = ipv4_geometry({16, 4, true, 3, 1});  // MTU + a few ACKs: shorter unroll, 1-4 % (1 M datagrams)
     // the two-class launch (block lists, ics_ctx::kIpv4TwoClass16 for the
     // crossover against 16 x 4 groups; round 2's per-wave version beat the
-    // 8-lane groups from 5/16 ACKs up, tools/ab_ipv4_mix.py)
+    // 8-lane groups from 5/16 ACKs up, git 7692616:tools/ab_ipv4_mix.py)
     two = hit && plan != icsum::kPlanWholeBatchSmall && mix.short16 >= ics_ctx::kIpv4TwoClass16 && mix.long16 == 0;
     // ACK-heavy mixes: 128 datagrams per block, so the block's one short
     // pass carries more of them (3/4 ACKs 78.4 -> 75.4 us, mix_probe blk32)
@@ -430,7 +433,7 @@ hipError_t device_wrap(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg
 // The device wrap's geometry: one lane per datagram for ACK-sized batches (a
 // fixed length, or a cached small plan with a mean <= kTinyMaxAvg: 1 M pure
 // ACKs in place 78.3 -> 36.6 us, 40-56 B 119.0 -> 47.4 us,
-// tools/ab_wrap_ack.py), else the fused kernel's geometry for the length
+// git 7692616:tools/ab_wrap_ack.py), else the fused kernel's geometry for the length
 // hint.  The plan kernels run behind the launch as plan_lookup asks (the
 // wrap's transmit buffer keeps its own cache slot: a stack's receive-side
 // verify in between does not evict it).
@@ -465,7 +468,7 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
   // it; in place only for long-segment mixes (its header stores cost the
   // same scattered write per datagram either way, and the per-segment wrap
   // is faster on short ones: 40..1040 B, 256 Ki: 40.3 / 44.7 us; config-4 mix
-  // 499.3 / 464.2 us, tools/ab_dispatch.py).  Headers apart, the receive-side
+  // 499.3 / 464.2 us, git 7692616:tools/ab_dispatch.py).  Headers apart, the receive-side
   // mix of empty and MTU payloads tiles too (256 Ki / 1 M: 48.8 / 40.5 and
   // 169.3 / 150.8 us), payloads nearly all empty (pure ACKs) do not (1 M:
   // 24.2 / 41.0 us; profiles/r4_ab_dispatch_tile.jsonl)
@@ -476,8 +479,10 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
   if (sp.offsets && (ctx->tile == 1 || tile_pick)) {  // the wrap (in place or headers apart) as a tile launch
     const uint32_t T = tile_segs_for(ctx, sp.n, plan >= 0 ? mix.avg : 0u);
     ICS_HIP(icsum::launch_tile_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), hdr_out, d_ip_ck, d_tcp_ck,
-                                    T, ctx->tile_blocks, st));
-    note(ctx, ICS_K_TILE, {int(T), hdr_out ? ICS_TILE_WRAP_APART : ICS_TILE_WRAP, true, 0, 1}, plan);
+                                    T, ctx->tile_blocks, st, ctx->tile_stream));
+    note(ctx, ICS_K_TILE,
+         {int(T), hdr_out ? ICS_TILE_WRAP_APART | (ctx->tile_stream ? ICS_TILE_STREAM : 0) : ICS_TILE_WRAP, true, 0, 1},
+         plan);
     return replan(ctx, sp, 64, req, st);
   }
   ICS_HIP(device_wrap(ctx, sp, d_msgs, hdr_out, d_ip_ck, d_tcp_ck, payload_only, g, plan, st));
@@ -617,6 +622,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "twoclass" && (v == 0 || v == 8 || v == 16 || v == 32)) ctx->twoclass = int(v);
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
+    else if (k == "stream" && (v == 0 || v == 1)) ctx->tile_stream = v == 1;
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);

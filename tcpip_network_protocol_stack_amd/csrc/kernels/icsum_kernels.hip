@@ -17,6 +17,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "icsum_device.h"
 #include "icsum_launch.h"
@@ -111,7 +112,7 @@ __device__ __forceinline__ uint64_t block_excl_scan(uint64_t v, uint64_t& total)
 // The choice is the cheapest plan under kPlanCost (below): every estimate is
 // in ns, a sum over the bins of max(bytes / rate, segments * per-segment
 // cost) plus the dispatch of the last bin's idle waves.
-// Measured under each forced plan (tools/ab_lastbin.py --var ICSUM_BIN_PLAN,
+// Measured under each forced plan (git 7692616:tools/ab_lastbin.py --var ICSUM_BIN_PLAN,
 // profiles/r1_ab_plans.jsonl), µs whole / split / whole16: config 4
 // 1429 / 1622 / 1682, 2 M bimodal 40+1460 B 525 / 473 / 364, 2 M x 4-6 KiB
 // 1515 / 1589 / 1593, 1 M x 1460 B 520 / 429 / 296, 1 M x 40 B 451 / 168 / 205.
@@ -119,8 +120,8 @@ struct PlanCostTable {
   // rates in GB/s (= bytes per ns), per-segment costs in ns x 100; sources in profiles/
   uint32_t whole_rate;            // whole: 64-lane groups over a long mix; config 4 whole 1429 us = 7.2 TB/s (r1_ab_plans)
   uint32_t whole_seg_c;           // whole: ns x 100 per segment floor; 1 M x 40 B whole 451 us (r1_ab_plans)
-  uint32_t split_fixed_ns;        // split: the scatter pass and the bins 0-3 launch, 26 us fixed (tools/ab_bins.py, r1_ab_bins)
-  uint32_t empty_wave_ps;         // every plan: an idle wave of the last bin's launch, 0.053 ns (tools/probe/dispatch_probe.hip)
+  uint32_t split_fixed_ns;        // split: the scatter pass and the bins 0-3 launch, 26 us fixed (git 7692616:tools/ab_bins.py, r1_ab_bins)
+  uint32_t empty_wave_ps;         // every plan: an idle wave of the last bin's launch, 0.053 ns (git 7692616:tools/probe/dispatch_probe.hip)
   uint32_t split_rate_bins;       // split: bins 0-3 from their lists, 5.0 TB/s (r1_ab_bins)
   uint32_t split_rate_last;       // split: last bin, segments no longer contiguous, 6.4 TB/s (r1_ab_bins)
   uint32_t split_seg_c;           // split: ns x 100 per listed segment (r1_ab_bins: 1 M x 40 B split 168 us)
@@ -469,7 +470,7 @@ __device__ __forceinline__ void checksum_entry(const uint8_t* __restrict__ bytes
   }
   // a bin launch whose bin is empty (the last bin under the split plan) is
   // dispatch-bound — ~0.05 ns per wave whatever the block shape (measured,
-  // tools/probe/dispatch_probe.hip) — so its waves leave before anything else
+  // git 7692616:tools/probe/dispatch_probe.hip) — so its waves leave before anything else
   if (src.list && resolve(src, n).items == 0) return;
   checksum_body<LPS, UNROLL, NT, MODE, OUT>(bytes, src, init, init_step, odd, odd_step, out, n, blk,
                                             gridDim.x);
@@ -657,7 +658,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_tiny(const uint8_t* __restr
 // short passes are done — claims the long ones 64 / LONG_LPS at a time from
 // an LDS counter (LONG_LPS lanes each, the line grid, unroll 8).  The fused
 // IPv4 launch's block lists (k_ipv4_twoclass); 2 M x 40 / 1460 B 230.8 ->
-// 224.8 us against the per-wave version (tools/probe/csum_mix_probe.hip).
+// 224.8 us against the per-wave version (git 7692616:tools/probe/csum_mix_probe.hip).
 template <int LONG_LPS, int SPW, int OUT>
 __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __restrict__ bytes, SegSrc src,
                                                               const uint32_t* __restrict__ init, uint32_t init_step,
@@ -774,7 +775,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
 // words) are issued before the first is consumed.  Every start is even (the
 // base is aligned, the stride a multiple of 16), so byte roles never swap.
 // Measured floor for 64 MiB + 4 MiB inits + 2 MiB outputs on MI355X:
-// ≈12.4 us (tools/probe/small_probe.hip).
+// ≈12.4 us (git 7692616:tools/probe/small_probe.hip).
 // (block blk of the launch; init_step 0 reads one shared zero word)
 template <int LPS, int SEGS, bool INIT, int OUT>
 __device__ __forceinline__ void checksum_dense_body(const u32x4* __restrict__ chunks, const uint32_t* __restrict__ init,
@@ -1640,7 +1641,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
 // neighbouring dwords each instead of 64 lines with one (one lane loading all
 // six dwords: six instructions of 64 lines; the memory side then saw ~1.9
 // 128-byte read requests per datagram for ~1.16 lines of header).  Measured
-// (tools/probe/router_probe.hip, profiles/r2_router_probe.jsonl): 1 M x 1500 B
+// (git 7692616:tools/probe/router_probe.hip, profiles/r2_router_probe.jsonl): 1 M x 1500 B
 // 59.8 -> 57.3 us; the read-only floor of the same headers is 35-41 us, the
 // rest is the scattered 8-byte write-back of every forwarded header.
 __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
@@ -1861,8 +1862,17 @@ __device__ __forceinline__ TileSeg tile_seg_load(const uint8_t* __restrict__ byt
                                                  uint64_t i, bool valid, uint64_t tend, const TileArgs& a,
                                                  const uint8_t* zpad, const uint32_t* zlast) {
   TileSeg g{};
-  g.s = valid ? off[i] : tend;
-  g.e = valid ? off[i + 1] : tend;
+  if constexpr (OP == kTileIpv4) {  // the header loads below depend on the bounds
+    g.s = valid ? off[i] : tend;
+    g.e = valid ? off[i + 1] : tend;
+  } else {
+    // i is in range for every lane (the caller clamps it) and an invalid
+    // lane's bounds are never used: plain loads, no default written into
+    // their registers first (which makes the compiler wait for every load
+    // still in flight, the stream's prefetched windows included)
+    g.s = off[i];
+    g.e = off[i + 1];
+  }
   if constexpr (OP == kTileSum) {
     g.w[0] = a.init[i * a.init_step];
     g.w[1] = a.odd[i * a.odd_step];
@@ -2204,6 +2214,332 @@ __global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, co
   }
 }
 
+// ------------------------- tile stream with a metadata wave (round 5) ------
+// k_tile keeps each tile's metadata (segment bounds, inits or message
+// records) in VGPRs loaded a tile ahead, between the windows' loads.  gfx9's
+// vmcnt retires loads in issue order, so every wait the compiler places for
+// those registers (the default written into a masked load's destination, the
+// phi copies between the two TileSeg sets) waits for all the window loads
+// issued before them: the stream drained at each tile start (s_waitcnt
+// vmcnt(0) in the ISA) and ran one to two windows deep inside a tile.
+// k_stream gives the roles to different waves of one block:
+//   * four stream waves issue NOTHING but window loads (no stores, no other
+//     loads): three register sets, two windows in flight while one is summed,
+//     and the prefetch runs on across tile boundaries;
+//   * a fifth, metadata wave loads the next tile's offsets into LDS (with the
+//     first point of each stream wave's range, so the stream waves search
+//     nothing) and, while the stream waves run tile j + 1, finishes tile j:
+//     F at every point, each segment's sums, its folded checksum or its
+//     40-byte header, the stores.  The last tile is finished by all 320
+//     threads.
+// The points of the lo = start operations (checksum, headers-apart wrap) are
+// the offsets themselves: segment t is [off[t], off[t+1]), m + 1 points per
+// tile, F(t + 1) - F(t) its sums.  One block barrier per tile; LDS (33 KiB)
+// and registers keep four blocks per CU.  Stream-wave point pass as k_tile's,
+// with the lane's point held in registers across windows (an LDS read per 64
+// points, not per window).
+constexpr uint32_t kSW = 4;                          // stream waves per block
+constexpr uint32_t kStreamBlock = (kSW + 1) * 64;    // + the metadata wave
+constexpr uint32_t kStreamResident = 1024;           // blocks resident at once: 4 per CU x 256 CUs
+
+template <int OP, int OUT>
+__global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restrict__ bytes,
+                                                         const uint64_t* __restrict__ off, uint64_t n, uint32_t T,
+                                                         TileArgs a, uint32_t remap) {
+  static_assert(OP == kTileSum || OP == kTileWrapApart, "k_stream: operations whose points are the offsets");
+  __shared__ uint64_t s_pt[2][kTileMax + 1];    // a tile's offsets off[i0 .. i0 + m]: its points
+  __shared__ uint32_t s_f[2][kTileMax + 1][2];  // F of each point over its stream wave's range (even, odd)
+  __shared__ uint32_t s_tot[2][kSW][2];         // each stream wave's sums
+  __shared__ uint32_t s_first[2][kSW];          // the first point of each stream wave's range
+  __shared__ uint32_t s_pre[kSW][kWinChunks][2];
+  __shared__ u32x4 s_raw[kSW][kWinChunks];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
+  const bool meta = wv == kSW;
+  const uint64_t ntiles = (n + T - 1) / T;
+  // A tile's geometry (scalar loads): segments, the 16-byte chunks of its
+  // bytes [first & ~15, off[i0 + m]), this wave's quarter of them and its
+  // windows (a multiple of 3: the window loop is unrolled by 3); the
+  // metadata wave's range is empty
+  struct Geo {
+    uint64_t i0, a0c, nch, quarter, wc0, wc1, nwin3;
+    uint32_t m;
+  };
+  auto geo_of = [&](uint64_t t) {
+    Geo g{};
+    if (t >= ntiles) return g;  // no tile: m = 0, every range empty
+    g.i0 = t * T;
+    g.m = uint32_t(n - g.i0 < T ? n - g.i0 : T);
+    const uint64_t first = off[g.i0], tend = off[g.i0 + g.m];
+    g.a0c = first >> 4;
+    g.nch = tend > (g.a0c << 4) ? ((tend + 15) >> 4) - g.a0c : 0;
+    const uint64_t q = (((g.nch + kSW - 1) / kSW) + 63) & ~uint64_t(63);
+    g.quarter = q ? q : 64;
+    const uint64_t w = meta ? kSW : wv;
+    g.wc0 = g.quarter * w < g.nch ? g.quarter * w : g.nch;
+    g.wc1 = g.wc0 + g.quarter < g.nch ? g.wc0 + g.quarter : g.nch;
+    g.nwin3 = ((g.wc1 - g.wc0 + kWinChunks - 1) / kWinChunks + 2) / 3 * 3;
+    return g;
+  };
+  // window k of a stream wave's range (as k_tile: raw buffer loads through a
+  // resource spanning exactly the window's chunks, zeros past it)
+  const uint32_t voff = lane * 16u;
+  auto load_win = [&](const Geo& g, uint64_t k, u32x4 (&v)[4]) {
+    const uint64_t c0 = g.wc0 + k * kWinChunks;
+    const uint64_t left = g.wc1 > c0 ? g.wc1 - c0 : 0;
+    const uint32_t len = uint32_t(left < kWinChunks ? left : kWinChunks);
+    const u32x4* pw = reinterpret_cast<const u32x4*>(bytes) + g.a0c + c0;
+#ifdef ICSUM_BOUNDS_CHECK
+    if (len) {
+      const uint8_t* lo8 = bytes + (g.a0c << 4);
+      ICS_CHECK16(pw, lo8, lo8 + (g.nch << 4));
+      ICS_CHECK16(pw + len - 1, lo8, lo8 + (g.nch << 4));
+    }
+#endif
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4*>(pw), 0, int(len * 16u), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)  // aux 2: non-temporal
+      v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 1024, 2));
+  };
+  u32x4 b0[4], b1[4], b2[4];
+
+  // ---- stream wave: tile g (points in buffer buf), the next tile gn's first
+  // two windows loaded by the last window group
+  auto stream_tile = [&](const Geo& g, const Geo& gn, uint32_t buf) {
+    const uint32_t npt = g.m + 1;
+    uint32_t cur = s_first[buf][wv];  // the first point not yet placed (wave-uniform)
+    uint32_t pbase = cur;             // this lane holds point pbase + lane: its chunk (tile-relative) and byte
+    uint64_t pc = ~uint64_t(0);
+    uint32_t pb = 0;
+    auto hold = [&]() {
+      const uint32_t pi = pbase + lane;
+      const uint64_t x = pi < npt ? s_pt[buf][pi] : ~uint64_t(0);
+      pc = pi < npt ? (x >> 4) - g.a0c : ~uint64_t(0);
+      pb = uint32_t(x) & 15u;
+    };
+    hold();
+    uint32_t ce = 0, co = 0;  // this wave's sums so far
+    auto window = [&](uint64_t k, const u32x4 (&v)[4]) {
+      const uint64_t c0 = g.wc0 + k * kWinChunks;
+      if (c0 >= g.wc1) return;  // uniform: a padding window
+      const uint64_t c1 = g.wc1 - c0 < kWinChunks ? g.wc1 : c0 + kWinChunks;
+      // chunks to LDS as loaded (chunk r = 64 u + lane), read back four
+      // consecutive ones per lane (4 lane .. 4 lane + 3): a lane prefix of
+      // three adds and ONE wave scan per role give every chunk's prefix
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s_raw[wv][uint32_t(u) * 64u + lane] = v[u];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      uint32_t pe[4], po[4], te = 0, to = 0;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint32_t ev = 0, od = 0;
+        acc_chunk(s_raw[wv][4u * lane + uint32_t(j)], ev, od);
+        pe[j] = te;
+        po[j] = to;
+        te += ev;
+        to += od;
+      }
+      const uint32_t ie = wave_prefix_incl(te), io = wave_prefix_incl(to);
+      const uint32_t xe = ce + ie - te, xo = co + io - to;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        s_pre[wv][4u * lane + uint32_t(j)][0] = xe + pe[j];
+        s_pre[wv][4u * lane + uint32_t(j)][1] = xo + po[j];
+      }
+      ce += __builtin_amdgcn_readlane(ie, 63);
+      co += __builtin_amdgcn_readlane(io, 63);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      // the points in this window: the held ones from `cur` on whose chunk
+      // is below c1 (sorted, so a prefix of them); a new set of 64 when all
+      // held points were placed
+      for (;;) {  // uniform
+        const uint32_t pi = pbase + lane;
+        const bool in = pi >= cur && pc < c1;
+        if (in) {
+          const uint32_t k2 = uint32_t(pc - c0);
+          uint32_t fe = s_pre[wv][k2][0], fo = s_pre[wv][k2][1];
+          acc_chunk(s_raw[wv][k2] & byte_range_mask(0u, pb), fe, fo);
+          s_f[buf][pi][0] = fe;
+          s_f[buf][pi][1] = fo;
+        }
+        cur += uint32_t(__builtin_popcountll(__ballot(in)));
+        if (cur < pbase + 64u) break;
+        pbase = cur;
+        hold();
+      }
+      __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
+    };
+    auto load_any = [&](uint64_t k, u32x4 (&v)[4]) {
+      if (k < g.nwin3) load_win(g, k, v);
+      else load_win(gn, k - g.nwin3, v);
+    };
+    for (uint64_t k = 0; k < g.nwin3; k += 3) {  // wave-uniform
+      load_any(k + 2, b2);
+      window(k, b0);
+      load_any(k + 3, b0);
+      window(k + 1, b1);
+      load_any(k + 4, b1);
+      window(k + 2, b2);
+    }
+    if (g.nwin3 == 0) {  // an empty range: the next tile's windows still go out now
+      load_win(gn, 0, b0);
+      load_win(gn, 1, b1);
+    }
+    if (lane == 0) {
+      s_tot[buf][wv][0] = ce;
+      s_tot[buf][wv][1] = co;
+    }
+  };
+
+  // ---- metadata wave: a tile's points into buffer buf and each stream
+  // wave's first point (the number of points below its range)
+  auto load_points = [&](const Geo& g, uint32_t buf) {
+    constexpr uint32_t kRounds = (kTileMax + 64) / 64;
+    uint64_t xs[kRounds];
+#pragma unroll
+    for (uint32_t r = 0; r < kRounds; ++r) {  // every load in flight at once
+      const uint32_t p = r * 64u + lane;
+      xs[r] = off[g.i0 + (p <= g.m ? p : g.m)];
+    }
+    uint32_t below[kSW] = {};
+#pragma unroll
+    for (uint32_t r = 0; r < kRounds; ++r) {
+      const uint32_t p = r * 64u + lane;
+      const bool ok = p <= g.m;
+      const uint64_t x = xs[r];
+      if (ok) s_pt[buf][p] = x;
+      const uint64_t c = (x >> 4) - g.a0c;
+#pragma unroll
+      for (uint32_t w = 1; w < kSW; ++w) {
+        const uint64_t wc0 = g.quarter * w < g.nch ? g.quarter * w : g.nch;
+        below[w] += uint32_t(__builtin_popcountll(__ballot(ok && c < wc0)));
+      }
+    }
+    if (lane < kSW) {
+      uint32_t v = 0;
+#pragma unroll
+      for (uint32_t w = 1; w < kSW; ++w) v = lane == w ? below[w] : v;
+      s_first[buf][lane] = v;
+    }
+  };
+
+  // ---- finishing a tile: segments t0, t0 + step, ..., R of them per thread
+  // (the metadata wave alone: 2 + 2 per lane; the last tile: one per thread
+  // of the block); the per-segment inputs of all R loaded first, then summed
+  // and stored
+  auto finish = [&](const Geo& g, uint32_t buf, uint32_t t0, uint32_t step, auto R_) {
+    constexpr uint32_t R = decltype(R_)::value;
+    uint32_t w[R][7];
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t t = t0 + r * step;
+      const uint64_t i = g.i0 + (t < g.m ? t : 0u);
+      if constexpr (OP == kTileSum) {
+        w[r][0] = a.init[i * a.init_step];
+        w[r][1] = a.odd[i * a.odd_step];
+      } else {
+        const uint32_t* rec = reinterpret_cast<const uint32_t*>(a.msgs + i);
+#pragma unroll
+        for (int k = 0; k < 7; ++k) w[r][k] = rec[k];
+      }
+    }
+    uint32_t te[kSW + 1], to[kSW + 1];  // the stream waves' totals before wave w
+    te[0] = to[0] = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kSW; ++q) {
+      te[q + 1] = te[q] + s_tot[buf][q][0];
+      to[q + 1] = to[q] + s_tot[buf][q][1];
+    }
+    auto F = [&](uint32_t p, uint64_t x, uint32_t& fe, uint32_t& fo) {
+      const uint64_t c = (x >> 4) - g.a0c;
+      if (c >= g.nch) {  // the aligned end of the last chunk: every byte is below it
+        fe = te[kSW];
+        fo = to[kSW];
+        return;
+      }
+      const uint32_t owner = uint32_t(c >= g.quarter) + uint32_t(c >= 2 * g.quarter) + uint32_t(c >= 3 * g.quarter);
+      uint32_t be = 0, bo = 0;
+#pragma unroll
+      for (uint32_t q = 1; q < kSW; ++q) {
+        be = owner == q ? te[q] : be;
+        bo = owner == q ? to[q] : bo;
+      }
+      fe = s_f[buf][p][0] + be;
+      fo = s_f[buf][p][1] + bo;
+    };
+    static_assert(kSW == 4, "F's owner: three quarter boundaries");
+#pragma unroll
+    for (uint32_t r = 0; r < R; ++r) {
+      const uint32_t t = t0 + r * step;
+      if (t >= g.m) break;
+      const uint64_t i = g.i0 + t;
+      const uint64_t s = s_pt[buf][t], e = s_pt[buf][t + 1];
+      uint32_t fle, flo, fhe, fho;
+      F(t, s, fle, flo);
+      F(t + 1, e, fhe, fho);
+      const uint32_t se = fhe - fle, so = fho - flo;  // sums of [s, e), roles by address
+      if constexpr (OP == kTileSum) {
+        const uint32_t sum = w[r][0] + combine_roles(se, so, (uint32_t(s) ^ w[r][1]) & 1u);
+        if (OUT == 0)
+          static_cast<uint16_t*>(a.out)[i] = fold_value(sum);
+        else
+          static_cast<uint32_t*>(a.out)[i] = sum;
+      } else {
+        uint32_t h[10], ipc = 0, tcv = 0;
+        wrap_header(u32x4{w[r][0], w[r][1], w[r][2], w[r][3]}, w[r][4], w[r][5], w[r][6] & 0xffffu, e - s,
+                    combine_roles(se, so, uint32_t(s) & 1u), h, ipc, tcv);
+        uint2* dst = reinterpret_cast<uint2*>(a.hdr_out + i * 10);
+#pragma unroll
+        for (int k = 0; k < 5; ++k) dst[k] = uint2{h[2 * k], h[2 * k + 1]};
+        if (a.ip_ck) a.ip_ck[i] = uint16_t(ipc);
+        if (a.tcp_ck) a.tcp_ck[i] = uint16_t(tcv);
+      }
+    }
+  };
+
+  // ---- the block's tiles: block_order's tile, then every gridDim-th; one
+  // block barrier per tile (B_j): before it the stream waves have summed
+  // tile j and the metadata wave has finished tile j - 1 and loaded tile
+  // j + 1's points; after it the stream waves run tile j + 1 while the
+  // metadata wave finishes tile j and loads tile j + 2's points into the
+  // buffer tile j used
+  uint64_t tile = block_order(remap);
+  if (tile >= ntiles) return;  // block-uniform, before any barrier
+  Geo g = geo_of(tile);
+  if (meta) {
+    load_points(g, 0);
+  } else {
+    load_win(g, 0, b0);
+    load_win(g, 1, b1);
+  }
+  Geo gn = geo_of(tile + gridDim.x);
+  __syncthreads();
+  if (meta && gn.m) load_points(gn, 1);
+  for (uint32_t j = 0;; ++j) {  // block-uniform
+    const uint32_t buf = j & 1u;
+    if (!meta) stream_tile(g, gn, buf);
+    __syncthreads();  // B_j
+    if (gn.m == 0) {  // the block's last tile: every thread finishes it
+      finish(g, buf, tid, kStreamBlock, std::integral_constant<uint32_t, 1>{});
+      break;
+    }
+    if (meta) {  // four segments per lane, in two halves (registers)
+      finish(g, buf, lane, 64u, std::integral_constant<uint32_t, 2>{});
+      finish(g, buf, lane + 128u, 64u, std::integral_constant<uint32_t, 2>{});
+      const Geo g2 = geo_of(tile + 2ull * gridDim.x);
+      if (g2.m) load_points(g2, buf);
+    }
+    tile += gridDim.x;
+    g = gn;
+    gn = geo_of(tile + gridDim.x);
+  }
+}
+
 // ------------------------------------------------- workload spec ---------
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 
@@ -2530,12 +2866,31 @@ hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_ou
   return hipGetLastError();
 }
 
+// k_stream for the operations whose points are the offsets (checksum, the
+// headers-apart wrap): a grid of at most the resident blocks (every
+// gridDim-th tile per block, the prefetch running across tiles), or
+// max_blocks
+
 template <int OP, int OUT>
-hipError_t launch_tile_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint32_t max_blocks, hipStream_t st) {
+hipError_t launch_stream_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint32_t max_blocks, hipStream_t st) {
+  const uint64_t tiles = (sp.n + T - 1) / T;
+  const uint64_t cap = max_blocks ? max_blocks : kStreamResident;
+  const uint32_t blocks = uint32_t(tiles < cap ? tiles : cap);
+  hipLaunchKernelGGL((k_stream<OP, OUT>), dim3(blocks), dim3(kStreamBlock), 0, st, sp.bytes, sp.offsets, sp.n, T, a,
+                     g_xcd_remap);
+  return hipGetLastError();
+}
+
+template <int OP, int OUT>
+hipError_t launch_tile_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint32_t max_blocks, hipStream_t st,
+                         bool stream = false) {
   if (!sp.offsets || sp.list || sp.n == 0 || T == 0 || T > kTileMax) return hipErrorInvalidValue;
+  if constexpr (OP == kTileSum || OP == kTileWrapApart) {
+    if (stream) return launch_stream_t<OP, OUT>(sp, a, T, max_blocks, st);
+  }
   const uint64_t tiles = (sp.n + T - 1) / T;
   // one block per tile by default (measured faster than a persistent grid of
-  // the resident blocks, tools/ab_tile.py); a capped grid (max_blocks) takes
+  // the resident blocks, git 7692616:tools/ab_tile.py); a capped grid (max_blocks) takes
   // every gridDim-th tile with the next one's loads overlapping its own
   const uint64_t cap = max_blocks ? max_blocks : kMaxGridBlocks;
   const uint32_t blocks = uint32_t(tiles < cap ? tiles : cap);
@@ -2547,7 +2902,7 @@ hipError_t launch_tile_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint3
 }  // namespace
 
 // Geometry choice from the (average) segment length, measured on MI355X
-// (tools/sweep_geometry.py; profiles/r1_sweep_geometry.jsonl,
+// (git 7692616:tools/sweep_geometry.py; profiles/r1_sweep_geometry.jsonl,
 // r1_sweep_line_grid.jsonl, r1_sweep_small.jsonl).  Small segments
 // (<= ~270 B): k_checksum_small with about one load slot per 16-byte chunk
 // and 2 segments per lane group in flight (64 B = 4 lanes x 1 load x 2).
@@ -2557,7 +2912,7 @@ hipError_t launch_tile_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint3
 // 8 loads), and 64 x 8 (8 KiB per wave step) looping for long segments.
 // Interior chunks stream non-temporally (read once).
 //
-// Round 2 (tools/sweep_geometry.py, profiles/r2_sweep_mtu.jsonl,
+// Round 2 (git 7692616:tools/sweep_geometry.py, profiles/r2_sweep_mtu.jsonl,
 // r2_sweep_mid.jsonl; 1 M segments, GB/s of the best vs the round-1 pick):
 // slots close above the chunks a line-anchored segment spans win — 1000 B
 // (16,5) 7569 vs (16,8) 6577, 1040 B (16,5) 7526 vs 6394, 1200 B (16,6) 7571
@@ -2797,15 +3152,15 @@ hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t*
 }
 
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t T, uint32_t max_blocks, hipStream_t st) {
+                                uint32_t T, uint32_t max_blocks, hipStream_t st, bool stream) {
   TileArgs a{};
   a.init = init ? init : static_cast<const uint32_t*>(sp.zero16);
   a.odd = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
   a.init_step = init ? 1u : 0u;
   a.odd_step = odd ? 1u : 0u;
   a.out = out;
-  return out_kind == 0 ? launch_tile_t<kTileSum, 0>(sp, a, T, max_blocks, st)
-                       : launch_tile_t<kTileSum, 1>(sp, a, T, max_blocks, st);
+  return out_kind == 0 ? launch_tile_t<kTileSum, 0>(sp, a, T, max_blocks, st, stream)
+                       : launch_tile_t<kTileSum, 1>(sp, a, T, max_blocks, st, stream);
 }
 
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
@@ -2819,13 +3174,13 @@ hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16
 }
 
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st) {
+                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st, bool stream) {
   TileArgs a{};
   a.msgs = msgs;
   a.hdr_out = hdr_out;
   a.ip_ck = ip_ck;
   a.tcp_ck = tcp_ck;
-  return hdr_out ? launch_tile_t<kTileWrapApart, 0>(sp, a, T, max_blocks, st)
+  return hdr_out ? launch_tile_t<kTileWrapApart, 0>(sp, a, T, max_blocks, st, stream)
                  : launch_tile_t<kTileWrap, 0>(sp, a, T, max_blocks, st);
 }
 

@@ -33,7 +33,8 @@ def engine_with(force=None, debug=False):
     """Generator: an Engine created with the ICSUM_FORCE test hook set to
     `force` ({key: value}: lps, unroll, mode, segs, bin, bin_min, bin_plan,
     bin_blocks, last_bin_lps, last_bin_blocks, dense_segs, twoclass,
-    wrap_passes, xcd_remap, zero_copy_max — INTEGRATION.md §6), read once at
+    wrap_passes, xcd_remap, zero_copy_max, tile, tile_segs, tile_blocks, stream,
+    poison_ticket — INTEGRATION.md §6), read once at
     ics_create."""
     import torch
 
@@ -48,6 +49,7 @@ def engine_with(force=None, debug=False):
         os.environ.pop("ICSUM_FORCE", None)
         if old is not None:
             os.environ["ICSUM_FORCE"] = old
+    eng.forced = dict(force or {})
     yield eng
     torch.cuda.synchronize()
     eng.close()

@@ -22,9 +22,15 @@ pytestmark = pytest.mark.gpu
 
 # automatic tile size on the persistent grid; one segment per tile; odd sizes;
 # few blocks, each streaming many tiles back to back (the next tile's first
-# windows in flight across every tile boundary)
+# windows in flight across every tile boundary; on k_stream the metadata wave
+# finishing tile j while the stream waves run tile j + 1, both point buffers
+# in turn) — the checksum and headers-apart wrap on k_stream (default) and on
+# k_tile (stream=0)
 TILE_FORCE = [{"tile": 1}, {"tile": 1, "tile_segs": 1}, {"tile": 1, "tile_segs": 7},
-              {"tile": 1, "tile_segs": 7, "tile_blocks": 5}, {"tile": 1, "tile_segs": 256, "tile_blocks": 3}]
+              {"tile": 1, "tile_segs": 7, "tile_blocks": 5}, {"tile": 1, "tile_segs": 256, "tile_blocks": 3},
+              {"tile": 1, "tile_segs": 64, "tile_blocks": 1}, {"tile": 1, "stream": 0},
+              {"tile": 1, "tile_segs": 7, "tile_blocks": 5, "stream": 0}]
+ICS_TILE_STREAM = 4
 
 
 @pytest.fixture(scope="module", params=TILE_FORCE, ids=force_id)
@@ -32,8 +38,14 @@ def tile_eng(request):
     yield from engine_with(request.param)
 
 
-def _assert_tile(eng):
-    assert eng.dispatch_info()["kernel"] == "tile"
+def _assert_tile(eng, streamable=True):
+    """the tile launch ran, in the form the engine's hooks ask for: the
+    checksum and headers-apart wrap (`streamable`) on k_stream unless
+    stream=0, the fused IPv4 kernel and the in-place wrap on k_tile"""
+    info = eng.dispatch_info()
+    assert info["kernel"] == "tile", info
+    stream = streamable and getattr(eng, "forced", {}).get("stream", 1) != 0
+    assert bool(info["unroll"] & ICS_TILE_STREAM) == stream, info
 
 
 def test_tile_kats(tile_eng):
@@ -154,7 +166,7 @@ def test_tile_ipv4_vs_oracle(tile_eng, orc, mix):
         want = orc.ipv4_tcp_batch(hb, n, mode, offsets=off)
         d = _t(buf)
         ip, tcp, st = tile_eng.ipv4_tcp_batch(d, mode, offsets=_t(off))
-        _assert_tile(tile_eng)
+        _assert_tile(tile_eng, streamable=False)
         assert (_u16(ip) == want[0]).all(), (mix, mode)
         assert (_u16(tcp) == want[1]).all(), (mix, mode)
         assert (st.cpu().numpy() == want[2]).all(), (mix, mode)
@@ -179,7 +191,7 @@ def test_tile_wrap_reproduces_reference_wire_bytes(tile_eng, lead):
     ip = torch.empty(len(cases), dtype=torch.int16, device="cuda")
     tcp = torch.empty(len(cases), dtype=torch.int16, device="cuda")
     tile_eng.tcp_wrap_batch(d, dm, n=len(cases), offsets=_t(off), ip_ck=ip, tcp_ck=tcp)
-    _assert_tile(tile_eng)
+    _assert_tile(tile_eng, streamable=False)
     got = d.cpu().numpy()
     for i, c in enumerate(cases):
         assert got[off[i]:off[i + 1]].tobytes().hex() == c["wire"], i
@@ -235,7 +247,9 @@ def test_tile_config4_full_size():
         assert hashlib.sha256(out.tobytes()).hexdigest() == g["out_sha256"]
 
 
-@pytest.fixture(scope="module", params=[{"tile": 1}, {"tile": 1, "tile_segs": 7, "tile_blocks": 5}], ids=force_id)
+@pytest.fixture(scope="module", params=[{"tile": 1}, {"tile": 1, "tile_segs": 7, "tile_blocks": 5},
+                                        {"tile": 1, "tile_segs": 64, "tile_blocks": 1},
+                                        {"tile": 1, "stream": 0}], ids=force_id)
 def tile_apart(request):
     yield from engine_with(request.param)
 
@@ -256,7 +270,7 @@ def test_tile_wrap_headers_apart(tile_apart, orc, lead):
     hd = torch.empty(len(cases) * 40, dtype=torch.uint8, device="cuda")
     dm = torch.from_numpy(_msgs_from_cases(cases).view(np.uint8).copy()).cuda()
     tile_apart.tcp_wrap_headers(_t(buf), dm, hd, n=len(cases), offsets=_t(off))
-    assert tile_apart.dispatch_info()["kernel"] == "tile"
+    _assert_tile(tile_apart)
     h = hd.cpu().numpy()
     for i, c in enumerate(cases):
         assert h[40 * i:40 * i + 40].tobytes().hex() == c["wire"][:80], i

@@ -1,0 +1,115 @@
+#!/usr/bin/env python3
+"""Dev measurement (round 5): the tile launch on k_stream (stream waves + a
+metadata wave per block, persistent grid) against k_tile, on the VERDICT r4
+shapes — the transmit mix (payloads of 0..1000 bytes: 40..1040-byte
+datagrams, or the payloads alone for the headers-apart wrap) at 256 Ki and
+1 M segments, and constant 770-byte segments given as offsets — for the
+checksum and ics_tcp_wrap_headers.  Each row: back to back (events around 20
+calls, median of 5 rounds, two batches rotated) and alone (events around one
+call after a synchronize, median of 40).  Variants through ICSUM_FORCE:
+k_tile at the automatic T, k_stream at the automatic T and at fixed T / grid
+caps.  Usage: python tools/ab_stream.py [rows] [variants]"""
+import json
+import os
+import statistics
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from _force import engine  # noqa: E402
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+PEAK = 8.0e12
+R = 2
+
+
+def b2b(fn, iters=20, rounds=5):
+    st = torch.cuda.current_stream()
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < 0.15:
+        for i in range(8):
+            fn(i)
+        torch.cuda.synchronize()
+    ts = []
+    for _ in range(rounds):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record(st)
+        for i in range(iters):
+            fn(i)
+        b.record(st)
+        torch.cuda.synchronize()
+        ts.append(a.elapsed_time(b) / 1e3 / iters)
+    return statistics.median(ts)
+
+
+def alone(fn, calls=40):
+    st = torch.cuda.current_stream()
+    ts = []
+    for i in range(calls + 5):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        torch.cuda.synchronize()
+        a.record(st)
+        fn(i)
+        b.record(st)
+        torch.cuda.synchronize()
+        if i >= 5:
+            ts.append(a.elapsed_time(b) / 1e3)
+    return statistics.median(ts)
+
+
+def batch(eng, lens, seed):
+    off = np.zeros(lens.size + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    d = eng.fill_bytes(torch.empty(int(off[-1]) + 16, dtype=torch.uint8, device="cuda"), seed)
+    return d, torch.from_numpy(off.view(np.int64)).cuda(), int(off[-1])
+
+
+VARIANTS = {
+    "tile": {"tile": 1, "stream": 0},
+    "stream": {"tile": 1},
+    "stream_T64": {"tile": 1, "tile_segs": 64},
+    "stream_T128": {"tile": 1, "tile_segs": 128},
+    "stream_T192": {"tile": 1, "tile_segs": 192},
+    "stream_T256": {"tile": 1, "tile_segs": 256},
+    "stream_T128_onepertile": {"tile": 1, "tile_segs": 128, "tile_blocks": 1 << 20},
+}
+
+
+def main():
+    rows = (sys.argv[1] if len(sys.argv) > 1 else "tx256k,tx1m,u770_256k,u770_1m").split(",")
+    names = (sys.argv[2] if len(sys.argv) > 2 else ",".join(VARIANTS)).split(",")
+    engs = {k: engine(**VARIANTS[k]) for k in names}
+    auto = engine()
+    rng = np.random.default_rng(3)
+    shapes = {"tx256k": (1 << 18, "tx"), "tx1m": (1 << 20, "tx"), "u770_256k": (1 << 18, "u770"),
+              "u770_1m": (1 << 20, "u770")}
+    for row in rows:
+        n, kind = shapes[row]
+        pays = rng.integers(0, 1001, n) if kind == "tx" else np.full(n, 730)
+        out = torch.empty(n, dtype=torch.int16, device="cuda")
+        hd = torch.empty(n * 40, dtype=torch.uint8, device="cuda")
+        msgs = torch.from_numpy(rng.integers(0, 256, n * 28, dtype=np.uint8)).cuda()
+        for op in ("checksum", "wrap_apart"):
+            lens = pays + 40 if op == "checksum" else pays
+            bs = [batch(auto, lens, 11 + r) for r in range(R)]
+            nb = bs[0][2]
+            for name, e in engs.items():
+                if op == "checksum":
+                    fn = lambda i, e=e: e.checksum_batch(bs[i % R][0], n=n, offsets=bs[i % R][1], out=out)
+                else:
+                    fn = lambda i, e=e: e.tcp_wrap_headers(bs[i % R][0], msgs, hd, n=n, offsets=bs[i % R][1])
+                tb = b2b(fn)
+                ta = alone(fn)
+                info = e.dispatch_info()
+                print(json.dumps({"row": f"{row}_{op}", "variant": name, "bytes": nb, "us_b2b": round(tb * 1e6, 2),
+                                  "frac_b2b": round(nb / tb / PEAK, 4), "us_alone": round(ta * 1e6, 2),
+                                  "frac_alone": round(nb / ta / PEAK, 4), "kernel": info["kernel"],
+                                  "T": info["lps"], "op": info["unroll"]}), flush=True)
+            del bs
+            torch.cuda.empty_cache()
+
+
+if __name__ == "__main__":
+    main()
