@@ -1820,6 +1820,16 @@ constexpr uint32_t kTileMax = kBlock;          // segments per tile
 constexpr uint32_t kWinChunks = 256;          // one wave window: 4 KiB, four loads per lane
 constexpr int kTileSum = 0, kTileIpv4 = 1, kTileWrap = 2, kTileWrapApart = 3;
 
+// LDS slot of chunk r of a window (16-byte slots): r ^ ((r >> 4) & 3).  The
+// window is written as loaded (lane l: chunks 64 u + l, eight contiguous
+// lanes per ds_write_b128 group: still conflict-free) and read back four
+// consecutive chunks per lane (lane L: 4 L .. 4 L + 3); without the swizzle
+// every ds_read_b128 lane group (16 lanes, banks (a / 4) mod 64) of that
+// read hits only 4 distinct 16-byte bank groups — 4-way conflicts
+// (SQ_LDS_BANK_CONFLICT 15 M cycles per 1 M x 770 B launch,
+// profiles/r5_pmc_stream.jsonl); with it each group's 16 lanes cover all 16.
+__device__ __forceinline__ uint32_t win_slot(uint32_t r) { return r ^ ((r >> 4) & 3u); }
+
 // inclusive prefix sum over the 64 lanes of a wave: row shifts 1, 2, 4, 8,
 // then row 0's total into row 1 and row 2's into row 3, then rows 0-1's into
 // rows 2-3
@@ -2047,7 +2057,7 @@ __global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, co
         const uint32_t r = uint32_t(u) * 64u + lane;
         u32x4 x = v[u];  // zeros past the range
         if (c0 == 0 && r == 0) x &= m0;
-        s_raw[wv][r] = x;
+        s_raw[wv][win_slot(r)] = x;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
@@ -2056,7 +2066,7 @@ __global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, co
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         uint32_t ev = 0, od = 0;
-        acc_chunk(s_raw[wv][4u * lane + uint32_t(j)], ev, od);
+        acc_chunk(s_raw[wv][win_slot(4u * lane + uint32_t(j))], ev, od);
         pe[j] = te;
         po[j] = to;
         te += ev;
@@ -2083,7 +2093,7 @@ __global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, co
         if (in) {
           const uint32_t k2 = uint32_t(c - c0);
           uint32_t pe = s_pre[wv][k2][0], po = s_pre[wv][k2][1];
-          acc_chunk(s_raw[wv][k2] & byte_range_mask(0u, uint32_t(x) & 15u), pe, po);
+          acc_chunk(s_raw[wv][win_slot(k2)] & byte_range_mask(0u, uint32_t(x) & 15u), pe, po);
           s_f[pi][0] = pe;
           s_f[pi][1] = po;
         }
@@ -2224,8 +2234,9 @@ __global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, co
 // vmcnt(0) in the ISA) and ran one to two windows deep inside a tile.
 // k_stream gives the roles to different waves of one block:
 //   * four stream waves issue NOTHING but window loads (no stores, no other
-//     loads): three register sets, two windows in flight while one is summed,
-//     and the prefetch runs on across tile boundaries;
+//     loads): three register sets, each reloaded as soon as its window is in
+//     LDS — three windows in flight while one is summed — and the prefetch
+//     runs on across tile boundaries;
 //   * a fifth, metadata wave loads the next tile's offsets into LDS (with the
 //     first point of each stream wave's range, so the stream waves search
 //     nothing) and, while the stream waves run tile j + 1, finishes tile j:
@@ -2259,8 +2270,8 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
   const uint64_t ntiles = (n + T - 1) / T;
   // A tile's geometry (scalar loads): segments, the 16-byte chunks of its
   // bytes [first & ~15, off[i0 + m]), this wave's quarter of them and its
-  // windows (a multiple of 3: the window loop is unrolled by 3); the
-  // metadata wave's range is empty
+  // windows (a multiple of 3, at least 3: the window loop is unrolled by 3);
+  // the metadata wave's range is empty
   struct Geo {
     uint64_t i0, a0c, nch, quarter, wc0, wc1, nwin3;
     uint32_t m;
@@ -2278,7 +2289,10 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
     const uint64_t w = meta ? kSW : wv;
     g.wc0 = g.quarter * w < g.nch ? g.quarter * w : g.nch;
     g.wc1 = g.wc0 + g.quarter < g.nch ? g.wc0 + g.quarter : g.nch;
-    g.nwin3 = ((g.wc1 - g.wc0 + kWinChunks - 1) / kWinChunks + 2) / 3 * 3;
+    // at least one group of three, so an empty range still issues the next
+    // tile's first windows through the loop's own load sites
+    const uint64_t nw3 = ((g.wc1 - g.wc0 + kWinChunks - 1) / kWinChunks + 2) / 3 * 3;
+    g.nwin3 = nw3 ? nw3 : 3;
     return g;
   };
   // window k of a stream wave's range (as k_tile: raw buffer loads through a
@@ -2304,8 +2318,10 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
   };
   u32x4 b0[4], b1[4], b2[4];
 
-  // ---- stream wave: tile g (points in buffer buf), the next tile gn's first
-  // two windows loaded by the last window group
+  // ---- stream wave: tile g (points in buffer buf); three register sets,
+  // each reloaded as soon as its window is in LDS, so three windows are in
+  // flight while one is summed; the last window group loads the next tile
+  // gn's first three
   auto stream_tile = [&](const Geo& g, const Geo& gn, uint32_t buf) {
     const uint32_t npt = g.m + 1;
     uint32_t cur = s_first[buf][wv];  // the first point not yet placed (wave-uniform)
@@ -2320,15 +2336,25 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
     };
     hold();
     uint32_t ce = 0, co = 0;  // this wave's sums so far
-    auto window = [&](uint64_t k, const u32x4 (&v)[4]) {
+    auto load_any = [&](uint64_t k, u32x4 (&v)[4]) {
+      if (k < g.nwin3) load_win(g, k, v);
+      else load_win(gn, k - g.nwin3, v);
+    };
+    auto window = [&](uint64_t k, u32x4 (&v)[4], uint64_t knext) {
       const uint64_t c0 = g.wc0 + k * kWinChunks;
-      if (c0 >= g.wc1) return;  // uniform: a padding window
-      const uint64_t c1 = g.wc1 - c0 < kWinChunks ? g.wc1 : c0 + kWinChunks;
+      const bool live = c0 < g.wc1;  // uniform; else a padding window
       // chunks to LDS as loaded (chunk r = 64 u + lane), read back four
       // consecutive ones per lane (4 lane .. 4 lane + 3): a lane prefix of
       // three adds and ONE wave scan per role give every chunk's prefix
+      if (live) {
 #pragma unroll
-      for (int u = 0; u < 4; ++u) s_raw[wv][uint32_t(u) * 64u + lane] = v[u];
+        for (int u = 0; u < 4; ++u) s_raw[wv][win_slot(uint32_t(u) * 64u + lane)] = v[u];
+      }
+      // the registers are free: window knext goes out now (one load site for
+      // both paths, so the loads' destination is the same registers)
+      load_any(knext, v);
+      if (!live) return;
+      const uint64_t c1 = g.wc1 - c0 < kWinChunks ? g.wc1 : c0 + kWinChunks;
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -2336,7 +2362,7 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         uint32_t ev = 0, od = 0;
-        acc_chunk(s_raw[wv][4u * lane + uint32_t(j)], ev, od);
+        acc_chunk(s_raw[wv][win_slot(4u * lane + uint32_t(j))], ev, od);
         pe[j] = te;
         po[j] = to;
         te += ev;
@@ -2363,7 +2389,7 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
         if (in) {
           const uint32_t k2 = uint32_t(pc - c0);
           uint32_t fe = s_pre[wv][k2][0], fo = s_pre[wv][k2][1];
-          acc_chunk(s_raw[wv][k2] & byte_range_mask(0u, pb), fe, fo);
+          acc_chunk(s_raw[wv][win_slot(k2)] & byte_range_mask(0u, pb), fe, fo);
           s_f[buf][pi][0] = fe;
           s_f[buf][pi][1] = fo;
         }
@@ -2374,21 +2400,10 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
       }
       __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
     };
-    auto load_any = [&](uint64_t k, u32x4 (&v)[4]) {
-      if (k < g.nwin3) load_win(g, k, v);
-      else load_win(gn, k - g.nwin3, v);
-    };
     for (uint64_t k = 0; k < g.nwin3; k += 3) {  // wave-uniform
-      load_any(k + 2, b2);
-      window(k, b0);
-      load_any(k + 3, b0);
-      window(k + 1, b1);
-      load_any(k + 4, b1);
-      window(k + 2, b2);
-    }
-    if (g.nwin3 == 0) {  // an empty range: the next tile's windows still go out now
-      load_win(gn, 0, b0);
-      load_win(gn, 1, b1);
+      window(k, b0, k + 3);
+      window(k + 1, b1, k + 4);
+      window(k + 2, b2, k + 5);
     }
     if (lane == 0) {
       s_tot[buf][wv][0] = ce;
@@ -2396,16 +2411,18 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
     }
   };
 
-  // ---- metadata wave: a tile's points into buffer buf and each stream
-  // wave's first point (the number of points below its range)
-  auto load_points = [&](const Geo& g, uint32_t buf) {
-    constexpr uint32_t kRounds = (kTileMax + 64) / 64;
-    uint64_t xs[kRounds];
+  // ---- metadata wave: a tile's points (fetch: every load in flight at
+  // once; store: into buffer buf, with each stream wave's first point = the
+  // number of points below its range)
+  constexpr uint32_t kRounds = (kTileMax + 64) / 64;
+  auto fetch_points = [&](const Geo& g, uint64_t (&xs)[kRounds]) {
 #pragma unroll
-    for (uint32_t r = 0; r < kRounds; ++r) {  // every load in flight at once
+    for (uint32_t r = 0; r < kRounds; ++r) {
       const uint32_t p = r * 64u + lane;
       xs[r] = off[g.i0 + (p <= g.m ? p : g.m)];
     }
+  };
+  auto store_points = [&](const Geo& g, uint32_t buf, const uint64_t (&xs)[kRounds]) {
     uint32_t below[kSW] = {};
 #pragma unroll
     for (uint32_t r = 0; r < kRounds; ++r) {
@@ -2429,12 +2446,13 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
   };
 
   // ---- finishing a tile: segments t0, t0 + step, ..., R of them per thread
-  // (the metadata wave alone: 2 + 2 per lane; the last tile: one per thread
-  // of the block); the per-segment inputs of all R loaded first, then summed
-  // and stored
-  auto finish = [&](const Geo& g, uint32_t buf, uint32_t t0, uint32_t step, auto R_) {
-    constexpr uint32_t R = decltype(R_)::value;
-    uint32_t w[R][7];
+  // (the metadata wave alone: four per lane; the last tile: one per thread
+  // of the block).  fetch: the per-segment words (checksum: init, parity;
+  // wrap: the 28-byte record), every load in flight at once; emit: F at the
+  // two points, the segment's sums, its output
+  constexpr uint32_t kWords = OP == kTileSum ? 2 : 7;
+  auto fetch = [&](const Geo& g, uint32_t t0, uint32_t step, auto& w) {
+    constexpr uint32_t R = std::extent<std::remove_reference_t<decltype(w)>>::value;
 #pragma unroll
     for (uint32_t r = 0; r < R; ++r) {
       const uint32_t t = t0 + r * step;
@@ -2448,7 +2466,10 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
         for (int k = 0; k < 7; ++k) w[r][k] = rec[k];
       }
     }
-    uint32_t te[kSW + 1], to[kSW + 1];  // the stream waves' totals before wave w
+  };
+  auto emit = [&](const Geo& g, uint32_t buf, uint32_t t0, uint32_t step, const auto& w) {
+    constexpr uint32_t R = std::extent<std::remove_reference_t<decltype(w)>>::value;
+    uint32_t te[kSW + 1], to[kSW + 1];  // the stream waves' totals before wave q
     te[0] = to[0] = 0;
 #pragma unroll
     for (uint32_t q = 0; q < kSW; ++q) {
@@ -2504,40 +2525,64 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
 
   // ---- the block's tiles: block_order's tile, then every gridDim-th; one
   // block barrier per tile (B_j): before it the stream waves have summed
-  // tile j and the metadata wave has finished tile j - 1 and loaded tile
+  // tile j and the metadata wave has finished tile j - 1 and stored tile
   // j + 1's points; after it the stream waves run tile j + 1 while the
-  // metadata wave finishes tile j and loads tile j + 2's points into the
-  // buffer tile j used
+  // metadata wave finishes tile j and stores tile j + 2's points into the
+  // buffer tile j used.  The two roles run their own loops (same barriers,
+  // same tiles), so the compiler's waits in the stream loop never see the
+  // metadata wave's loads.
   uint64_t tile = block_order(remap);
   if (tile >= ntiles) return;  // block-uniform, before any barrier
   Geo g = geo_of(tile);
+  Geo gn = geo_of(tile + gridDim.x);
+  uint32_t buf = 0;
   if (meta) {
-    load_points(g, 0);
+    uint64_t xs[kRounds];
+    fetch_points(g, xs);
+    store_points(g, 0, xs);
+    __syncthreads();
+    Geo gnn = geo_of(tile + 2ull * gridDim.x);
+    if (gn.m) {
+      fetch_points(gn, xs);
+      store_points(gn, 1, xs);
+    }
+    for (;;) {
+      __syncthreads();  // B_j
+      if (gn.m == 0) break;
+      // one memory round trip per tile: tile j's words (four segments per
+      // lane), tile j + 2's points and tile j + 3's geometry all requested
+      // before any is used
+      uint32_t w[(kTileMax + 63) / 64][kWords];
+      fetch(g, lane, 64u, w);
+      if (gnn.m) fetch_points(gnn, xs);
+      const Geo g3 = geo_of(tile + 3ull * gridDim.x);
+      emit(g, buf, lane, 64u, w);
+      if (gnn.m) store_points(gnn, buf, xs);
+      tile += gridDim.x;
+      g = gn;
+      gn = gnn;
+      gnn = g3;
+      buf ^= 1u;
+    }
   } else {
     load_win(g, 0, b0);
     load_win(g, 1, b1);
-  }
-  Geo gn = geo_of(tile + gridDim.x);
-  __syncthreads();
-  if (meta && gn.m) load_points(gn, 1);
-  for (uint32_t j = 0;; ++j) {  // block-uniform
-    const uint32_t buf = j & 1u;
-    if (!meta) stream_tile(g, gn, buf);
-    __syncthreads();  // B_j
-    if (gn.m == 0) {  // the block's last tile: every thread finishes it
-      finish(g, buf, tid, kStreamBlock, std::integral_constant<uint32_t, 1>{});
-      break;
+    load_win(g, 2, b2);
+    __syncthreads();
+    for (;;) {
+      stream_tile(g, gn, buf);
+      __syncthreads();  // B_j
+      if (gn.m == 0) break;
+      tile += gridDim.x;
+      g = gn;
+      gn = geo_of(tile + gridDim.x);
+      buf ^= 1u;
     }
-    if (meta) {  // four segments per lane, in two halves (registers)
-      finish(g, buf, lane, 64u, std::integral_constant<uint32_t, 2>{});
-      finish(g, buf, lane + 128u, 64u, std::integral_constant<uint32_t, 2>{});
-      const Geo g2 = geo_of(tile + 2ull * gridDim.x);
-      if (g2.m) load_points(g2, buf);
-    }
-    tile += gridDim.x;
-    g = gn;
-    gn = geo_of(tile + gridDim.x);
   }
+  // the block's last tile: every thread finishes it
+  uint32_t w1[1][kWords];
+  fetch(g, tid, kStreamBlock, w1);
+  emit(g, buf, tid, kStreamBlock, w1);
 }
 
 // ------------------------------------------------- workload spec ---------

@@ -8,7 +8,8 @@ checksum and ics_tcp_wrap_headers.  Each row: back to back (events around 20
 calls, median of 5 rounds, two batches rotated) and alone (events around one
 call after a synchronize, median of 40).  Variants through ICSUM_FORCE:
 k_tile at the automatic T, k_stream at the automatic T and at fixed T / grid
-caps.  Usage: python tools/ab_stream.py [rows] [variants]"""
+caps.  Usage: python tools/ab_stream.py [rows] [variants] [ops]; AB_LIGHT=1: a
+few calls per row (counter passes)."""
 import json
 import os
 import statistics
@@ -25,10 +26,15 @@ PEAK = 8.0e12
 R = 2
 
 
+LIGHT = bool(os.environ.get("AB_LIGHT"))  # counter passes: a few calls per row
+
+
 def b2b(fn, iters=20, rounds=5):
+    if LIGHT:
+        iters, rounds = 3, 1
     st = torch.cuda.current_stream()
     t0 = time.perf_counter()
-    while time.perf_counter() - t0 < 0.15:
+    while time.perf_counter() - t0 < (0.0 if LIGHT else 0.15):
         for i in range(8):
             fn(i)
         torch.cuda.synchronize()
@@ -45,6 +51,8 @@ def b2b(fn, iters=20, rounds=5):
 
 
 def alone(fn, calls=40):
+    if LIGHT:
+        calls = 2
     st = torch.cuda.current_stream()
     ts = []
     for i in range(calls + 5):
@@ -71,15 +79,16 @@ VARIANTS = {
     "stream": {"tile": 1},
     "stream_T64": {"tile": 1, "tile_segs": 64},
     "stream_T128": {"tile": 1, "tile_segs": 128},
-    "stream_T192": {"tile": 1, "tile_segs": 192},
     "stream_T256": {"tile": 1, "tile_segs": 256},
     "stream_T128_onepertile": {"tile": 1, "tile_segs": 128, "tile_blocks": 1 << 20},
+    "stream_T64_b768": {"tile": 1, "tile_segs": 64, "tile_blocks": 768},
 }
 
 
 def main():
     rows = (sys.argv[1] if len(sys.argv) > 1 else "tx256k,tx1m,u770_256k,u770_1m").split(",")
     names = (sys.argv[2] if len(sys.argv) > 2 else ",".join(VARIANTS)).split(",")
+    ops = (sys.argv[3] if len(sys.argv) > 3 else "checksum,wrap_apart").split(",")
     engs = {k: engine(**VARIANTS[k]) for k in names}
     auto = engine()
     rng = np.random.default_rng(3)
@@ -91,7 +100,7 @@ def main():
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         hd = torch.empty(n * 40, dtype=torch.uint8, device="cuda")
         msgs = torch.from_numpy(rng.integers(0, 256, n * 28, dtype=np.uint8)).cuda()
-        for op in ("checksum", "wrap_apart"):
+        for op in ops:
             lens = pays + 40 if op == "checksum" else pays
             bs = [batch(auto, lens, 11 + r) for r in range(R)]
             nb = bs[0][2]
@@ -109,6 +118,18 @@ def main():
                                   "T": info["lps"], "op": info["unroll"]}), flush=True)
             del bs
             torch.cuda.empty_cache()
+        # the fixed-stride kernel over the same number of bytes (770-byte
+        # rows: the streaming reference a tile launch is measured against)
+        if kind == "u770":
+            ds = [auto.fill_bytes(torch.empty(n * 770, dtype=torch.uint8, device="cuda"), 5, pos0=r * n * 770)
+                  for r in range(R)]
+            fn = lambda i: auto.checksum_batch(ds[i % R], n=n, stride=770, seg_len=770, out=out)
+            tb, ta = b2b(fn), alone(fn)
+            print(json.dumps({"row": f"{row}_fixed_stride", "variant": "k_checksum", "bytes": n * 770,
+                              "us_b2b": round(tb * 1e6, 2), "frac_b2b": round(n * 770 / tb / PEAK, 4),
+                              "us_alone": round(ta * 1e6, 2), "frac_alone": round(n * 770 / ta / PEAK, 4),
+                              "kernel": auto.dispatch_info()["kernel"], "T": 0, "op": 0}), flush=True)
+            del ds
 
 
 if __name__ == "__main__":
