@@ -304,7 +304,7 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
  *   ICS_K_CHECKSUM .. ICS_K_WRAP_2PASS  lanes per segment / loads in flight per lane
  *   ICS_K_TWOCLASS, ICS_K_IPV4_TWOCLASS  long-segment lanes (16) / segments per wave (16 or 32; 8 only under ICSUM_FORCE twoclass=8)
  *   ICS_K_BATCHV  the ICS_BV_* shape of the last launch group / batches in the call
- *   ICS_K_TILE    segments per tile (T) / ICS_TILE_* operation, | ICS_TILE_STREAM for the k_stream form
+ *   ICS_K_TILE    segments per tile (T) / ICS_TILE_* operation, | ICS_TILE_STREAM / ICS_TILE_SPAN for those forms
  *   ICS_K_ROUTER, ICS_K_ROUTER_HDRS  0 / 0 */
 #define ICS_BV_DENSE64 0 /* fixed stride == length == 64 B, 16-byte aligned */
 #define ICS_BV_TINY 1    /* one lane per segment (ACK-sized fixed lengths) */
@@ -317,6 +317,7 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 #define ICS_TILE_WRAP 2
 #define ICS_TILE_WRAP_APART 3
 #define ICS_TILE_STREAM 4 /* or'ed in: k_stream (stream waves + a metadata wave per block; checksum, wrap apart) */
+#define ICS_TILE_SPAN 8   /* or'ed in: k_span (one wave per 63 segments; checksum, wrap apart) */
 typedef struct ics_dispatch_info_t {
   uint64_t plan_hits;      /* lookups that found this batch's landed plan */
   uint64_t plan_misses;    /* lookups that did not (first call, plan still in flight) */

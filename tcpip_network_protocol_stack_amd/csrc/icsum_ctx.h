@@ -96,9 +96,9 @@ struct ics_ctx {
   uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order
   uint32_t twoclass_lds = 0;    // dynamic LDS bytes per two-class block (residency cap; ICSUM_FORCE twoclass_lds)
   uint32_t tile_segs = 0, tile_blocks = 0;
-  // the checksum and headers-apart wrap tile launches on k_stream (a
-  // metadata wave per block, round 5) or, false, on k_tile (ICSUM_FORCE stream)
-  bool tile_stream = true;
+  // the form of the checksum and headers-apart wrap tile launches
+  // (icsum::TileForm: 0 k_tile, 1 k_stream, 2 k_span; ICSUM_FORCE tile_form)
+  int tile_form = 2;
   // device wrap: 0 = two passes (payload sums, then a header launch) when
   // the headers go to an array of their own and the batch has at least
   // kWrapTwoPassMin datagrams, otherwise one pass (headers stored inside the

@@ -35,6 +35,12 @@ uint32_t tile_segs_for(const ics_ctx* ctx, uint64_t n, uint32_t avg) {
   return uint32_t(T);
 }
 
+// ics_dispatch_info's report of the checksum / headers-apart wrap form
+int tile_form_bits(const ics_ctx* ctx) {
+  return ctx->tile_form == icsum::kTileFormStream ? ICS_TILE_STREAM
+         : ctx->tile_form == icsum::kTileFormSpan ? ICS_TILE_SPAN : 0;
+}
+
 bool wrap_two_pass(const ics_ctx* ctx, bool headers_apart, uint64_t n) {
   return ctx->wrap_passes == 2 || (ctx->wrap_passes == 0 && headers_apart && n >= ics_ctx::kWrapTwoPassMin);
 }
@@ -230,8 +236,8 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   if (sp.offsets && ctx->tile == 1) {  // test hook: the tile launch on every offsets batch
     const uint32_t T = tile_segs_for(ctx, sp.n, 0);
     ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st,
-                                                ctx->tile_stream));
-    note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM | (ctx->tile_stream ? ICS_TILE_STREAM : 0), true, 0, 1});
+                                                ctx->tile_form));
+    note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM | tile_form_bits(ctx), true, 0, 1});
     return ICS_OK;
   }
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
@@ -288,8 +294,8 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     if (hit && !mix8 && hit_plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, sp.n, false)) {
       const uint32_t T = tile_segs_for(ctx, sp.n, mix.avg);
       ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st,
-                                                ctx->tile_stream));
-      note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM | (ctx->tile_stream ? ICS_TILE_STREAM : 0), true, 0, 1},
+                                                ctx->tile_form));
+      note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM | tile_form_bits(ctx), true, 0, 1},
            int(hit_plan));
       return replan(ctx, sp, lps, req, st);
     }
@@ -479,9 +485,9 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
   if (sp.offsets && (ctx->tile == 1 || tile_pick)) {  // the wrap (in place or headers apart) as a tile launch
     const uint32_t T = tile_segs_for(ctx, sp.n, plan >= 0 ? mix.avg : 0u);
     ICS_HIP(icsum::launch_tile_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), hdr_out, d_ip_ck, d_tcp_ck,
-                                    T, ctx->tile_blocks, st, ctx->tile_stream));
+                                    T, ctx->tile_blocks, st, ctx->tile_form));
     note(ctx, ICS_K_TILE,
-         {int(T), hdr_out ? ICS_TILE_WRAP_APART | (ctx->tile_stream ? ICS_TILE_STREAM : 0) : ICS_TILE_WRAP, true, 0, 1},
+         {int(T), hdr_out ? ICS_TILE_WRAP_APART | tile_form_bits(ctx) : ICS_TILE_WRAP, true, 0, 1},
          plan);
     return replan(ctx, sp, 64, req, st);
   }
@@ -622,7 +628,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "twoclass" && (v == 0 || v == 8 || v == 16 || v == 32)) ctx->twoclass = int(v);
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
-    else if (k == "stream" && (v == 0 || v == 1)) ctx->tile_stream = v == 1;
+    else if (k == "tile_form" && v >= 0 && v <= 2) ctx->tile_form = int(v);
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);

@@ -1100,6 +1100,12 @@ __device__ __forceinline__ void ipv4_result(uint8_t* __restrict__ dg, uint64_t s
   if (status) status[seg] = uint8_t(v.st);
 }
 
+#ifdef ICSUM_STAMPS
+// diagnostic build only (tools/probe/verify_stamps.hip): per block of
+// k_ipv4_twoclass, s_memrealtime (100 MHz) at its start and end, and HW_ID
+__device__ uint64_t g_block_stamps[1u << 16][3];
+#endif
+
 // What ipv4_result needs, kept per datagram by k_ipv4_twoclass COMPUTE /
 // VERIFY, which computes the block's verdicts at its end one datagram per
 // lane instead of in one lane of each group per claim: the nine dwords as
@@ -1305,6 +1311,9 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
   VRec* const stash = kStash ? recs : nullptr;
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
+#ifdef ICSUM_STAMPS
+  const uint64_t stamp0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
   __syncthreads();
   const uint64_t b0 = uint64_t(block_order(remap)) * kPer;  // the block's datagrams [b0, b0 + kPer)
@@ -1373,6 +1382,15 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
     if (tcp_ck) tcp_ck[i] = uint16_t(tcv);
     if (status) status[i] = uint8_t(st);
   }
+#ifdef ICSUM_STAMPS
+  if (threadIdx.x == 0 && blockIdx.x < (1u << 16)) {
+    uint32_t hw;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+    g_block_stamps[blockIdx.x][0] = stamp0;
+    g_block_stamps[blockIdx.x][1] = __builtin_amdgcn_s_memrealtime();
+    g_block_stamps[blockIdx.x][2] = hw;
+  }
+#endif
 }
 
 // ------------------------------------------------- multi-batch launches ---
@@ -2249,6 +2267,12 @@ __global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, co
 // and registers keep four blocks per CU.  Stream-wave point pass as k_tile's,
 // with the lane's point held in registers across windows (an LDS read per 64
 // points, not per window).
+#ifdef ICSUM_STAMPS
+// diagnostic build only (tools/probe/stream_stamps.hip): per block and wave,
+// shader-clock cycles spent working on tiles, waiting at the tile barrier,
+// finishing the last tile, and the tiles seen
+__device__ uint64_t g_stream_stamps[4096][5][4];
+#endif
 constexpr uint32_t kSW = 4;                          // stream waves per block
 constexpr uint32_t kStreamBlock = (kSW + 1) * 64;    // + the metadata wave
 constexpr uint32_t kStreamResident = 1024;           // blocks resident at once: 4 per CU x 256 CUs
@@ -2564,10 +2588,13 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
       gnn = g3;
       buf ^= 1u;
     }
-  } else {
+  } else {  // in this order: the loop consumes b0 first, and vmcnt retires loads in issue order
     load_win(g, 0, b0);
+    __builtin_amdgcn_sched_barrier(0);
     load_win(g, 1, b1);
+    __builtin_amdgcn_sched_barrier(0);
     load_win(g, 2, b2);
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
     for (;;) {
       stream_tile(g, gn, buf);
@@ -2583,6 +2610,168 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
   uint32_t w1[1][kWords];
   fetch(g, tid, kStreamBlock, w1);
   emit(g, buf, tid, kStreamBlock, w1);
+}
+
+// ---------------------------------------- wave spans (round 5) -------------
+// k_span: every wave on its own.  Wave w owns segments [63 w, 63 w + 63) of
+// an offsets batch and streams their bytes [off[i0] & ~15, off[i0 + m]) as
+// one range in 4 KiB windows (k_stream's window pass: three register sets,
+// each reloaded as soon as its window is in LDS, swizzled slots, one wave
+// scan per role).  Lane p holds point p = off[i0 + p] (p <= m <= 63) in
+// registers for the whole span: the window holding it sets the lane's F
+// (prefix + masked chunk) — no point lists, loops or LDS buffers — and
+// segment t's sums are F(t + 1) - F(t), lane t + 1's value one shuffle away.
+// No block barrier and no block-level state: a block is four independent
+// waves, and the hardware dispatcher balances them over the chip the way it
+// does one-shot waves (a persistent or one-tile-per-block grid leaves the
+// chip's last waves unbalanced: static tiles 72 %, one-shot waves 82 % of
+// 8 TB/s streaming the same 141 MB, profiles/r5_probe_grab.jsonl).
+// Checksum (init, parity; u16 or raw u32) and the headers-apart wrap (the
+// payloads' sums, each 40-byte header written to its array).
+constexpr uint32_t kSpanSegs = 63;  // segments per wave: 64 points, one per lane
+
+template <int OP, int OUT>
+__global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                 uint64_t n, TileArgs a, uint32_t remap) {
+  static_assert(OP == kTileSum || OP == kTileWrapApart, "k_span: operations whose points are the offsets");
+  constexpr uint32_t kWaves = kBlock / 64;
+  __shared__ uint32_t s_pre[kWaves][kWinChunks][2];
+  __shared__ u32x4 s_raw[kWaves][kWinChunks];
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint64_t i0 = (uint64_t(block_order(remap)) * kWaves + wv) * kSpanSegs;
+  if (i0 >= n) return;  // wave-uniform; no block barrier anywhere
+  const uint32_t m = uint32_t(n - i0 < kSpanSegs ? n - i0 : kSpanSegs);
+  // the points (one load per lane), then every per-segment word the outputs
+  // need — all in flight before the first window is requested, so the
+  // outputs never wait for a load issued after the stream
+  const uint64_t x = off[i0 + (lane <= m ? lane : m)];
+  const uint32_t t = lane < m ? lane : 0u;  // this lane's segment (lanes >= m: a harmless copy of segment 0)
+  constexpr uint32_t kWords = OP == kTileSum ? 2 : 7;
+  uint32_t w[kWords];
+  if constexpr (OP == kTileSum) {
+    w[0] = a.init[(i0 + t) * a.init_step];
+    w[1] = a.odd[(i0 + t) * a.odd_step];
+  } else {
+    const uint32_t* rec = reinterpret_cast<const uint32_t*>(a.msgs + i0 + t);
+#pragma unroll
+    for (uint32_t k = 0; k < 7; ++k) w[k] = rec[k];
+  }
+  const uint64_t first = __builtin_amdgcn_readfirstlane(uint32_t(x)) |
+                         (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(x >> 32))) << 32);
+  const uint64_t tend = uint64_t(__builtin_amdgcn_readlane(uint32_t(x), m)) |
+                        (uint64_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), m)) << 32);
+  const uint64_t a0c = first >> 4;
+  const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
+  const uint64_t nw = (nch + kWinChunks - 1) / kWinChunks;
+  const uint64_t nwin3 = nw ? (nw + 2) / 3 * 3 : 3;
+  // this lane's point: chunk (span-relative) and byte; lanes past m hold none
+  const uint64_t pc = lane <= m ? (x >> 4) - a0c : ~uint64_t(0);
+  const uint32_t pb = uint32_t(x) & 15u;
+  const uint32_t voff = lane * 16u;
+  auto load_win = [&](uint64_t k, u32x4 (&v)[4]) {
+    const uint64_t c0 = k * kWinChunks;
+    const uint64_t left = nch > c0 ? nch - c0 : 0;
+    const uint32_t len = uint32_t(left < kWinChunks ? left : kWinChunks);
+    const u32x4* pw = reinterpret_cast<const u32x4*>(bytes) + a0c + (len ? c0 : 0);
+#ifdef ICSUM_BOUNDS_CHECK
+    if (len) {
+      const uint8_t* lo8 = bytes + (a0c << 4);
+      ICS_CHECK16(pw, lo8, lo8 + (nch << 4));
+      ICS_CHECK16(pw + len - 1, lo8, lo8 + (nch << 4));
+    }
+#endif
+    const __amdgpu_buffer_rsrc_t rs =
+        __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4*>(pw), 0, int(len * 16u), 0x00020000);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)  // aux 2: non-temporal
+      v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 1024, 2));
+  };
+  u32x4 b0[4], b1[4], b2[4];
+  // in this order: the loop consumes b0 first, and vmcnt retires loads in issue order
+  load_win(0, b0);
+  __builtin_amdgcn_sched_barrier(0);
+  load_win(1, b1);
+  __builtin_amdgcn_sched_barrier(0);
+  load_win(2, b2);
+  __builtin_amdgcn_sched_barrier(0);
+  uint32_t ce = 0, co = 0;  // the span's sums so far
+  uint32_t fe = 0, fo = 0;  // F of this lane's point (set by the window holding it)
+  auto window = [&](uint64_t k, u32x4 (&v)[4]) {
+    const uint64_t c0 = k * kWinChunks;
+    const bool live = c0 < nch;  // uniform; else a padding window
+    if (live) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s_raw[wv][win_slot(uint32_t(u) * 64u + lane)] = v[u];
+    }
+    load_win(k + 3, v);  // the registers are free: window k + 3 goes out now (one load site)
+    if (!live) return;
+    const uint64_t c1 = nch - c0 < kWinChunks ? nch : c0 + kWinChunks;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    uint32_t pe[4], po[4], te = 0, to = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint32_t ev = 0, od = 0;
+      acc_chunk(s_raw[wv][win_slot(4u * lane + uint32_t(j))], ev, od);
+      pe[j] = te;
+      po[j] = to;
+      te += ev;
+      to += od;
+    }
+    const uint32_t ie = wave_prefix_incl(te), io = wave_prefix_incl(to);
+    const uint32_t xe = ce + ie - te, xo = co + io - to;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s_pre[wv][4u * lane + uint32_t(j)][0] = xe + pe[j];
+      s_pre[wv][4u * lane + uint32_t(j)][1] = xo + po[j];
+    }
+    ce += __builtin_amdgcn_readlane(ie, 63);
+    co += __builtin_amdgcn_readlane(io, 63);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (pc >= c0 && pc < c1) {  // this lane's point is in this window
+      const uint32_t k2 = uint32_t(pc - c0);
+      fe = s_pre[wv][k2][0];
+      fo = s_pre[wv][k2][1];
+      acc_chunk(s_raw[wv][win_slot(k2)] & byte_range_mask(0u, pb), fe, fo);
+    }
+    __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
+  };
+  for (uint64_t k = 0; k < nwin3; k += 3) {  // wave-uniform
+    window(k, b0);
+    window(k + 1, b1);
+    window(k + 2, b2);
+  }
+  if (lane <= m && pc >= nch) {  // the aligned end of the last chunk: every byte is below it
+    fe = ce;
+    fo = co;
+  }
+  // segment t = [point t, point t + 1): lane t + 1's F one shuffle away
+  const uint32_t he = __shfl_down(fe, 1), ho = __shfl_down(fo, 1);
+  if (lane < m) {
+    const uint64_t i = i0 + lane;
+    const uint32_t se = he - fe, so = ho - fo;  // sums of [s, e), roles by address
+    if constexpr (OP == kTileSum) {
+      const uint32_t sum = w[0] + combine_roles(se, so, (uint32_t(x) ^ w[1]) & 1u);
+      if (OUT == 0)
+        static_cast<uint16_t*>(a.out)[i] = fold_value(sum);
+      else
+        static_cast<uint32_t*>(a.out)[i] = sum;
+    } else {
+      const uint64_t e = uint64_t(__shfl_down(uint32_t(x), 1)) | (uint64_t(__shfl_down(uint32_t(x >> 32), 1)) << 32);
+      uint32_t h[10], ipc = 0, tcv = 0;
+      wrap_header(u32x4{w[0], w[1], w[2], w[3]}, w[4], w[5], w[6] & 0xffffu, e - x,
+                  combine_roles(se, so, uint32_t(x) & 1u), h, ipc, tcv);
+      uint2* dst = reinterpret_cast<uint2*>(a.hdr_out + i * 10);
+#pragma unroll
+      for (int k = 0; k < 5; ++k) dst[k] = uint2{h[2 * k], h[2 * k + 1]};
+      if (a.ip_ck) a.ip_ck[i] = uint16_t(ipc);
+      if (a.tcp_ck) a.tcp_ck[i] = uint16_t(tcv);
+    }
+  }
 }
 
 // ------------------------------------------------- workload spec ---------
@@ -2926,12 +3115,24 @@ hipError_t launch_stream_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uin
   return hipGetLastError();
 }
 
+// k_span: one wave per kSpanSegs segments, four independent waves per block
+template <int OP, int OUT>
+hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, hipStream_t st) {
+  const uint64_t waves = (sp.n + kSpanSegs - 1) / kSpanSegs;
+  const uint64_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
+  if (blocks > kMaxGridBlocks) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((k_span<OP, OUT>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes, sp.offsets, sp.n, a,
+                     g_xcd_remap);
+  return hipGetLastError();
+}
+
 template <int OP, int OUT>
 hipError_t launch_tile_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint32_t max_blocks, hipStream_t st,
-                         bool stream = false) {
+                         int form = 0) {
   if (!sp.offsets || sp.list || sp.n == 0 || T == 0 || T > kTileMax) return hipErrorInvalidValue;
   if constexpr (OP == kTileSum || OP == kTileWrapApart) {
-    if (stream) return launch_stream_t<OP, OUT>(sp, a, T, max_blocks, st);
+    if (form == kTileFormStream) return launch_stream_t<OP, OUT>(sp, a, T, max_blocks, st);
+    if (form == kTileFormSpan) return launch_span_t<OP, OUT>(sp, a, st);
   }
   const uint64_t tiles = (sp.n + T - 1) / T;
   // one block per tile by default (measured faster than a persistent grid of
@@ -3197,15 +3398,15 @@ hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t*
 }
 
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t T, uint32_t max_blocks, hipStream_t st, bool stream) {
+                                uint32_t T, uint32_t max_blocks, hipStream_t st, int form) {
   TileArgs a{};
   a.init = init ? init : static_cast<const uint32_t*>(sp.zero16);
   a.odd = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
   a.init_step = init ? 1u : 0u;
   a.odd_step = odd ? 1u : 0u;
   a.out = out;
-  return out_kind == 0 ? launch_tile_t<kTileSum, 0>(sp, a, T, max_blocks, st, stream)
-                       : launch_tile_t<kTileSum, 1>(sp, a, T, max_blocks, st, stream);
+  return out_kind == 0 ? launch_tile_t<kTileSum, 0>(sp, a, T, max_blocks, st, form)
+                       : launch_tile_t<kTileSum, 1>(sp, a, T, max_blocks, st, form);
 }
 
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
@@ -3219,13 +3420,13 @@ hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16
 }
 
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st, bool stream) {
+                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st, int form) {
   TileArgs a{};
   a.msgs = msgs;
   a.hdr_out = hdr_out;
   a.ip_ck = ip_ck;
   a.tcp_ck = tcp_ck;
-  return hdr_out ? launch_tile_t<kTileWrapApart, 0>(sp, a, T, max_blocks, st, stream)
+  return hdr_out ? launch_tile_t<kTileWrapApart, 0>(sp, a, T, max_blocks, st, form)
                  : launch_tile_t<kTileWrap, 0>(sp, a, T, max_blocks, st);
 }
 

@@ -184,11 +184,14 @@ hipError_t launch_router_hdrs(const SegSpec& sp, uint32_t* hdr_out, uint8_t* sta
 // lengths; max_blocks 0: one block per tile (capped, grid-stride beyond).
 // Checksum (out_kind as launch_checksum), the fused IPv4/TCP kernel (mode as
 // launch_ipv4_tcp) and the in-place wrap (as launch_tcp_wrap in place).
-// stream: the checksum and the headers-apart wrap on k_stream instead (four
-// stream waves + a metadata wave per block; max_blocks 0: the 1024 resident
-// blocks, each taking every gridDim-th tile)
+// form (the checksum and the headers-apart wrap only): kTileFormTile k_tile;
+// kTileFormStream k_stream (four stream waves + a metadata wave per block;
+// max_blocks 0: the 1024 resident blocks, each taking every gridDim-th
+// tile); kTileFormSpan k_span (one wave per 63 segments, no block state; T
+// and max_blocks unused)
+enum TileForm : int { kTileFormTile = 0, kTileFormStream = 1, kTileFormSpan = 2 };
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t T, uint32_t max_blocks, hipStream_t st, bool stream);
+                                uint32_t T, uint32_t max_blocks, hipStream_t st, int form);
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
                             uint32_t T, uint32_t max_blocks, hipStream_t st);
 
@@ -213,7 +216,7 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
 // the wrap as a tile launch: in place (hdr_out null) or, with hdr_out, the
 // payload-only batch of ics_tcp_wrap_headers with its headers to hdr_out
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st, bool stream);
+                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st, int form);
 // pass 2 of the two-pass wrap alone (k_tcp_hdr): headers from the records and
 // the payload sums pass 1 left in `sums` (roles from each payload's start)
 hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t* sums, uint32_t* hdr_out,

@@ -24,13 +24,15 @@ pytestmark = pytest.mark.gpu
 # few blocks, each streaming many tiles back to back (the next tile's first
 # windows in flight across every tile boundary; on k_stream the metadata wave
 # finishing tile j while the stream waves run tile j + 1, both point buffers
-# in turn) — the checksum and headers-apart wrap on k_stream (default) and on
-# k_tile (stream=0)
+# in turn) — the checksum and headers-apart wrap in each form: k_span (the
+# default: one wave per 63 segments), k_stream (tile_form=1) and k_tile
+# (tile_form=0); the fused IPv4 kernel and the in-place wrap always on k_tile
 TILE_FORCE = [{"tile": 1}, {"tile": 1, "tile_segs": 1}, {"tile": 1, "tile_segs": 7},
-              {"tile": 1, "tile_segs": 7, "tile_blocks": 5}, {"tile": 1, "tile_segs": 256, "tile_blocks": 3},
-              {"tile": 1, "tile_segs": 64, "tile_blocks": 1}, {"tile": 1, "stream": 0},
-              {"tile": 1, "tile_segs": 7, "tile_blocks": 5, "stream": 0}]
-ICS_TILE_STREAM = 4
+              {"tile": 1, "tile_form": 1}, {"tile": 1, "tile_form": 1, "tile_segs": 7, "tile_blocks": 5},
+              {"tile": 1, "tile_form": 1, "tile_segs": 256, "tile_blocks": 3},
+              {"tile": 1, "tile_form": 1, "tile_segs": 64, "tile_blocks": 1}, {"tile": 1, "tile_form": 0},
+              {"tile": 1, "tile_form": 0, "tile_segs": 7, "tile_blocks": 5}]
+ICS_TILE_FORM_BITS = {0: 0, 1: 4, 2: 8}  # ICS_TILE_STREAM, ICS_TILE_SPAN
 
 
 @pytest.fixture(scope="module", params=TILE_FORCE, ids=force_id)
@@ -40,12 +42,13 @@ def tile_eng(request):
 
 def _assert_tile(eng, streamable=True):
     """the tile launch ran, in the form the engine's hooks ask for: the
-    checksum and headers-apart wrap (`streamable`) on k_stream unless
-    stream=0, the fused IPv4 kernel and the in-place wrap on k_tile"""
+    checksum and headers-apart wrap (`streamable`) on k_span unless
+    tile_form says otherwise, the fused IPv4 kernel and the in-place wrap on
+    k_tile"""
     info = eng.dispatch_info()
     assert info["kernel"] == "tile", info
-    stream = streamable and getattr(eng, "forced", {}).get("stream", 1) != 0
-    assert bool(info["unroll"] & ICS_TILE_STREAM) == stream, info
+    form = getattr(eng, "forced", {}).get("tile_form", 2) if streamable else 0
+    assert info["unroll"] & 12 == ICS_TILE_FORM_BITS[form], info
 
 
 def test_tile_kats(tile_eng):
@@ -247,9 +250,9 @@ def test_tile_config4_full_size():
         assert hashlib.sha256(out.tobytes()).hexdigest() == g["out_sha256"]
 
 
-@pytest.fixture(scope="module", params=[{"tile": 1}, {"tile": 1, "tile_segs": 7, "tile_blocks": 5},
-                                        {"tile": 1, "tile_segs": 64, "tile_blocks": 1},
-                                        {"tile": 1, "stream": 0}], ids=force_id)
+@pytest.fixture(scope="module", params=[{"tile": 1}, {"tile": 1, "tile_form": 1, "tile_segs": 7, "tile_blocks": 5},
+                                        {"tile": 1, "tile_form": 1, "tile_segs": 64, "tile_blocks": 1},
+                                        {"tile": 1, "tile_form": 0}], ids=force_id)
 def tile_apart(request):
     yield from engine_with(request.param)
 

@@ -75,13 +75,10 @@ def batch(eng, lens, seed):
 
 
 VARIANTS = {
-    "tile": {"tile": 1, "stream": 0},
-    "stream": {"tile": 1},
-    "stream_T64": {"tile": 1, "tile_segs": 64},
-    "stream_T128": {"tile": 1, "tile_segs": 128},
-    "stream_T256": {"tile": 1, "tile_segs": 256},
-    "stream_T128_onepertile": {"tile": 1, "tile_segs": 128, "tile_blocks": 1 << 20},
-    "stream_T64_b768": {"tile": 1, "tile_segs": 64, "tile_blocks": 768},
+    "tile": {"tile": 1, "tile_form": 0},
+    "stream": {"tile": 1, "tile_form": 1},
+    "stream_T256": {"tile": 1, "tile_form": 1, "tile_segs": 256},
+    "span": {"tile": 1, "tile_form": 2},
 }
 
 
