@@ -2657,10 +2657,16 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
 #pragma unroll
     for (uint32_t k = 0; k < 7; ++k) w[k] = rec[k];
   }
-  const uint64_t first = __builtin_amdgcn_readfirstlane(uint32_t(x)) |
-                         (uint64_t(__builtin_amdgcn_readfirstlane(uint32_t(x >> 32))) << 32);
-  const uint64_t tend = uint64_t(__builtin_amdgcn_readlane(uint32_t(x), m)) |
-                        (uint64_t(__builtin_amdgcn_readlane(uint32_t(x >> 32), m)) << 32);
+  // (the lane builtins return int: widen through uint32_t, or a low word of
+  // 2^31 and up sign-extends into the high one)
+  auto lane64 = [](uint64_t v, uint32_t l, bool first_lane) {
+    const uint32_t lo = uint32_t(first_lane ? __builtin_amdgcn_readfirstlane(uint32_t(v))
+                                            : __builtin_amdgcn_readlane(uint32_t(v), l));
+    const uint32_t hi = uint32_t(first_lane ? __builtin_amdgcn_readfirstlane(uint32_t(v >> 32))
+                                            : __builtin_amdgcn_readlane(uint32_t(v >> 32), l));
+    return uint64_t(lo) | (uint64_t(hi) << 32);
+  };
+  const uint64_t first = lane64(x, 0, true), tend = lane64(x, m, false);
   const uint64_t a0c = first >> 4;
   const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
   const uint64_t nw = (nch + kWinChunks - 1) / kWinChunks;
@@ -2749,8 +2755,11 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
     fe = ce;
     fo = co;
   }
-  // segment t = [point t, point t + 1): lane t + 1's F one shuffle away
+  // segment t = [point t, point t + 1): lane t + 1's F (and point) one
+  // shuffle away — taken by every lane, outside the branch below (a shuffle
+  // from a lane the branch disables reads nothing defined)
   const uint32_t he = __shfl_down(fe, 1), ho = __shfl_down(fo, 1);
+  const uint64_t e = uint64_t(__shfl_down(uint32_t(x), 1)) | (uint64_t(__shfl_down(uint32_t(x >> 32), 1)) << 32);
   if (lane < m) {
     const uint64_t i = i0 + lane;
     const uint32_t se = he - fe, so = ho - fo;  // sums of [s, e), roles by address
@@ -2761,7 +2770,6 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
       else
         static_cast<uint32_t*>(a.out)[i] = sum;
     } else {
-      const uint64_t e = uint64_t(__shfl_down(uint32_t(x), 1)) | (uint64_t(__shfl_down(uint32_t(x >> 32), 1)) << 32);
       uint32_t h[10], ipc = 0, tcv = 0;
       wrap_header(u32x4{w[0], w[1], w[2], w[3]}, w[4], w[5], w[6] & 0xffffu, e - x,
                   combine_roles(se, so, uint32_t(x) & 1u), h, ipc, tcv);
