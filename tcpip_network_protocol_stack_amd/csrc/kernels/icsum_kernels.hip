@@ -2630,7 +2630,7 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
 // payloads' sums, each 40-byte header written to its array).
 constexpr uint32_t kSpanSegs = 63;  // segments per wave: 64 points, one per lane
 
-template <int OP, int OUT>
+template <int OP, int OUT, bool STRIDE>
 __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                  uint64_t n, TileArgs a, uint32_t remap) {
   static_assert(OP == kTileSum || OP == kTileWrapApart, "k_span: operations whose points are the offsets");
@@ -2639,24 +2639,33 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
   __shared__ u32x4 s_raw[kWaves][kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t i0 = (uint64_t(block_order(remap)) * kWaves + wv) * kSpanSegs;
-  if (i0 >= n) return;  // wave-uniform; no block barrier anywhere
+  const uint64_t nspans = (n + kSpanSegs - 1) / kSpanSegs;
+  // one span per wave; STRIDE (batches of more spans than 2^24 blocks hold):
+  // grid-stride beyond the grid.  Wave-uniform, no block barrier anywhere.
+  auto span_body = [&](uint64_t span) {
+  const uint64_t i0 = span * kSpanSegs;
   const uint32_t m = uint32_t(n - i0 < kSpanSegs ? n - i0 : kSpanSegs);
-  // the points (one load per lane), then every per-segment word the outputs
-  // need — all in flight before the first window is requested, so the
-  // outputs never wait for a load issued after the stream
+  // the points (one load per lane) and, for the checksum, the per-segment
+  // words — in flight before the first window is requested, so the outputs
+  // never wait for a load issued after the stream
   const uint64_t x = off[i0 + (lane <= m ? lane : m)];
   const uint32_t t = lane < m ? lane : 0u;  // this lane's segment (lanes >= m: a harmless copy of segment 0)
   constexpr uint32_t kWords = OP == kTileSum ? 2 : 7;
   uint32_t w[kWords];
-  if constexpr (OP == kTileSum) {
-    w[0] = a.init[(i0 + t) * a.init_step];
-    w[1] = a.odd[(i0 + t) * a.odd_step];
-  } else {
-    const uint32_t* rec = reinterpret_cast<const uint32_t*>(a.msgs + i0 + t);
+  auto fetch_words = [&]() {
+    if constexpr (OP == kTileSum) {
+      w[0] = a.init[(i0 + t) * a.init_step];
+      w[1] = a.odd[(i0 + t) * a.odd_step];
+    } else {
+      const uint32_t* rec = reinterpret_cast<const uint32_t*>(a.msgs + i0 + t);
 #pragma unroll
-    for (uint32_t k = 0; k < 7; ++k) w[k] = rec[k];
-  }
+      for (uint32_t k = 0; k < 7; ++k) w[k] = rec[k];
+    }
+  };
+  // the checksum's two words ride along the stream; the wrap's 28-byte
+  // record is fetched after it (7 registers fewer across the window loop:
+  // 5 waves / SIMD instead of 4)
+  if constexpr (OP == kTileSum) fetch_words();
   // (the lane builtins return int: widen through uint32_t, or a low word of
   // 2^31 and up sign-extends into the high one)
   auto lane64 = [](uint64_t v, uint32_t l, bool first_lane) {
@@ -2755,6 +2764,7 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
     fe = ce;
     fo = co;
   }
+  if constexpr (OP != kTileSum) fetch_words();
   // segment t = [point t, point t + 1): lane t + 1's F (and point) one
   // shuffle away — taken by every lane, outside the branch below (a shuffle
   // from a lane the branch disables reads nothing defined)
@@ -2770,15 +2780,37 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
       else
         static_cast<uint32_t*>(a.out)[i] = sum;
     } else {
-      uint32_t h[10], ipc = 0, tcv = 0;
+      uint32_t ipc = 0, tcv = 0;
+      // the header into the wave's (now idle) window slots: 10 dwords per
+      // segment, the span's m headers contiguous
+      uint32_t* const stage = reinterpret_cast<uint32_t*>(&s_raw[wv][0]);
       wrap_header(u32x4{w[0], w[1], w[2], w[3]}, w[4], w[5], w[6] & 0xffffu, e - x,
-                  combine_roles(se, so, uint32_t(x) & 1u), h, ipc, tcv);
-      uint2* dst = reinterpret_cast<uint2*>(a.hdr_out + i * 10);
-#pragma unroll
-      for (int k = 0; k < 5; ++k) dst[k] = uint2{h[2 * k], h[2 * k + 1]};
+                  combine_roles(se, so, uint32_t(x) & 1u), stage + lane * 10u, ipc, tcv);
       if (a.ip_ck) a.ip_ck[i] = uint16_t(ipc);
       if (a.tcp_ck) a.tcp_ck[i] = uint16_t(tcv);
     }
+  }
+  if constexpr (OP == kTileWrapApart) {
+    // the span's 10 m header dwords are one contiguous run of hdr_out:
+    // coalesced 256-byte stores instead of 40-byte strides per lane
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const uint32_t* const stage = reinterpret_cast<const uint32_t*>(&s_raw[wv][0]);
+    uint32_t* const dst = a.hdr_out + i0 * 10;
+#pragma unroll
+    for (uint32_t j = 0; j < 10; ++j) {
+      const uint32_t q = j * 64u + lane;
+      if (q < m * 10u) dst[q] = stage[q];
+    }
+  }
+  __builtin_amdgcn_wave_barrier();  // the next span rewrites s_pre / s_raw
+  };
+  const uint64_t span0 = uint64_t(block_order(remap)) * kWaves + wv;
+  if constexpr (STRIDE) {
+    for (uint64_t span = span0; span < nspans; span += uint64_t(gridDim.x) * kWaves) span_body(span);
+  } else if (span0 < nspans) {
+    span_body(span0);
   }
 }
 
@@ -3128,9 +3160,12 @@ template <int OP, int OUT>
 hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, hipStream_t st) {
   const uint64_t waves = (sp.n + kSpanSegs - 1) / kSpanSegs;
   const uint64_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
-  if (blocks > kMaxGridBlocks) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((k_span<OP, OUT>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes, sp.offsets, sp.n, a,
-                     g_xcd_remap);
+  if (blocks <= kMaxGridBlocks)
+    hipLaunchKernelGGL((k_span<OP, OUT, false>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes, sp.offsets,
+                       sp.n, a, g_xcd_remap);
+  else  // more spans than one grid: grid-stride
+    hipLaunchKernelGGL((k_span<OP, OUT, true>), dim3(uint32_t(kMaxGridBlocks)), dim3(kBlock), 0, st, sp.bytes,
+                       sp.offsets, sp.n, a, g_xcd_remap);
   return hipGetLastError();
 }
 

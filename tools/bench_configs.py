@@ -84,6 +84,26 @@ def emit(name, nbytes, t, meta_bytes=0, **kw):
                       "frac_hbm_peak": round(gbs / PEAK, 4), "metadata_bytes": meta_bytes, **kw}), flush=True)
 
 
+def rx_batch(eng, n, ack_frac, seed):
+    """n raw IPv4/TCP datagrams back to back (packed offsets): a share
+    ack_frac of 40-byte pure ACKs, the rest 1500-byte data segments, header
+    fields set and both checksums PATCHed valid on the device"""
+    rng = np.random.default_rng(seed)
+    lens = np.where(rng.random(n) < ack_frac, 40, 1500).astype(np.uint64)
+    off = np.zeros(n + 1, dtype=np.uint64)
+    off[1:] = np.cumsum(lens)
+    buf = rng.integers(0, 256, int(off[-1]) + 16, dtype=np.uint8)
+    s = off[:-1].astype(np.int64)
+    buf[s], buf[s + 1] = 0x45, 0
+    buf[s + 2], buf[s + 3] = (lens >> 8).astype(np.uint8), (lens & 255).astype(np.uint8)
+    buf[s + 6], buf[s + 7], buf[s + 8], buf[s + 9] = 0x40, 0, 64, 6
+    buf[s + 32] = 0x50  # TCP data offset 5
+    d = torch.from_numpy(buf).cuda()
+    doff = torch.from_numpy(off.view(np.int64)).cuda()
+    eng.ipv4_tcp_batch(d, 2, n=n, offsets=doff)  # PATCH: valid checksums
+    return d, doff, int(off[-1])
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--only", default="ns,ipv4,tcp64,mixed,bimodal,jumbo,jumbo_all,host,streams")
@@ -331,15 +351,12 @@ def main():
         del d
 
     if "rxmix" in only:  # received traffic: raw IPv4/TCP datagrams, ACKs among MTU segments, valid headers
-        sys.path.insert(0, os.path.join(ROOT, "tools"))
-        from ab_ipv4_mix import batch
-
         n = 1 << 20
         ip = torch.empty(n, dtype=torch.int16, device=dev)
         tcp = torch.empty(n, dtype=torch.int16, device=dev)
         stt = torch.empty(n, dtype=torch.uint8, device=dev)
         for af in (0.25, 0.5, 0.75):
-            d, doff, nbytes = batch(eng, n, af, 11)
+            d, doff, nbytes = rx_batch(eng, n, af, 11)
             t = timed(lambda i=0: eng.ipv4_tcp_batch(d, 1, n=n, offsets=doff, ip_ck=ip, tcp_ck=tcp, status=stt),
                       args.iters)
             info = eng.dispatch_info()
