@@ -2630,7 +2630,7 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
 // payloads' sums, each 40-byte header written to its array).
 constexpr uint32_t kSpanSegs = 63;  // segments per wave: 64 points, one per lane
 
-template <int OP, int OUT, bool STRIDE>
+template <int OP, int OUT, bool STRIDE, int NSETS>
 __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
                                                  uint64_t n, TileArgs a, uint32_t remap) {
   static_assert(OP == kTileSum || OP == kTileWrapApart, "k_span: operations whose points are the offsets");
@@ -2679,7 +2679,7 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
   const uint64_t a0c = first >> 4;
   const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
   const uint64_t nw = (nch + kWinChunks - 1) / kWinChunks;
-  const uint64_t nwin3 = nw ? (nw + 2) / 3 * 3 : 3;
+  const uint64_t nwinS = nw ? (nw + NSETS - 1) / NSETS * NSETS : NSETS;  // whole rounds of the register sets
   // this lane's point: chunk (span-relative) and byte; lanes past m hold none
   const uint64_t pc = lane <= m ? (x >> 4) - a0c : ~uint64_t(0);
   const uint32_t pb = uint32_t(x) & 15u;
@@ -2702,14 +2702,19 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
     for (int u = 0; u < 4; ++u)  // aux 2: non-temporal
       v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 1024, 2));
   };
-  u32x4 b0[4], b1[4], b2[4];
+  // NSETS register sets (2 or 3), each reloaded as soon as its window is in
+  // LDS: NSETS windows in flight while one is summed
+  static_assert(NSETS == 2 || NSETS == 3, "k_span: two or three register sets");
+  u32x4 b0[4], b1[4], b2[NSETS == 3 ? 4 : 1];
   // in this order: the loop consumes b0 first, and vmcnt retires loads in issue order
   load_win(0, b0);
   __builtin_amdgcn_sched_barrier(0);
   load_win(1, b1);
   __builtin_amdgcn_sched_barrier(0);
-  load_win(2, b2);
-  __builtin_amdgcn_sched_barrier(0);
+  if constexpr (NSETS == 3) {
+    load_win(2, reinterpret_cast<u32x4(&)[4]>(b2));
+    __builtin_amdgcn_sched_barrier(0);
+  }
   uint32_t ce = 0, co = 0;  // the span's sums so far
   uint32_t fe = 0, fo = 0;  // F of this lane's point (set by the window holding it)
   auto window = [&](uint64_t k, u32x4 (&v)[4]) {
@@ -2719,8 +2724,13 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
 #pragma unroll
       for (int u = 0; u < 4; ++u) s_raw[wv][win_slot(uint32_t(u) * 64u + lane)] = v[u];
     }
-    load_win(k + 3, v);  // the registers are free: window k + 3 goes out now (one load site)
+    load_win(k + NSETS, v);  // the registers are free: window k + NSETS goes out now (one load site)
     if (!live) return;
+#ifdef ICSUM_SPAN_PROBE_STREAM_ONLY
+    // diagnostic build only (tools/probe/span_probe.hip): the loads and the
+    // LDS writes, no scan, prefix or points (results wrong, time only)
+    if (live) return;
+#endif
     const uint64_t c1 = nch - c0 < kWinChunks ? nch : c0 + kWinChunks;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -2755,10 +2765,10 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
     }
     __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
   };
-  for (uint64_t k = 0; k < nwin3; k += 3) {  // wave-uniform
+  for (uint64_t k = 0; k < nwinS; k += NSETS) {  // wave-uniform
     window(k, b0);
     window(k + 1, b1);
-    window(k + 2, b2);
+    if constexpr (NSETS == 3) window(k + 2, reinterpret_cast<u32x4(&)[4]>(b2));
   }
   if (lane <= m && pc >= nch) {  // the aligned end of the last chunk: every byte is below it
     fe = ce;
@@ -3155,16 +3165,21 @@ hipError_t launch_stream_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uin
   return hipGetLastError();
 }
 
-// k_span: one wave per kSpanSegs segments, four independent waves per block
+// k_span: one wave per kSpanSegs segments, four independent waves per block;
+// register sets per wave (process-wide, ICSUM_FORCE span_sets; dev A/B)
+uint32_t g_span_sets = 3;
 template <int OP, int OUT>
 hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, hipStream_t st) {
   const uint64_t waves = (sp.n + kSpanSegs - 1) / kSpanSegs;
   const uint64_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
-  if (blocks <= kMaxGridBlocks)
-    hipLaunchKernelGGL((k_span<OP, OUT, false>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes, sp.offsets,
-                       sp.n, a, g_xcd_remap);
-  else  // more spans than one grid: grid-stride
-    hipLaunchKernelGGL((k_span<OP, OUT, true>), dim3(uint32_t(kMaxGridBlocks)), dim3(kBlock), 0, st, sp.bytes,
+  if (blocks > kMaxGridBlocks)  // more spans than one grid: grid-stride
+    hipLaunchKernelGGL((k_span<OP, OUT, true, 3>), dim3(uint32_t(kMaxGridBlocks)), dim3(kBlock), 0, st, sp.bytes,
+                       sp.offsets, sp.n, a, g_xcd_remap);
+  else if (g_span_sets == 2)
+    hipLaunchKernelGGL((k_span<OP, OUT, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
+                       sp.offsets, sp.n, a, g_xcd_remap);
+  else
+    hipLaunchKernelGGL((k_span<OP, OUT, false, 3>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
                        sp.offsets, sp.n, a, g_xcd_remap);
   return hipGetLastError();
 }
@@ -3342,6 +3357,7 @@ hipError_t launch_checksum_bins(const SegSpec& sp, const uint32_t* init, const u
 }
 
 void set_xcd_remap(uint32_t run_log2) { g_xcd_remap = run_log2 < 31 ? run_log2 : 31; }
+void set_span_sets(uint32_t sets) { g_span_sets = sets == 2 ? 2u : 3u; }
 
 bool bounds_checked_build() {
 #ifdef ICSUM_BOUNDS_CHECK

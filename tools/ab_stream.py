@@ -79,6 +79,7 @@ VARIANTS = {
     "stream": {"tile": 1, "tile_form": 1},
     "stream_T256": {"tile": 1, "tile_form": 1, "tile_segs": 256},
     "span": {"tile": 1, "tile_form": 2},
+    "span2": {"tile": 1, "tile_form": 2, "span_sets": 2},
 }
 
 
