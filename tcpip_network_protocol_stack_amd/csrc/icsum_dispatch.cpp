@@ -630,6 +630,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
     else if (k == "tile_form" && v >= 0 && v <= 2) ctx->tile_form = int(v);
     else if (k == "span_sets" && (v == 2 || v == 3)) icsum::set_span_sets(uint32_t(v));
+    else if (k == "span_segs" && v >= 1 && v <= 63) icsum::set_span_segs(uint32_t(v));
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);

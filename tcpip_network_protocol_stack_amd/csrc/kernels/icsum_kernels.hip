@@ -2628,23 +2628,23 @@ __global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restri
 // 8 TB/s streaming the same 141 MB, profiles/r5_probe_grab.jsonl).
 // Checksum (init, parity; u16 or raw u32) and the headers-apart wrap (the
 // payloads' sums, each 40-byte header written to its array).
-constexpr uint32_t kSpanSegs = 63;  // segments per wave: 64 points, one per lane
+constexpr uint32_t kSpanSegs = 63;  // most segments per wave: 64 points, one per lane
 
 template <int OP, int OUT, bool STRIDE, int NSETS>
 __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                 uint64_t n, TileArgs a, uint32_t remap) {
+                                                 uint64_t n, uint32_t S, TileArgs a, uint32_t remap) {
   static_assert(OP == kTileSum || OP == kTileWrapApart, "k_span: operations whose points are the offsets");
   constexpr uint32_t kWaves = kBlock / 64;
   __shared__ uint32_t s_pre[kWaves][kWinChunks][2];
   __shared__ u32x4 s_raw[kWaves][kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nspans = (n + kSpanSegs - 1) / kSpanSegs;
+  const uint64_t nspans = (n + S - 1) / S;  // S (1..63) segments per span
   // one span per wave; STRIDE (batches of more spans than 2^24 blocks hold):
   // grid-stride beyond the grid.  Wave-uniform, no block barrier anywhere.
   auto span_body = [&](uint64_t span) {
-  const uint64_t i0 = span * kSpanSegs;
-  const uint32_t m = uint32_t(n - i0 < kSpanSegs ? n - i0 : kSpanSegs);
+  const uint64_t i0 = span * S;
+  const uint32_t m = uint32_t(n - i0 < S ? n - i0 : S);
   // the points (one load per lane) and, for the checksum, the per-segment
   // words — in flight before the first window is requested, so the outputs
   // never wait for a load issued after the stream
@@ -2727,9 +2727,15 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
     load_win(k + NSETS, v);  // the registers are free: window k + NSETS goes out now (one load site)
     if (!live) return;
 #ifdef ICSUM_SPAN_PROBE_STREAM_ONLY
-    // diagnostic build only (tools/probe/span_probe.hip): the loads and the
-    // LDS writes, no scan, prefix or points (results wrong, time only)
-    if (live) return;
+    // diagnostic build only (tools/probe/span_probe.hip): the loads, the LDS
+    // writes and one read back per lane, no scan, prefix or points (results
+    // wrong, time only)
+    if (live) {
+      const u32x4 r = s_raw[wv][win_slot(4u * lane)];
+      ce += r.x ^ r.y ^ r.z ^ r.w;
+      __builtin_amdgcn_wave_barrier();
+      return;
+    }
 #endif
     const uint64_t c1 = nch - c0 < kWinChunks ? nch : c0 + kWinChunks;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -3165,22 +3171,25 @@ hipError_t launch_stream_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uin
   return hipGetLastError();
 }
 
-// k_span: one wave per kSpanSegs segments, four independent waves per block;
-// register sets per wave (process-wide, ICSUM_FORCE span_sets; dev A/B)
+// k_span: one wave per g_span_segs segments, four independent waves per
+// block; segments per span and register sets per wave are process-wide
+// (ICSUM_FORCE span_segs / span_sets; dev A/B)
 uint32_t g_span_sets = 3;
+uint32_t g_span_segs = kSpanSegs;
 template <int OP, int OUT>
 hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, hipStream_t st) {
-  const uint64_t waves = (sp.n + kSpanSegs - 1) / kSpanSegs;
+  const uint32_t S = g_span_segs;
+  const uint64_t waves = (sp.n + S - 1) / S;
   const uint64_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
   if (blocks > kMaxGridBlocks)  // more spans than one grid: grid-stride
     hipLaunchKernelGGL((k_span<OP, OUT, true, 3>), dim3(uint32_t(kMaxGridBlocks)), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.n, a, g_xcd_remap);
+                       sp.offsets, sp.n, S, a, g_xcd_remap);
   else if (g_span_sets == 2)
     hipLaunchKernelGGL((k_span<OP, OUT, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.n, a, g_xcd_remap);
+                       sp.offsets, sp.n, S, a, g_xcd_remap);
   else
     hipLaunchKernelGGL((k_span<OP, OUT, false, 3>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.n, a, g_xcd_remap);
+                       sp.offsets, sp.n, S, a, g_xcd_remap);
   return hipGetLastError();
 }
 
@@ -3358,6 +3367,7 @@ hipError_t launch_checksum_bins(const SegSpec& sp, const uint32_t* init, const u
 
 void set_xcd_remap(uint32_t run_log2) { g_xcd_remap = run_log2 < 31 ? run_log2 : 31; }
 void set_span_sets(uint32_t sets) { g_span_sets = sets == 2 ? 2u : 3u; }
+void set_span_segs(uint32_t segs) { g_span_segs = segs >= 1 && segs <= kSpanSegs ? segs : kSpanSegs; }
 
 bool bounds_checked_build() {
 #ifdef ICSUM_BOUNDS_CHECK

@@ -165,6 +165,8 @@ hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const 
 void set_xcd_remap(uint32_t run_log2);
 // register sets per k_span wave: 2 or 3 (process-wide; ICSUM_FORCE span_sets)
 void set_span_sets(uint32_t sets);
+// segments per k_span wave, 1..63 (process-wide; ICSUM_FORCE span_segs)
+void set_span_segs(uint32_t segs);
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);

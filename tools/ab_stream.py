@@ -80,6 +80,9 @@ VARIANTS = {
     "stream_T256": {"tile": 1, "tile_form": 1, "tile_segs": 256},
     "span": {"tile": 1, "tile_form": 2},
     "span2": {"tile": 1, "tile_form": 2, "span_sets": 2},
+    "span_S15": {"tile": 1, "tile_form": 2, "span_segs": 15, "span_sets": 3},
+    "span_S31": {"tile": 1, "tile_form": 2, "span_segs": 31, "span_sets": 3},
+    "span_S63": {"tile": 1, "tile_form": 2, "span_segs": 63, "span_sets": 3},
 }
 
 

@@ -28,7 +28,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr uint32_t kWin = 4096;
 
-template <int AUX = 2, bool LANE64 = false>
+// LANE64: lane L loads bytes [64 L + 16 u, +16) (lane-contiguous); PIECES:
+// instruction u, lane group g = L / 16 loads [1024 g + 256 u + 16 (L % 16), +16)
+// (four 256-byte pieces per instruction, k_checksum's 16-lane line grid)
+template <int AUX = 2, bool LANE64 = false, bool PIECES = false>
 __device__ __forceinline__ void load_win(const uint8_t* base, uint64_t off, uint64_t end, u32x4 (&v)[4]) {
   const uint32_t lane = threadIdx.x & 63u;
   const uint64_t left = end > off ? end - off : 0;
@@ -37,8 +40,10 @@ __device__ __forceinline__ void load_win(const uint8_t* base, uint64_t off, uint
       __builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t*>(base + (off < end ? off : 0)), 0, int(len), 0x00020000);
 #pragma unroll
   for (int u = 0; u < 4; ++u)
-    v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, LANE64 ? lane * 64u : lane * 16u,
-                                                                           LANE64 ? u * 16 : u * 1024, AUX));
+    v[u] = __builtin_bit_cast(
+        u32x4, __builtin_amdgcn_raw_buffer_load_b128(
+                   rs, LANE64 ? lane * 64u : PIECES ? (lane >> 4) * 1024u + (lane & 15u) * 16u : lane * 16u,
+                   LANE64 ? u * 16 : PIECES ? u * 256 : u * 1024, AUX));
 }
 
 // one-shot waves: wave w reads windows [w D, (w + 1) D) (contiguous D x 4 KiB)
@@ -58,23 +63,29 @@ __global__ __launch_bounds__(256) void k_oneshot(const uint8_t* __restrict__ buf
   out[(uint64_t(blockIdx.x) * 256 + threadIdx.x) & ((8u << 16) - 1)] = acc;
 }
 
-template <int D, int AUX = 2, bool LANE64 = false>
-__global__ __launch_bounds__(256) void k_pattern(const uint8_t* __restrict__ buf, uint64_t nbytes,
+template <int D, int AUX = 2, bool LANE64 = false, bool XCD = false, bool PIECES = false>
+__global__ __launch_bounds__(256) void k_pattern(const uint8_t* __restrict__ buf_all, uint64_t nbytes_all,
                                                  uint32_t* __restrict__ out) {
   extern __shared__ uint32_t pad[];
   const uint32_t wv = threadIdx.x >> 6;
-  const uint64_t waves = uint64_t(gridDim.x) * 4, first = uint64_t(blockIdx.x) * 4 + wv;
+  // XCD: block b runs on XCD b % 8 (round-robin dispatch); each XCD sweeps
+  // its own contiguous eighth of the buffer
+  const uint32_t nx = XCD ? 8u : 1u, x = XCD ? blockIdx.x % 8u : 0u;
+  const uint64_t part = (nbytes_all / nx) & ~uint64_t(kWin - 1);
+  const uint8_t* buf = buf_all + x * part;
+  const uint64_t nbytes = x + 1 == nx ? nbytes_all - x * part : part;
+  const uint64_t waves = uint64_t(gridDim.x / nx) * 4, first = uint64_t(blockIdx.x / nx) * 4 + wv;
   const uint64_t st = waves * kWin;
   uint32_t acc = 0;
   u32x4 b[D][4];
 #pragma unroll
-  for (int d = 0; d < D; ++d) load_win<AUX, LANE64>(buf, (first + d * waves) * kWin, nbytes, b[d]);
+  for (int d = 0; d < D; ++d) load_win<AUX, LANE64, PIECES>(buf, (first + d * waves) * kWin, nbytes, b[d]);
   for (uint64_t o = first * kWin; o < nbytes; o += D * st) {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) acc += b[d][u].x + b[d][u].y + b[d][u].z + b[d][u].w;
-      load_win<AUX, LANE64>(buf, o + (D + d) * st, nbytes, b[d]);
+      load_win<AUX, LANE64, PIECES>(buf, o + (D + d) * st, nbytes, b[d]);
     }
   }
   if (acc == 0x12345678u) pad[threadIdx.x] = acc;  // never true; keeps pad referenced
@@ -98,9 +109,9 @@ int main() {
     const char* name;
     K k;
     int d, bpc;  // bpc 0: one-shot grid, all blocks the data needs
-  } runs[] = {{"persist_nt", k_pattern<3, 2>, 3, 4}, {"persist_nt_lane64", k_pattern<3, 2, true>, 3, 4},
-              {"persist_nt", k_pattern<3, 2>, 3, 5}, {"persist_nt_lane64", k_pattern<3, 2, true>, 3, 5},
-              {"persist_nt", k_pattern<3, 2>, 3, 4}, {"persist_nt_lane64", k_pattern<3, 2, true>, 3, 4}};
+  } runs[] = {{"persist_nt", k_pattern<3, 2>, 3, 4}, {"persist_nt_pieces", k_pattern<3, 2, false, false, true>, 3, 4},
+              {"persist_nt", k_pattern<3, 2>, 3, 5}, {"persist_nt_pieces", k_pattern<3, 2, false, false, true>, 3, 5},
+              {"persist_nt", k_pattern<2, 2>, 2, 6}, {"persist_nt_pieces", k_pattern<2, 2, false, false, true>, 2, 6}};
   for (const Run& r : runs) {
     const uint32_t grid = r.bpc ? uint32_t(r.bpc) * 256 : uint32_t((nbytes / kWin + 4 * r.d - 1) / (4 * r.d));
     const size_t lds = r.bpc ? (160 * 1024) / r.bpc - 1024 : 0;

@@ -26,6 +26,10 @@
     }                                                            \
   } while (0)
 
+__global__ void k_empty(uint32_t* p) {
+  if (threadIdx.x == 0 && blockIdx.x == 0 && p) p[0] = 1;
+}
+
 int main(int argc, char** argv) {
   const uint64_t n = argc > 1 ? std::strtoull(argv[1], nullptr, 0) : (1u << 18);
   std::mt19937_64 rng(11);
@@ -83,6 +87,22 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     b2b.push_back(ms * 1000.f / 20.f);
   }
+  // the fixed cost of one launch from an idle stream, HIP events around it:
+  // an empty kernel of one block and of the VERIFY launch's 4096 blocks
+  std::vector<float> empty1, emptyN;
+  for (int i = 0; i < 50; ++i)
+    for (int which = 0; which < 2; ++which) {
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0, nullptr));
+      hipLaunchKernelGGL(k_empty, dim3(which ? uint32_t((n + 63) / 64) : 1u), dim3(256), 0, nullptr, nullptr);
+      CK(hipEventRecord(e1, nullptr));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      (which ? emptyN : empty1).push_back(ms * 1000.f);
+    }
+  std::sort(empty1.begin(), empty1.end());
+  std::sort(emptyN.begin(), emptyN.end());
   std::sort(alone.begin(), alone.end());
   std::sort(b2b.begin(), b2b.end());
   uint64_t t0 = ~0ull, t1 = 0, lastStart = 0;
@@ -107,10 +127,11 @@ int main(int argc, char** argv) {
               "\"span_us\": %.2f, \"start_us\": {\"p50\": %.2f, \"p90\": %.2f, \"last\": %.2f}, "
               "\"end_us\": {\"first\": %.2f, \"p50\": %.2f, \"p90\": %.2f, \"p99\": %.2f, \"last\": %.2f}, "
               "\"block_us\": {\"p10\": %.2f, \"p50\": %.2f, \"p90\": %.2f, \"max\": %.2f}, \"frac_alone\": %.4f, "
-              "\"frac_span\": %.4f}\n",
+              "\"frac_span\": %.4f, \"empty_launch_us\": {\"one_block\": %.2f, \"same_grid\": %.2f}}\n",
               (unsigned long long)n, (unsigned long long)blocks, bytes, alone[alone.size() / 2], b2b[2],
               0.01 * double(t1 - t0), q(starts, 0.5), q(starts, 0.9), q(starts, 1.0), q(ends, 0.0), q(ends, 0.5),
               q(ends, 0.9), q(ends, 0.99), q(ends, 1.0), q(dur, 0.1), q(dur, 0.5), q(dur, 0.9), q(dur, 1.0),
-              bytes / (alone[alone.size() / 2] * 1e3) / 8000.0, bytes / (0.01 * double(t1 - t0) * 1e3) / 8000.0);
+              bytes / (alone[alone.size() / 2] * 1e3) / 8000.0, bytes / (0.01 * double(t1 - t0) * 1e3) / 8000.0,
+              empty1[empty1.size() / 2], emptyN[emptyN.size() / 2]);
   return 0;
 }
