@@ -298,13 +298,13 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 #define ICS_K_WRAP_2PASS 10      /* k_tcp_wrap (payload sums) + k_tcp_hdr */
 #define ICS_K_ROUTER 11          /* k_router_ttl */
 #define ICS_K_BATCHV 12          /* several batches in one launch (ics_*_batchv) */
-#define ICS_K_TILE 13            /* k_tile: an offsets batch as one packed stream, T segments per block */
+#define ICS_K_TILE 13            /* k_span: an offsets batch as one packed stream, 63 segments per wave */
 #define ICS_K_ROUTER_HDRS 14     /* k_router_hdrs: the router step, forwarded headers apart */
 /* last_lps / last_unroll by kernel:
  *   ICS_K_CHECKSUM .. ICS_K_WRAP_2PASS  lanes per segment / loads in flight per lane
  *   ICS_K_TWOCLASS, ICS_K_IPV4_TWOCLASS  long-segment lanes (16) / segments per wave (16 or 32; 8 only under ICSUM_FORCE twoclass=8)
  *   ICS_K_BATCHV  the ICS_BV_* shape of the last launch group / batches in the call
- *   ICS_K_TILE    segments per tile (T) / ICS_TILE_* operation, | ICS_TILE_STREAM / ICS_TILE_SPAN for those forms
+ *   ICS_K_TILE    segments per wave (63) / ICS_TILE_* operation
  *   ICS_K_ROUTER, ICS_K_ROUTER_HDRS  0 / 0 */
 #define ICS_BV_DENSE64 0 /* fixed stride == length == 64 B, 16-byte aligned */
 #define ICS_BV_TINY 1    /* one lane per segment (ACK-sized fixed lengths) */
@@ -316,8 +316,6 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 #define ICS_TILE_IPV4 1
 #define ICS_TILE_WRAP 2
 #define ICS_TILE_WRAP_APART 3
-#define ICS_TILE_STREAM 4 /* or'ed in: k_stream (stream waves + a metadata wave per block; checksum, wrap apart) */
-#define ICS_TILE_SPAN 8   /* or'ed in: k_span (one wave per 63 segments; checksum, wrap apart) */
 typedef struct ics_dispatch_info_t {
   uint64_t plan_hits;      /* lookups that found this batch's landed plan */
   uint64_t plan_misses;    /* lookups that did not (first call, plan still in flight) */

@@ -83,22 +83,17 @@ struct ics_ctx {
   int dense_segs = 4;            // k_checksum_dense segments per lane group in flight (0: off)
   int bin_plan = -1;  // -1: decided on the device per batch; forced: 0 whole, 1 split, 2 whole16, 3 wholeS
   int twoclass = 0;   // 0: auto; 16 / 32: every offsets batch through the two-class launch (that many per wave)
-  // tile launches of offsets batches (k_tile): -1 auto, 0 never, 1 every
-  // offsets batch (checksum, fused IPv4, in-place wrap); tile_segs = T
-  // segments per tile (0: tile_segs_for), tile_blocks = grid cap (0: one block per tile)
+  // tile launches of offsets batches (k_span): -1 auto, 0 never, 1 every
+  // offsets batch (checksum, fused IPv4, wraps); span_segs: segments per
+  // wave (0: span_segs_for)
   int tile = -1;
+  uint32_t span_segs = 0;
+  static constexpr uint64_t kSpanBytes = 20 << 10;  // segment bytes per span (span_segs_for)
   static constexpr uint64_t kTileMin = uint64_t(1) << 17;  // tile launches from this many segments (AUTO)
   static constexpr uint32_t kTileMaxAvg = 1024;            // ... and up to this mean length (tile_wins)
   static constexpr uint32_t kTileApartShort16 = 12;       // headers-apart wrap: below 12/16 empty-ish payloads
-  static constexpr uint64_t kTileBytes = 96 << 10;        // segment bytes per tile (tile_segs_for)
-  static constexpr uint64_t kTileResident = 1024;          // tile blocks resident at once: 4 per CU x 256 CUs
-  static constexpr uint64_t kTileRoundBytes = 160 << 10;   // largest tile taken to fit all tiles in one round
   uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order
   uint32_t twoclass_lds = 0;    // dynamic LDS bytes per two-class block (residency cap; ICSUM_FORCE twoclass_lds)
-  uint32_t tile_segs = 0, tile_blocks = 0;
-  // the form of the checksum and headers-apart wrap tile launches
-  // (icsum::TileForm: 0 k_tile, 1 k_stream, 2 k_span; ICSUM_FORCE tile_form)
-  int tile_form = 2;
   // device wrap: 0 = two passes (payload sums, then a header launch) when
   // the headers go to an array of their own and the batch has at least
   // kWrapTwoPassMin datagrams, otherwise one pass (headers stored inside the

@@ -16,29 +16,20 @@ static_assert(icsum::kBvDense64 == ICS_BV_DENSE64 && icsum::kBvTiny == ICS_BV_TI
                   icsum::kBvLane1 == ICS_BV_LANE1,
               "multi-batch shapes are reported as ICS_BV_*");
 
-// Segments per tile of a tile launch (k_tile): the forced value; without a
-// mean length (the test hook on an unplanned batch) as many as keep >= 1024
-// tiles up to 128; with the cached plan's mean length, about kTileBytes of
-// segments per tile (128..256), and all the tiles in one round of resident
-// blocks (kTileResident: 4 per CU, LDS-bound) when a tile of up to
-// kTileRoundBytes does it.  Measured (tools/ab_tile_T.py,
-// profiles/r4_ab_tile_T.jsonl, us, T = 64..256): 0..1000-byte payloads best
-// at 192 from 192 Ki to 1 M datagrams except 256 at 256 Ki (one round:
-// headers-apart wrap 32.6 -> 30.5), 770-byte segments best at 128 except
-// 192 at 192 Ki (one round).
-uint32_t tile_segs_for(const ics_ctx* ctx, uint64_t n, uint32_t avg) {
-  if (ctx->tile_segs) return std::min<uint32_t>(ctx->tile_segs, 256);
-  if (avg == 0) return uint32_t(std::clamp<uint64_t>(n / 1024, 16, 128));
-  uint64_t T = std::clamp<uint64_t>((ics_ctx::kTileBytes / avg + 16) & ~uint64_t(31), 128, 256);
-  const uint64_t one = (n + ics_ctx::kTileResident - 1) / ics_ctx::kTileResident;  // T of a single round
-  if ((n + T - 1) / T > ics_ctx::kTileResident && one <= 256 && one * avg <= ics_ctx::kTileRoundBytes) T = one;
-  return uint32_t(T);
-}
-
-// ics_dispatch_info's report of the checksum / headers-apart wrap form
-int tile_form_bits(const ics_ctx* ctx) {
-  return ctx->tile_form == icsum::kTileFormStream ? ICS_TILE_STREAM
-         : ctx->tile_form == icsum::kTileFormSpan ? ICS_TILE_SPAN : 0;
+// Segments per k_span wave: the forced value; with the cached plan's mean
+// length (capped at 4095 by the plan), about ics_ctx::kSpanBytes of segments
+// per span, 1..63 (a wave streams its span alone: spans of long segments
+// leave the chip a few long-lived waves); without one, 63.  Measured
+// (tools/ab_stream.py; profiles/r5n_ab_span_size.jsonl,
+// r5o_ab_span_size_fine.jsonl; us back to back, S = 4 / 16 / 32 / 63): 1 M
+// x 40..1040 B checksum 236.3 / 89.9 / 83.9 / 91.2, VERIFY 315.7 / 122.3 /
+// 111.6 / 122.2; 1 M x 770 B checksum 250.4 / 129.1 / 118.4 / 123.1;
+// 128 Ki of config 4's 64 B..64 KiB mix VERIFY 191.5 / 209.3 / 221.1 /
+// 265.9 — flat from about 16 to 40 KiB per span.
+uint32_t span_segs_for(const ics_ctx* ctx, uint32_t avg) {
+  if (ctx->span_segs) return ctx->span_segs;
+  if (avg == 0) return 63;
+  return uint32_t(std::clamp<uint64_t>(ics_ctx::kSpanBytes / avg, 1, 63));
 }
 
 bool wrap_two_pass(const ics_ctx* ctx, bool headers_apart, uint64_t n) {
@@ -234,10 +225,9 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     return ICS_OK;
   }
   if (sp.offsets && ctx->tile == 1) {  // test hook: the tile launch on every offsets batch
-    const uint32_t T = tile_segs_for(ctx, sp.n, 0);
-    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st,
-                                                ctx->tile_form));
-    note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM | tile_form_bits(ctx), true, 0, 1});
+    const uint32_t S = span_segs_for(ctx, 0);
+    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st));
+    note(ctx, ICS_K_TILE, {int(S), ICS_TILE_CHECKSUM, true, 0, 1});
     return ICS_OK;
   }
   const bool binned = sp.offsets && sp.n <= 0xFFFFFFFFull &&
@@ -292,11 +282,9 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     const bool hit = plan_lookup(ctx, sp, true, &hit_plan, &req, &mix);
     const bool mix8 = hit && hit_plan != icsum::kPlanWholeBatchSmall && short_mix(mix);
     if (hit && !mix8 && hit_plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, sp.n, false)) {
-      const uint32_t T = tile_segs_for(ctx, sp.n, mix.avg);
-      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, T, ctx->tile_blocks, st,
-                                                ctx->tile_form));
-      note(ctx, ICS_K_TILE, {int(T), ICS_TILE_CHECKSUM | tile_form_bits(ctx), true, 0, 1},
-           int(hit_plan));
+      const uint32_t S = span_segs_for(ctx, mix.avg);
+      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st));
+      note(ctx, ICS_K_TILE, {int(S), ICS_TILE_CHECKSUM, true, 0, 1}, int(hit_plan));
       return replan(ctx, sp, lps, req, st);
     }
     if (hit && (hit_plan != icsum::kPlanSplitBins || mix8)) {
@@ -367,8 +355,8 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   // kernels running behind the first and every 64th launch (DESIGN.md §4,
   // git 7692616:tools/ab_ipv4_mix.py, profiles/r2_ipv4_mix_sweep.jsonl)
   bool two = false, tile = false;
+  uint32_t span_avg = 0;  // the cached plan's mean length (span_segs_for)
   int spw = 16;
-  uint32_t tile_avg = 0;  // the cached plan's mean length (tile_segs_for)
   PlanReq req;
   int plan_used = -1;
   if (d_offsets && !forced_geometry(ctx) && !ctx->twoclass && n >= ics_ctx::kSmallPlanMin && n <= 0xFFFFFFFFull) {
@@ -392,16 +380,16 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
     spw = mix.short16 >= ics_ctx::kIpv4TwoClassWide16 ? 32 : 16;
     plan_used = hit ? int(plan) : -1;
     tile = hit && !two && plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, n, true);
-    tile_avg = hit ? mix.avg : 0u;
+    span_avg = hit ? mix.avg : 0u;
   }
   if (d_offsets && ctx->twoclass) {  // test hook
     two = true;
     spw = ctx->twoclass;
   }
   if (d_offsets && (ctx->tile == 1 || tile)) {  // the test hook, or the cached mix favours the tile launch
-    const uint32_t T = tile_segs_for(ctx, n, tile_avg);
-    ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, T, ctx->tile_blocks, st));
-    note(ctx, ICS_K_TILE, {int(T), ICS_TILE_IPV4, true, 0, 1}, plan_used);
+    const uint32_t S = span_segs_for(ctx, span_avg);
+    ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, S, st));
+    note(ctx, ICS_K_TILE, {int(S), ICS_TILE_IPV4, true, 0, 1}, plan_used);
     return replan(ctx, sp, 64, req, st);
   }
   hipError_t le = hipErrorInvalidValue;
@@ -483,12 +471,10 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
                                        : !short_mix(mix) && ctx->tile != 0 && sp.n >= ics_ctx::kTileMin &&
                                              mix.long16 >= 4);
   if (sp.offsets && (ctx->tile == 1 || tile_pick)) {  // the wrap (in place or headers apart) as a tile launch
-    const uint32_t T = tile_segs_for(ctx, sp.n, plan >= 0 ? mix.avg : 0u);
+    const uint32_t S = span_segs_for(ctx, plan >= 0 ? mix.avg : 0u);
     ICS_HIP(icsum::launch_tile_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), hdr_out, d_ip_ck, d_tcp_ck,
-                                    T, ctx->tile_blocks, st, ctx->tile_form));
-    note(ctx, ICS_K_TILE,
-         {int(T), hdr_out ? ICS_TILE_WRAP_APART | tile_form_bits(ctx) : ICS_TILE_WRAP, true, 0, 1},
-         plan);
+                                    S, st));
+    note(ctx, ICS_K_TILE, {int(S), hdr_out ? ICS_TILE_WRAP_APART : ICS_TILE_WRAP, true, 0, 1}, plan);
     return replan(ctx, sp, 64, req, st);
   }
   ICS_HIP(device_wrap(ctx, sp, d_msgs, hdr_out, d_ip_ck, d_tcp_ck, payload_only, g, plan, st));
@@ -628,16 +614,12 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "twoclass" && (v == 0 || v == 8 || v == 16 || v == 32)) ctx->twoclass = int(v);
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
-    else if (k == "tile_form" && v >= 0 && v <= 2) ctx->tile_form = int(v);
-    else if (k == "span_sets" && (v == 2 || v == 3)) icsum::set_span_sets(uint32_t(v));
-    else if (k == "span_segs" && v >= 1 && v <= 63) icsum::set_span_segs(uint32_t(v));
+    else if (k == "span_segs" && v >= 0 && v <= 63) ctx->span_segs = uint32_t(v);
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);
     else if (k == "poison_ticket" && v > 0 && v <= 0xFFFFFFFFll) ctx->poison_ticket = uint32_t(v);
     else if (k == "tile" && v >= -1 && v <= 1) ctx->tile = int(v);
-    else if (k == "tile_segs" && v >= 0 && v <= 256) ctx->tile_segs = uint32_t(v);
-    else if (k == "tile_blocks" && v >= 0) ctx->tile_blocks = uint32_t(v);
     else return fail(ICS_ERR_INVALID, "ICSUM_FORCE: unknown or out-of-range '%s'", item.c_str());
   }
   return ICS_OK;

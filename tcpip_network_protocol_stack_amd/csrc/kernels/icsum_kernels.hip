@@ -1811,30 +1811,20 @@ __global__ __launch_bounds__(kBlock) void k_router_hdrs(const uint8_t* __restric
 
 // ------------------------------------------ tile launches (offsets) -------
 // An offsets batch is one packed byte stream: segment i = [off[i], off[i+1]).
-// A tile = T consecutive segments (T <= 256: one per thread of the block),
-// and the block streams the tile's bytes [off[i0] & ~15, off[i0 + T]) whole,
-// whatever the segment lengths: no lane idles on an ACK-sized segment and no
-// lane group waits on an MTU-sized one (the per-segment launches above map
-// one segment to a lane group).  Each wave takes a contiguous quarter of the
-// tile's 16-byte chunks and streams it on its own — windows of 256 chunks,
-// four coalesced dwordx4 loads per lane, two windows' loads in flight while
-// one is summed, no block barrier — keeping the exclusive prefix of its
-// chunks' even / odd byte sums (a DPP scan per wave instruction).  The
-// segments' points (thread t: lo_t <= hi_t, sorted over the tile) are read
-// off by the wave whose window holds them: F(x), the sums of the wave's bytes
-// below x, is the prefix at x's chunk plus that chunk masked below x.  After
-// one barrier, F(x) gains the earlier waves' totals and segment t's sums over
-// [lo_t, hi_t) are F(hi_t) - F(lo_t): exact in uint32 (addition mod 2^32),
-// roles by address parity.
+// The tile launch streams it by position, whatever the segment lengths: no
+// lane idles on an ACK-sized segment and no lane group waits on an MTU-sized
+// one (the per-segment launches above map one segment to a lane group).
+// Segment i's sums over [lo_i, hi_i) are F(hi_i) - F(lo_i), F(x) the sums of
+// the stream's bytes below x: exact in uint32 (addition mod 2^32), roles by
+// address parity.
 //   checksum  lo = start                        (checksum.h:20-41)
 //   IPv4/TCP  lo = start + 4 hlen (TCP part)    (ipv4_header.cpp:50, tcp_segment.cpp:11-18)
 //   wrap      lo = start + 40 (the payload)     (tcp_over_ip.cpp:69-88)
 //   wrap, headers apart: lo = start (segments are payloads), the headers go
-//             to an array of their own, 40 * T contiguous bytes per tile
-// Bytes below the tile's first segment in its first chunk are masked off in
-// every sum that can see them, so a neighbouring tile's in-place stores
-// (PATCH, wrap) never reach one; this tile's own stores follow its stream.
-constexpr uint32_t kTileMax = kBlock;          // segments per tile
+//             to an array of their own, 40 contiguous bytes per segment
+// k_span below runs it; round 4's k_tile (a block per T segments, each wave
+// streaming a quarter of the tile, the points sorted in LDS) is gone since
+// round 5 (git c581ecc; profiles/r5k_ab_span_ops.jsonl).
 constexpr uint32_t kWinChunks = 256;          // one wave window: 4 KiB, four loads per lane
 constexpr int kTileSum = 0, kTileIpv4 = 1, kTileWrap = 2, kTileWrapApart = 3;
 
@@ -1877,812 +1867,89 @@ struct TileArgs {
   uint32_t* hdr_out;
 };
 
-// One segment's inputs besides its bytes, loaded a tile ahead: its offsets and
-// the operation's per-segment words (checksum: initial sum and parity; IPv4:
-// the header dwords and the TCP fields at start + 20; wrap: the message record)
-struct TileSeg {
-  uint64_t s, e;
-  uint32_t w[9];
-};
-
-template <int OP>
-__device__ __forceinline__ TileSeg tile_seg_load(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                 uint64_t i, bool valid, uint64_t tend, const TileArgs& a,
-                                                 const uint8_t* zpad, const uint32_t* zlast) {
-  TileSeg g{};
-  if constexpr (OP == kTileIpv4) {  // the header loads below depend on the bounds
-    g.s = valid ? off[i] : tend;
-    g.e = valid ? off[i + 1] : tend;
-  } else {
-    // i is in range for every lane (the caller clamps it) and an invalid
-    // lane's bounds are never used: plain loads, no default written into
-    // their registers first (which makes the compiler wait for every load
-    // still in flight, the stream's prefetched windows included)
-    g.s = off[i];
-    g.e = off[i + 1];
-  }
-  if constexpr (OP == kTileSum) {
-    g.w[0] = a.init[i * a.init_step];
-    g.w[1] = a.odd[i * a.odd_step];
-  } else if constexpr (OP == kTileIpv4) {
-    // the raw dwords of load_hdr and load_tcp_fields (start + 20): aligned on the host side of alignbyte
-    const bool hdr = valid && g.e - g.s >= 20;
-    const uint32_t* last = hdr ? last_dword(bytes + g.e) : zlast;
-    const uint8_t* hp = hdr ? bytes + g.s : zpad;
-    const uint32_t* q = reinterpret_cast<const uint32_t*>(hp - (reinterpret_cast<uintptr_t>(hp) & 3u));
-#pragma unroll
-    for (int k = 0; k < 5; ++k) g.w[k] = q[k];
-    g.w[5] = *(q + 5 < last ? q + 5 : last);
-    const bool tcpf = hdr && g.e - (g.s + 20) >= 18;
-    const uint8_t* tp = tcpf ? bytes + g.s + 32 : zpad;
-    const uint32_t* tq = reinterpret_cast<const uint32_t*>(tp - (reinterpret_cast<uintptr_t>(tp) & 3u));
-    const uint32_t* tlast = tcpf ? last : zlast;
-    g.w[6] = tq[0];
-    g.w[7] = tq[1];
-    g.w[8] = *(tq + 2 < tlast ? tq + 2 : tlast);
-  } else {  // both wraps: the message record
-    const uint32_t* r = reinterpret_cast<const uint32_t*>(a.msgs + i);
-#pragma unroll
-    for (int k = 0; k < 7; ++k) g.w[k] = r[k];
-  }
-  return g;
-}
-
-template <int OP, int OUT>
-__global__ __launch_bounds__(kBlock) void k_tile(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                 uint64_t n, uint32_t T, TileArgs a, uint32_t remap,
-                                                 const u32x4* __restrict__ zero16) {
-  constexpr uint32_t kWaves = kBlock / 64;
-  __shared__ uint64_t s_pt[2 * kTileMax];    // the tile's points, sorted: lo_0, hi_0, lo_1, hi_1, ...
-  __shared__ uint32_t s_f[2 * kTileMax][2];  // F of each point over its wave's range (even, odd sums)
-  __shared__ uint32_t s_pre[kWaves][kWinChunks][2];  // each wave's window: exclusive prefix per chunk
-  // ... and its chunks (masked to the tile); the wrap's staged headers once the stream is done
-  __shared__ u32x4 s_raw[kWaves][kWinChunks];
-  __shared__ uint32_t s_tot[kWaves][2];
-  static_assert(sizeof(s_raw) >= 10 * kTileMax * 4, "the wraps stage their headers in s_raw");
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform, in a scalar register
-  const uint64_t ntiles = (n + T - 1) / T;
-  const uint8_t* const zpad = reinterpret_cast<const uint8_t*>(zero16);
-  const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zero16) + 7;
-  // A tile's geometry (block-uniform, scalar loads): its segments, bytes,
-  // 16-byte chunks and this wave's quarter of them in windows of kWinChunks
-  // (counted up to a multiple of 4: the window loop below is unrolled by 4)
-  struct Geo {
-    uint64_t i0, first, a0, nch, quarter, wc0, wc1, nwin4;
-    uint32_t m;
-  };
-  auto geo_of = [&](uint64_t t) {
-    Geo g{};
-    if (t >= ntiles) return g;  // no tile: every range empty
-    g.i0 = t * T;
-    g.m = uint32_t(n - g.i0 < T ? n - g.i0 : T);
-    g.first = off[g.i0];
-    const uint64_t tend = off[g.i0 + g.m];
-    g.a0 = g.first & ~uint64_t(15);
-    g.nch = tend > g.a0 ? (tend - g.a0 + 15) >> 4 : 0;
-    const uint64_t q = (((g.nch + kWaves - 1) / kWaves) + 63) & ~uint64_t(63);
-    g.quarter = q ? q : 64;
-    g.wc0 = g.quarter * wv < g.nch ? g.quarter * wv : g.nch;
-    g.wc1 = g.wc0 + g.quarter < g.nch ? g.wc0 + g.quarter : g.nch;
-    g.nwin4 = ((g.wc1 - g.wc0 + kWinChunks - 1) / kWinChunks + 3) & ~uint64_t(3);
-    return g;
-  };
-  // window k of a tile: chunks [c0, c0 + len) (wave-uniform), read with
-  // buffer loads through a scalar resource spanning exactly those chunks: the
-  // lane offset is one 32-bit register for every window, instruction u adds u
-  // KiB as an immediate, and chunks past the range (a short last window, a
-  // window past the end, no tile at all) read as zeros without touching memory
-  const uint32_t voff = lane * 16u;
-  auto load_win = [&](const Geo& g, uint64_t k, u32x4 (&v)[4]) {
-    const uint64_t c0 = g.wc0 + k * kWinChunks;
-    const uint64_t left = g.wc1 > c0 ? g.wc1 - c0 : 0;
-    const uint32_t len = uint32_t(left < kWinChunks ? left : kWinChunks);
-    const u32x4* pw = reinterpret_cast<const u32x4*>(bytes + g.a0) + c0;
-#ifdef ICSUM_BOUNDS_CHECK
-    if (len) {  // the window's first and last chunk inside the tile's envelope
-      const uint8_t* lo8 = bytes + g.a0;
-      ICS_CHECK16(pw, lo8, lo8 + (g.nch << 4));
-      ICS_CHECK16(pw + len - 1, lo8, lo8 + (g.nch << 4));
-    }
-#endif
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4*>(pw), 0, int(len * 16u), 0x00020000);
-#pragma unroll
-    for (int u = 0; u < 4; ++u)  // aux 2: non-temporal
-      v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 1024, 2));
-  };
-  uint64_t tile = block_order(remap);
-  Geo g = geo_of(tile);
-  // this thread's segment of the first tile, then the tile's first three windows
-  TileSeg sg_a = tile_seg_load<OP>(bytes, off, g.i0 + (tid < g.m ? tid : 0u), tid < g.m, off[g.i0 + g.m], a, zpad,
-                                   zlast);
-  TileSeg sg_b{};
-  u32x4 b0[4], b1[4], b2[4], b3[4];
-  load_win(g, 0, b0);
-  load_win(g, 1, b1);
-  load_win(g, 2, b2);
-  // One tile: g, its segments' words in cur_sg; the next tile of this block
-  // is gn, whose words go to nxt_sg and whose first three windows are loaded
-  // by this tile's last window group.  The two TileSeg sets alternate between
-  // the loop's two calls (no register copy of a load still in flight, which
-  // would drain every outstanding load at the tile boundary).
-  auto run_tile = [&](const Geo& gn, const TileSeg& cur_sg, TileSeg& nxt_sg) {
-    const bool valid = tid < g.m;
-    const uint64_t i = g.i0 + (valid ? tid : 0u);
-    const uint64_t s = cur_sg.s, e = cur_sg.e;
-#ifdef ICSUM_BOUNDS_CHECK
-    if (valid && e < s) bounds_fail(kBoundsOffsets, i);
-#endif
-    // ---- this tile's points; the per-segment words of the next tile requested
-    Hdr h{};
-    uint32_t tf0 = 0, tf1 = 0;
-    bool hdr = false;
-    uint64_t lo = s;
-    if constexpr (OP == kTileIpv4) {
-      hdr = valid && e - s >= 20;
-      const uint32_t sh = uint32_t(s) & 3u, tsh = uint32_t(s + 32) & 3u;
-#pragma unroll
-      for (int k = 0; k < 5; ++k) h.w[k] = __builtin_amdgcn_alignbyte(cur_sg.w[k + 1], cur_sg.w[k], sh);
-      tf0 = __builtin_amdgcn_alignbyte(cur_sg.w[7], cur_sg.w[6], tsh);
-      tf1 = __builtin_amdgcn_alignbyte(cur_sg.w[8], cur_sg.w[7], tsh);
-      if (hdr) {
-        uint64_t o = 4u * (h.byte(0) & 0x0fu);  // options skipped (ipv4_header.cpp:50)
-        if (o < 20) o = 20;
-        if (o > e - s) o = e - s;
-        lo = s + o;
-      } else {
-        lo = e;
-      }
-    } else if constexpr (OP == kTileWrap) {
-      lo = e - s >= 40 ? s + 40 : e;
-    }
-    nxt_sg = tile_seg_load<OP>(bytes, off, gn.i0 + (tid < gn.m ? tid : 0u), tid < gn.m,
-                               gn.m ? off[gn.i0 + gn.m] : 0, a, zpad, zlast);
-    if (valid) {
-      s_pt[2 * tid] = lo;
-      s_pt[2 * tid + 1] = e;
-    }
-    __syncthreads();
-    const uint32_t npt = 2 * g.m;
-    const uint64_t a0c = g.a0 >> 4;
-    auto chunk_of = [&](uint64_t x) { return (x >> 4) - a0c; };
-    const u32x4 m0 = byte_range_mask(uint32_t(g.first) & 15u, 16u);  // chunk 0: the tile's bytes only
-    // this wave's first point: the first whose chunk is >= wc0 (uniform binary search)
-    uint32_t cur = 0;
-    {
-      uint32_t lo_i = 0, hi_i = npt;
-      while (lo_i < hi_i) {
-        const uint32_t mid = (lo_i + hi_i) >> 1;
-        if (chunk_of(s_pt[mid]) < g.wc0) lo_i = mid + 1;
-        else hi_i = mid;
-      }
-      cur = __builtin_amdgcn_readfirstlane(lo_i);
-    }
-    uint32_t ce = 0, co = 0;  // this wave's sums so far
-    auto window = [&](uint64_t k, const u32x4 (&v)[4]) {
-      const uint64_t c0 = g.wc0 + k * kWinChunks;
-      if (c0 >= g.wc1) return;  // uniform
-      const uint32_t len = uint32_t(g.wc1 - c0 < kWinChunks ? g.wc1 - c0 : kWinChunks);
-      const uint64_t c1 = c0 + len;
-      // the window's chunks to LDS as loaded (chunk r = 64 u + lane), then
-      // read back four consecutive ones per lane (chunks 4 lane .. 4 lane + 3):
-      // a lane's prefix over its own four is three adds, and ONE wave scan of
-      // the lane totals (per role) gives every chunk's exclusive prefix —
-      // instead of a wave scan per loaded row (four per role)
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const uint32_t r = uint32_t(u) * 64u + lane;
-        u32x4 x = v[u];  // zeros past the range
-        if (c0 == 0 && r == 0) x &= m0;
-        s_raw[wv][win_slot(r)] = x;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      uint32_t pe[4], po[4], te = 0, to = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t ev = 0, od = 0;
-        acc_chunk(s_raw[wv][win_slot(4u * lane + uint32_t(j))], ev, od);
-        pe[j] = te;
-        po[j] = to;
-        te += ev;
-        to += od;
-      }
-      const uint32_t ie = wave_prefix_incl(te), io = wave_prefix_incl(to);
-      const uint32_t xe = ce + ie - te, xo = co + io - to;  // sums of the window's chunks below 4 lane
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s_pre[wv][4u * lane + uint32_t(j)][0] = xe + pe[j];
-        s_pre[wv][4u * lane + uint32_t(j)][1] = xo + po[j];
-      }
-      ce += __builtin_amdgcn_readlane(ie, 63);
-      co += __builtin_amdgcn_readlane(io, 63);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // the points in this window, 64 per round (sorted: a prefix of the lanes)
-      for (;;) {  // uniform
-        const uint32_t pi = cur + lane;
-        const uint64_t x = pi < npt ? s_pt[pi] : ~uint64_t(0);
-        const uint64_t c = pi < npt ? chunk_of(x) : ~uint64_t(0);
-        const bool in = c < c1;
-        if (in) {
-          const uint32_t k2 = uint32_t(c - c0);
-          uint32_t pe = s_pre[wv][k2][0], po = s_pre[wv][k2][1];
-          acc_chunk(s_raw[wv][win_slot(k2)] & byte_range_mask(0u, uint32_t(x) & 15u), pe, po);
-          s_f[pi][0] = pe;
-          s_f[pi][1] = po;
-        }
-        const uint32_t cnt = uint32_t(__builtin_popcountll(__ballot(in)));
-        cur += cnt;
-        if (cnt < 64) break;
-      }
-      __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
-    };
-    // Four register sets in turn: three windows' loads in flight while one is
-    // summed.  Loads past this tile's windows fetch the next tile's first
-    // three (a window past any range returns at once: a uniform branch), so
-    // the stream does not pause at the tile boundary.
-    auto load_any = [&](uint64_t k, u32x4 (&v)[4]) {
-      if (k < g.nwin4) load_win(g, k, v);
-      else load_win(gn, k - g.nwin4, v);
-    };
-    for (uint64_t k = 0; k < g.nwin4; k += 4) {  // wave-uniform
-      load_any(k + 3, b3);
-      window(k, b0);
-      load_any(k + 4, b0);
-      window(k + 1, b1);
-      load_any(k + 5, b1);
-      window(k + 2, b2);
-      load_any(k + 6, b2);
-      window(k + 3, b3);
-    }
-    if (g.nwin4 == 0) {  // an empty quarter: the next tile's windows still go out now
-      load_win(gn, 0, b0);
-      load_win(gn, 1, b1);
-      load_win(gn, 2, b2);
-    }
-    if (lane == 0) {
-      s_tot[wv][0] = ce;
-      s_tot[wv][1] = co;
-    }
-    __syncthreads();
-    // F(x) = x's sums within its wave's range + the earlier waves' totals; a
-    // point at the aligned end of the last chunk: every chunk is below it
-    auto F = [&](uint32_t pi, uint64_t x, uint32_t& fe, uint32_t& fo) {
-      const uint64_t c = chunk_of(x);
-      const uint32_t owner = c >= g.nch ? kWaves : uint32_t(c / g.quarter);
-      fe = c >= g.nch ? 0u : s_f[pi][0];
-      fo = c >= g.nch ? 0u : s_f[pi][1];
-#pragma unroll
-      for (uint32_t w = 0; w < kWaves; ++w) {
-        fe += w < owner ? s_tot[w][0] : 0u;
-        fo += w < owner ? s_tot[w][1] : 0u;
-      }
-    };
-    uint32_t fle = 0, flo = 0, fhe = 0, fho = 0;
-    if (valid) {
-      F(2 * tid, lo, fle, flo);
-      F(2 * tid + 1, e, fhe, fho);
-    }
-    const uint32_t se = fhe - fle, so = fho - flo;  // sums of [lo, e)
-    if constexpr (OP == kTileSum) {
-      if (valid) {
-        const uint32_t sum = cur_sg.w[0] + combine_roles(se, so, (uint32_t(lo) ^ cur_sg.w[1]) & 1u);
-        if (OUT == 0)
-          static_cast<uint16_t*>(a.out)[i] = fold_value(sum);
-        else
-          static_cast<uint32_t*>(a.out)[i] = sum;
-      }
-    } else if constexpr (OP == kTileIpv4) {
-      if (valid) {
-        if (hdr && lo != s + 20) {  // options: the TCP fields at the real start
-          tf0 = tf1 = 0;
-          if (e - lo >= 18) load_tcp_fields(bytes + lo, last_dword(bytes + e), tf0, tf1);
-        }
-        ipv4_result(bytes, s, e, lo, hdr, h, tf0, tf1, combine_roles(se, so, uint32_t(lo) & 1u), a.mode, i,
-                    a.ip_ck, a.tcp_ck, a.status);
-      }
-    } else {
-      uint32_t* const stage = reinterpret_cast<uint32_t*>(&s_raw[0][0]);  // the stream is done with it
-      const bool ok = valid && (OP == kTileWrapApart || e - s >= 40);
-      uint32_t ipc = 0, tcv = 0;
-      const u32x4 ra = {cur_sg.w[0], cur_sg.w[1], cur_sg.w[2], cur_sg.w[3]};
-      if (valid) wrap_header(ra, cur_sg.w[4], cur_sg.w[5], cur_sg.w[6] & 0xffffu, e - lo,
-                             combine_roles(se, so, uint32_t(lo) & 1u), stage + tid * 10, ipc, tcv);
-      if (valid) {
-        if (a.ip_ck) a.ip_ck[i] = ok ? uint16_t(ipc) : uint16_t(0);
-        if (a.tcp_ck) a.tcp_ck[i] = ok ? uint16_t(tcv) : uint16_t(0);
-      }
-      __syncthreads();
-      if constexpr (OP == kTileWrapApart) {
-        // the tile's headers are 10 * m consecutive dwords of the array: plain coalesced stores
-        uint32_t* const dst = a.hdr_out + g.i0 * 10;
-#pragma unroll 2
-        for (uint32_t j = 0; j < 10; ++j) {
-          const uint32_t t = j * kBlock + tid;
-          if (t < 10 * g.m) dst[t] = stage[t];
-        }
-      } else {
-        // in place: dword t of the tile = dword t % 10 of datagram t / 10
-        // (neighbouring lanes, neighbouring bytes), 256 per store round
-#pragma unroll 2
-        for (uint32_t j = 0; j < 10; ++j) {
-          const uint32_t t = j * kBlock + tid, d = t / 10, k = t - d * 10;
-          if (d < g.m) {
-            const uint64_t ds = d ? s_pt[2 * d - 1] : g.first, de = s_pt[2 * d + 1];
-            if (de - ds >= 40) {
-              const uint32_t v = stage[t];
-              uint8_t* q8 = bytes + ds + 4 * k;
-              if ((reinterpret_cast<uintptr_t>(q8) & 3u) == 0) {
-                *reinterpret_cast<uint32_t*>(q8) = v;
-              } else {
-#pragma unroll
-                for (int b = 0; b < 4; ++b) q8[b] = uint8_t(v >> (8 * b));
-              }
-            }
-          }
-        }
-      }
-    }
-    __syncthreads();  // the shared arrays are the next tile's
-  };
-  while (tile < ntiles) {  // block-uniform; two tiles per pass, the TileSeg sets in turn
-    Geo gn = geo_of(tile + gridDim.x);
-    run_tile(gn, sg_a, sg_b);
-    tile += gridDim.x;
-    g = gn;
-    if (tile >= ntiles) break;
-    gn = geo_of(tile + gridDim.x);
-    run_tile(gn, sg_b, sg_a);
-    tile += gridDim.x;
-    g = gn;
-  }
-}
-
-// ------------------------- tile stream with a metadata wave (round 5) ------
-// k_tile keeps each tile's metadata (segment bounds, inits or message
-// records) in VGPRs loaded a tile ahead, between the windows' loads.  gfx9's
-// vmcnt retires loads in issue order, so every wait the compiler places for
-// those registers (the default written into a masked load's destination, the
-// phi copies between the two TileSeg sets) waits for all the window loads
-// issued before them: the stream drained at each tile start (s_waitcnt
-// vmcnt(0) in the ISA) and ran one to two windows deep inside a tile.
-// k_stream gives the roles to different waves of one block:
-//   * four stream waves issue NOTHING but window loads (no stores, no other
-//     loads): three register sets, each reloaded as soon as its window is in
-//     LDS — three windows in flight while one is summed — and the prefetch
-//     runs on across tile boundaries;
-//   * a fifth, metadata wave loads the next tile's offsets into LDS (with the
-//     first point of each stream wave's range, so the stream waves search
-//     nothing) and, while the stream waves run tile j + 1, finishes tile j:
-//     F at every point, each segment's sums, its folded checksum or its
-//     40-byte header, the stores.  The last tile is finished by all 320
-//     threads.
-// The points of the lo = start operations (checksum, headers-apart wrap) are
-// the offsets themselves: segment t is [off[t], off[t+1]), m + 1 points per
-// tile, F(t + 1) - F(t) its sums.  One block barrier per tile; LDS (33 KiB)
-// and registers keep four blocks per CU.  Stream-wave point pass as k_tile's,
-// with the lane's point held in registers across windows (an LDS read per 64
-// points, not per window).
-#ifdef ICSUM_STAMPS
-// diagnostic build only (tools/probe/stream_stamps.hip): per block and wave,
-// shader-clock cycles spent working on tiles, waiting at the tile barrier,
-// finishing the last tile, and the tiles seen
-__device__ uint64_t g_stream_stamps[4096][5][4];
-#endif
-constexpr uint32_t kSW = 4;                          // stream waves per block
-constexpr uint32_t kStreamBlock = (kSW + 1) * 64;    // + the metadata wave
-constexpr uint32_t kStreamResident = 1024;           // blocks resident at once: 4 per CU x 256 CUs
-
-template <int OP, int OUT>
-__global__ __launch_bounds__(kStreamBlock) void k_stream(const uint8_t* __restrict__ bytes,
-                                                         const uint64_t* __restrict__ off, uint64_t n, uint32_t T,
-                                                         TileArgs a, uint32_t remap) {
-  static_assert(OP == kTileSum || OP == kTileWrapApart, "k_stream: operations whose points are the offsets");
-  __shared__ uint64_t s_pt[2][kTileMax + 1];    // a tile's offsets off[i0 .. i0 + m]: its points
-  __shared__ uint32_t s_f[2][kTileMax + 1][2];  // F of each point over its stream wave's range (even, odd)
-  __shared__ uint32_t s_tot[2][kSW][2];         // each stream wave's sums
-  __shared__ uint32_t s_first[2][kSW];          // the first point of each stream wave's range
-  __shared__ uint32_t s_pre[kSW][kWinChunks][2];
-  __shared__ u32x4 s_raw[kSW][kWinChunks];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);  // wave-uniform
-  const bool meta = wv == kSW;
-  const uint64_t ntiles = (n + T - 1) / T;
-  // A tile's geometry (scalar loads): segments, the 16-byte chunks of its
-  // bytes [first & ~15, off[i0 + m]), this wave's quarter of them and its
-  // windows (a multiple of 3, at least 3: the window loop is unrolled by 3);
-  // the metadata wave's range is empty
-  struct Geo {
-    uint64_t i0, a0c, nch, quarter, wc0, wc1, nwin3;
-    uint32_t m;
-  };
-  auto geo_of = [&](uint64_t t) {
-    Geo g{};
-    if (t >= ntiles) return g;  // no tile: m = 0, every range empty
-    g.i0 = t * T;
-    g.m = uint32_t(n - g.i0 < T ? n - g.i0 : T);
-    const uint64_t first = off[g.i0], tend = off[g.i0 + g.m];
-    g.a0c = first >> 4;
-    g.nch = tend > (g.a0c << 4) ? ((tend + 15) >> 4) - g.a0c : 0;
-    const uint64_t q = (((g.nch + kSW - 1) / kSW) + 63) & ~uint64_t(63);
-    g.quarter = q ? q : 64;
-    const uint64_t w = meta ? kSW : wv;
-    g.wc0 = g.quarter * w < g.nch ? g.quarter * w : g.nch;
-    g.wc1 = g.wc0 + g.quarter < g.nch ? g.wc0 + g.quarter : g.nch;
-    // at least one group of three, so an empty range still issues the next
-    // tile's first windows through the loop's own load sites
-    const uint64_t nw3 = ((g.wc1 - g.wc0 + kWinChunks - 1) / kWinChunks + 2) / 3 * 3;
-    g.nwin3 = nw3 ? nw3 : 3;
-    return g;
-  };
-  // window k of a stream wave's range (as k_tile: raw buffer loads through a
-  // resource spanning exactly the window's chunks, zeros past it)
-  const uint32_t voff = lane * 16u;
-  auto load_win = [&](const Geo& g, uint64_t k, u32x4 (&v)[4]) {
-    const uint64_t c0 = g.wc0 + k * kWinChunks;
-    const uint64_t left = g.wc1 > c0 ? g.wc1 - c0 : 0;
-    const uint32_t len = uint32_t(left < kWinChunks ? left : kWinChunks);
-    const u32x4* pw = reinterpret_cast<const u32x4*>(bytes) + g.a0c + c0;
-#ifdef ICSUM_BOUNDS_CHECK
-    if (len) {
-      const uint8_t* lo8 = bytes + (g.a0c << 4);
-      ICS_CHECK16(pw, lo8, lo8 + (g.nch << 4));
-      ICS_CHECK16(pw + len - 1, lo8, lo8 + (g.nch << 4));
-    }
-#endif
-    const __amdgpu_buffer_rsrc_t rs =
-        __builtin_amdgcn_make_buffer_rsrc(const_cast<u32x4*>(pw), 0, int(len * 16u), 0x00020000);
-#pragma unroll
-    for (int u = 0; u < 4; ++u)  // aux 2: non-temporal
-      v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 1024, 2));
-  };
-  u32x4 b0[4], b1[4], b2[4];
-
-  // ---- stream wave: tile g (points in buffer buf); three register sets,
-  // each reloaded as soon as its window is in LDS, so three windows are in
-  // flight while one is summed; the last window group loads the next tile
-  // gn's first three
-  auto stream_tile = [&](const Geo& g, const Geo& gn, uint32_t buf) {
-    const uint32_t npt = g.m + 1;
-    uint32_t cur = s_first[buf][wv];  // the first point not yet placed (wave-uniform)
-    uint32_t pbase = cur;             // this lane holds point pbase + lane: its chunk (tile-relative) and byte
-    uint64_t pc = ~uint64_t(0);
-    uint32_t pb = 0;
-    auto hold = [&]() {
-      const uint32_t pi = pbase + lane;
-      const uint64_t x = pi < npt ? s_pt[buf][pi] : ~uint64_t(0);
-      pc = pi < npt ? (x >> 4) - g.a0c : ~uint64_t(0);
-      pb = uint32_t(x) & 15u;
-    };
-    hold();
-    uint32_t ce = 0, co = 0;  // this wave's sums so far
-    auto load_any = [&](uint64_t k, u32x4 (&v)[4]) {
-      if (k < g.nwin3) load_win(g, k, v);
-      else load_win(gn, k - g.nwin3, v);
-    };
-    auto window = [&](uint64_t k, u32x4 (&v)[4], uint64_t knext) {
-      const uint64_t c0 = g.wc0 + k * kWinChunks;
-      const bool live = c0 < g.wc1;  // uniform; else a padding window
-      // chunks to LDS as loaded (chunk r = 64 u + lane), read back four
-      // consecutive ones per lane (4 lane .. 4 lane + 3): a lane prefix of
-      // three adds and ONE wave scan per role give every chunk's prefix
-      if (live) {
-#pragma unroll
-        for (int u = 0; u < 4; ++u) s_raw[wv][win_slot(uint32_t(u) * 64u + lane)] = v[u];
-      }
-      // the registers are free: window knext goes out now (one load site for
-      // both paths, so the loads' destination is the same registers)
-      load_any(knext, v);
-      if (!live) return;
-      const uint64_t c1 = g.wc1 - c0 < kWinChunks ? g.wc1 : c0 + kWinChunks;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      uint32_t pe[4], po[4], te = 0, to = 0;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint32_t ev = 0, od = 0;
-        acc_chunk(s_raw[wv][win_slot(4u * lane + uint32_t(j))], ev, od);
-        pe[j] = te;
-        po[j] = to;
-        te += ev;
-        to += od;
-      }
-      const uint32_t ie = wave_prefix_incl(te), io = wave_prefix_incl(to);
-      const uint32_t xe = ce + ie - te, xo = co + io - to;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        s_pre[wv][4u * lane + uint32_t(j)][0] = xe + pe[j];
-        s_pre[wv][4u * lane + uint32_t(j)][1] = xo + po[j];
-      }
-      ce += __builtin_amdgcn_readlane(ie, 63);
-      co += __builtin_amdgcn_readlane(io, 63);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // the points in this window: the held ones from `cur` on whose chunk
-      // is below c1 (sorted, so a prefix of them); a new set of 64 when all
-      // held points were placed
-      for (;;) {  // uniform
-        const uint32_t pi = pbase + lane;
-        const bool in = pi >= cur && pc < c1;
-        if (in) {
-          const uint32_t k2 = uint32_t(pc - c0);
-          uint32_t fe = s_pre[wv][k2][0], fo = s_pre[wv][k2][1];
-          acc_chunk(s_raw[wv][win_slot(k2)] & byte_range_mask(0u, pb), fe, fo);
-          s_f[buf][pi][0] = fe;
-          s_f[buf][pi][1] = fo;
-        }
-        cur += uint32_t(__builtin_popcountll(__ballot(in)));
-        if (cur < pbase + 64u) break;
-        pbase = cur;
-        hold();
-      }
-      __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
-    };
-    for (uint64_t k = 0; k < g.nwin3; k += 3) {  // wave-uniform
-      window(k, b0, k + 3);
-      window(k + 1, b1, k + 4);
-      window(k + 2, b2, k + 5);
-    }
-    if (lane == 0) {
-      s_tot[buf][wv][0] = ce;
-      s_tot[buf][wv][1] = co;
-    }
-  };
-
-  // ---- metadata wave: a tile's points (fetch: every load in flight at
-  // once; store: into buffer buf, with each stream wave's first point = the
-  // number of points below its range)
-  constexpr uint32_t kRounds = (kTileMax + 64) / 64;
-  auto fetch_points = [&](const Geo& g, uint64_t (&xs)[kRounds]) {
-#pragma unroll
-    for (uint32_t r = 0; r < kRounds; ++r) {
-      const uint32_t p = r * 64u + lane;
-      xs[r] = off[g.i0 + (p <= g.m ? p : g.m)];
-    }
-  };
-  auto store_points = [&](const Geo& g, uint32_t buf, const uint64_t (&xs)[kRounds]) {
-    uint32_t below[kSW] = {};
-#pragma unroll
-    for (uint32_t r = 0; r < kRounds; ++r) {
-      const uint32_t p = r * 64u + lane;
-      const bool ok = p <= g.m;
-      const uint64_t x = xs[r];
-      if (ok) s_pt[buf][p] = x;
-      const uint64_t c = (x >> 4) - g.a0c;
-#pragma unroll
-      for (uint32_t w = 1; w < kSW; ++w) {
-        const uint64_t wc0 = g.quarter * w < g.nch ? g.quarter * w : g.nch;
-        below[w] += uint32_t(__builtin_popcountll(__ballot(ok && c < wc0)));
-      }
-    }
-    if (lane < kSW) {
-      uint32_t v = 0;
-#pragma unroll
-      for (uint32_t w = 1; w < kSW; ++w) v = lane == w ? below[w] : v;
-      s_first[buf][lane] = v;
-    }
-  };
-
-  // ---- finishing a tile: segments t0, t0 + step, ..., R of them per thread
-  // (the metadata wave alone: four per lane; the last tile: one per thread
-  // of the block).  fetch: the per-segment words (checksum: init, parity;
-  // wrap: the 28-byte record), every load in flight at once; emit: F at the
-  // two points, the segment's sums, its output
-  constexpr uint32_t kWords = OP == kTileSum ? 2 : 7;
-  auto fetch = [&](const Geo& g, uint32_t t0, uint32_t step, auto& w) {
-    constexpr uint32_t R = std::extent<std::remove_reference_t<decltype(w)>>::value;
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) {
-      const uint32_t t = t0 + r * step;
-      const uint64_t i = g.i0 + (t < g.m ? t : 0u);
-      if constexpr (OP == kTileSum) {
-        w[r][0] = a.init[i * a.init_step];
-        w[r][1] = a.odd[i * a.odd_step];
-      } else {
-        const uint32_t* rec = reinterpret_cast<const uint32_t*>(a.msgs + i);
-#pragma unroll
-        for (int k = 0; k < 7; ++k) w[r][k] = rec[k];
-      }
-    }
-  };
-  auto emit = [&](const Geo& g, uint32_t buf, uint32_t t0, uint32_t step, const auto& w) {
-    constexpr uint32_t R = std::extent<std::remove_reference_t<decltype(w)>>::value;
-    uint32_t te[kSW + 1], to[kSW + 1];  // the stream waves' totals before wave q
-    te[0] = to[0] = 0;
-#pragma unroll
-    for (uint32_t q = 0; q < kSW; ++q) {
-      te[q + 1] = te[q] + s_tot[buf][q][0];
-      to[q + 1] = to[q] + s_tot[buf][q][1];
-    }
-    auto F = [&](uint32_t p, uint64_t x, uint32_t& fe, uint32_t& fo) {
-      const uint64_t c = (x >> 4) - g.a0c;
-      if (c >= g.nch) {  // the aligned end of the last chunk: every byte is below it
-        fe = te[kSW];
-        fo = to[kSW];
-        return;
-      }
-      const uint32_t owner = uint32_t(c >= g.quarter) + uint32_t(c >= 2 * g.quarter) + uint32_t(c >= 3 * g.quarter);
-      uint32_t be = 0, bo = 0;
-#pragma unroll
-      for (uint32_t q = 1; q < kSW; ++q) {
-        be = owner == q ? te[q] : be;
-        bo = owner == q ? to[q] : bo;
-      }
-      fe = s_f[buf][p][0] + be;
-      fo = s_f[buf][p][1] + bo;
-    };
-    static_assert(kSW == 4, "F's owner: three quarter boundaries");
-#pragma unroll
-    for (uint32_t r = 0; r < R; ++r) {
-      const uint32_t t = t0 + r * step;
-      if (t >= g.m) break;
-      const uint64_t i = g.i0 + t;
-      const uint64_t s = s_pt[buf][t], e = s_pt[buf][t + 1];
-      uint32_t fle, flo, fhe, fho;
-      F(t, s, fle, flo);
-      F(t + 1, e, fhe, fho);
-      const uint32_t se = fhe - fle, so = fho - flo;  // sums of [s, e), roles by address
-      if constexpr (OP == kTileSum) {
-        const uint32_t sum = w[r][0] + combine_roles(se, so, (uint32_t(s) ^ w[r][1]) & 1u);
-        if (OUT == 0)
-          static_cast<uint16_t*>(a.out)[i] = fold_value(sum);
-        else
-          static_cast<uint32_t*>(a.out)[i] = sum;
-      } else {
-        uint32_t h[10], ipc = 0, tcv = 0;
-        wrap_header(u32x4{w[r][0], w[r][1], w[r][2], w[r][3]}, w[r][4], w[r][5], w[r][6] & 0xffffu, e - s,
-                    combine_roles(se, so, uint32_t(s) & 1u), h, ipc, tcv);
-        uint2* dst = reinterpret_cast<uint2*>(a.hdr_out + i * 10);
-#pragma unroll
-        for (int k = 0; k < 5; ++k) dst[k] = uint2{h[2 * k], h[2 * k + 1]};
-        if (a.ip_ck) a.ip_ck[i] = uint16_t(ipc);
-        if (a.tcp_ck) a.tcp_ck[i] = uint16_t(tcv);
-      }
-    }
-  };
-
-  // ---- the block's tiles: block_order's tile, then every gridDim-th; one
-  // block barrier per tile (B_j): before it the stream waves have summed
-  // tile j and the metadata wave has finished tile j - 1 and stored tile
-  // j + 1's points; after it the stream waves run tile j + 1 while the
-  // metadata wave finishes tile j and stores tile j + 2's points into the
-  // buffer tile j used.  The two roles run their own loops (same barriers,
-  // same tiles), so the compiler's waits in the stream loop never see the
-  // metadata wave's loads.
-  uint64_t tile = block_order(remap);
-  if (tile >= ntiles) return;  // block-uniform, before any barrier
-  Geo g = geo_of(tile);
-  Geo gn = geo_of(tile + gridDim.x);
-  uint32_t buf = 0;
-  if (meta) {
-    uint64_t xs[kRounds];
-    fetch_points(g, xs);
-    store_points(g, 0, xs);
-    __syncthreads();
-    Geo gnn = geo_of(tile + 2ull * gridDim.x);
-    if (gn.m) {
-      fetch_points(gn, xs);
-      store_points(gn, 1, xs);
-    }
-    for (;;) {
-      __syncthreads();  // B_j
-      if (gn.m == 0) break;
-      // one memory round trip per tile: tile j's words (four segments per
-      // lane), tile j + 2's points and tile j + 3's geometry all requested
-      // before any is used
-      uint32_t w[(kTileMax + 63) / 64][kWords];
-      fetch(g, lane, 64u, w);
-      if (gnn.m) fetch_points(gnn, xs);
-      const Geo g3 = geo_of(tile + 3ull * gridDim.x);
-      emit(g, buf, lane, 64u, w);
-      if (gnn.m) store_points(gnn, buf, xs);
-      tile += gridDim.x;
-      g = gn;
-      gn = gnn;
-      gnn = g3;
-      buf ^= 1u;
-    }
-  } else {  // in this order: the loop consumes b0 first, and vmcnt retires loads in issue order
-    load_win(g, 0, b0);
-    __builtin_amdgcn_sched_barrier(0);
-    load_win(g, 1, b1);
-    __builtin_amdgcn_sched_barrier(0);
-    load_win(g, 2, b2);
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    for (;;) {
-      stream_tile(g, gn, buf);
-      __syncthreads();  // B_j
-      if (gn.m == 0) break;
-      tile += gridDim.x;
-      g = gn;
-      gn = geo_of(tile + gridDim.x);
-      buf ^= 1u;
-    }
-  }
-  // the block's last tile: every thread finishes it
-  uint32_t w1[1][kWords];
-  fetch(g, tid, kStreamBlock, w1);
-  emit(g, buf, tid, kStreamBlock, w1);
-}
-
 // ---------------------------------------- wave spans (round 5) -------------
-// k_span: every wave on its own.  Wave w owns segments [63 w, 63 w + 63) of
-// an offsets batch and streams their bytes [off[i0] & ~15, off[i0 + m]) as
-// one range in 4 KiB windows (k_stream's window pass: three register sets,
-// each reloaded as soon as its window is in LDS, swizzled slots, one wave
-// scan per role).  Lane p holds point p = off[i0 + p] (p <= m <= 63) in
-// registers for the whole span: the window holding it sets the lane's F
-// (prefix + masked chunk) — no point lists, loops or LDS buffers — and
-// segment t's sums are F(t + 1) - F(t), lane t + 1's value one shuffle away.
+// k_span: every wave on its own.  Wave w owns segments [S w, S w + S) of an
+// offsets batch (S <= 63: the dispatch sizes spans from the batch's mean
+// length) and streams their bytes [off[i0] & ~15, off[i0 + m]) as
+// one range in 4 KiB windows: three register sets, each reloaded as soon as
+// its window is in LDS (three windows in flight while one is summed), the
+// window written to swizzled LDS slots as loaded and read back four chunks
+// per lane, one wave scan per role.  Lane p holds point A = off[i0 + p]
+// (p <= m <= S) in registers for the whole span: the window holding it sets
+// the lane's F (prefix + masked chunk) — no point lists, loops or LDS buffers
+// — and segment t's sums up to its end are F(t + 1), lane t + 1's value one
+// shuffle away.  The lo = start operations (checksum; headers-apart wrap)
+// take segment t's sums as F(t + 1) - F(t); the others give lane t a second
+// point B = lo_t (IPv4: start + 4 IHL, the header's first dword fetched
+// before the stream; in-place wrap: start + 40) and take F(t + 1) - F(B).
 // No block barrier and no block-level state: a block is four independent
 // waves, and the hardware dispatcher balances them over the chip the way it
 // does one-shot waves (a persistent or one-tile-per-block grid leaves the
 // chip's last waves unbalanced: static tiles 72 %, one-shot waves 82 % of
 // 8 TB/s streaming the same 141 MB, profiles/r5_probe_grab.jsonl).
-// Checksum (init, parity; u16 or raw u32) and the headers-apart wrap (the
-// payloads' sums, each 40-byte header written to its array).
+// Every F of a span comes from the wave's single copy of each window, so
+// bytes of a neighbouring span's segments that share a boundary chunk (and
+// that span's in-place stores into them) cancel out of every difference.
+// Per-segment words the outputs need are fetched after the stream (the
+// checksum's two ride along it): fewer registers across the window loop.
 constexpr uint32_t kSpanSegs = 63;  // most segments per wave: 64 points, one per lane
 
-template <int OP, int OUT, bool STRIDE, int NSETS>
-__global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                 uint64_t n, uint32_t S, TileArgs a, uint32_t remap) {
-  static_assert(OP == kTileSum || OP == kTileWrapApart, "k_span: operations whose points are the offsets");
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v) {
+  return uint64_t(uint32_t(__shfl_down(uint32_t(v), 1))) | (uint64_t(uint32_t(__shfl_down(uint32_t(v >> 32), 1))) << 32);
+}
+
+template <int OP, int OUT, bool STRIDE>
+__global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
+                                                 uint64_t n, uint32_t S, TileArgs a, uint32_t remap,
+                                                 const u32x4* __restrict__ zero16) {
+  constexpr bool TWO = OP == kTileIpv4 || OP == kTileWrap;  // a second point per lane: lo_t
   constexpr uint32_t kWaves = kBlock / 64;
   __shared__ uint32_t s_pre[kWaves][kWinChunks][2];
   __shared__ u32x4 s_raw[kWaves][kWinChunks];
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint64_t nspans = (n + S - 1) / S;  // S (1..63) segments per span
+  const uint64_t nspans = (n + S - 1) / S;
   // one span per wave; STRIDE (batches of more spans than 2^24 blocks hold):
   // grid-stride beyond the grid.  Wave-uniform, no block barrier anywhere.
   auto span_body = [&](uint64_t span) {
   const uint64_t i0 = span * S;
   const uint32_t m = uint32_t(n - i0 < S ? n - i0 : S);
-  // the points (one load per lane) and, for the checksum, the per-segment
-  // words — in flight before the first window is requested, so the outputs
-  // never wait for a load issued after the stream
+  const bool valid = lane < m;
+  const uint64_t i = i0 + (valid ? lane : 0u);  // lanes >= m: a harmless copy of segment 0
+  // point A (one load per lane) and, for the checksum, the per-segment words —
+  // in flight before the first window is requested
   const uint64_t x = off[i0 + (lane <= m ? lane : m)];
-  const uint32_t t = lane < m ? lane : 0u;  // this lane's segment (lanes >= m: a harmless copy of segment 0)
-  constexpr uint32_t kWords = OP == kTileSum ? 2 : 7;
-  uint32_t w[kWords];
-  auto fetch_words = [&]() {
-    if constexpr (OP == kTileSum) {
-      w[0] = a.init[(i0 + t) * a.init_step];
-      w[1] = a.odd[(i0 + t) * a.odd_step];
-    } else {
-      const uint32_t* rec = reinterpret_cast<const uint32_t*>(a.msgs + i0 + t);
-#pragma unroll
-      for (uint32_t k = 0; k < 7; ++k) w[k] = rec[k];
-    }
-  };
-  // the checksum's two words ride along the stream; the wrap's 28-byte
-  // record is fetched after it (7 registers fewer across the window loop:
-  // 5 waves / SIMD instead of 4)
-  if constexpr (OP == kTileSum) fetch_words();
+  uint32_t w[OP == kTileSum ? 2 : 7];
+  if constexpr (OP == kTileSum) {
+    w[0] = a.init[i * a.init_step];
+    w[1] = a.odd[i * a.odd_step];
+  }
+  // segment t = [x, e): e is lane t + 1's point (taken by every lane)
+  const uint64_t e = shfl_down64(x);
+#ifdef ICSUM_BOUNDS_CHECK
+  if (valid && e < x) bounds_fail(kBoundsOffsets, i);
+#endif
+  // IPv4: the header's first dword (the IHL) requested before the stream
+  const bool hdr = OP == kTileIpv4 && valid && e - x >= 20;
+  uint32_t d0 = 0;
+  if constexpr (OP == kTileIpv4) {
+    const uint8_t* hp = hdr ? bytes + x : reinterpret_cast<const uint8_t*>(zero16);
+    d0 = *reinterpret_cast<const uint32_t*>(hp - (reinterpret_cast<uintptr_t>(hp) & 3u));
+  }
   // (the lane builtins return int: widen through uint32_t, or a low word of
   // 2^31 and up sign-extends into the high one)
   auto lane64 = [](uint64_t v, uint32_t l, bool first_lane) {
-    const uint32_t lo = uint32_t(first_lane ? __builtin_amdgcn_readfirstlane(uint32_t(v))
-                                            : __builtin_amdgcn_readlane(uint32_t(v), l));
-    const uint32_t hi = uint32_t(first_lane ? __builtin_amdgcn_readfirstlane(uint32_t(v >> 32))
-                                            : __builtin_amdgcn_readlane(uint32_t(v >> 32), l));
-    return uint64_t(lo) | (uint64_t(hi) << 32);
+    const uint32_t lo32 = uint32_t(first_lane ? __builtin_amdgcn_readfirstlane(uint32_t(v))
+                                              : __builtin_amdgcn_readlane(uint32_t(v), l));
+    const uint32_t hi32 = uint32_t(first_lane ? __builtin_amdgcn_readfirstlane(uint32_t(v >> 32))
+                                              : __builtin_amdgcn_readlane(uint32_t(v >> 32), l));
+    return uint64_t(lo32) | (uint64_t(hi32) << 32);
   };
   const uint64_t first = lane64(x, 0, true), tend = lane64(x, m, false);
   const uint64_t a0c = first >> 4;
   const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
   const uint64_t nw = (nch + kWinChunks - 1) / kWinChunks;
-  const uint64_t nwinS = nw ? (nw + NSETS - 1) / NSETS * NSETS : NSETS;  // whole rounds of the register sets
-  // this lane's point: chunk (span-relative) and byte; lanes past m hold none
-  const uint64_t pc = lane <= m ? (x >> 4) - a0c : ~uint64_t(0);
-  const uint32_t pb = uint32_t(x) & 15u;
+  const uint64_t nwin3 = nw ? (nw + 2) / 3 * 3 : 3;  // whole rounds of the three register sets
   const uint32_t voff = lane * 16u;
   auto load_win = [&](uint64_t k, u32x4 (&v)[4]) {
     const uint64_t c0 = k * kWinChunks;
@@ -2702,21 +1969,40 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
     for (int u = 0; u < 4; ++u)  // aux 2: non-temporal
       v[u] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff, u * 1024, 2));
   };
-  // NSETS register sets (2 or 3), each reloaded as soon as its window is in
-  // LDS: NSETS windows in flight while one is summed
-  static_assert(NSETS == 2 || NSETS == 3, "k_span: two or three register sets");
-  u32x4 b0[4], b1[4], b2[NSETS == 3 ? 4 : 1];
+  u32x4 b0[4], b1[4], b2[4];
   // in this order: the loop consumes b0 first, and vmcnt retires loads in issue order
   load_win(0, b0);
   __builtin_amdgcn_sched_barrier(0);
   load_win(1, b1);
   __builtin_amdgcn_sched_barrier(0);
-  if constexpr (NSETS == 3) {
-    load_win(2, reinterpret_cast<u32x4(&)[4]>(b2));
-    __builtin_amdgcn_sched_barrier(0);
+  load_win(2, b2);
+  __builtin_amdgcn_sched_barrier(0);
+  // point B, once the windows are out: IPv4 past the header (options skipped,
+  // ipv4_header.cpp:50), the in-place wrap past the 40 header bytes it rewrites
+  uint64_t lo = x;
+  if constexpr (OP == kTileIpv4) {
+    uint64_t o = 4u * ((d0 >> (8u * (uint32_t(x) & 3u))) & 0x0fu);
+    if (o < 20) o = 20;
+    if (hdr && o > e - x) o = e - x;
+    lo = hdr ? x + o : e;
+  } else if constexpr (OP == kTileWrap) {
+    lo = valid && e - x >= 40 ? x + 40 : e;
   }
+  // the lane's points: chunk (span-relative) and byte; lanes past m hold no A, lanes >= m no B
+  const uint64_t pc = lane <= m ? (x >> 4) - a0c : ~uint64_t(0);
+  const uint32_t pb = uint32_t(x) & 15u;
+  const uint64_t qc = TWO && valid ? (lo >> 4) - a0c : ~uint64_t(0);
+  const uint32_t qb = uint32_t(lo) & 15u;
   uint32_t ce = 0, co = 0;  // the span's sums so far
-  uint32_t fe = 0, fo = 0;  // F of this lane's point (set by the window holding it)
+  uint32_t fe = 0, fo = 0;  // F of point A (set by the window holding it)
+  uint32_t ge = 0, go = 0;  // F of point B
+  // F at a point inside window [c0, c1): its chunk's prefix + the chunk's bytes below it
+  auto point_F = [&](uint64_t c, uint32_t b, uint64_t c0, uint32_t& fe_, uint32_t& fo_) {
+    const uint32_t k2 = uint32_t(c - c0);
+    fe_ = s_pre[wv][k2][0];
+    fo_ = s_pre[wv][k2][1];
+    acc_chunk(s_raw[wv][win_slot(k2)] & byte_range_mask(0u, b), fe_, fo_);
+  };
   auto window = [&](uint64_t k, u32x4 (&v)[4]) {
     const uint64_t c0 = k * kWinChunks;
     const bool live = c0 < nch;  // uniform; else a padding window
@@ -2724,13 +2010,13 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
 #pragma unroll
       for (int u = 0; u < 4; ++u) s_raw[wv][win_slot(uint32_t(u) * 64u + lane)] = v[u];
     }
-    load_win(k + NSETS, v);  // the registers are free: window k + NSETS goes out now (one load site)
+    load_win(k + 3, v);  // the registers are free: window k + 3 goes out now (one load site)
     if (!live) return;
 #ifdef ICSUM_SPAN_PROBE_STREAM_ONLY
     // diagnostic build only (tools/probe/span_probe.hip): the loads, the LDS
     // writes and one read back per lane, no scan, prefix or points (results
     // wrong, time only)
-    if (live) {
+    {
       const u32x4 r = s_raw[wv][win_slot(4u * lane)];
       ce += r.x ^ r.y ^ r.z ^ r.w;
       __builtin_amdgcn_wave_barrier();
@@ -2763,61 +2049,108 @@ __global__ __launch_bounds__(kBlock) void k_span(const uint8_t* __restrict__ byt
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (pc >= c0 && pc < c1) {  // this lane's point is in this window
-      const uint32_t k2 = uint32_t(pc - c0);
-      fe = s_pre[wv][k2][0];
-      fo = s_pre[wv][k2][1];
-      acc_chunk(s_raw[wv][win_slot(k2)] & byte_range_mask(0u, pb), fe, fo);
+    if (pc >= c0 && pc < c1) point_F(pc, pb, c0, fe, fo);
+    if constexpr (TWO) {
+      if (qc >= c0 && qc < c1) point_F(qc, qb, c0, ge, go);
     }
     __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
   };
-  for (uint64_t k = 0; k < nwinS; k += NSETS) {  // wave-uniform
+  for (uint64_t k = 0; k < nwin3; k += 3) {  // wave-uniform
     window(k, b0);
     window(k + 1, b1);
-    if constexpr (NSETS == 3) window(k + 2, reinterpret_cast<u32x4(&)[4]>(b2));
+    window(k + 2, b2);
   }
-  if (lane <= m && pc >= nch) {  // the aligned end of the last chunk: every byte is below it
+  // a point at the aligned end of the last chunk: every byte is below it
+  if (lane <= m && pc >= nch) {
     fe = ce;
     fo = co;
   }
-  if constexpr (OP != kTileSum) fetch_words();
-  // segment t = [point t, point t + 1): lane t + 1's F (and point) one
-  // shuffle away — taken by every lane, outside the branch below (a shuffle
-  // from a lane the branch disables reads nothing defined)
+  if constexpr (TWO) {
+    if (valid && qc >= nch) {
+      ge = ce;
+      go = co;
+    }
+  } else {
+    ge = fe;
+    go = fo;
+  }
+  // segment t's sums up to its end: lane t + 1's F (every lane shuffles,
+  // outside the branches below: a shuffle from a lane a branch disables
+  // reads nothing defined)
   const uint32_t he = __shfl_down(fe, 1), ho = __shfl_down(fo, 1);
-  const uint64_t e = uint64_t(__shfl_down(uint32_t(x), 1)) | (uint64_t(__shfl_down(uint32_t(x >> 32), 1)) << 32);
-  if (lane < m) {
-    const uint64_t i = i0 + lane;
-    const uint32_t se = he - fe, so = ho - fo;  // sums of [s, e), roles by address
-    if constexpr (OP == kTileSum) {
+  const uint32_t se = he - ge, so = ho - go;  // sums of [lo, e), roles by address
+  if constexpr (OP == kTileSum) {
+    if (valid) {
       const uint32_t sum = w[0] + combine_roles(se, so, (uint32_t(x) ^ w[1]) & 1u);
       if (OUT == 0)
         static_cast<uint16_t*>(a.out)[i] = fold_value(sum);
       else
         static_cast<uint32_t*>(a.out)[i] = sum;
-    } else {
-      uint32_t ipc = 0, tcv = 0;
-      // the header into the wave's (now idle) window slots: 10 dwords per
-      // segment, the span's m headers contiguous
-      uint32_t* const stage = reinterpret_cast<uint32_t*>(&s_raw[wv][0]);
-      wrap_header(u32x4{w[0], w[1], w[2], w[3]}, w[4], w[5], w[6] & 0xffffu, e - x,
-                  combine_roles(se, so, uint32_t(x) & 1u), stage + lane * 10u, ipc, tcv);
-      if (a.ip_ck) a.ip_ck[i] = uint16_t(ipc);
-      if (a.tcp_ck) a.tcp_ck[i] = uint16_t(tcv);
     }
-  }
-  if constexpr (OP == kTileWrapApart) {
-    // the span's 10 m header dwords are one contiguous run of hdr_out:
-    // coalesced 256-byte stores instead of 40-byte strides per lane
+  } else if constexpr (OP == kTileIpv4) {
+    // the header and the TCP fields at the real start of the TCP part (after
+    // the stream: no window load waits behind them)
+    if (valid) {
+      const uint32_t* last = last_dword(bytes + e);
+      Hdr h{};
+      uint32_t tf0 = 0, tf1 = 0;
+      if (hdr) {
+        h = load_hdr(bytes + x, last);
+        if (e - lo >= 18) load_tcp_fields(bytes + lo, last, tf0, tf1);
+      }
+      ipv4_result(bytes, x, e, lo, hdr, h, tf0, tf1, combine_roles(se, so, uint32_t(lo) & 1u), a.mode, i, a.ip_ck,
+                  a.tcp_ck, a.status);
+    }
+  } else {
+    // the message record, then the header into the wave's (now idle) window
+    // slots: 10 dwords per segment, the span's m headers contiguous
+    const uint32_t* rec = reinterpret_cast<const uint32_t*>(a.msgs + i);
+#pragma unroll
+    for (uint32_t k = 0; k < 7; ++k) w[k] = rec[k];
+    uint32_t* const stage = reinterpret_cast<uint32_t*>(&s_raw[wv][0]);
+    const bool ok = valid && (OP == kTileWrapApart || e - x >= 40);
+    if (valid) {
+      uint32_t ipc = 0, tcv = 0;
+      wrap_header(u32x4{w[0], w[1], w[2], w[3]}, w[4], w[5], w[6] & 0xffffu, e - lo,
+                  combine_roles(se, so, uint32_t(lo) & 1u), stage + lane * 10u, ipc, tcv);
+      if (a.ip_ck) a.ip_ck[i] = ok ? uint16_t(ipc) : uint16_t(0);
+      if (a.tcp_ck) a.tcp_ck[i] = ok ? uint16_t(tcv) : uint16_t(0);
+    }
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const uint32_t* const stage = reinterpret_cast<const uint32_t*>(&s_raw[wv][0]);
-    uint32_t* const dst = a.hdr_out + i0 * 10;
+    if constexpr (OP == kTileWrapApart) {
+      // the span's 10 m header dwords are one contiguous run of hdr_out:
+      // coalesced 256-byte stores instead of 40-byte strides per lane
+      uint32_t* const dst = a.hdr_out + i0 * 10;
 #pragma unroll
-    for (uint32_t j = 0; j < 10; ++j) {
-      const uint32_t q = j * 64u + lane;
-      if (q < m * 10u) dst[q] = stage[q];
+      for (uint32_t j = 0; j < 10; ++j) {
+        const uint32_t q = j * 64u + lane;
+        if (q < m * 10u) dst[q] = stage[q];
+      }
+    } else {
+      // in place: dword q of the span = dword q % 10 of segment q / 10
+      // (neighbouring lanes, neighbouring bytes); its start and whether it
+      // holds a header come from lane q / 10 (every lane shuffles)
+      const uint32_t okw = ok ? 1u : 0u;
+#pragma unroll 2
+      for (uint32_t j = 0; j < 10; ++j) {
+        const uint32_t q = j * 64u + lane, d = q / 10u, k = q - d * 10u;
+        const uint32_t src = d < 64u ? d : 63u;
+        const uint64_t ds = uint64_t(uint32_t(__shfl(uint32_t(x), int(src)))) |
+                            (uint64_t(uint32_t(__shfl(uint32_t(x >> 32), int(src)))) << 32);
+        const uint32_t dok = uint32_t(__shfl(okw, int(src)));
+        if (d < m && dok) {
+          const uint32_t v = stage[q];
+          uint8_t* q8 = bytes + ds + 4u * k;
+          if ((reinterpret_cast<uintptr_t>(q8) & 3u) == 0) {
+            *reinterpret_cast<uint32_t*>(q8) = v;
+          } else {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) q8[b] = uint8_t(v >> (8 * b));
+          }
+        }
+      }
     }
   }
   __builtin_amdgcn_wave_barrier();  // the next span rewrites s_pre / s_raw
@@ -3156,59 +2489,20 @@ hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_ou
   return hipGetLastError();
 }
 
-// k_stream for the operations whose points are the offsets (checksum, the
-// headers-apart wrap): a grid of at most the resident blocks (every
-// gridDim-th tile per block, the prefetch running across tiles), or
-// max_blocks
-
+// k_span: one wave per S segments, four independent waves per block
 template <int OP, int OUT>
-hipError_t launch_stream_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint32_t max_blocks, hipStream_t st) {
-  const uint64_t tiles = (sp.n + T - 1) / T;
-  const uint64_t cap = max_blocks ? max_blocks : kStreamResident;
-  const uint32_t blocks = uint32_t(tiles < cap ? tiles : cap);
-  hipLaunchKernelGGL((k_stream<OP, OUT>), dim3(blocks), dim3(kStreamBlock), 0, st, sp.bytes, sp.offsets, sp.n, T, a,
-                     g_xcd_remap);
-  return hipGetLastError();
-}
-
-// k_span: one wave per g_span_segs segments, four independent waves per
-// block; segments per span and register sets per wave are process-wide
-// (ICSUM_FORCE span_segs / span_sets; dev A/B)
-uint32_t g_span_sets = 3;
-uint32_t g_span_segs = kSpanSegs;
-template <int OP, int OUT>
-hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, hipStream_t st) {
-  const uint32_t S = g_span_segs;
+hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, uint32_t S, hipStream_t st) {
+  if (!sp.offsets || sp.list || sp.n == 0 || S == 0 || S > kSpanSegs) return hipErrorInvalidValue;
   const uint64_t waves = (sp.n + S - 1) / S;
   const uint64_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
+  uint8_t* const bytes = const_cast<uint8_t*>(sp.bytes);
+  const u32x4* const z = static_cast<const u32x4*>(sp.zero16);
   if (blocks > kMaxGridBlocks)  // more spans than one grid: grid-stride
-    hipLaunchKernelGGL((k_span<OP, OUT, true, 3>), dim3(uint32_t(kMaxGridBlocks)), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.n, S, a, g_xcd_remap);
-  else if (g_span_sets == 2)
-    hipLaunchKernelGGL((k_span<OP, OUT, false, 2>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.n, S, a, g_xcd_remap);
+    hipLaunchKernelGGL((k_span<OP, OUT, true>), dim3(uint32_t(kMaxGridBlocks)), dim3(kBlock), 0, st, bytes,
+                       sp.offsets, sp.n, S, a, g_xcd_remap, z);
   else
-    hipLaunchKernelGGL((k_span<OP, OUT, false, 3>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, sp.bytes,
-                       sp.offsets, sp.n, S, a, g_xcd_remap);
-  return hipGetLastError();
-}
-
-template <int OP, int OUT>
-hipError_t launch_tile_t(const SegSpec& sp, const TileArgs& a, uint32_t T, uint32_t max_blocks, hipStream_t st,
-                         int form = 0) {
-  if (!sp.offsets || sp.list || sp.n == 0 || T == 0 || T > kTileMax) return hipErrorInvalidValue;
-  if constexpr (OP == kTileSum || OP == kTileWrapApart) {
-    if (form == kTileFormStream) return launch_stream_t<OP, OUT>(sp, a, T, max_blocks, st);
-    if (form == kTileFormSpan) return launch_span_t<OP, OUT>(sp, a, st);
-  }
-  const uint64_t tiles = (sp.n + T - 1) / T;
-  // one block per tile by default (measured faster than a persistent grid of
-  // the resident blocks, git 7692616:tools/ab_tile.py); a capped grid (max_blocks) takes
-  // every gridDim-th tile with the next one's loads overlapping its own
-  const uint64_t cap = max_blocks ? max_blocks : kMaxGridBlocks;
-  const uint32_t blocks = uint32_t(tiles < cap ? tiles : cap);
-  hipLaunchKernelGGL((k_tile<OP, OUT>), dim3(blocks), dim3(kBlock), 0, st, const_cast<uint8_t*>(sp.bytes),
-                     sp.offsets, sp.n, T, a, g_xcd_remap, static_cast<const u32x4*>(sp.zero16));
+    hipLaunchKernelGGL((k_span<OP, OUT, false>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, bytes, sp.offsets,
+                       sp.n, S, a, g_xcd_remap, z);
   return hipGetLastError();
 }
 
@@ -3366,8 +2660,6 @@ hipError_t launch_checksum_bins(const SegSpec& sp, const uint32_t* init, const u
 }
 
 void set_xcd_remap(uint32_t run_log2) { g_xcd_remap = run_log2 < 31 ? run_log2 : 31; }
-void set_span_sets(uint32_t sets) { g_span_sets = sets == 2 ? 2u : 3u; }
-void set_span_segs(uint32_t segs) { g_span_segs = segs >= 1 && segs <= kSpanSegs ? segs : kSpanSegs; }
 
 bool bounds_checked_build() {
 #ifdef ICSUM_BOUNDS_CHECK
@@ -3467,36 +2759,34 @@ hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t*
 }
 
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t T, uint32_t max_blocks, hipStream_t st, int form) {
+                                uint32_t S, hipStream_t st) {
   TileArgs a{};
   a.init = init ? init : static_cast<const uint32_t*>(sp.zero16);
   a.odd = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
   a.init_step = init ? 1u : 0u;
   a.odd_step = odd ? 1u : 0u;
   a.out = out;
-  return out_kind == 0 ? launch_tile_t<kTileSum, 0>(sp, a, T, max_blocks, st, form)
-                       : launch_tile_t<kTileSum, 1>(sp, a, T, max_blocks, st, form);
+  return out_kind == 0 ? launch_span_t<kTileSum, 0>(sp, a, S, st) : launch_span_t<kTileSum, 1>(sp, a, S, st);
 }
 
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                            uint32_t T, uint32_t max_blocks, hipStream_t st) {
+                            uint32_t S, hipStream_t st) {
   TileArgs a{};
   a.mode = mode;
   a.ip_ck = ip_ck;
   a.tcp_ck = tcp_ck;
   a.status = status;
-  return launch_tile_t<kTileIpv4, 0>(sp, a, T, max_blocks, st);
+  return launch_span_t<kTileIpv4, 0>(sp, a, S, st);
 }
 
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st, int form) {
+                            uint16_t* tcp_ck, uint32_t S, hipStream_t st) {
   TileArgs a{};
   a.msgs = msgs;
   a.hdr_out = hdr_out;
   a.ip_ck = ip_ck;
   a.tcp_ck = tcp_ck;
-  return hdr_out ? launch_tile_t<kTileWrapApart, 0>(sp, a, T, max_blocks, st, form)
-                 : launch_tile_t<kTileWrap, 0>(sp, a, T, max_blocks, st);
+  return hdr_out ? launch_span_t<kTileWrapApart, 0>(sp, a, S, st) : launch_span_t<kTileWrap, 0>(sp, a, S, st);
 }
 
 uint64_t batchv_blocks(int cls, uint64_t n) {

@@ -163,10 +163,6 @@ hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const 
 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
 void set_xcd_remap(uint32_t run_log2);
-// register sets per k_span wave: 2 or 3 (process-wide; ICSUM_FORCE span_sets)
-void set_span_sets(uint32_t sets);
-// segments per k_span wave, 1..63 (process-wide; ICSUM_FORCE span_segs)
-void set_span_segs(uint32_t segs);
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
@@ -183,21 +179,14 @@ hipError_t launch_router_ttl(const SegSpec& sp, uint8_t* status, hipStream_t st)
 // the datagrams read only (k_router_hdrs)
 hipError_t launch_router_hdrs(const SegSpec& sp, uint32_t* hdr_out, uint8_t* status, hipStream_t st);
 
-// Tile launches of offsets batches (k_tile): T (1..256) consecutive segments
-// per block, the tile's bytes streamed whole in 16 KiB windows whatever the
-// lengths; max_blocks 0: one block per tile (capped, grid-stride beyond).
-// Checksum (out_kind as launch_checksum), the fused IPv4/TCP kernel (mode as
-// launch_ipv4_tcp) and the in-place wrap (as launch_tcp_wrap in place).
-// form (the checksum and the headers-apart wrap only): kTileFormTile k_tile;
-// kTileFormStream k_stream (four stream waves + a metadata wave per block;
-// max_blocks 0: the 1024 resident blocks, each taking every gridDim-th
-// tile); kTileFormSpan k_span (one wave per 63 segments, no block state; T
-// and max_blocks unused)
-enum TileForm : int { kTileFormTile = 0, kTileFormStream = 1, kTileFormSpan = 2 };
+// Tile launches of offsets batches (k_span): one wave per S (1..63)
+// consecutive segments, the span's bytes streamed whole in 4 KiB windows
+// whatever the lengths.  Checksum (out_kind as launch_checksum), the fused IPv4/TCP kernel
+// (mode as launch_ipv4_tcp) and the in-place wrap (as launch_tcp_wrap in place).
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t T, uint32_t max_blocks, hipStream_t st, int form);
+                                uint32_t S, hipStream_t st);
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                            uint32_t T, uint32_t max_blocks, hipStream_t st);
+                            uint32_t S, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg
 // (include/icsum.h), 28 bytes.
@@ -220,7 +209,7 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
 // the wrap as a tile launch: in place (hdr_out null) or, with hdr_out, the
 // payload-only batch of ics_tcp_wrap_headers with its headers to hdr_out
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t T, uint32_t max_blocks, hipStream_t st, int form);
+                            uint16_t* tcp_ck, uint32_t S, hipStream_t st);
 // pass 2 of the two-pass wrap alone (k_tcp_hdr): headers from the records and
 // the payload sums pass 1 left in `sums` (roles from each payload's start)
 hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t* sums, uint32_t* hdr_out,

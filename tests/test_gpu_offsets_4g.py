@@ -10,7 +10,7 @@ the unfolded sums under the tiny, small, dense, two-class and line-grid
 kernels and under every binned plan; the fused IPv4/TCP kernel in COMPUTE,
 VERIFY and PATCH (one lane, 4/8/16/64-lane groups, the two-class launch, the
 plan-cache path); the device wrap in place and with the headers apart, one
-and two passes; the tile launch (round 4) for the checksum, the fused kernel
+and two passes; the tile launch (k_span) for the checksum, the fused kernel
 and both wraps; the router step — into sentinel-filled outputs, and compared
 with the oracle (oracle/icsum_oracle.c) on the bytes around each boundary and
 at both ends of the batch.  The bug class this pins: a 64-bit offset or start
@@ -150,7 +150,7 @@ OFF_FORCE = [None,
              {"lps": 8, "unroll": 2, "mode": 2, "segs": 2},
              {"lps": 16, "unroll": 8, "mode": 3}, {"lps": 64, "unroll": 8, "mode": 3},
              {"twoclass": 8}, {"twoclass": 16}, {"twoclass": 32},
-             {"tile": 1}, {"tile": 1, "tile_segs": 7}]
+             {"tile": 1}]
 
 
 @pytest.fixture(scope="module", params=OFF_FORCE, ids=lambda f: force_id(f or {}))
@@ -216,7 +216,7 @@ def _place(t, buf, rel, bnd, how):
 IPV4_FORCE = [None, {"twoclass": 32}, {"lps": 1, "unroll": 4, "mode": 4}, {"lps": 4, "unroll": 1, "mode": 2},
               {"lps": 8, "unroll": 2, "mode": 2}, {"lps": 8, "unroll": 8, "mode": 3},
               {"lps": 16, "unroll": 7, "mode": 3}, {"lps": 16, "unroll": 8, "mode": 3},
-              {"lps": 64, "unroll": 8, "mode": 3}, {"tile": 1}, {"tile": 1, "tile_segs": 7}]
+              {"lps": 64, "unroll": 8, "mode": 3}, {"tile": 1}]
 IPV4_MIX = {"ack": [40, 41, 42, 43], "bimodal": [40, 41, 1460, 1500],
             "tricky": [0, 7, 19, 20, 39, 40, 41, 63, 64, 65, 100, 1460, 1500, 9000]}
 
@@ -333,8 +333,7 @@ def _msgs(rng, n):
     return m
 
 
-@pytest.fixture(scope="module", params=[None, {"wrap_passes": 1}, {"wrap_passes": 2}, {"tile": 1},
-                                        {"tile": 1, "tile_segs": 7}],
+@pytest.fixture(scope="module", params=[None, {"wrap_passes": 1}, {"wrap_passes": 2}, {"tile": 1}],
                 ids=lambda f: force_id(f or {}))
 def weng4(request):
     yield from engine_with(request.param)

@@ -1,14 +1,14 @@
-"""GPU parity of the tile launches of offsets batches (k_tile: T consecutive
-segments per block, the tile's bytes streamed whole — each wave a contiguous
-quarter in 4 KiB windows — and each segment's sum = F(hi) - F(lo) of the
-running prefix), forced on every
-offsets batch with the `tile` test hook at several tile sizes — one segment
-per tile, odd sizes that leave a short last tile, the automatic size and the
-full 256 — and with a capped grid (tiles in a grid-stride loop): checksum
-(u16, raw u32 sums with carried parity), the fused IPv4/TCP kernel in all
-three modes (PATCH's in-place stores racing nothing: tiles mask the bytes
-below their first segment), the in-place wrap and the headers-apart wrap, against the golden KATs,
-the reference's own wrap output (tests/golden/tcp_wrap.json) and the oracle.
+"""GPU parity of the tile launch of offsets batches (k_span: one wave per 63
+consecutive segments, the span's bytes streamed whole in 4 KiB windows, each
+segment's sums = F(hi) - F(lo) of the running prefix), forced on every
+offsets batch with the `tile` test hook — short last spans, one-segment
+batches, spans of empty segments, offsets past 2^31 and 2^32 (config 4 at
+full size) and more spans than one grid holds (grid-stride): checksum (u16,
+raw u32 sums with carried parity), the fused IPv4/TCP kernel in all three
+modes (PATCH's in-place stores racing a neighbouring span's boundary chunk:
+every F of a span comes from one copy of each window, so those bytes cancel),
+the in-place wrap and the headers-apart wrap, against the golden KATs, the
+reference's own wrap output (tests/golden/tcp_wrap.json) and the oracle.
 Bar: bit-exact."""
 import numpy as np
 import pytest
@@ -20,19 +20,9 @@ from test_gpu_twoclass import _check, _sentinel
 
 pytestmark = pytest.mark.gpu
 
-# automatic tile size on the persistent grid; one segment per tile; odd sizes;
-# few blocks, each streaming many tiles back to back (the next tile's first
-# windows in flight across every tile boundary; on k_stream the metadata wave
-# finishing tile j while the stream waves run tile j + 1, both point buffers
-# in turn) — the checksum and headers-apart wrap in each form: k_span (the
-# default: one wave per 63 segments), k_stream (tile_form=1) and k_tile
-# (tile_form=0); the fused IPv4 kernel and the in-place wrap always on k_tile
-TILE_FORCE = [{"tile": 1}, {"tile": 1, "tile_segs": 1}, {"tile": 1, "tile_segs": 7},
-              {"tile": 1, "tile_form": 1}, {"tile": 1, "tile_form": 1, "tile_segs": 7, "tile_blocks": 5},
-              {"tile": 1, "tile_form": 1, "tile_segs": 256, "tile_blocks": 3},
-              {"tile": 1, "tile_form": 1, "tile_segs": 64, "tile_blocks": 1}, {"tile": 1, "tile_form": 0},
-              {"tile": 1, "tile_form": 0, "tile_segs": 7, "tile_blocks": 5}]
-ICS_TILE_FORM_BITS = {0: 0, 1: 4, 2: 8}  # ICS_TILE_STREAM, ICS_TILE_SPAN
+# the tile launch (k_span) on every offsets batch: 63 segments per wave (or
+# the plan's span size), one, and an odd size that leaves short last spans
+TILE_FORCE = [{"tile": 1}, {"tile": 1, "span_segs": 1}, {"tile": 1, "span_segs": 7}]
 
 
 @pytest.fixture(scope="module", params=TILE_FORCE, ids=force_id)
@@ -40,15 +30,12 @@ def tile_eng(request):
     yield from engine_with(request.param)
 
 
-def _assert_tile(eng, streamable=True):
-    """the tile launch ran, in the form the engine's hooks ask for: the
-    checksum and headers-apart wrap (`streamable`) on k_span unless
-    tile_form says otherwise, the fused IPv4 kernel and the in-place wrap on
-    k_tile"""
+def _assert_tile(eng):
+    """the tile launch (k_span) ran, at the forced span size if any"""
     info = eng.dispatch_info()
     assert info["kernel"] == "tile", info
-    form = getattr(eng, "forced", {}).get("tile_form", 2) if streamable else 0
-    assert info["unroll"] & 12 == ICS_TILE_FORM_BITS[form], info
+    S = getattr(eng, "forced", {}).get("span_segs", 0)
+    assert info["lps"] == S if S else 1 <= info["lps"] <= 63, info
 
 
 def test_tile_kats(tile_eng):
@@ -169,7 +156,7 @@ def test_tile_ipv4_vs_oracle(tile_eng, orc, mix):
         want = orc.ipv4_tcp_batch(hb, n, mode, offsets=off)
         d = _t(buf)
         ip, tcp, st = tile_eng.ipv4_tcp_batch(d, mode, offsets=_t(off))
-        _assert_tile(tile_eng, streamable=False)
+        _assert_tile(tile_eng)
         assert (_u16(ip) == want[0]).all(), (mix, mode)
         assert (_u16(tcp) == want[1]).all(), (mix, mode)
         assert (st.cpu().numpy() == want[2]).all(), (mix, mode)
@@ -194,7 +181,7 @@ def test_tile_wrap_reproduces_reference_wire_bytes(tile_eng, lead):
     ip = torch.empty(len(cases), dtype=torch.int16, device="cuda")
     tcp = torch.empty(len(cases), dtype=torch.int16, device="cuda")
     tile_eng.tcp_wrap_batch(d, dm, n=len(cases), offsets=_t(off), ip_ck=ip, tcp_ck=tcp)
-    _assert_tile(tile_eng, streamable=False)
+    _assert_tile(tile_eng)
     got = d.cpu().numpy()
     for i, c in enumerate(cases):
         assert got[off[i]:off[i + 1]].tobytes().hex() == c["wire"], i
@@ -250,9 +237,7 @@ def test_tile_config4_full_size():
         assert hashlib.sha256(out.tobytes()).hexdigest() == g["out_sha256"]
 
 
-@pytest.fixture(scope="module", params=[{"tile": 1}, {"tile": 1, "tile_form": 1, "tile_segs": 7, "tile_blocks": 5},
-                                        {"tile": 1, "tile_form": 1, "tile_segs": 64, "tile_blocks": 1},
-                                        {"tile": 1, "tile_form": 0}], ids=force_id)
+@pytest.fixture(scope="module", params=TILE_FORCE, ids=force_id)
 def tile_apart(request):
     yield from engine_with(request.param)
 

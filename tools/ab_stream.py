@@ -1,15 +1,16 @@
 #!/usr/bin/env python3
-"""Dev measurement (round 5): the tile launch on k_stream (stream waves + a
-metadata wave per block, persistent grid) against k_tile, on the VERDICT r4
-shapes — the transmit mix (payloads of 0..1000 bytes: 40..1040-byte
-datagrams, or the payloads alone for the headers-apart wrap) at 256 Ki and
-1 M segments, and constant 770-byte segments given as offsets — for the
-checksum and ics_tcp_wrap_headers.  Each row: back to back (events around 20
-calls, median of 5 rounds, two batches rotated) and alone (events around one
-call after a synchronize, median of 40).  Variants through ICSUM_FORCE:
-k_tile at the automatic T, k_stream at the automatic T and at fixed T / grid
-caps.  Usage: python tools/ab_stream.py [rows] [variants] [ops]; AB_LIGHT=1: a
-few calls per row (counter passes)."""
+"""Dev measurement (round 5): the tile launch (k_span, one wave per 63
+segments) against the per-segment launches (and, in git c581ecc, against
+round 4's k_tile: profiles/r5k_ab_span_ops.jsonl), on the VERDICT r4 shapes — the transmit mix
+(payloads of 0..1000 bytes: 40..1040-byte datagrams, or the payloads alone
+for the headers-apart wrap) at 256 Ki and 1 M segments, and constant
+770-byte segments given as offsets — for the checksum, ics_tcp_wrap_headers
+(wrap_apart), the in-place wrap and the fused IPv4 kernel's VERIFY / PATCH
+(random bytes: header lengths of 20..60).  Each row: back to back (events
+around 20 calls, median of 5 rounds, two batches rotated) and alone (events
+around one call after a synchronize, median of 40).  Variants through
+ICSUM_FORCE.  Usage: python tools/ab_stream.py [rows] [variants] [ops];
+AB_LIGHT=1: a few calls per row (counter passes)."""
 import json
 import os
 import statistics
@@ -18,6 +19,7 @@ import time
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from _force import engine  # noqa: E402
+from tcpip_network_protocol_stack_amd.engine import mixed_offsets  # noqa: E402
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
@@ -75,14 +77,10 @@ def batch(eng, lens, seed):
 
 
 VARIANTS = {
-    "tile": {"tile": 1, "tile_form": 0},
-    "stream": {"tile": 1, "tile_form": 1},
-    "stream_T256": {"tile": 1, "tile_form": 1, "tile_segs": 256},
-    "span": {"tile": 1, "tile_form": 2},
-    "span2": {"tile": 1, "tile_form": 2, "span_sets": 2},
-    "span_S15": {"tile": 1, "tile_form": 2, "span_segs": 15, "span_sets": 3},
-    "span_S31": {"tile": 1, "tile_form": 2, "span_segs": 31, "span_sets": 3},
-    "span_S63": {"tile": 1, "tile_form": 2, "span_segs": 63, "span_sets": 3},
+    "auto": {},                  # the default dispatch
+    "span": {"tile": 1},         # the tile launch, k_span (span size: the plan's, or 63)
+    "per_segment": {"tile": 0},  # the per-segment / two-class launches
+    **{f"S{k}": {"tile": 1, "span_segs": k} for k in range(1, 64)},
 }
 
 
@@ -94,22 +92,30 @@ def main():
     auto = engine()
     rng = np.random.default_rng(3)
     shapes = {"tx256k": (1 << 18, "tx"), "tx1m": (1 << 20, "tx"), "u770_256k": (1 << 18, "u770"),
-              "u770_1m": (1 << 20, "u770")}
+              "u770_1m": (1 << 20, "u770"), "c4_128k": (1 << 17, "c4")}
     for row in rows:
         n, kind = shapes[row]
-        pays = rng.integers(0, 1001, n) if kind == "tx" else np.full(n, 730)
+        if kind == "c4":  # BASELINE config 4's length mix (64 B - 64 KiB), 128 Ki segments
+            pays = np.diff(mixed_offsets(n, 4).astype(np.int64)) - 40
+        else:
+            pays = rng.integers(0, 1001, n) if kind == "tx" else np.full(n, 730)
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         hd = torch.empty(n * 40, dtype=torch.uint8, device="cuda")
         msgs = torch.from_numpy(rng.integers(0, 256, n * 28, dtype=np.uint8)).cuda()
         for op in ops:
-            lens = pays + 40 if op == "checksum" else pays
+            lens = pays if op == "wrap_apart" else pays + 40
             bs = [batch(auto, lens, 11 + r) for r in range(R)]
             nb = bs[0][2]
             for name, e in engs.items():
                 if op == "checksum":
                     fn = lambda i, e=e: e.checksum_batch(bs[i % R][0], n=n, offsets=bs[i % R][1], out=out)
-                else:
+                elif op == "wrap_apart":
                     fn = lambda i, e=e: e.tcp_wrap_headers(bs[i % R][0], msgs, hd, n=n, offsets=bs[i % R][1])
+                elif op == "wrap":
+                    fn = lambda i, e=e: e.tcp_wrap_batch(bs[i % R][0], msgs, n=n, offsets=bs[i % R][1])
+                else:
+                    mode = {"verify": 1, "patch": 2}[op]
+                    fn = lambda i, e=e, mode=mode: e.ipv4_tcp_batch(bs[i % R][0], mode, n=n, offsets=bs[i % R][1])
                 tb = b2b(fn)
                 ta = alone(fn)
                 info = e.dispatch_info()
