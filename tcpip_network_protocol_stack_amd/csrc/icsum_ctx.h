@@ -89,7 +89,7 @@ struct ics_ctx {
   int tile = -1;
   uint32_t span_segs = 0;
   static constexpr uint64_t kSpanBytes = 20 << 10;  // segment bytes per span (span_segs_for)
-  static constexpr uint64_t kTileMin = uint64_t(1) << 17;  // tile launches from this many segments (AUTO)
+  static constexpr uint64_t kTileMin = uint64_t(1) << 16;  // tile launches from this many segments (AUTO)
   static constexpr uint32_t kTileMaxAvg = 1024;            // ... and up to this mean length (tile_wins)
   static constexpr uint32_t kTileApartShort16 = 12;       // headers-apart wrap: below 12/16 empty-ish payloads
   uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order

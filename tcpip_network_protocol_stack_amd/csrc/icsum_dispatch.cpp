@@ -170,18 +170,22 @@ int replan(ics_ctx* ctx, const icsum::SegSpec& sp, uint32_t lps, const PlanReq& 
 // profiles/r2_csum_mix_sweep.jsonl), now the two-class launch (launch_mix)
 bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m.long16 == 0; }
 
-// The tile launch (k_tile) for an offsets batch whose device-reported mix
+// The tile launch (k_span) for an offsets batch whose device-reported mix
 // favours it: from kTileMin segments, a mean length of at most kTileMaxAvg
 // bytes (variable lengths leave per-segment lane groups idle), or — for the
-// fused IPv4 kernel and the wraps, which have no length binning — a sixteenth
-// or more of the bytes in segments over 1920 bytes.  Short-heavy mixes keep
-// the two-class launches (checked first by the callers), MTU-sized means the
-// 16-lane line grid.  git 7692616:tools/ab_dispatch.py, profiles/r4_ab_dispatch.jsonl
-// (256 Ki / 1 M segments, us, default vs tile): checksum 40..1040 B 37.1 /
-// 29.2 and 279.3 / 92.2, 770 B 40.0 / 35.7 and 153.4 / 122.6, MTU 56.7 /
-// 63.9; VERIFY 40..1040 B 40.0 / 34.5 and 150.0 / 116.9, config-4 mix 412.4 /
-// 387.1; headers-apart wrap 40..1040 B 39.6 / 32.0 and 138.7 / 109.0, MTU
-// 67.1 / 70.1; at 64 Ki the default wins or ties.
+// wraps, which have no length binning — a sixteenth or more of the bytes in
+// segments over 1920 bytes; the fused IPv4 kernel on every mix but the
+// short-heavy ones (ipv4_device).  Short-heavy mixes keep the two-class
+// launches (checked first by the callers), MTU-sized means the 16-lane line
+// grid.  tools/ab_stream.py, profiles/r5l_ab_span_vs_per_segment.jsonl,
+// r5m_ab_c4.jsonl, r5p_ab_span_thresholds.jsonl (us back to back,
+// per-segment vs span): checksum 40..1040 B 256 Ki / 1 M 35.7 / 27.0 and
+// 286.7 / 89.3, 770 B 1 M 153.0 / 122.8, MTU 1 M 212.2 / 236.8, 64 Ki 11.1 /
+// 11.3; VERIFY 40..1040 B 64 Ki / 1 M 16.1 / 11.9 and 204.9 / 123.5, MTU
+// 256 Ki / 1 M 70.4 / 61.3 and 264.6 / 237.6, 128 Ki of config 4's mix
+// 233.5 / 192.3; headers-apart wrap 40..1040 B 64 Ki / 1 M 11.7 / 9.8 and
+// 137.4 / 103.4, MTU 1 M 244.8 / 265.2; in-place wrap 40..1040 B 1 M 156.9 /
+// 156.3, 770 B 1 M 193.2 / 207.2, config 4's mix 265.6 / 230.6.
 bool tile_wins(const ics_ctx* ctx, const PlanMix& m, uint64_t n, bool fused) {
   if (ctx->tile == 0 || n < ics_ctx::kTileMin) return false;
   return m.avg <= ics_ctx::kTileMaxAvg || (fused && m.long16 >= 4);
@@ -379,7 +383,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
     // pass carries more of them (3/4 ACKs 78.4 -> 75.4 us, mix_probe blk32)
     spw = mix.short16 >= ics_ctx::kIpv4TwoClassWide16 ? 32 : 16;
     plan_used = hit ? int(plan) : -1;
-    tile = hit && !two && plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, n, true);
+    tile = hit && !two && plan != icsum::kPlanWholeBatchSmall && ctx->tile != 0 && n >= ics_ctx::kTileMin;
     span_avg = hit ? mix.avg : 0u;
   }
   if (d_offsets && ctx->twoclass) {  // test hook

@@ -92,13 +92,14 @@ def main():
     auto = engine()
     rng = np.random.default_rng(3)
     shapes = {"tx256k": (1 << 18, "tx"), "tx1m": (1 << 20, "tx"), "u770_256k": (1 << 18, "u770"),
-              "u770_1m": (1 << 20, "u770"), "c4_128k": (1 << 17, "c4")}
+              "u770_1m": (1 << 20, "u770"), "c4_128k": (1 << 17, "c4"), "tx64k": (1 << 16, "tx"),
+              "mtu256k": (1 << 18, "mtu"), "mtu1m": (1 << 20, "mtu")}
     for row in rows:
         n, kind = shapes[row]
         if kind == "c4":  # BASELINE config 4's length mix (64 B - 64 KiB), 128 Ki segments
             pays = np.diff(mixed_offsets(n, 4).astype(np.int64)) - 40
         else:
-            pays = rng.integers(0, 1001, n) if kind == "tx" else np.full(n, 730)
+            pays = rng.integers(0, 1001, n) if kind == "tx" else np.full(n, 1460 if kind == "mtu" else 730)
         out = torch.empty(n, dtype=torch.int16, device="cuda")
         hd = torch.empty(n * 40, dtype=torch.uint8, device="cuda")
         msgs = torch.from_numpy(rng.integers(0, 256, n * 28, dtype=np.uint8)).cuda()
@@ -125,16 +126,17 @@ def main():
                                   "T": info["lps"], "op": info["unroll"]}), flush=True)
             del bs
             torch.cuda.empty_cache()
-        # the fixed-stride kernel over the same number of bytes (770-byte
+        # the fixed-stride kernel over the same number of bytes (constant-length
         # rows: the streaming reference a tile launch is measured against)
-        if kind == "u770":
-            ds = [auto.fill_bytes(torch.empty(n * 770, dtype=torch.uint8, device="cuda"), 5, pos0=r * n * 770)
+        if kind in ("u770", "mtu"):
+            L = int(pays[0]) + 40
+            ds = [auto.fill_bytes(torch.empty(n * L, dtype=torch.uint8, device="cuda"), 5, pos0=r * n * L)
                   for r in range(R)]
-            fn = lambda i: auto.checksum_batch(ds[i % R], n=n, stride=770, seg_len=770, out=out)
+            fn = lambda i: auto.checksum_batch(ds[i % R], n=n, stride=L, seg_len=L, out=out)
             tb, ta = b2b(fn), alone(fn)
-            print(json.dumps({"row": f"{row}_fixed_stride", "variant": "k_checksum", "bytes": n * 770,
-                              "us_b2b": round(tb * 1e6, 2), "frac_b2b": round(n * 770 / tb / PEAK, 4),
-                              "us_alone": round(ta * 1e6, 2), "frac_alone": round(n * 770 / ta / PEAK, 4),
+            print(json.dumps({"row": f"{row}_fixed_stride", "variant": "k_checksum", "bytes": n * L,
+                              "us_b2b": round(tb * 1e6, 2), "frac_b2b": round(n * L / tb / PEAK, 4),
+                              "us_alone": round(ta * 1e6, 2), "frac_alone": round(n * L / ta / PEAK, 4),
                               "kernel": auto.dispatch_info()["kernel"], "T": 0, "op": 0}), flush=True)
             del ds
 
