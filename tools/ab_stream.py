@@ -93,10 +93,13 @@ def main():
     rng = np.random.default_rng(3)
     shapes = {"tx256k": (1 << 18, "tx"), "tx1m": (1 << 20, "tx"), "u770_256k": (1 << 18, "u770"),
               "u770_1m": (1 << 20, "u770"), "c4_128k": (1 << 17, "c4"), "tx64k": (1 << 16, "tx"),
-              "mtu256k": (1 << 18, "mtu"), "mtu1m": (1 << 20, "mtu")}
+              "mtu256k": (1 << 18, "mtu"), "mtu1m": (1 << 20, "mtu"), "rx256k": (1 << 18, "rx50"),
+              "rx1m25": (1 << 20, "rx25"), "rx1m50": (1 << 20, "rx50"), "rx1m75": (1 << 20, "rx75")}
     for row in rows:
         n, kind = shapes[row]
-        if kind == "c4":  # BASELINE config 4's length mix (64 B - 64 KiB), 128 Ki segments
+        if kind.startswith("rx"):  # received traffic: ACKs (40 B) among MTU datagrams, the share in the name
+            pays = np.where(rng.random(n) < int(kind[2:]) / 100, 0, 1460)
+        elif kind == "c4":  # BASELINE config 4's length mix (64 B - 64 KiB), 128 Ki segments
             pays = np.diff(mixed_offsets(n, 4).astype(np.int64)) - 40
         else:
             pays = rng.integers(0, 1001, n) if kind == "tx" else np.full(n, 1460 if kind == "mtu" else 730)
@@ -106,6 +109,8 @@ def main():
         for op in ops:
             lens = pays if op == "wrap_apart" else pays + 40
             bs = [batch(auto, lens, 11 + r) for r in range(R)]
+            for d, o, _ in bs:  # IPv4, IHL 5 at every datagram start (the rest random)
+                d[o[:-1][torch.from_numpy(lens).cuda() >= 20]] = 0x45
             nb = bs[0][2]
             for name, e in engs.items():
                 if op == "checksum":
