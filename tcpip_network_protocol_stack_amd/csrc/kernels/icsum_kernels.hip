@@ -1924,28 +1924,21 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
     w[0] = a.init[i * a.init_step];
     w[1] = a.odd[i * a.odd_step];
   }
-  // segment t = [x, e): e is lane t + 1's point (taken by every lane)
-  const uint64_t e = shfl_down64(x);
-#ifdef ICSUM_BOUNDS_CHECK
-  if (valid && e < x) bounds_fail(kBoundsOffsets, i);
-#endif
-  // IPv4: the header's first dword (the IHL) requested before the stream
-  const bool hdr = OP == kTileIpv4 && valid && e - x >= 20;
+  // the span's byte range: two scalar loads at wave-uniform indices (the
+  // stream's addresses wait for the scalar cache, not for the vector load)
+  const uint64_t first = off[i0], tend = off[i0 + m];
+  // segment t = [x, e): e is lane t + 1's point (taken by every lane).  IPv4
+  // takes it before the stream, for the header's first dword (the IHL); the
+  // other operations after the stream is requested
+  uint64_t e = 0;
+  bool hdr = false;
   uint32_t d0 = 0;
   if constexpr (OP == kTileIpv4) {
+    e = shfl_down64(x);
+    hdr = valid && e - x >= 20;
     const uint8_t* hp = hdr ? bytes + x : reinterpret_cast<const uint8_t*>(zero16);
     d0 = *reinterpret_cast<const uint32_t*>(hp - (reinterpret_cast<uintptr_t>(hp) & 3u));
   }
-  // (the lane builtins return int: widen through uint32_t, or a low word of
-  // 2^31 and up sign-extends into the high one)
-  auto lane64 = [](uint64_t v, uint32_t l, bool first_lane) {
-    const uint32_t lo32 = uint32_t(first_lane ? __builtin_amdgcn_readfirstlane(uint32_t(v))
-                                              : __builtin_amdgcn_readlane(uint32_t(v), l));
-    const uint32_t hi32 = uint32_t(first_lane ? __builtin_amdgcn_readfirstlane(uint32_t(v >> 32))
-                                              : __builtin_amdgcn_readlane(uint32_t(v >> 32), l));
-    return uint64_t(lo32) | (uint64_t(hi32) << 32);
-  };
-  const uint64_t first = lane64(x, 0, true), tend = lane64(x, m, false);
   const uint64_t a0c = first >> 4;
   const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
   const uint64_t nw = (nch + kWinChunks - 1) / kWinChunks;
@@ -1977,6 +1970,10 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
   __builtin_amdgcn_sched_barrier(0);
   load_win(2, b2);
   __builtin_amdgcn_sched_barrier(0);
+  if constexpr (OP != kTileIpv4) e = shfl_down64(x);
+#ifdef ICSUM_BOUNDS_CHECK
+  if (valid && e < x) bounds_fail(kBoundsOffsets, i);
+#endif
   // point B, once the windows are out: IPv4 past the header (options skipped,
   // ipv4_header.cpp:50), the in-place wrap past the 40 header bytes it rewrites
   uint64_t lo = x;
@@ -2055,11 +2052,15 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
     }
     __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
   };
-  for (uint64_t k = 0; k < nwin3; k += 3) {  // wave-uniform
+  // wave-uniform; nwin3 >= 3, so a do-while: no zero-trip test for the
+  // compiler to sink the first three windows' loads behind
+  uint64_t k = 0;
+  do {
     window(k, b0);
     window(k + 1, b1);
     window(k + 2, b2);
-  }
+    k += 3;
+  } while (k < nwin3);
   // a point at the aligned end of the last chunk: every byte is below it
   if (lane <= m && pc >= nch) {
     fe = ce;
