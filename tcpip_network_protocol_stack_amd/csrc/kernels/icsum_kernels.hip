@@ -1939,7 +1939,10 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
     const uint8_t* hp = hdr ? bytes + x : reinterpret_cast<const uint8_t*>(zero16);
     d0 = *reinterpret_cast<const uint32_t*>(hp - (reinterpret_cast<uintptr_t>(hp) & 3u));
   }
-  const uint64_t a0c = first >> 4;
+  // the windows start on the 128-byte line (of `bytes`) holding the first
+  // byte, so each 1 KiB load instruction covers 8 whole lines, not 9 partial
+  // ones; the chunks below `first` enter every F of the span alike and cancel
+  const uint64_t a0c = (first >> 7) << 3;
   const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
   const uint64_t nw = (nch + kWinChunks - 1) / kWinChunks;
   const uint64_t nwin3 = nw ? (nw + 2) / 3 * 3 : 3;  // whole rounds of the three register sets

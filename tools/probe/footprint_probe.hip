@@ -97,7 +97,10 @@ __device__ __forceinline__ uint32_t line_primed(const uint8_t* base, uint64_t s,
 // 7 quarters: the wave's flat range (four segments' bytes) cut in four
 // quarters at 16-byte chunks, group g streaming quarter g at 256 B per
 // instruction (buffer loads); 8 the same with the quarters cut at 128-byte
-// lines and the range's start on a line
+// lines and the range's start on a line; 9 / 10: 7 / 8 with global loads;
+// 11: 10 with each group's first and last chunk loaded first with the
+// default (L2-allocating) policy by its lanes 0 / 1 (mode 3's priming);
+// 12: flat with global loads, primed the same way per wave
 template <int SHAPE, int U>
 __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ buf, uint64_t n, uint32_t L,
                                                uint32_t* __restrict__ out) {
@@ -119,17 +122,35 @@ __global__ __launch_bounds__(256) void k_probe(const uint8_t* __restrict__ buf, 
   } else if (SHAPE == 4) {
     const uint64_t per = uint64_t(U) * 1024, s0 = w * per, e0 = std::min<uint64_t>(n * L, s0 + per);
     if (s0 < e0) acc = sum_loads_g<U>(buf + s0, uint32_t(e0 - s0), lane * 16u, 1024u);
+  } else if (SHAPE == 12) {
+    const uint64_t s0 = w * 4 * L, e0 = std::min<uint64_t>(n * L, s0 + 4ull * L);
+    if (s0 < e0) {
+      const u32x4* pr = reinterpret_cast<const u32x4*>(buf + s0);
+      const uint32_t last = uint32_t((e0 - s0 - 1) >> 4);
+      const u32x4 bnd = pr[lane == 1 ? last : 0u];
+      acc = sum_loads_g<U>(buf + s0, uint32_t(e0 - s0), lane * 16u, 1024u) + (lane < 2 ? bnd.x : 0u);
+    }
   } else if (SHAPE == 5 || SHAPE == 6) {
     const uint64_t seg = w * 4 + (lane >> 4);
     if (seg < n) acc = line_primed<U, SHAPE == 6>(buf, seg * L, seg * L + L, lane & 15u);
   } else {
     const uint64_t s0r = w * 4 * L, e0 = std::min<uint64_t>(n * L, s0r + 4ull * L);
-    const uint64_t s0 = SHAPE == 8 ? (s0r & ~uint64_t(127)) : (s0r & ~uint64_t(15));
+    const bool lines = SHAPE == 8 || SHAPE == 10 || SHAPE == 11;
+    const uint64_t s0 = lines ? (s0r & ~uint64_t(127)) : (s0r & ~uint64_t(15));
     if (s0 < e0) {
-      const uint64_t unit = SHAPE == 8 ? 128 : 16;
+      const uint64_t unit = lines ? 128 : 16;
       const uint64_t q = ((e0 - s0 + 4 * unit - 1) / (4 * unit)) * unit;  // quarter length
       const uint64_t g = lane >> 4, qs = s0 + g * q, qe = std::min<uint64_t>(e0, qs + q);
-      acc = sum_loads<U>(buf + qs, uint32_t(qe > qs ? qe - qs : 0), (lane & 15u) * 16u, 256u);
+      if (SHAPE == 11 && qe > qs) {
+        const u32x4* pr = reinterpret_cast<const u32x4*>(buf + qs);
+        const uint32_t last = uint32_t((qe - qs - 1) >> 4);
+        const u32x4 bnd = pr[(lane & 15u) == 1 ? last : 0u];
+        acc = (lane & 15u) < 2 ? bnd.x : 0u;
+      }
+      if (SHAPE == 9 || SHAPE == 10 || SHAPE == 11)
+        acc += sum_loads_g<U>(buf + qs, uint32_t(qe > qs ? qe - qs : 0), (lane & 15u) * 16u, 256u);
+      else
+        acc = sum_loads<U>(buf + qs, uint32_t(qe > qs ? qe - qs : 0), (lane & 15u) * 16u, 256u);
     }
   }
   // one store per 16 lanes (k_checksum writes 2 bytes per segment)
@@ -164,7 +185,12 @@ int main() {
               {"line_primed_global", k_probe<5, 7>, 1500, 5, 7}, {"line_primed_buffer", k_probe<6, 7>, 1500, 6, 7},
               {"line_primed_global", k_probe<5, 4>, 770, 5, 4},  {"line_primed_buffer", k_probe<6, 4>, 770, 6, 4},
               {"quarters", k_probe<7, 6>, 1500, 7, 6}, {"quarters_lines", k_probe<8, 7>, 1500, 8, 7},
-              {"quarters", k_probe<7, 4>, 770, 7, 4},  {"quarters_lines", k_probe<8, 4>, 770, 8, 4}};
+              {"quarters", k_probe<7, 4>, 770, 7, 4},  {"quarters_lines", k_probe<8, 4>, 770, 8, 4},
+              {"quarters_global", k_probe<9, 6>, 1500, 9, 6}, {"quarters_lines_global", k_probe<10, 7>, 1500, 10, 7},
+              {"quarters_global", k_probe<9, 4>, 770, 9, 4},  {"quarters_lines_global", k_probe<10, 4>, 770, 10, 4},
+              {"quarters_lines_global_primed", k_probe<11, 7>, 1500, 11, 7},
+              {"quarters_lines_global_primed", k_probe<11, 4>, 770, 11, 4},
+              {"flat_global_primed", k_probe<12, 6>, 1500, 12, 6}, {"flat_global_primed", k_probe<12, 4>, 770, 12, 4}};
   for (const Run& r : runs) {
     const uint64_t bytes = n * r.L;
     const uint64_t waves = (r.shape == 2 || r.shape == 4) ? (bytes + uint64_t(r.u) * 1024 - 1) / (uint64_t(r.u) * 1024) : (n + 3) / 4;

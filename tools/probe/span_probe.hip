@@ -46,7 +46,7 @@ int main() {
     CK(hipMalloc(&dout, n * 2));
     auto launch = [&](int i) {
       icsum::SegSpec sp{d[i & 1], doff[i & 1], 0, 0, n, zero};
-      CK(icsum::launch_tile_checksum(sp, nullptr, nullptr, dout, 0, nullptr));
+      CK(icsum::launch_tile_checksum(sp, nullptr, nullptr, dout, 0, 63, nullptr));
     };
     for (int i = 0; i < 50; ++i) launch(i);
     CK(hipDeviceSynchronize());
