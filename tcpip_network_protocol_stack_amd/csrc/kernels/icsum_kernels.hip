@@ -1945,7 +1945,11 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
   const uint64_t a0c = (first >> 7) << 3;
   const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
   const uint64_t nw = (nch + kWinChunks - 1) / kWinChunks;
-  const uint64_t nwin3 = nw ? (nw + 2) / 3 * 3 : 3;  // whole rounds of the three register sets
+  // three register sets per wave: two windows in flight while one is summed
+  // (two sets, 6 waves / SIMD, and three sets forced to 5 waves / SIMD by
+  // spilling both measured equal or slower: profiles/r5y_ab_span_sets_waves.jsonl)
+  constexpr uint32_t kSets = 3;
+  const uint64_t nwin3 = nw ? (nw + kSets - 1) / kSets * kSets : kSets;  // whole rounds of the sets
   const uint32_t voff = lane * 16u;
   auto load_win = [&](uint64_t k, u32x4 (&v)[4]) {
     const uint64_t c0 = k * kWinChunks;
@@ -1979,25 +1983,30 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
 #endif
   // point B, once the windows are out: IPv4 past the header (options skipped,
   // ipv4_header.cpp:50), the in-place wrap past the 40 header bytes it rewrites
-  uint64_t lo = x;
-  if constexpr (OP == kTileIpv4) {
-    uint64_t o = 4u * ((d0 >> (8u * (uint32_t(x) & 3u))) & 0x0fu);
-    if (o < 20) o = 20;
-    if (hdr && o > e - x) o = e - x;
-    lo = hdr ? x + o : e;
-  } else if constexpr (OP == kTileWrap) {
-    lo = valid && e - x >= 40 ? x + 40 : e;
-  }
-  // the lane's points: chunk (span-relative) and byte; lanes past m hold no A, lanes >= m no B
-  const uint64_t pc = lane <= m ? (x >> 4) - a0c : ~uint64_t(0);
+  auto point_b = [&](uint64_t e_) {
+    uint64_t lo_ = x;
+    if constexpr (OP == kTileIpv4) {
+      uint64_t o = 4u * ((d0 >> (8u * (uint32_t(x) & 3u))) & 0x0fu);
+      if (o < 20) o = 20;
+      if (hdr && o > e_ - x) o = e_ - x;
+      lo_ = hdr ? x + o : e_;
+    } else if constexpr (OP == kTileWrap) {
+      lo_ = valid && e_ - x >= 40 ? x + 40 : e_;
+    }
+    return lo_;
+  };
+  const uint64_t lo = point_b(e);
+  // the lane's points: chunk (span-relative, 32 bits) and byte; lanes past m
+  // hold no A, lanes >= m no B
+  const uint32_t pc = lane <= m ? uint32_t((x >> 4) - a0c) : ~0u;
   const uint32_t pb = uint32_t(x) & 15u;
-  const uint64_t qc = TWO && valid ? (lo >> 4) - a0c : ~uint64_t(0);
+  const uint32_t qc = TWO && valid ? uint32_t((lo >> 4) - a0c) : ~0u;
   const uint32_t qb = uint32_t(lo) & 15u;
   uint32_t ce = 0, co = 0;  // the span's sums so far
   uint32_t fe = 0, fo = 0;  // F of point A (set by the window holding it)
   uint32_t ge = 0, go = 0;  // F of point B
   // F at a point inside window [c0, c1): its chunk's prefix + the chunk's bytes below it
-  auto point_F = [&](uint64_t c, uint32_t b, uint64_t c0, uint32_t& fe_, uint32_t& fo_) {
+  auto point_F = [&](uint32_t c, uint32_t b, uint64_t c0, uint32_t& fe_, uint32_t& fo_) {
     const uint32_t k2 = uint32_t(c - c0);
     fe_ = s_pre[wv][k2][0];
     fo_ = s_pre[wv][k2][1];
@@ -2010,7 +2019,7 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
 #pragma unroll
       for (int u = 0; u < 4; ++u) s_raw[wv][win_slot(uint32_t(u) * 64u + lane)] = v[u];
     }
-    load_win(k + 3, v);  // the registers are free: window k + 3 goes out now (one load site)
+    load_win(k + kSets, v);  // the registers are free: window k + kSets goes out now (one load site)
     if (!live) return;
 #ifdef ICSUM_SPAN_PROBE_STREAM_ONLY
     // diagnostic build only (tools/probe/span_probe.hip): the loads, the LDS
@@ -2049,20 +2058,20 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    if (pc >= c0 && pc < c1) point_F(pc, pb, c0, fe, fo);
+    if (pc >= c0 && pc < c1) point_F(pc, pb, c0, fe, fo);  // (~0u: no point, past any window)
     if constexpr (TWO) {
       if (qc >= c0 && qc < c1) point_F(qc, qb, c0, ge, go);
     }
     __builtin_amdgcn_wave_barrier();  // the next window rewrites s_pre / s_raw
   };
-  // wave-uniform; nwin3 >= 3, so a do-while: no zero-trip test for the
+  // wave-uniform; nwin3 >= kSets, so a do-while: no zero-trip test for the
   // compiler to sink the first three windows' loads behind
   uint64_t k = 0;
   do {
     window(k, b0);
     window(k + 1, b1);
     window(k + 2, b2);
-    k += 3;
+    k += kSets;
   } while (k < nwin3);
   // a point at the aligned end of the last chunk: every byte is below it
   if (lane <= m && pc >= nch) {
