@@ -1945,9 +1945,10 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
   const uint64_t a0c = (first >> 7) << 3;
   const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
   const uint64_t nw = (nch + kWinChunks - 1) / kWinChunks;
-  // three register sets per wave: two windows in flight while one is summed
-  // (two sets, 6 waves / SIMD, and three sets forced to 5 waves / SIMD by
-  // spilling both measured equal or slower: profiles/r5y_ab_span_sets_waves.jsonl)
+  // three register sets per wave, each reloaded as soon as its window is in
+  // LDS: up to three windows in flight (two sets at 6 waves / SIMD, and three
+  // forced to 5 waves / SIMD by spilling, measured equal or slower:
+  // profiles/r5y_ab_span_sets_waves.jsonl)
   constexpr uint32_t kSets = 3;
   const uint64_t nwin3 = nw ? (nw + kSets - 1) / kSets * kSets : kSets;  // whole rounds of the sets
   const uint32_t voff = lane * 16u;
