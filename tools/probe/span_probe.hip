@@ -2,8 +2,8 @@
 // kernel file: as shipped, and with -DICSUM_SPAN_PROBE_STREAM_ONLY (every
 // window only loaded and written to LDS; results wrong, time only).  Times the
 // checksum span launch on the transmit mix (256 Ki segments of 40..1040 B)
-// and on 1 M x 770 B offsets, back to back (HIP events around 20 launches,
-// median of 5).
+// and on 1 M x 770 B offsets at S = 8, 16, 32, 63 segments per span, back to
+// back (HIP events around 20 launches, median of 5).
 #include "../../tcpip_network_protocol_stack_amd/csrc/kernels/icsum_kernels.hip"
 
 #include <algorithm>
@@ -30,7 +30,8 @@ int main() {
 #else
   const char* build = "shipped";
 #endif
-  for (int shape = 0; shape < 2; ++shape) {
+  for (int shape = 0; shape < 2; ++shape)
+  for (uint32_t S : {8u, 16u, 32u, 63u}) {
     const uint64_t n = shape == 0 ? (1u << 18) : (1u << 20);
     std::vector<uint64_t> off(n + 1, 0);
     for (uint64_t i = 0; i < n; ++i) off[i + 1] = off[i] + (shape == 0 ? 40 + rng() % 1001 : 770);
@@ -46,7 +47,7 @@ int main() {
     CK(hipMalloc(&dout, n * 2));
     auto launch = [&](int i) {
       icsum::SegSpec sp{d[i & 1], doff[i & 1], 0, 0, n, zero};
-      CK(icsum::launch_tile_checksum(sp, nullptr, nullptr, dout, 0, 63, nullptr));
+      CK(icsum::launch_tile_checksum(sp, nullptr, nullptr, dout, 0, S, nullptr));
     };
     for (int i = 0; i < 50; ++i) launch(i);
     CK(hipDeviceSynchronize());
@@ -64,8 +65,9 @@ int main() {
       ts.push_back(ms * 1000.f / 20.f);
     }
     std::sort(ts.begin(), ts.end());
-    std::printf("{\"build\": \"%s\", \"shape\": \"%s\", \"bytes\": %llu, \"us\": %.2f, \"frac\": %.4f}\n", build,
-                shape == 0 ? "tx256k" : "u770_1m", (unsigned long long)off[n], ts[2], off[n] / (ts[2] * 1e3) / 8000.0);
+    std::printf("{\"build\": \"%s\", \"shape\": \"%s\", \"S\": %u, \"bytes\": %llu, \"us\": %.2f, \"frac\": %.4f}\n",
+                build, shape == 0 ? "tx256k" : "u770_1m", S, (unsigned long long)off[n], ts[2],
+                off[n] / (ts[2] * 1e3) / 8000.0);
     for (int r = 0; r < 2; ++r) {
       CK(hipFree(d[r]));
       CK(hipFree(doff[r]));
