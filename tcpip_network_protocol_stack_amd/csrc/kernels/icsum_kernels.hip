@@ -392,15 +392,22 @@ __device__ __forceinline__ uint32_t block_order(uint32_t run_log2) {
 // system-scope release (cumulative: one L2 write-back per block, not per
 // wave) puts them where the host reads them before it takes a ticket; the
 // block with the last ticket resets the ticket word and releases the
-// completion value into the host word.  A no-op (one uniform branch) for
-// every device-path launch.  Every thread of the block must reach it:
-// kernels call their body first.
+// completion value into the host word.  A one-block launch (a tick of up to
+// 16 MTU datagrams) skips the ticket and releases the word at once: the
+// agent-scope atomic behind the system-scope release cost 1.7-1.9 us of a
+// 9-13 us call (profiles/r5_tick_latency_single_block_ab.jsonl).  A no-op
+// (one uniform branch) for every device-path launch.  Every thread of the
+// block must reach it: kernels call their body first.
 __device__ __forceinline__ void signal_done(const Done& d) {
   if (d.flag == nullptr) return;
   __builtin_amdgcn_s_waitcnt(0);
   __syncthreads();
   if (threadIdx.x == 0) {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");  // system scope
+    if (gridDim.x == 1) {  // the only block (a tick of a few datagrams): no ticket to draw
+      __hip_atomic_store(d.flag, d.value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
     const uint32_t t = __hip_atomic_fetch_add(d.ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
     if (t == gridDim.x - 1) {
       __hip_atomic_store(d.ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
