@@ -22,6 +22,14 @@
  *                           (n+1 monotone uint64 offsets; starts may be odd /
  *                           unaligned — byte roles are relative to each start)
  *       d_offsets == NULL : segment i = bytes[i*stride, i*stride + seg_len)
+ *   - Byte bases (d_bytes, d_dgrams, d_payloads, h_bytes, ...) may lie at ANY
+ *     address, as InternetChecksum::add takes any string_view
+ *     (util/tools/checksum.h:20-28): e.g. the IPv4 datagrams of a frame arena
+ *     14 bytes in.  Loads stay inside the 16-byte-aligned blocks that hold a
+ *     segment's bytes (never outside the pages of the batch).  Only the
+ *     record arrays d_msgs / d_hdrs must be 4-byte aligned (ICS_ERR_INVALID
+ *     otherwise); fixed stride == length == 64 B runs the dense kernel only
+ *     from a 16-byte-aligned base (same results either way).
  *   - A context is bound to one device and may be used from several host
  *     threads (launch calls are thread-safe; the host-memory *_host calls
  *     serialise on an internal staging lock).
@@ -298,14 +306,18 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 #define ICS_K_WRAP_2PASS 10      /* k_tcp_wrap (payload sums) + k_tcp_hdr */
 #define ICS_K_ROUTER 11          /* k_router_ttl */
 #define ICS_K_BATCHV 12          /* several batches in one launch (ics_*_batchv) */
-#define ICS_K_TILE 13            /* k_span: an offsets batch as one packed stream, 63 segments per wave */
+#define ICS_K_TILE 13            /* k_span: an offsets batch as one packed stream, S (1..63) segments per wave */
 #define ICS_K_ROUTER_HDRS 14     /* k_router_hdrs: the router step, forwarded headers apart */
+#define ICS_K_TICK 15            /* k_tick: a zero-copy *_host tick of <= 16 offsets segments, offsets in the kernel arguments */
 /* last_lps / last_unroll by kernel:
  *   ICS_K_CHECKSUM .. ICS_K_WRAP_2PASS  lanes per segment / loads in flight per lane
  *   ICS_K_TWOCLASS, ICS_K_IPV4_TWOCLASS  long-segment lanes (16) / segments per wave (16 or 32; 8 only under ICSUM_FORCE twoclass=8)
  *   ICS_K_BATCHV  the ICS_BV_* shape of the last launch group / batches in the call
- *   ICS_K_TILE    segments per wave (63) / ICS_TILE_* operation
- *   ICS_K_ROUTER, ICS_K_ROUTER_HDRS  0 / 0 */
+ *   ICS_K_TILE    segments per wave S / ICS_TILE_* operation; S is chosen per
+ *                 call, clamp(20 KiB / mean segment length, 1, 63) from the
+ *                 cached plan (ICSUM_FORCE span_segs pins it)
+ *   ICS_K_ROUTER, ICS_K_ROUTER_HDRS  0 / 0
+ *   ICS_K_TICK    16 / 8 (a 16-lane group per segment, one block) */
 #define ICS_BV_DENSE64 0 /* fixed stride == length == 64 B, 16-byte aligned */
 #define ICS_BV_TINY 1    /* one lane per segment (ACK-sized fixed lengths) */
 #define ICS_BV_SMALL 2   /* 4-lane groups, two segments in flight */

@@ -59,7 +59,7 @@ class DgramBatch(ctypes.Structure):
 # ICS_K_* kernel ids of ics_dispatch_info_t.last_kernel
 KERNELS = {1: "checksum", 2: "small", 3: "tiny", 4: "dense", 5: "twoclass", 6: "binned", 7: "ipv4",
            8: "ipv4_twoclass", 9: "wrap", 10: "wrap_2pass", 11: "router", 12: "batchv", 13: "tile",
-           14: "router_hdrs"}
+           14: "router_hdrs", 15: "tick"}
 
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64

@@ -88,8 +88,11 @@ struct ics_ctx {
   // wave (0: span_segs_for)
   int tile = -1;
   uint32_t span_segs = 0;
+  uint32_t span_blocks = 0;
+  int tick_inline = 1;  // zero-copy ticks of <= kTickSegs offsets segments through k_tick (ICSUM_FORCE tick_inline=0: off)  // test hook: grid cap of the tile launch (0: none), reaches its grid-stride form
   static constexpr uint64_t kSpanBytes = 20 << 10;  // segment bytes per span (span_segs_for)
   static constexpr uint64_t kTileMin = uint64_t(1) << 16;  // tile launches from this many segments (AUTO)
+  static constexpr uint64_t kTileMinChecksum = uint64_t(1) << 17;  // ... of the plain checksum (tile_wins)
   static constexpr uint32_t kTileMaxAvg = 1024;            // ... and up to this mean length (tile_wins)
   static constexpr uint32_t kTileApartShort16 = 12;       // headers-apart wrap: below 12/16 empty-ish payloads
   uint32_t twoclass_remap = 0;  // block_order run length (log2) of the two-class launches; 0: hardware order

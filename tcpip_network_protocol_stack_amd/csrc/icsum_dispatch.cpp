@@ -186,8 +186,11 @@ bool short_mix(const PlanMix& m) { return m.short16 >= ics_ctx::kShortMix16 && m
 // 233.5 / 192.3; headers-apart wrap 40..1040 B 64 Ki / 1 M 11.7 / 9.8 and
 // 137.4 / 103.4, MTU 1 M 244.8 / 265.2; in-place wrap 40..1040 B 1 M 156.9 /
 // 156.3, 770 B 1 M 193.2 / 207.2, config 4's mix 265.6 / 230.6.
+// The plain checksum keeps the per-segment launches up to kTileMinChecksum
+// (64 Ki 40..1040 B: 11.1 us per segment vs 11.3 us span above); VERIFY and
+// the headers-apart wrap already win at 64 Ki (16.1 / 11.9, 11.7 / 9.8 us).
 bool tile_wins(const ics_ctx* ctx, const PlanMix& m, uint64_t n, bool fused) {
-  if (ctx->tile == 0 || n < ics_ctx::kTileMin) return false;
+  if (ctx->tile == 0 || n < (fused ? ics_ctx::kTileMin : ics_ctx::kTileMinChecksum)) return false;
   return m.avg <= ics_ctx::kTileMaxAvg || (fused && m.long16 >= 4);
 }
 
@@ -230,7 +233,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   }
   if (sp.offsets && ctx->tile == 1) {  // test hook: the tile launch on every offsets batch
     const uint32_t S = span_segs_for(ctx, 0);
-    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st));
+    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st, ctx->span_blocks));
     note(ctx, ICS_K_TILE, {int(S), ICS_TILE_CHECKSUM, true, 0, 1});
     return ICS_OK;
   }
@@ -287,7 +290,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     const bool mix8 = hit && hit_plan != icsum::kPlanWholeBatchSmall && short_mix(mix);
     if (hit && !mix8 && hit_plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, sp.n, false)) {
       const uint32_t S = span_segs_for(ctx, mix.avg);
-      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st));
+      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st, ctx->span_blocks));
       note(ctx, ICS_K_TILE, {int(S), ICS_TILE_CHECKSUM, true, 0, 1}, int(hit_plan));
       return replan(ctx, sp, lps, req, st);
     }
@@ -392,7 +395,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   }
   if (d_offsets && (ctx->tile == 1 || tile)) {  // the test hook, or the cached mix favours the tile launch
     const uint32_t S = span_segs_for(ctx, span_avg);
-    ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, S, st));
+    ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, S, st, ctx->span_blocks));
     note(ctx, ICS_K_TILE, {int(S), ICS_TILE_IPV4, true, 0, 1}, plan_used);
     return replan(ctx, sp, 64, req, st);
   }
@@ -477,7 +480,7 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
   if (sp.offsets && (ctx->tile == 1 || tile_pick)) {  // the wrap (in place or headers apart) as a tile launch
     const uint32_t S = span_segs_for(ctx, plan >= 0 ? mix.avg : 0u);
     ICS_HIP(icsum::launch_tile_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), hdr_out, d_ip_ck, d_tcp_ck,
-                                    S, st));
+                                    S, st, ctx->span_blocks));
     note(ctx, ICS_K_TILE, {int(S), hdr_out ? ICS_TILE_WRAP_APART : ICS_TILE_WRAP, true, 0, 1}, plan);
     return replan(ctx, sp, 64, req, st);
   }
@@ -619,6 +622,8 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "wrap_passes" && v >= 0 && v <= 2) ctx->wrap_passes = uint32_t(v);
     else if (k == "xcd_remap") icsum::set_xcd_remap(uint32_t(v));
     else if (k == "span_segs" && v >= 0 && v <= 63) ctx->span_segs = uint32_t(v);
+    else if (k == "span_blocks" && v >= 0 && v <= 0xFFFFFF) ctx->span_blocks = uint32_t(v);
+    else if (k == "tick_inline" && (v == 0 || v == 1)) ctx->tick_inline = int(v);
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);

@@ -252,6 +252,14 @@ void free_staging(ics_ctx* ctx) {
 // synchronisation).
 namespace {
 
+// ics_dispatch_info's "last call" fields for a host-memory call's launch
+void note_host(ics_ctx* ctx, int kernel, int lps, int unroll) {
+  ctx->last_kernel.store(kernel, std::memory_order_relaxed);
+  ctx->last_lps.store(lps, std::memory_order_relaxed);
+  ctx->last_unroll.store(unroll, std::memory_order_relaxed);
+  ctx->last_plan.store(-1, std::memory_order_relaxed);
+}
+
 int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offsets, uint64_t stride,
                  uint64_t seg_len, const uint32_t* h_init, uint64_t n, int mode, uint16_t* out_a, uint16_t* out_b,
                  uint8_t* out_c, const ics_tcp_msg* h_msgs) {
@@ -378,7 +386,21 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
     if (zc) sp.done = icsum::Done{ctx->d_ticket + 16 * slot, ctx->h_flag + 8 * slot, flag_of[slot]};
     const uint64_t avg = h_offsets ? nb / m : seg_len;
     const icsum::Geometry g = geometry_for(ctx, avg);
-    if (kind == 2) {
+    // a zero-copy tick of a few segments with offsets: the offsets travel in
+    // the kernel arguments (k_tick), not as a dependent PCIe read
+    const bool tick = zc && h_offsets && kind != 2 && m <= icsum::kTickSegs && ctx->tick_inline;
+    if (tick) {
+      const uint32_t* d_init = nullptr;
+      if (kind == 0 && h_init) {
+        std::memcpy(ctx->h_init[slot], h_init + c.i0, m * 4);
+        d_init = reinterpret_cast<const uint32_t*>(ctx->h_init[slot]);
+      }
+      uint16_t* a = reinterpret_cast<uint16_t*>(res);
+      const int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;  // PATCH: fields written at retire
+      ICS_HIP(icsum::launch_tick(in, ctx->h_off[slot], uint32_t(m), kind == 0 ? 0 : 1, d_init, a, dev_mode, a, a + m,
+                                 res + m * 4, ctx->d_zero, sp.done, st));
+      note_host(ctx, ICS_K_TICK, 16, 8);
+    } else if (kind == 2) {
       std::memcpy(ctx->h_msg[slot], h_msgs + c.i0, m * sizeof(ics_tcp_msg));
       const void* msgs = nullptr;
       ICS_HIP(h2d(ctx->d_msg[slot], ctx->h_msg[slot], m * sizeof(ics_tcp_msg), &msgs));
@@ -388,6 +410,8 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
                                      wrap_two_pass(ctx, true, m) ? ctx->d_sums[slot] : nullptr, ipv4_geometry(g),
                                      0, st));
       ICS_HIP(d2h(ctx->h_hdr[slot], ctx->d_hdr[slot], m * 40));
+      note_host(ctx, wrap_two_pass(ctx, true, m) ? ICS_K_WRAP_2PASS : ICS_K_WRAP, ipv4_geometry(g).lps,
+                ipv4_geometry(g).unroll);
     } else if (kind == 0) {
       const uint32_t* d_init = nullptr;
       if (h_init) {
@@ -398,6 +422,8 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
       }
       ICS_HIP(icsum::launch_checksum(sp, d_init, nullptr, res, 0, g, 0, st));
       ICS_HIP(d2h(ctx->h_out[slot], ctx->d_out[slot], m * 2));
+      note_host(ctx, g.mode == icsum::kModeTiny ? ICS_K_TINY : g.segs > 1 ? ICS_K_SMALL : ICS_K_CHECKSUM, g.lps,
+                g.unroll);
     } else {
       uint16_t* a = reinterpret_cast<uint16_t*>(res);
       uint16_t* b = a + m;
@@ -410,6 +436,7 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
       const icsum::Geometry gi = h_offsets ? ipv4_geometry(g) : ipv4_fixed_geometry(ctx, ipv4_geometry(g), seg_len);
       ICS_HIP(icsum::launch_ipv4_tcp(sp, dev_mode, a, b, s, gi, 0, st));
       ICS_HIP(d2h(ctx->h_out[slot], ctx->d_out[slot], m * 5));
+      note_host(ctx, ICS_K_IPV4, gi.lps, gi.unroll);
     }
     if (!zc) ICS_HIP(hipEventRecord(ctx->ev[slot], st));
     pending[slot] = c;

@@ -50,6 +50,20 @@ __device__ __forceinline__ void bounds_check16(const void* p, const uint8_t* lo,
 #define ICS_CHECK16(p, lo, hi) ((void)0)
 #endif
 
+// ---- byte bases at any address -------------------------------------------
+// The reference sums bytes at any address (InternetChecksum::add takes any
+// string_view, checksum.h:20-28; a receive arena of Ethernet frames holds its
+// IPv4 datagrams 14 bytes in, network_interface.cpp:51).  Every kernel works
+// in the frame of the 16-byte-aligned address at or below its byte base: it
+// moves the base down by frame_shift(base) and adds the shift to every
+// segment bound, so chunk loads, 128-byte lines and byte roles are absolute
+// and a boundary load never leaves the 16-byte block — hence the page — that
+// holds a byte of the batch.  (Pointer arithmetic, not an integer mask: the
+// base stays a global pointer.)
+__device__ __forceinline__ uint32_t frame_shift(const void* p) {
+  return uint32_t(reinterpret_cast<uintptr_t>(p) & 15u);
+}
+
 constexpr uint32_t kEvenBytes = 0x00010001u;  // bytes 0 and 2 of a dword
 constexpr uint32_t kOddBytes = 0x01000100u;   // bytes 1 and 3 of a dword
 

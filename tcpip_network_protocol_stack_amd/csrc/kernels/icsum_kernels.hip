@@ -32,9 +32,11 @@ namespace {
 
 constexpr int kBlock = 256;
 
+// segment i's bounds in the kernel's frame (sh = frame_shift of the batch's
+// byte base, icsum_device.h)
 __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets, uint64_t stride,
                                            uint64_t seg_len, uint64_t i, uint64_t& s,
-                                           uint64_t& e) {
+                                           uint64_t& e, uint32_t sh) {
   if (offsets) {
     s = offsets[i];
     e = offsets[i + 1];
@@ -45,6 +47,8 @@ __device__ __forceinline__ void seg_bounds(const uint64_t* __restrict__ offsets,
     s = i * stride;
     e = s + seg_len;
   }
+  s += sh;
+  e += sh;
 }
 
 // ------------------------------------------------------- length binning ---
@@ -235,7 +239,16 @@ struct SegSrc {
   const u32x4* list;     // bin launch: this bin's entries
   const uint32_t* meta;  // bin launch: the binning pass's sizes and plan
   int bin;
+  uint32_t shift = 0;    // frame_shift of the byte base, set by the kernel (rebase)
 };
+
+// the kernel's frame of its byte base (icsum_device.h): bytes moved down to
+// the 16-byte-aligned address, the shift recorded for src_decode
+template <typename T>
+__device__ __forceinline__ T* rebase(T* bytes, SegSrc& src) {
+  src.shift = frame_shift(bytes);
+  return bytes - src.shift;
+}
 
 // A launch's work, resolved once at kernel start: the bin's list (split plan)
 // or, for the last bin's launch under the whole-batch plan, every segment by
@@ -291,7 +304,7 @@ __device__ __forceinline__ void src_decode(const SegSrc& src, const Work& w, uin
       s = uint64_t(m.ent.x) | (uint64_t(m.ent.y) << 32);
       e = s + m.ent.z;
     } else {
-      seg_bounds(src.offsets, 0, 0, seg, s, e);
+      seg_bounds(src.offsets, 0, 0, seg, s, e, 0u);
     }
   } else {
     seg = gi;
@@ -306,6 +319,8 @@ __device__ __forceinline__ void src_decode(const SegSrc& src, const Work& w, uin
       e = s + src.seg_len;
     }
   }
+  s += src.shift;  // the kernel's frame (rebase)
+  e += src.shift;
 }
 
 __device__ __forceinline__ void src_locate(const SegSrc& src, const Work& w, uint64_t gi, uint64_t n,
@@ -491,6 +506,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum(const uint8_t* __restrict__
                                                      uint32_t odd_step,
                                                      void* __restrict__ out, uint64_t n, uint32_t remap,
                                                      const u32x4* __restrict__ zero16, Done done) {
+  bytes = rebase(bytes, src);
   checksum_entry<LPS, UNROLL, NT, MODE, OUT>(bytes, src, init, init_step, odd, odd_step, out, n, remap, zero16);
   signal_done(done);
 }
@@ -584,6 +600,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_small(const uint8_t* __rest
                                                            uint32_t odd_step,
                                                            const u32x4* __restrict__ zero16,
                                                            void* __restrict__ out, uint64_t n, Done done) {
+  bytes = rebase(bytes, src);
   checksum_small_body<LPS, UNROLL, SEGS, OUT>(bytes, src, init, init_step, odd, odd_step, zero16, out, n,
                                               blockIdx.x, gridDim.x);
   signal_done(done);
@@ -653,6 +670,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_tiny(const uint8_t* __restr
                                                           const uint8_t* __restrict__ odd, uint32_t odd_step,
                                                           const u32x4* __restrict__ zero16, void* __restrict__ out,
                                                           uint64_t n, Done done) {
+  bytes = rebase(bytes, src);
   checksum_tiny_body<OUT>(bytes, src, init, init_step, odd, odd_step, zero16, out, n, blockIdx.x, gridDim.x);
   signal_done(done);
 }
@@ -678,6 +696,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_twoclass(const uint8_t* __r
   __shared__ uint32_t cnt[3];  // long, short, long claimed
   __shared__ uint32_t o_sum[kPer];  // the block's sums, written out as one coalesced row at the end
   const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+  bytes = rebase(bytes, src);
   if (threadIdx.x < 3) cnt[threadIdx.x] = 0;
   __syncthreads();
   const Work w{n, nullptr};
@@ -838,6 +857,7 @@ __global__ __launch_bounds__(kBlock) void k_checksum_bins(const uint8_t* __restr
                                                           const u32x4* __restrict__ zero16,
                                                           void* __restrict__ out, uint64_t n, uint32_t nblk) {
   const uint32_t b = blockIdx.x / nblk, blk = blockIdx.x - b * nblk;
+  bytes = rebase(bytes, src);
   SegSrc bs = src;
   bs.list = src.list + uint64_t(b) * n;
   bs.bin = int(b);
@@ -1258,13 +1278,15 @@ __device__ __forceinline__ void ipv4_body(uint8_t* __restrict__ dg, const uint64
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(nblk) * kGroups;
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;  // zpad: 32 zero bytes
+  const uint32_t bsh = frame_shift(dg);
+  dg -= bsh;
   for (uint64_t g0 = uint64_t(blk) * kGroups; g0 < n; g0 += step) {
     const uint64_t seg = g0 + threadIdx.x / LPS;
     const bool valid = seg < n;
     // offsets from a clamped index, unconditionally (a load under a divergent
     // branch is waited for at the join, before the stream below is issued)
     uint64_t s, e;
-    seg_bounds(offsets, stride, dlen, valid ? seg : n - 1, s, e);
+    seg_bounds(offsets, stride, dlen, valid ? seg : n - 1, s, e, bsh);
     if (!valid) e = s;
     ipv4_item<LPS, UNROLL, NT, MODE>(dg, s, e, seg, valid, lane, mode, ip_ck, tcp_ck, status, zpad, zlast);
   }
@@ -1326,8 +1348,10 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_twoclass(uint8_t* __restrict__ 
   const uint64_t b0 = uint64_t(block_order(remap)) * kPer;  // the block's datagrams [b0, b0 + kPer)
   const uint64_t seg = b0 + wv * SPW + (lane < SPW ? lane : 0u);
   const bool valid = seg < n && lane < SPW;
+  const uint32_t bsh = frame_shift(dg);
+  dg -= bsh;
   uint64_t s, e;
-  seg_bounds(offsets, stride, dlen, seg < n ? seg : n - 1, s, e);
+  seg_bounds(offsets, stride, dlen, seg < n ? seg : n - 1, s, e, bsh);
   if (!valid) e = s;
   const bool is_short = e - s <= 64;
   const uint64_t lmask = __ballot(valid && !is_short), smask = __ballot(valid && is_short);
@@ -1434,17 +1458,18 @@ __global__ __launch_bounds__(kBlock) void k_checksum_batchv(BvTable<BvSeg> t, co
   const uint32_t* ip = b.init ? b.init : reinterpret_cast<const uint32_t*>(zero16);
   const uint32_t is = b.init ? 1u : 0u;
   const uint8_t* op = reinterpret_cast<const uint8_t*>(zero16);
-  const SegSrc src{b.offsets, b.stride, b.seg_len, nullptr, nullptr, -1};
+  SegSrc src{b.offsets, b.stride, b.seg_len, nullptr, nullptr, -1};
+  const uint8_t* const bytes = rebase(b.bytes, src);  // the dense class is chosen for aligned bases only
   if constexpr (CLS == kBvDense64)
     checksum_dense_body<4, 4, true, 0>(reinterpret_cast<const u32x4*>(b.bytes), ip, is, b.out, b.n, lb);
   else if constexpr (CLS == kBvTiny)
-    checksum_tiny_body<0>(b.bytes, src, ip, is, op, 0u, zero16, b.out, b.n, lb, nb);
+    checksum_tiny_body<0>(bytes, src, ip, is, op, 0u, zero16, b.out, b.n, lb, nb);
   else if constexpr (CLS == kBvSmall)
-    checksum_small_body<4, 2, 2, 0>(b.bytes, src, ip, is, op, 0u, zero16, b.out, b.n, lb, nb);
+    checksum_small_body<4, 2, 2, 0>(bytes, src, ip, is, op, 0u, zero16, b.out, b.n, lb, nb);
   else if constexpr (CLS == kBvLine16)
-    checksum_body<16, 8, true, 3, 0>(b.bytes, src, ip, is, op, 0u, b.out, b.n, lb, nb);
+    checksum_body<16, 8, true, 3, 0>(bytes, src, ip, is, op, 0u, b.out, b.n, lb, nb);
   else
-    checksum_body<64, 8, true, 3, 0>(b.bytes, src, ip, is, op, 0u, b.out, b.n, lb, nb);
+    checksum_body<64, 8, true, 3, 0>(bytes, src, ip, is, op, 0u, b.out, b.n, lb, nb);
 }
 
 template <int CLS>
@@ -1463,6 +1488,52 @@ __global__ __launch_bounds__(kBlock) void k_ipv4_batchv(BvTable<BvDgram> t, int 
   else
     ipv4_body<64, 8, true, 3>(b.dgrams, b.offsets, b.stride, b.dlen, b.n, mode, b.ip_ck, b.tcp_ck, b.status, zpad,
                               lb, nb);
+}
+
+// ------------------------------------------------- per-tick host calls ----
+// A zero-copy host call of at most kTickSegs segments with offsets (a TUN or
+// socket loop's tick, INTEGRATION.md §4 "Per-tick host batches"): one block,
+// a 16-lane group per segment, the n + 1 offsets in the kernel arguments.  The
+// grid-wide kernels read them from the caller's page-locked offsets, a
+// dependent PCIe round trip ahead of the first payload load (1.3-1.6 us of a
+// 10-13 us call, profiles/r5_tick_latency.jsonl); here the first loads are
+// the payload bytes.  OP 0: checksum (u16 value), 1: the fused IPv4/TCP item.
+template <int OP>
+__global__ __launch_bounds__(kBlock) void k_tick(uint8_t* __restrict__ bytes, TickOffsets t, uint32_t n,
+                                                 const uint32_t* __restrict__ init, uint32_t init_step,
+                                                 uint16_t* __restrict__ out, int mode, uint16_t* __restrict__ ip_ck,
+                                                 uint16_t* __restrict__ tcp_ck, uint8_t* __restrict__ status,
+                                                 const uint8_t* __restrict__ zpad, Done done) {
+  const uint32_t g = threadIdx.x >> 4, lane = threadIdx.x & 15u;
+  const uint32_t bsh = frame_shift(bytes);
+  bytes -= bsh;
+  const bool valid = g < n;
+  const uint32_t gi = valid ? g : n - 1;  // n >= 1: idle groups read segment n - 1's bounds
+  // the wave's four groups' five bounds by scalar loads at a wave-uniform
+  // index (all in flight at once), then each group picks its pair
+  const uint32_t w4 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 4u;
+  uint64_t o[5];
+#pragma unroll
+  for (uint32_t k = 0; k < 5; ++k) o[k] = t.o[w4 + k];
+  const uint32_t q = gi - w4;  // 0..3 in a wave holding a segment (idle groups: segment n - 1's)
+  uint64_t s = o[0], e = o[1];
+#pragma unroll
+  for (uint32_t k = 1; k < 4; ++k)
+    if (q == k) s = o[k], e = o[k + 1];
+  if (w4 >= n) s = e = 0;  // a wave past the last segment (uniform): an empty one, never stored
+  s += bsh;
+  e = valid ? e + bsh : s;
+  if constexpr (OP == 0) {
+    const uint32_t i0 = init[gi * init_step];
+    uint32_t ev = 0, od = 0;
+    seg_sums<16, 8, true, 3>(bytes, s, e, lane, ev, od);
+    const uint32_t tot = group_sum<16>(combine_roles(ev, od, uint32_t(s) & 1u));
+    if (valid && lane == 15) out[g] = fold_value(i0 + tot);
+  } else {
+    const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
+    ipv4_item<16, 8, true, 3>(bytes, s, e, g, valid, lane, mode, ip_ck, tcp_ck, status, zpad, zlast);
+  }
+  signal_done(done);
 }
 
 // ------------------------------------------- device-side wrap (f2) -------
@@ -1490,12 +1561,14 @@ __global__ __launch_bounds__(kBlock) void k_tcp_wrap(uint8_t* __restrict__ dg,
   constexpr uint32_t kGroups = kBlock / LPS;
   const uint32_t lane = threadIdx.x & (LPS - 1);
   const uint64_t step = uint64_t(gridDim.x) * kGroups;
+  const uint32_t bsh = frame_shift(dg);
+  dg -= bsh;
   for (uint64_t g0 = uint64_t(block_order(remap)) * kGroups; g0 < n; g0 += step) {
     const uint64_t seg = g0 + threadIdx.x / LPS;
     const bool valid = seg < n;
     const uint64_t idx = valid ? seg : n - 1;  // clamped index: every load unconditional
     uint64_t s, e;
-    seg_bounds(offsets, stride, dlen, idx, s, e);
+    seg_bounds(offsets, stride, dlen, idx, s, e, bsh);
     if (!valid) e = s;
     // payload_only: segment i is the payload alone, its headers go to hdr_out
     const bool ok = valid && (payload_only || e - s >= 40);
@@ -1607,6 +1680,8 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
   __shared__ uint32_t stage[kBlock / 64][64 * 10];  // 10 KiB: each wave's 640 header dwords
   const uint32_t lane64 = threadIdx.x & 63u;
   uint32_t* const sw = stage[threadIdx.x >> 6];
+  const uint32_t bsh = frame_shift(dg);
+  dg -= bsh;
   for (uint64_t b0 = uint64_t(blockIdx.x) * kBlock; b0 < n; b0 += uint64_t(gridDim.x) * kBlock) {
     const uint64_t base = b0 + (threadIdx.x & ~63u);  // the wave's first datagram
     if (base >= n) continue;                          // wave-uniform
@@ -1614,7 +1689,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
     const bool valid = i < n;
     const uint64_t idx = valid ? i : n - 1;
     uint64_t s, e;
-    seg_bounds(offsets, stride, dlen, idx, s, e);
+    seg_bounds(offsets, stride, dlen, idx, s, e, bsh);
     const bool ok = valid && (payload_only || e - s >= 40);
     // the record as dwordx4 + dwordx3 (ics_tcp_msg: src, dst, seqno, ackno;
     // sport | dport << 16; window | flags << 16 | ttl << 24; id)
@@ -1677,13 +1752,15 @@ __global__ __launch_bounds__(kBlock) void k_router_ttl(uint8_t* __restrict__ dg,
   constexpr uint32_t kG = kBlock / 2;
   const uint32_t lane = threadIdx.x & 1u;
   const uint64_t step = uint64_t(gridDim.x) * kG;
+  const uint32_t bsh = frame_shift(dg);
+  dg -= bsh;
   // the loop bound is uniform per block (group base index), so both lanes of
   // every pair reach the shuffles together
   for (uint64_t g0 = uint64_t(blockIdx.x) * kG; g0 < n; g0 += step) {
     const uint64_t i = g0 + threadIdx.x / 2;
     const bool valid = i < n;
     uint64_t s, e;
-    seg_bounds(offsets, stride, dlen, valid ? i : n - 1, s, e);
+    seg_bounds(offsets, stride, dlen, valid ? i : n - 1, s, e, bsh);
     const bool hdr = valid && e - s >= 20;
     uint8_t* p = dg + s;
     const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
@@ -1760,11 +1837,13 @@ __global__ __launch_bounds__(kBlock) void k_router_hdrs(const uint8_t* __restric
   const uint32_t lane = threadIdx.x & 1u, lane64 = threadIdx.x & 63u;
   uint32_t* const sw = stage[threadIdx.x >> 6];
   const uint64_t step = uint64_t(gridDim.x) * kG;
+  const uint32_t bsh = frame_shift(dg);
+  dg -= bsh;
   for (uint64_t g0 = uint64_t(blockIdx.x) * kG; g0 < n; g0 += step) {  // uniform per block
     const uint64_t i = g0 + threadIdx.x / 2;
     const bool valid = i < n;
     uint64_t s, e;
-    seg_bounds(offsets, stride, dlen, valid ? i : n - 1, s, e);
+    seg_bounds(offsets, stride, dlen, valid ? i : n - 1, s, e, bsh);
     const bool hdr = valid && e - s >= 20;
     const uint8_t* p = dg + s;
     const uint32_t sh = uint32_t(reinterpret_cast<uintptr_t>(p) & 3u);
@@ -1916,6 +1995,8 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
   const uint32_t lane = threadIdx.x & 63u;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const uint64_t nspans = (n + S - 1) / S;
+  const uint32_t bsh = frame_shift(bytes);  // the kernel's frame (icsum_device.h): points and windows absolute
+  bytes -= bsh;
   // one span per wave; STRIDE (batches of more spans than 2^24 blocks hold):
   // grid-stride beyond the grid.  Wave-uniform, no block barrier anywhere.
   auto span_body = [&](uint64_t span) {
@@ -1925,7 +2006,7 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
   const uint64_t i = i0 + (valid ? lane : 0u);  // lanes >= m: a harmless copy of segment 0
   // point A (one load per lane) and, for the checksum, the per-segment words —
   // in flight before the first window is requested
-  const uint64_t x = off[i0 + (lane <= m ? lane : m)];
+  const uint64_t x = off[i0 + (lane <= m ? lane : m)] + bsh;
   uint32_t w[OP == kTileSum ? 2 : 7];
   if constexpr (OP == kTileSum) {
     w[0] = a.init[i * a.init_step];
@@ -1933,18 +2014,19 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
   }
   // the span's byte range: two scalar loads at wave-uniform indices (the
   // stream's addresses wait for the scalar cache, not for the vector load)
-  const uint64_t first = off[i0], tend = off[i0 + m];
+  const uint64_t first = off[i0] + bsh, tend = off[i0 + m] + bsh;
   // segment t = [x, e): e is lane t + 1's point (taken by every lane).  IPv4
   // takes it before the stream, for the header's first dword (the IHL); the
   // other operations after the stream is requested
   uint64_t e = 0;
   bool hdr = false;
-  uint32_t d0 = 0;
+  uint32_t d0 = 0, d0sh = 0;  // the dword holding header byte 0 and that byte's place in it
   if constexpr (OP == kTileIpv4) {
     e = shfl_down64(x);
     hdr = valid && e - x >= 20;
     const uint8_t* hp = hdr ? bytes + x : reinterpret_cast<const uint8_t*>(zero16);
-    d0 = *reinterpret_cast<const uint32_t*>(hp - (reinterpret_cast<uintptr_t>(hp) & 3u));
+    d0sh = uint32_t(reinterpret_cast<uintptr_t>(hp) & 3u);
+    d0 = *reinterpret_cast<const uint32_t*>(hp - d0sh);
   }
   // the windows start on the 128-byte line (of `bytes`) holding the first
   // byte, so each 1 KiB load instruction covers 8 whole lines, not 9 partial
@@ -1994,7 +2076,7 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
   auto point_b = [&](uint64_t e_) {
     uint64_t lo_ = x;
     if constexpr (OP == kTileIpv4) {
-      uint64_t o = 4u * ((d0 >> (8u * (uint32_t(x) & 3u))) & 0x0fu);
+      uint64_t o = 4u * ((d0 >> (8u * d0sh)) & 0x0fu);  // the byte in the frame of the load
       if (o < 20) o = 20;
       if (hdr && o > e_ - x) o = e_ - x;
       lo_ = hdr ? x + o : e_;
@@ -2512,14 +2594,15 @@ hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_ou
 
 // k_span: one wave per S segments, four independent waves per block
 template <int OP, int OUT>
-hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, uint32_t S, hipStream_t st) {
+hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, uint32_t S, hipStream_t st, uint32_t max_blocks) {
   if (!sp.offsets || sp.list || sp.n == 0 || S == 0 || S > kSpanSegs) return hipErrorInvalidValue;
   const uint64_t waves = (sp.n + S - 1) / S;
   const uint64_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
+  const uint64_t cap = max_blocks && max_blocks < kMaxGridBlocks ? max_blocks : kMaxGridBlocks;
   uint8_t* const bytes = const_cast<uint8_t*>(sp.bytes);
   const u32x4* const z = static_cast<const u32x4*>(sp.zero16);
-  if (blocks > kMaxGridBlocks)  // more spans than one grid: grid-stride
-    hipLaunchKernelGGL((k_span<OP, OUT, true>), dim3(uint32_t(kMaxGridBlocks)), dim3(kBlock), 0, st, bytes,
+  if (blocks > cap)  // more spans than one grid: grid-stride
+    hipLaunchKernelGGL((k_span<OP, OUT, true>), dim3(uint32_t(cap)), dim3(kBlock), 0, st, bytes,
                        sp.offsets, sp.n, S, a, g_xcd_remap, z);
   else
     hipLaunchKernelGGL((k_span<OP, OUT, false>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, bytes, sp.offsets,
@@ -2779,35 +2862,57 @@ hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t*
   return hipGetLastError();
 }
 
+hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n, int op, const uint32_t* init,
+                       uint16_t* out, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
+                       const void* zero16, const Done& done, hipStream_t st) {
+  if (n == 0 || n > kTickSegs || !bytes || !offsets) return hipErrorInvalidValue;
+  TickOffsets t{};
+  for (uint32_t j = 0; j <= n; ++j) t.o[j] = offsets[j];
+  uint8_t* const b = const_cast<uint8_t*>(bytes);
+  const uint32_t* ip = init ? init : static_cast<const uint32_t*>(zero16);
+  const uint8_t* z = static_cast<const uint8_t*>(zero16);
+  if (op == 0)
+    hipLaunchKernelGGL(k_tick<0>, dim3(1), dim3(kBlock), 0, st, b, t, n, ip, init ? 1u : 0u, out, 0, nullptr, nullptr,
+                       nullptr, z, done);
+  else if (mode >= 0 && mode <= 2)
+    hipLaunchKernelGGL(k_tick<1>, dim3(1), dim3(kBlock), 0, st, b, t, n, ip, 0u, nullptr, mode, ip_ck, tcp_ck, status,
+                       z, done);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t S, hipStream_t st) {
+                                uint32_t S, hipStream_t st, uint32_t max_blocks) {
   TileArgs a{};
   a.init = init ? init : static_cast<const uint32_t*>(sp.zero16);
   a.odd = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
   a.init_step = init ? 1u : 0u;
   a.odd_step = odd ? 1u : 0u;
   a.out = out;
-  return out_kind == 0 ? launch_span_t<kTileSum, 0>(sp, a, S, st) : launch_span_t<kTileSum, 1>(sp, a, S, st);
+  return out_kind == 0 ? launch_span_t<kTileSum, 0>(sp, a, S, st, max_blocks)
+                       : launch_span_t<kTileSum, 1>(sp, a, S, st, max_blocks);
 }
 
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                            uint32_t S, hipStream_t st) {
+                            uint32_t S, hipStream_t st, uint32_t max_blocks) {
   TileArgs a{};
   a.mode = mode;
   a.ip_ck = ip_ck;
   a.tcp_ck = tcp_ck;
   a.status = status;
-  return launch_span_t<kTileIpv4, 0>(sp, a, S, st);
+  return launch_span_t<kTileIpv4, 0>(sp, a, S, st, max_blocks);
 }
 
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t S, hipStream_t st) {
+                            uint16_t* tcp_ck, uint32_t S, hipStream_t st, uint32_t max_blocks) {
   TileArgs a{};
   a.msgs = msgs;
   a.hdr_out = hdr_out;
   a.ip_ck = ip_ck;
   a.tcp_ck = tcp_ck;
-  return hdr_out ? launch_span_t<kTileWrapApart, 0>(sp, a, S, st) : launch_span_t<kTileWrap, 0>(sp, a, S, st);
+  return hdr_out ? launch_span_t<kTileWrapApart, 0>(sp, a, S, st, max_blocks)
+                 : launch_span_t<kTileWrap, 0>(sp, a, S, st, max_blocks);
 }
 
 uint64_t batchv_blocks(int cls, uint64_t n) {

@@ -183,10 +183,26 @@ hipError_t launch_router_hdrs(const SegSpec& sp, uint32_t* hdr_out, uint8_t* sta
 // consecutive segments, the span's bytes streamed whole in 4 KiB windows
 // whatever the lengths.  Checksum (out_kind as launch_checksum), the fused IPv4/TCP kernel
 // (mode as launch_ipv4_tcp) and the in-place wrap (as launch_tcp_wrap in place).
+// max_blocks (test hook ICSUM_FORCE span_blocks; 0: none): a grid of more
+// blocks runs the grid-stride instantiation with that many, as batches of
+// more spans than 2^24 blocks hold do
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t S, hipStream_t st);
+                                uint32_t S, hipStream_t st, uint32_t max_blocks = 0);
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                            uint32_t S, hipStream_t st);
+                            uint32_t S, hipStream_t st, uint32_t max_blocks = 0);
+
+// Per-tick zero-copy host calls (k_tick): at most kTickSegs segments of an
+// offsets batch in one block, the n + 1 offsets (relative to `bytes`) copied
+// into the kernel arguments; op 0 checksum (u16 out, init nullable), op 1 the
+// fused IPv4/TCP kernel (mode, the three outputs nullable).  `done` as the
+// zero-copy launches take it.
+constexpr uint32_t kTickSegs = 16;
+struct TickOffsets {
+  uint64_t o[kTickSegs + 1];
+};
+hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n, int op, const uint32_t* init,
+                       uint16_t* out, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
+                       const void* zero16, const Done& done, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg
 // (include/icsum.h), 28 bytes.
@@ -209,7 +225,7 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
 // the wrap as a tile launch: in place (hdr_out null) or, with hdr_out, the
 // payload-only batch of ics_tcp_wrap_headers with its headers to hdr_out
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t S, hipStream_t st);
+                            uint16_t* tcp_ck, uint32_t S, hipStream_t st, uint32_t max_blocks = 0);
 // pass 2 of the two-pass wrap alone (k_tcp_hdr): headers from the records and
 // the payload sums pass 1 left in `sums` (roles from each payload's start)
 hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t* sums, uint32_t* hdr_out,

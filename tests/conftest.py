@@ -33,7 +33,7 @@ def engine_with(force=None, debug=False):
     """Generator: an Engine created with the ICSUM_FORCE test hook set to
     `force` ({key: value}: lps, unroll, mode, segs, bin, bin_min, bin_plan,
     bin_blocks, last_bin_lps, last_bin_blocks, dense_segs, twoclass,
-    wrap_passes, xcd_remap, zero_copy_max, tile,
+    wrap_passes, xcd_remap, zero_copy_max, tile, span_segs, span_blocks,
     poison_ticket — INTEGRATION.md §6), read once at
     ics_create."""
     import torch

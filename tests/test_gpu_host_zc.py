@@ -214,7 +214,9 @@ def test_poisoned_ticket_fails_once_then_recovers(orc):
     staging exists) never has a block draw the last ticket, so the call's
     completion word stays unwritten: that call fails with ICS_ERR_HIP, and
     wait_flag zeroes the slot's ticket before returning — the next call on
-    the same context and slot is exact, and so are the ones after it."""
+    the same context and slot is exact, and so are the ones after it.  A
+    one-block launch (up to 16 MTU datagrams) draws no ticket: it succeeds on
+    the poisoned slot and leaves the poison for the first multi-block call."""
     from conftest import engine_with
     from tcpip_network_protocol_stack_amd._lib import IcsumError
 
@@ -224,13 +226,16 @@ def test_poisoned_ticket_fails_once_then_recovers(orc):
     init = rng.integers(0, 1 << 32, n, dtype=np.uint32)
     want = orc.checksum_batch(buf, n, stride=L, seg_len=L, init=init)
     for eng in engine_with({"zero_copy_max": str(1 << 30), "poison_ticket": str(1 << 30)}):
+        # 8 datagrams: one block, no ticket drawn — exact, the poison stays
+        got = eng.checksum_batch_host(buf[:8 * L], 8, stride=L, seg_len=L, init=init[:8])
+        assert (got == want[:8]).all()
         with pytest.raises(IcsumError) as e:
             eng.checksum_batch_host(buf, n, stride=L, seg_len=L, init=init)
         assert "icsum error -2" in str(e.value) and "completion word was not written" in str(e.value)
         for _ in range(3):  # recovered: slot 0 counts from zero again
             got = eng.checksum_batch_host(buf, n, stride=L, seg_len=L, init=init)
             assert (got == want).all()
-        assert eng.dispatch_info()["host_zero_copy"] == 4
+        assert eng.dispatch_info()["host_zero_copy"] == 5
 
 
 @pytest.mark.parametrize("pinned", [False, True])
@@ -270,3 +275,48 @@ def test_error_after_chunks_in_flight_drains_slots(orc, pinned):
         assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all()
     finally:
         next(gen, None)
+
+
+@pytest.fixture(scope="module", params=["auto", "0"], ids=["tick", "no_tick"])
+def tick_eng(request):
+    from conftest import engine_with
+
+    yield from engine_with(None if request.param == "auto" else {"tick_inline": request.param})
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("base", [0, 1, 14])
+def test_tick_offsets_in_kernel_arguments(tick_eng, orc, pinned, base):
+    """A zero-copy tick of <= 16 offsets segments runs k_tick, its offsets in
+    the kernel arguments (no dependent PCIe read of them): checksum with and
+    without inits and the fused IPv4 kernel in every mode, 1..16 segments of
+    every header shape and of up to 5000 bytes (more than one 16 x 8 pass),
+    at an unaligned address; 17 segments take the grid launches.  With
+    tick_inline=0 the same calls take the per-segment kernels.  Every result
+    equals the oracle's."""
+    import torch
+
+    from test_gpu_parity import _random_datagrams
+
+    rng = np.random.default_rng(0x71C + base + 7 * pinned)
+    want_tick = not tick_eng.forced
+    for n in (1, 2, 5, 16, 17):
+        segs = _random_datagrams(rng, n)
+        segs[0] = segs[0] + rng.integers(0, 256, 3500, dtype=np.uint8).tobytes()  # a long one
+        buf, off = pack_contiguous(segs, int(rng.integers(0, 16)))
+        alloc = torch.empty(buf.size + base, dtype=torch.uint8, pin_memory=pinned).numpy()
+        h = alloc[base:]
+        h[:] = buf
+        init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        for ini in (init, None):
+            got = tick_eng.checksum_batch_host(h, n, offsets=off, init=ini)
+            assert (got == orc.checksum_batch(buf, n, offsets=off, init=ini)).all(), (n, base)
+            assert (tick_eng.dispatch_info()["kernel"] == "tick") == (want_tick and n <= 16), n
+        for mode in (0, 1, 2):
+            h[:] = buf
+            hb = buf.copy()
+            w = orc.ipv4_tcp_batch(hb, n, mode, offsets=off)
+            ip, tcp, st = tick_eng.ipv4_tcp_batch_host(h, n, mode, offsets=off)
+            assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), (n, mode, base)
+            assert (h == hb).all(), (n, mode, base)
+            assert (tick_eng.dispatch_info()["kernel"] == "tick") == (want_tick and n <= 16), (n, mode)

@@ -3,7 +3,8 @@ consecutive segments, the span's bytes streamed whole in 4 KiB windows, each
 segment's sums = F(hi) - F(lo) of the running prefix), forced on every
 offsets batch with the `tile` test hook — short last spans, one-segment
 batches, spans of empty segments, offsets past 2^31 and 2^32 (config 4 at
-full size) and more spans than one grid holds (grid-stride): checksum (u16,
+full size) and the grid-stride form that more spans than one grid holds take
+(reached with a capped grid, the span_blocks hook): checksum (u16,
 raw u32 sums with carried parity), the fused IPv4/TCP kernel in all three
 modes (PATCH's in-place stores racing a neighbouring span's boundary chunk:
 every F of a span comes from one copy of each window, so those bytes cancel),
@@ -21,8 +22,13 @@ from test_gpu_twoclass import _check, _sentinel
 pytestmark = pytest.mark.gpu
 
 # the tile launch (k_span) on every offsets batch: 63 segments per wave (or
-# the plan's span size), one, and an odd size that leaves short last spans
-TILE_FORCE = [{"tile": 1}, {"tile": 1, "span_segs": 1}, {"tile": 1, "span_segs": 7}]
+# the plan's span size), one, and an odd size that leaves short last spans;
+# then the grid-stride instantiation (k_span<..., STRIDE=true>, which a batch
+# of more spans than 2^24 blocks hold takes) with the grid capped to a few
+# blocks by the span_blocks hook, so each wave runs many spans in turn and
+# reuses its LDS windows and register sets across them
+TILE_FORCE = [{"tile": 1}, {"tile": 1, "span_segs": 1}, {"tile": 1, "span_segs": 7},
+              {"tile": 1, "span_segs": 1, "span_blocks": 3}, {"tile": 1, "span_segs": 7, "span_blocks": 5}]
 
 
 @pytest.fixture(scope="module", params=TILE_FORCE, ids=force_id)

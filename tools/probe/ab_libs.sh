@@ -4,6 +4,7 @@
 set -e
 L=tcpip_network_protocol_stack_amd/libicsum.so
 cp $L /tmp/libicsum_keep.so
+trap 'cp /tmp/libicsum_keep.so $L' EXIT  # the in-tree build back whatever happens
 rows=$1; rounds=$2; shift 2
 for r in $(seq 1 $rounds); do
   for v in "$@"; do
@@ -11,4 +12,3 @@ for r in $(seq 1 $rounds); do
     timeout -k 10 200 python tools/bench_configs.py --only $rows | sed "s|^{|{\"lib\": \"$(basename $v)\", |"
   done
 done
-cp /tmp/libicsum_keep.so $L

@@ -6,8 +6,10 @@
 // libicsum.so side by side (dlopen, RTLD_LOCAL) and times them interleaved on
 // the same buffers; every build's outputs must equal the first's.
 //   g++ -O2 -std=c++17 -I../../include tick_latency.cpp -o tick_latency -ldl
-//   tick_latency libA.so [libB.so ...]
-// Environment: TICK_OPS (comma list of verify, verify_off, checksum, wrap;
+//   tick_latency libA.so[@FORCE] [libB.so[@FORCE] ...]
+// (@FORCE: that context is created with ICSUM_FORCE=FORCE, e.g.
+// lib.so@tick_inline=0 — one build, two dispatch choices, one process)
+// Environment: TICK_OPS (comma list of verify, verify_off, checksum, checksum_off, wrap;
 // default all), TICK_SIZES (comma list of batch sizes, default 1..8192),
 // TICK_MEM (pinned | pageable, default both), TICK_CALLS (timed calls per
 // round, default 200).  Checksum calls pass per-segment inits (the NS
@@ -51,12 +53,15 @@ void sym(void* h, const char* name, F& f) {
   }
 }
 
-Lib open_lib(const char* path) {
+Lib open_lib(const char* arg) {
   Lib l;
-  l.path = path;
-  void* h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+  l.path = arg;
+  const std::string a(arg);
+  const size_t at = a.find('@');
+  const std::string path = a.substr(0, at);
+  void* h = dlopen(path.c_str(), RTLD_NOW | RTLD_LOCAL);
   if (!h) {
-    fprintf(stderr, "dlopen %s: %s\n", path, dlerror());
+    fprintf(stderr, "dlopen %s: %s\n", path.c_str(), dlerror());
     exit(1);
   }
   sym(h, "ics_create", l.create);
@@ -66,7 +71,10 @@ Lib open_lib(const char* path) {
   sym(h, "ics_ipv4_tcp_batch_host", l.ipv4_host);
   sym(h, "ics_tcp_wrap_batch_host", l.wrap_host);
   sym(h, "ics_last_error", l.last_error);
-  if (l.create(0, &l.ctx) != ICS_OK) {
+  if (at != std::string::npos) setenv("ICSUM_FORCE", a.substr(at + 1).c_str(), 1);
+  const int rc = l.create(0, &l.ctx);
+  unsetenv("ICSUM_FORCE");
+  if (rc != ICS_OK) {
     fprintf(stderr, "ics_create: %s\n", l.last_error());
     exit(1);
   }
@@ -125,7 +133,7 @@ int main(int argc, char** argv) {
   const char* mem_only = getenv("TICK_MEM");
   std::vector<uint32_t> inits(kMaxN);
   for (auto& v : inits) v = uint32_t(rng());
-  const char* ops[] = {"verify", "verify_off", "checksum", "wrap"};
+  const char* ops[] = {"verify", "verify_off", "checksum", "checksum_off", "wrap"};
   const char* only = getenv("TICK_OPS");  // comma list of ops to run (default: all)
   std::vector<uint64_t> offs(kMaxN + 1);
   for (uint64_t i = 0; i <= kMaxN; ++i) offs[i] = i * kL;
@@ -150,6 +158,8 @@ int main(int argc, char** argv) {
                 check(l, l.ipv4_host(l.ctx, src, offs.data(), 0, 0, n, ICS_MODE_VERIFY, a, b, st));
               else if (op[0] == 'v')
                 check(l, l.ipv4_host(l.ctx, src, nullptr, kL, kL, n, ICS_MODE_VERIFY, a, b, st));
+              else if (!strcmp(op, "checksum_off"))
+                check(l, l.checksum_host(l.ctx, src, offs.data(), 0, 0, inits.data(), a, n));
               else if (op[0] == 'c')
                 check(l, l.checksum_host(l.ctx, src, nullptr, kL, kL, inits.data(), a, n));
               else
