@@ -33,7 +33,10 @@ Pinned host_pinned(const void* p) {
 int ensure_staging(ics_ctx* ctx) {
   if (ctx->staged) return ICS_OK;
   for (int k = 0; k < ctx->nslots; ++k) {
-    ICS_HIP(hipStreamCreateWithFlags(&ctx->st[k], hipStreamNonBlocking));
+    if (ctx->slot_prio)
+      ICS_HIP(hipStreamCreateWithPriority(&ctx->st[k], hipStreamNonBlocking, ctx->slot_prio));
+    else
+      ICS_HIP(hipStreamCreateWithFlags(&ctx->st[k], hipStreamNonBlocking));
     ICS_HIP(hipEventCreateWithFlags(&ctx->ev[k], hipEventDisableTiming));
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_in[k]), ctx->slot_bytes, 0));
     ICS_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->d_in[k]), ctx->slot_bytes));

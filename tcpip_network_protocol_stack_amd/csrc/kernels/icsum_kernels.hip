@@ -1507,22 +1507,23 @@ __global__ __launch_bounds__(kBlock) void k_tick(uint8_t* __restrict__ bytes, Ti
   const uint32_t g = threadIdx.x >> 4, lane = threadIdx.x & 15u;
   const uint32_t bsh = frame_shift(bytes);
   bytes -= bsh;
-  const bool valid = g < n;
-  const uint32_t gi = valid ? g : n - 1;  // n >= 1: idle groups read segment n - 1's bounds
   // the wave's four groups' five bounds by scalar loads at a wave-uniform
-  // index (all in flight at once), then each group picks its pair
+  // index, in the kernel's first batch of argument loads (nothing they
+  // depend on is loaded: the array is zero past n, an idle group's segment
+  // is empty), then each group picks its pair
   const uint32_t w4 = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6) * 4u;
   uint64_t o[5];
 #pragma unroll
   for (uint32_t k = 0; k < 5; ++k) o[k] = t.o[w4 + k];
-  const uint32_t q = gi - w4;  // 0..3 in a wave holding a segment (idle groups: segment n - 1's)
+  const uint32_t q = g & 3u;
   uint64_t s = o[0], e = o[1];
 #pragma unroll
   for (uint32_t k = 1; k < 4; ++k)
     if (q == k) s = o[k], e = o[k + 1];
-  if (w4 >= n) s = e = 0;  // a wave past the last segment (uniform): an empty one, never stored
+  const bool valid = g < n;
   s += bsh;
   e = valid ? e + bsh : s;
+  const uint32_t gi = valid ? g : 0u;
   if constexpr (OP == 0) {
     const uint32_t i0 = init[gi * init_step];
     uint32_t ev = 0, od = 0;

@@ -138,46 +138,71 @@ int main(int argc, char** argv) {
   std::vector<uint64_t> offs(kMaxN + 1);
   for (uint64_t i = 0; i <= kMaxN; ++i) offs[i] = i * kL;
   const int rounds = 5, calls = getenv("TICK_CALLS") ? std::max(10, atoi(getenv("TICK_CALLS"))) : 200;
-  for (const char* op : ops)
-    for (int mem = 0; mem < 2; ++mem) {
-      if (only && !strstr(only, op)) continue;
-      if (mem_only && strcmp(mem_only, mem ? "pinned" : "pageable")) continue;
-      for (uint64_t n : sizes) {
-        uint8_t* src = mem ? pinned : pageable.data();
-        std::vector<std::vector<double>> t(libs.size());
-        std::vector<std::vector<uint8_t>> res(libs.size(), std::vector<uint8_t>(n * kL + n * 5));
-        for (int r = 0; r < rounds; ++r)
-          for (size_t k = 0; k < libs.size(); ++k) {
-            const Lib& l = libs[k];
-            uint16_t* a = reinterpret_cast<uint16_t*>(res[k].data());
+  // every (build, op) pair of a size and memory kind is timed interleaved call
+  // by call, the first pair rotating per call: each pair's calls follow every
+  // other pair's equally often (blocks of calls per build or per op measured
+  // ~1 us position biases on identical code)
+  struct Var {
+    size_t k;
+    const char* op;
+  };
+  for (int mem = 0; mem < 2; ++mem) {
+    if (mem_only && strcmp(mem_only, mem ? "pinned" : "pageable")) continue;
+    for (uint64_t n : sizes) {
+      uint8_t* src = mem ? pinned : pageable.data();
+      std::vector<Var> vars;
+      for (const char* op : ops)
+        if (!only || strstr(only, op))
+          for (size_t k = 0; k < libs.size(); ++k) vars.push_back({k, op});
+      if (only) {  // exact names only ("verify" must not select "verify_off")
+        std::vector<Var> keep;
+        for (const Var& v : vars) {
+          const size_t len = strlen(v.op);
+          for (const char* p = strstr(only, v.op); p; p = strstr(p + 1, v.op))
+            if ((p == only || p[-1] == ',') && (p[len] == ',' || p[len] == 0)) {
+              keep.push_back(v);
+              break;
+            }
+        }
+        vars.swap(keep);
+      }
+      std::vector<std::vector<double>> t(vars.size());
+      std::vector<std::vector<uint8_t>> res(vars.size(), std::vector<uint8_t>(n * kL + n * 5));
+      for (int r = 0; r < rounds; ++r)
+        for (int c = 0; c < calls + 10; ++c)
+          for (size_t jj = 0; jj < vars.size(); ++jj) {
+            const size_t j = (jj + size_t(c)) % vars.size();
+            const Lib& l = libs[vars[j].k];
+            const char* op = vars[j].op;
+            uint16_t* a = reinterpret_cast<uint16_t*>(res[j].data());
             uint16_t* b = a + n;
             uint8_t* st = reinterpret_cast<uint8_t*>(b + n);
-            for (int c = 0; c < calls + 10; ++c) {
-              const auto t0 = clk::now();
-              if (!strcmp(op, "verify_off"))
-                check(l, l.ipv4_host(l.ctx, src, offs.data(), 0, 0, n, ICS_MODE_VERIFY, a, b, st));
-              else if (op[0] == 'v')
-                check(l, l.ipv4_host(l.ctx, src, nullptr, kL, kL, n, ICS_MODE_VERIFY, a, b, st));
-              else if (!strcmp(op, "checksum_off"))
-                check(l, l.checksum_host(l.ctx, src, offs.data(), 0, 0, inits.data(), a, n));
-              else if (op[0] == 'c')
-                check(l, l.checksum_host(l.ctx, src, nullptr, kL, kL, inits.data(), a, n));
-              else
-                check(l, l.wrap_host(l.ctx, src, nullptr, kL, kL, n, msgs.data()));
-              if (c >= 10) t[k].push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
-            }
-            if (op[0] == 'w') memcpy(res[k].data() + n * 5, src, n * kL);  // the wrapped wire bytes
+            const auto t0 = clk::now();
+            if (!strcmp(op, "verify_off"))
+              check(l, l.ipv4_host(l.ctx, src, offs.data(), 0, 0, n, ICS_MODE_VERIFY, a, b, st));
+            else if (op[0] == 'v')
+              check(l, l.ipv4_host(l.ctx, src, nullptr, kL, kL, n, ICS_MODE_VERIFY, a, b, st));
+            else if (!strcmp(op, "checksum_off"))
+              check(l, l.checksum_host(l.ctx, src, offs.data(), 0, 0, inits.data(), a, n));
+            else if (op[0] == 'c')
+              check(l, l.checksum_host(l.ctx, src, nullptr, kL, kL, inits.data(), a, n));
+            else
+              check(l, l.wrap_host(l.ctx, src, nullptr, kL, kL, n, msgs.data()));
+            if (c >= 10) t[j].push_back(std::chrono::duration<double, std::micro>(clk::now() - t0).count());
+            if (op[0] == 'w') memcpy(res[j].data() + n * 5, src, n * kL);  // the wrapped wire bytes
           }
-        for (size_t k = 0; k < libs.size(); ++k) {
-          const bool same = res[k] == res[0];
-          printf("{\"op\": \"%s\", \"mem\": \"%s\", \"n\": %llu, \"bytes\": %llu, \"lib\": \"%s\", \"p10_us\": %.2f, "
-                 "\"p50_us\": %.2f, \"p90_us\": %.2f, \"same_as_first\": %s}\n",
-                 op, mem ? "pinned" : "pageable", (unsigned long long)n, (unsigned long long)(n * kL),
-                 libs[k].path.c_str(), pct(t[k], 0.1), pct(t[k], 0.5), pct(t[k], 0.9), same ? "true" : "false");
-          fflush(stdout);
-        }
+      for (size_t j = 0; j < vars.size(); ++j) {
+        size_t first = j;  // the same op's first build
+        while (first > 0 && !strcmp(vars[first - 1].op, vars[j].op)) --first;
+        const bool same = res[j] == res[first];
+        printf("{\"op\": \"%s\", \"mem\": \"%s\", \"n\": %llu, \"bytes\": %llu, \"lib\": \"%s\", \"p10_us\": %.2f, "
+               "\"p50_us\": %.2f, \"p90_us\": %.2f, \"same_as_first\": %s}\n",
+               vars[j].op, mem ? "pinned" : "pageable", (unsigned long long)n, (unsigned long long)(n * kL),
+               libs[vars[j].k].path.c_str(), pct(t[j], 0.1), pct(t[j], 0.5), pct(t[j], 0.9), same ? "true" : "false");
+        fflush(stdout);
       }
     }
+  }
   for (auto& l : libs) l.destroy(l.ctx);
   return 0;
 }
