@@ -81,9 +81,6 @@ VARIANTS = {
     "span": {"tile": 1},         # the tile launch, k_span (span size: the plan's, or 63)
     "per_segment": {"tile": 0},  # the per-segment / two-class launches
     **{f"S{k}": {"tile": 1, "span_segs": k} for k in range(1, 64)},
-    "piece": {"tile": 1, "tile_piece": 1},  # the tile launch as one-shot pieces (k_piece, round 6)
-    **{f"P{k}": {"tile": 1, "tile_piece": 1, "piece_bytes": k} for k in (1024, 2048, 3072, 4096, 6144, 8192, 12288)},
-    **{f"K12P{k}": {"tile": 1, "tile_piece": 1, "piece_k": 12, "piece_bytes": k} for k in (8192, 12288, 16384, 20480)},
 }
 
 
