@@ -1,10 +1,10 @@
 #!/bin/bash
-# Driver-equivalent check on the round-5 code: GPU tests, smoke, bench N=1
+# Driver-equivalent check on the round-6 code: GPU tests, smoke, bench N=1
 # (PMC, CPU baseline, host-inclusive) and its rocprof kernel stats, the
 # one-card N=2 rehearsal, then the bench_configs rows.
 set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
-O=gpurun_out/${1:-r5full}; mkdir -p $O
+O=gpurun_out/${1:-r6full}; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 240 --timeout-method thread -p no:cacheprovider > $O/pytest.log 2>&1
 timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1
 timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err
