@@ -345,15 +345,18 @@ def host_inclusive(eng, data, init, out, n, seg, passes=3, calls=300):
             "GB_s": round(n * seg * passes / el / 1e9, 2), "outputs_equal_device": same,
             "tick_p50": tick, "tick_note": f"{seg}-byte segments, {calls} ctypes calls, preallocated outputs, buffer addresses taken once",
             "tick_p50_cpp": tick_cpp_guarded(calls),
+            "tick_p50_cpp_server": tick_cpp_guarded(calls, "tick_server=20000"),
             "tick_cpp_note": "the same calls from C++ (tools/probe/tick_latency, dlopen of the in-tree libicsum.so, "
-                             "1500-byte segments with inits, page-locked), no interpreter in the loop"}
+                             "1500-byte segments with inits, page-locked), no interpreter in the loop; _server: "
+                             "with the resident tick server (ics_set_tick_server, 20 ms idle), no launch per call"}
 
 
-def tick_cpp(calls):
+def tick_cpp(calls, force=None):
     """p50 of per-tick ics_checksum_batch_host calls timed in C++ (a child
-    process: the interpreter's ctypes overhead is not in these numbers)"""
+    process: the interpreter's ctypes overhead is not in these numbers);
+    force: the context's ICSUM_FORCE (e.g. the resident tick server)"""
     exe = os.path.join(ROOT, "tools", "probe", "tick_latency")
-    lib = os.path.join(ROOT, "tcpip_network_protocol_stack_amd", "libicsum.so")
+    lib = os.path.join(ROOT, "tcpip_network_protocol_stack_amd", "libicsum.so") + (f"@{force}" if force else "")
     if not os.path.exists(exe):
         return None
     env = dict(os.environ, TICK_OPS="checksum", TICK_SIZES="1,16", TICK_MEM="pinned", TICK_CALLS=str(calls))
@@ -367,11 +370,11 @@ def tick_cpp(calls):
     return out
 
 
-def tick_cpp_guarded(calls):
+def tick_cpp_guarded(calls, force=None):
     """tick_cpp, reported and never fatal (like pmc_traffic): a failure of
     this secondary figure must not cost the line its headline"""
     try:
-        return tick_cpp(calls)
+        return tick_cpp(calls, force)
     except Exception as e:
         return {"error": f"{type(e).__name__}: {str(e)[-200:]}"}
 

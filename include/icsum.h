@@ -278,6 +278,17 @@ int ics_tcp_wrap_batch_host(ics_ctx* ctx, void* h_dgrams, const uint64_t* h_offs
 int ics_tcp_wrap_headers_host(ics_ctx* ctx, const void* h_payloads, const uint64_t* h_offsets, uint64_t stride,
                               uint64_t payload_len, uint64_t n, const ics_tcp_msg* h_msgs, void* h_hdrs);
 
+/* Resident tick server (not a reference interface).  idle_us > 0: the
+ * zero-copy *_host calls of at most 16 segments (checksum, fused IPv4 in any
+ * mode; fixed stride or offsets) are taken by a one-block kernel that stays
+ * resident on the context's GPU between calls and reads each call's job from
+ * a mailbox in page-locked memory — no kernel launch per call.  It leaves
+ * after idle_us microseconds without a call (the next call launches it
+ * again) or on ics_set_tick_server(ctx, 0) / ics_destroy.  While it is
+ * resident the device is busy: hipDeviceSynchronize waits until it leaves.
+ * Results are identical to the launched path.  0 (default): off. */
+int ics_set_tick_server(ics_ctx* ctx, uint32_t idle_us);
+
 /* ---- device memory helpers for FFI callers without an allocator -------- */
 int ics_malloc(ics_ctx* ctx, void** d_ptr, size_t bytes);
 int ics_free(ics_ctx* ctx, void* d_ptr);
@@ -309,6 +320,7 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
 #define ICS_K_TILE 13            /* k_span: an offsets batch as one packed stream, S (1..63) segments per wave */
 #define ICS_K_ROUTER_HDRS 14     /* k_router_hdrs: the router step, forwarded headers apart */
 #define ICS_K_TICK 15            /* k_tick: a zero-copy *_host tick of <= 16 offsets segments, offsets in the kernel arguments */
+#define ICS_K_TICK_SERVER 16     /* the resident tick server took the tick (ics_set_tick_server) */
 /* last_lps / last_unroll by kernel:
  *   ICS_K_CHECKSUM .. ICS_K_WRAP_2PASS  lanes per segment / loads in flight per lane
  *   ICS_K_TWOCLASS, ICS_K_IPV4_TWOCLASS  long-segment lanes (16) / segments per wave (16 or 32; 8 only under ICSUM_FORCE twoclass=8)
@@ -317,7 +329,7 @@ int ics_stream_synchronize(ics_ctx* ctx, void* stream);
  *                 call, clamp(20 KiB / mean segment length, 1, 63) from the
  *                 cached plan (ICSUM_FORCE span_segs pins it)
  *   ICS_K_ROUTER, ICS_K_ROUTER_HDRS  0 / 0
- *   ICS_K_TICK    16 / 8 (a 16-lane group per segment, one block) */
+ *   ICS_K_TICK, ICS_K_TICK_SERVER  16 / 8 (a 16-lane group per segment, one block) */
 #define ICS_BV_DENSE64 0 /* fixed stride == length == 64 B, 16-byte aligned */
 #define ICS_BV_TINY 1    /* one lane per segment (ACK-sized fixed lengths) */
 #define ICS_BV_SMALL 2   /* 4-lane groups, two segments in flight */

@@ -59,7 +59,7 @@ class DgramBatch(ctypes.Structure):
 # ICS_K_* kernel ids of ics_dispatch_info_t.last_kernel
 KERNELS = {1: "checksum", 2: "small", 3: "tiny", 4: "dense", 5: "twoclass", 6: "binned", 7: "ipv4",
            8: "ipv4_twoclass", 9: "wrap", 10: "wrap_2pass", 11: "router", 12: "batchv", 13: "tile",
-           14: "router_hdrs", 15: "tick"}
+           14: "router_hdrs", 15: "tick", 16: "tick_server"}
 
 _p = ctypes.c_void_p
 _u64 = ctypes.c_uint64
@@ -78,6 +78,7 @@ SIGNATURES = {
     "ics_checksum_batch": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _u64, _p]),
     "ics_sum_batch": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _p, _u64, _p]),
     "ics_set_binning": (_int, [_p, _int]),
+    "ics_set_tick_server": (_int, [_p, ctypes.c_uint32]),
     "ics_fold_batch": (_int, [_p, _p, _p, _u64, _p]),
     "ics_ipv4_tcp_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p, _p]),
     "ics_router_ttl_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p]),

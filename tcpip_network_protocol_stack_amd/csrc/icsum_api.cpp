@@ -191,6 +191,15 @@ int ics_set_binning(ics_ctx* ctx, int mode) {
   return ICS_OK;
 }
 
+int ics_set_tick_server(ics_ctx* ctx, uint32_t idle_us) {
+  if (int rc = bind(ctx)) return rc;
+  if (idle_us > 10000000u) return fail(ICS_ERR_INVALID, "tick server idle time %u us above 10 s", idle_us);
+  std::lock_guard<std::mutex> lock(ctx->mu);  // the *_host calls' lock: no job in flight
+  const int rc = icsum::detail::server_stop(ctx);  // a running server keeps its old idle time: restart it
+  ctx->srv_idle_us = idle_us;
+  return rc;
+}
+
 int ics_fold_batch(ics_ctx* ctx, const uint32_t* d_sum, uint16_t* d_out, uint64_t n, void* stream) {
   if (int rc = bind(ctx)) return rc;
   if (n == 0) return ICS_OK;

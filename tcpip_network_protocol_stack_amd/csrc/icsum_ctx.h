@@ -211,6 +211,16 @@ struct ics_ctx {
   // ICSUM_COPY_THREADS, default min(8, hardware threads))
   size_t copy_threads = 8;
   std::unique_ptr<icsum::detail::WorkerPool> copy_pool;
+  // resident tick server (ics_set_tick_server; icsum_host.cpp): zero-copy
+  // ticks of <= kTickSegs segments go to a kernel that stays resident
+  // between ticks and takes them from a mailbox in coherent page-locked
+  // memory — no launch per tick.  srv_idle_us 0: off.
+  uint32_t srv_idle_us = 0;
+  icsum::TickMailbox* h_mb = nullptr;
+  hipStream_t st_srv = nullptr;
+  uint32_t srv_seq = 0;       // the last job posted
+  bool srv_launched = false;  // a server was launched (its `state` word says whether it still runs)
+  uint64_t n_srv_jobs = 0, n_srv_launches = 0;
 };
 
 namespace icsum::detail {
@@ -302,5 +312,7 @@ int host_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offse
                   uint8_t* out_c, const ics_tcp_msg* h_msgs = nullptr);
 // Release the pipeline's staging slots (ics_destroy).
 void free_staging(ics_ctx* ctx);
+// the resident tick server: quit word, wait for the kernel to leave (ICS_OK when none runs)
+int server_stop(ics_ctx* ctx);
 
 }  // namespace icsum::detail

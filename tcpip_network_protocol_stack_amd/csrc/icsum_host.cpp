@@ -218,6 +218,11 @@ int wait_flag(ics_ctx* ctx, int k, uint64_t v) {
 }  // namespace
 
 void free_staging(ics_ctx* ctx) {
+  (void)server_stop(ctx);
+  if (ctx->st_srv) (void)hipStreamDestroy(ctx->st_srv);
+  ctx->st_srv = nullptr;
+  if (ctx->h_mb) (void)hipHostFree(ctx->h_mb);
+  ctx->h_mb = nullptr;
   for (int k = 0; k < ics_ctx::kMaxSlots; ++k) {
     if (ctx->st[k]) (void)hipStreamSynchronize(ctx->st[k]);
     if (ctx->h_in[k]) (void)hipHostFree(ctx->h_in[k]);
@@ -242,6 +247,86 @@ void free_staging(ics_ctx* ctx) {
   ctx->d_ticket = nullptr;
   ctx->staged = false;
   ctx->wrap_staged = false;
+}
+
+// ---- resident tick server (k_tick_server, icsum_launch.h TickMailbox) ----
+namespace {
+
+uint64_t mb_load(const uint64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
+void mb_store(uint64_t* p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+
+int server_launch(ics_ctx* ctx) {
+  if (!ctx->h_mb) {
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_mb), sizeof(icsum::TickMailbox), hipHostMallocCoherent));
+    std::memset(static_cast<void*>(ctx->h_mb), 0, sizeof(icsum::TickMailbox));
+    if (!host_pinned(ctx->h_mb).kernel) return fail(ICS_ERR_HIP, "tick server: mailbox not device-visible");
+    ICS_HIP(hipStreamCreateWithFlags(&ctx->st_srv, hipStreamNonBlocking));
+  }
+  mb_store(&ctx->h_mb->state, icsum::kSrvRunning);
+  const uint32_t expect = uint32_t(mb_load(&ctx->h_mb->done)) + 1u;  // the oldest job not done
+  ICS_HIP(icsum::launch_tick_server(ctx->h_mb, ctx->d_zero, expect, ctx->srv_idle_us, ctx->st_srv));
+  ctx->srv_launched = true;
+  ++ctx->n_srv_launches;
+  return ICS_OK;
+}
+
+// the job's descriptor words, each stamped with its sequence number; the
+// server takes the job once every word it uses carries that number
+int server_post(ics_ctx* ctx, int op, int mode, const void* bytes, const uint32_t* init, void* res,
+                const uint64_t* rel_off, uint64_t stride, uint64_t seg_len, uint32_t n, uint32_t* seq) {
+  if (!ctx->srv_launched || mb_load(&ctx->h_mb->state) == icsum::kSrvExited)
+    if (int rc = server_launch(ctx)) return rc;
+  const uint32_t k = ++ctx->srv_seq;
+  const uint64_t stamp = uint64_t(k) << 32;
+  uint64_t* w = ctx->h_mb->w;
+  auto put = [&](uint32_t i, uint64_t v32) { __atomic_store_n(&w[i], stamp | (v32 & 0xffffffffull), __ATOMIC_RELAXED); };
+  const uint64_t b = reinterpret_cast<uintptr_t>(bytes), ini = reinterpret_cast<uintptr_t>(init),
+                 r = reinterpret_cast<uintptr_t>(res);
+  for (uint32_t j = 0; j < n; ++j) {
+    const uint64_t s0 = rel_off ? rel_off[j] : j * stride;
+    put(icsum::kSrvHead + 2 * j, s0);
+    put(icsum::kSrvHead + 2 * j + 1, rel_off ? rel_off[j + 1] - s0 : seg_len);
+  }
+  put(1, b);
+  put(2, b >> 32);
+  put(3, ini);
+  put(4, ini >> 32);
+  put(5, r);
+  put(6, r >> 32);
+  put(0, uint64_t(op) | (uint64_t(mode) << 4) | (uint64_t(n) << 8));
+  ++ctx->n_srv_jobs;
+  *seq = k;
+  return ICS_OK;
+}
+
+// spin until the server reports job k done; a server that idled out (or hit
+// its lifetime) before taking the job is launched again, and it takes it
+int server_wait(ics_ctx* ctx, uint32_t k) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t i = 1;; ++i) {
+    if (int32_t(uint32_t(mb_load(&ctx->h_mb->done)) - k) >= 0) return ICS_OK;
+    if ((i & 255) == 0) {
+      if (mb_load(&ctx->h_mb->state) == icsum::kSrvExited)
+        if (int rc = server_launch(ctx)) return rc;
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
+        (void)server_stop(ctx);
+        ctx->srv_idle_us = 0;  // off: the calls after this one take the launches
+        return fail(ICS_ERR_HIP, "tick server: job not done within 2 s (server turned off)");
+      }
+    }
+  }
+}
+
+}  // namespace
+
+int server_stop(ics_ctx* ctx) {
+  if (!ctx->h_mb || !ctx->srv_launched) return ICS_OK;
+  mb_store(&ctx->h_mb->w[icsum::kSrvQuit], 1);
+  const hipError_t e = hipStreamSynchronize(ctx->st_srv);  // the server exits on the quit word
+  mb_store(&ctx->h_mb->w[icsum::kSrvQuit], 0);
+  ctx->srv_launched = false;
+  if (e != hipSuccess) return fail(ICS_ERR_HIP, "tick server: %s", hipGetErrorString(e));
+  return ICS_OK;
 }
 
 // kind 0: checksum batch (u16 out); kind 1: ipv4_tcp batch (ip u16, tcp u16, status u8);
@@ -274,10 +359,15 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
   Chunk pending[ics_ctx::kMaxSlots];
   bool busy[ics_ctx::kMaxSlots] = {};
   uint64_t flag_of[ics_ctx::kMaxSlots] = {};  // zero-copy chunk: its completion word's value (0: event)
+  uint32_t srv_of[ics_ctx::kMaxSlots] = {};   // a tick-server job: its sequence number (0: none)
   uint32_t piece_sum = 0;  // running sum of the long segment whose pieces are in flight
   auto retire = [&](int k) -> int {
     if (!busy[k]) return ICS_OK;
-    if (flag_of[k]) {
+    if (srv_of[k]) {
+      const uint32_t job = srv_of[k];
+      srv_of[k] = 0;
+      if (int rc = server_wait(ctx, job)) return rc;
+    } else if (flag_of[k]) {
       if (int rc = wait_flag(ctx, k, flag_of[k])) return rc;
     } else {
       ICS_HIP(hipEventSynchronize(ctx->ev[k]));
@@ -392,7 +482,21 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
     // a zero-copy tick of a few segments with offsets: the offsets travel in
     // the kernel arguments (k_tick), not as a dependent PCIe read
     const bool tick = zc && h_offsets && kind != 2 && m <= icsum::kTickSegs && ctx->tick_inline;
-    if (tick) {
+    const bool srv = zc && kind != 2 && m <= icsum::kTickSegs && ctx->srv_idle_us && (h_offsets || nb < (1u << 31));
+    if (srv) {  // the resident tick server takes it: no launch
+      const uint32_t* d_init = nullptr;
+      if (kind == 0 && h_init) {
+        std::memcpy(ctx->h_init[slot], h_init + c.i0, m * 4);
+        d_init = reinterpret_cast<const uint32_t*>(ctx->h_init[slot]);
+      }
+      const int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;  // PATCH: fields written at retire
+      uint32_t k = 0;
+      if (int rc = server_post(ctx, kind == 0 ? 0 : 1, dev_mode, in, d_init, res, h_offsets ? ctx->h_off[slot] : nullptr,
+                               stride, seg_len, uint32_t(m), &k))
+        return rc;
+      srv_of[slot] = k;
+      note_host(ctx, ICS_K_TICK_SERVER, 16, 8);
+    } else if (tick) {
       const uint32_t* d_init = nullptr;
       if (kind == 0 && h_init) {
         std::memcpy(ctx->h_init[slot], h_init + c.i0, m * 4);

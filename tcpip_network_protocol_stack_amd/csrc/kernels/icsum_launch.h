@@ -204,6 +204,30 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
                        uint16_t* out, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
                        const void* zero16, const Done& done, hipStream_t st);
 
+// Resident tick server (k_tick_server): one block that stays resident and
+// takes per-tick jobs from this mailbox in coherent page-locked host memory.
+// Descriptor word k = payload (low 32 bits) | job sequence number (high 32):
+//   w[0] = op (0 checksum, 1 fused IPv4) | mode << 4 | n << 8   (n <= kTickSegs)
+//   w[1], w[2] = the bytes' (device-visible) address, low / high half
+//   w[3], w[4] = per-segment inits (0: none; op 0)
+//   w[5], w[6] = the result area: u16 x n values (op 0) or u16 ip, u16 tcp,
+//                u8 status x n (op 1)
+//   w[kSrvHead + 2 j], w[kSrvHead + 2 j + 1] = segment j's start (relative to
+//                the bytes) and length
+// w[kSrvQuit] != 0: exit.  The device writes `done` (the last finished
+// sequence number) and, when it exits, `state` = kSrvExited.
+constexpr uint32_t kSrvHead = 7, kSrvQuit = 63;
+constexpr uint64_t kSrvRunning = 1, kSrvExited = 2;
+struct alignas(256) TickMailbox {
+  uint64_t w[64];
+  uint64_t done;
+  uint64_t state;
+  uint64_t pad[30];
+};
+static_assert(kSrvHead + 2 * kTickSegs <= kSrvQuit, "the descriptor fits below the quit word");
+hipError_t launch_tick_server(TickMailbox* mb, const void* zero16, uint32_t expect, uint32_t idle_us,
+                              hipStream_t st);
+
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg
 // (include/icsum.h), 28 bytes.
 struct TcpMsg {

@@ -72,6 +72,12 @@ class Engine:
         (ics_set_binning)."""
         self._check(self.lib.ics_set_binning(self.ctx, int(mode)))
 
+    def set_tick_server(self, idle_us):
+        """ics_set_tick_server: idle_us > 0 keeps a resident kernel that takes
+        the zero-copy *_host calls of <= 16 segments without a launch (it
+        leaves after idle_us without a call); 0 stops it."""
+        self._check(self.lib.ics_set_tick_server(self.ctx, int(idle_us)))
+
     def dispatch_info(self):
         """ics_dispatch_info: {'plan_hits', 'plan_misses', 'plan_requests',
         'kernel' (name of the last call's main launch), 'lps', 'unroll', 'plan',

@@ -320,3 +320,91 @@ def test_tick_offsets_in_kernel_arguments(tick_eng, orc, pinned, base):
             assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), (n, mode, base)
             assert (h == hb).all(), (n, mode, base)
             assert (tick_eng.dispatch_info()["kernel"] == "tick") == (want_tick and n <= 16), (n, mode)
+
+
+@pytest.fixture(scope="module")
+def srv_eng():
+    from conftest import engine_with
+
+    for eng in engine_with({"tick_server": 3000}):  # resident; leaves after 3 ms without a call
+        yield eng
+        eng.set_tick_server(0)
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+@pytest.mark.parametrize("base", [0, 3])
+def test_tick_server_vs_oracle(srv_eng, orc, pinned, base):
+    """The resident tick server (ics_set_tick_server) takes every zero-copy
+    call of <= 16 segments — checksum with and without inits, the fused IPv4
+    kernel in every mode, offsets and fixed strides, every header shape, a
+    3.5 KB segment, unaligned addresses — from its mailbox, no launch; 17
+    segments take the launches.  Every result equals the oracle's."""
+    import torch
+
+    from test_gpu_parity import _random_datagrams
+
+    rng = np.random.default_rng(0x5E7 + base + 5 * pinned)
+    for n in (1, 2, 16, 17, 3):
+        segs = _random_datagrams(rng, n)
+        segs[0] = segs[0] + rng.integers(0, 256, 3500, dtype=np.uint8).tobytes()
+        buf, off = pack_contiguous(segs, int(rng.integers(0, 16)))
+        alloc = torch.empty(buf.size + base, dtype=torch.uint8, pin_memory=pinned).numpy()
+        h = alloc[base:]
+        h[:] = buf
+        init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+        want_kernel = "tick_server" if n <= 16 else None
+        for ini in (init, None):
+            got = srv_eng.checksum_batch_host(h, n, offsets=off, init=ini)
+            assert (got == orc.checksum_batch(buf, n, offsets=off, init=ini)).all(), (n, base)
+            k = srv_eng.dispatch_info()["kernel"]
+            assert (k == "tick_server") == (want_kernel is not None), (n, k)
+        for mode in (0, 1, 2):
+            h[:] = buf
+            hb = buf.copy()
+            w = orc.ipv4_tcp_batch(hb, n, mode, offsets=off)
+            ip, tcp, st = srv_eng.ipv4_tcp_batch_host(h, n, mode, offsets=off)
+            assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), (n, mode, base)
+            assert (h == hb).all(), (n, mode, base)
+        # fixed stride (1500 B datagrams)
+        L = 1500
+        fb = np.zeros(n * L, dtype=np.uint8)
+        for i, sg in enumerate(segs):
+            fb[i * L:(i + 1) * L] = np.frombuffer((bytes(sg) + bytes(L))[:L], dtype=np.uint8)
+        fa = torch.empty(fb.size + base, dtype=torch.uint8, pin_memory=pinned).numpy()
+        fh = fa[base:]
+        for mode in (1, 2):
+            fh[:] = fb
+            hb = fb.copy()
+            w = orc.ipv4_tcp_batch(hb, n, mode, stride=L, dgram_len=L)
+            ip, tcp, st = srv_eng.ipv4_tcp_batch_host(fh, n, mode, stride=L, dgram_len=L)
+            assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), (n, mode, base, "fixed")
+            assert (fh == hb).all(), (n, mode, base, "fixed")
+
+
+def test_tick_server_idle_exit_relaunch_and_stop(orc):
+    """The server leaves after its idle time and the next call launches it
+    again (exact results across many exits); ics_set_tick_server(0) stops it
+    (calls take k_tick), turning it back on resumes the server path, and
+    ics_destroy with a resident server returns."""
+    import time
+
+    from conftest import engine_with
+
+    rng = np.random.default_rng(0x5E8)
+    segs = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in (40, 1500, 576, 1)]
+    buf, off = pack_contiguous(segs, 5)
+    want = orc.checksum_batch(buf, len(segs), offsets=off)
+    for eng in engine_with({"tick_server": 500}):  # 0.5 ms idle: it leaves between most calls below
+        for i in range(40):
+            got = eng.checksum_batch_host(buf, len(segs), offsets=off)
+            assert (got == want).all(), i
+            assert eng.dispatch_info()["kernel"] == "tick_server"
+            time.sleep(0.002 if i % 2 else 0.0)
+        eng.set_tick_server(0)
+        assert (eng.checksum_batch_host(buf, len(segs), offsets=off) == want).all()
+        assert eng.dispatch_info()["kernel"] == "tick"
+        eng.set_tick_server(100000)
+        for _ in range(5):
+            assert (eng.checksum_batch_host(buf, len(segs), offsets=off) == want).all()
+            assert eng.dispatch_info()["kernel"] == "tick_server"
+        # leave it resident: the engine's close (ics_destroy) stops it
