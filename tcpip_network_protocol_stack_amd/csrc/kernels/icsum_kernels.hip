@@ -1588,6 +1588,9 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const u
     // a resident kernel gets no launch-time cache invalidation: without this
     // system-scope acquire its loads of the reused staging slots would hit
     // the previous job's lines still held in L1 / L2
+    // (the L2 holds such lines: without it, or with the CU's L1 alone
+    // invalidated, the tests read the previous job's bytes;
+    // profiles/r6_tick_server_inv.jsonl)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
     // the job: checksum (op 0) or the fused IPv4 item (op 1, mode), n <= 16
     // segments at [bytes + s_j, + len_j), results into the page-locked area

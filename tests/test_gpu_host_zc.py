@@ -16,6 +16,7 @@ pass on stale results."""
 import numpy as np
 import pytest
 
+from conftest import force_id
 from helpers import pack_contiguous
 
 pytestmark = pytest.mark.gpu
@@ -322,11 +323,14 @@ def test_tick_offsets_in_kernel_arguments(tick_eng, orc, pinned, base):
             assert (tick_eng.dispatch_info()["kernel"] == "tick") == (want_tick and n <= 16), (n, mode)
 
 
-@pytest.fixture(scope="module")
-def srv_eng():
+SRV_FORCE = [{"tick_server": 3000}]  # resident; leaves after 3 ms without a call
+
+
+@pytest.fixture(scope="module", params=SRV_FORCE, ids=force_id)
+def srv_eng(request):
     from conftest import engine_with
 
-    for eng in engine_with({"tick_server": 3000}):  # resident; leaves after 3 ms without a call
+    for eng in engine_with(request.param):
         yield eng
         eng.set_tick_server(0)
 
