@@ -280,20 +280,25 @@ int server_post(ics_ctx* ctx, int op, int mode, const void* bytes, const uint32_
   const uint64_t stamp = uint64_t(k) << 32;
   uint64_t* w = ctx->h_mb->w;
   auto put = [&](uint32_t i, uint64_t v32) { __atomic_store_n(&w[i], stamp | (v32 & 0xffffffffull), __ATOMIC_RELAXED); };
-  const uint64_t b = reinterpret_cast<uintptr_t>(bytes), ini = reinterpret_cast<uintptr_t>(init),
+  // w[3..4]: the wrap's message records (device-visible); the checksum's
+  // inits (the caller's host array) travel as words below, never as an address
+  const uint64_t b = reinterpret_cast<uintptr_t>(bytes), ini = op == 2 ? reinterpret_cast<uintptr_t>(init) : 0,
                  r = reinterpret_cast<uintptr_t>(res);
   for (uint32_t j = 0; j < n; ++j) {
     const uint64_t s0 = rel_off ? rel_off[j] : j * stride;
     put(icsum::kSrvHead + 2 * j, s0);
     put(icsum::kSrvHead + 2 * j + 1, rel_off ? rel_off[j + 1] - s0 : seg_len);
   }
+  const bool inits = op == 0 && init;  // checksum inits: in the descriptor itself
+  if (inits)
+    for (uint32_t j = 0; j < n; ++j) put(icsum::kSrvInit + j, init[j]);
   put(1, b);
   put(2, b >> 32);
   put(3, ini);
   put(4, ini >> 32);
   put(5, r);
   put(6, r >> 32);
-  put(0, uint64_t(op) | (uint64_t(mode) << 4) | (uint64_t(n) << 8));
+  put(0, uint64_t(op) | (uint64_t(mode) << 4) | (uint64_t(n) << 8) | (uint64_t(inits) << 16));
   ++ctx->n_srv_jobs;
   *seq = k;
   return ICS_OK;
@@ -482,17 +487,22 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
     // a zero-copy tick of a few segments with offsets: the offsets travel in
     // the kernel arguments (k_tick), not as a dependent PCIe read
     const bool tick = zc && h_offsets && kind != 2 && m <= icsum::kTickSegs && ctx->tick_inline;
-    const bool srv = zc && kind != 2 && m <= icsum::kTickSegs && ctx->srv_idle_us && (h_offsets || nb < (1u << 31));
+    const bool srv = zc && m <= icsum::kTickSegs && ctx->srv_idle_us && (h_offsets || nb < (1u << 31));
     if (srv) {  // the resident tick server takes it: no launch
-      const uint32_t* d_init = nullptr;
+      const uint32_t* d_init = nullptr;  // checksum: the inits; wrap: the message records
+      void* out = res;
+      int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;  // PATCH: fields written at retire
       if (kind == 0 && h_init) {
-        std::memcpy(ctx->h_init[slot], h_init + c.i0, m * 4);
-        d_init = reinterpret_cast<const uint32_t*>(ctx->h_init[slot]);
+        d_init = h_init + c.i0;  // copied into the descriptor (server_post)
+      } else if (kind == 2) {
+        std::memcpy(ctx->h_msg[slot], h_msgs + c.i0, m * sizeof(ics_tcp_msg));
+        d_init = reinterpret_cast<const uint32_t*>(ctx->h_msg[slot]);
+        out = ctx->h_hdr[slot];
+        dev_mode = mode;  // 1: payload only (headers apart)
       }
-      const int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;  // PATCH: fields written at retire
       uint32_t k = 0;
-      if (int rc = server_post(ctx, kind == 0 ? 0 : 1, dev_mode, in, d_init, res, h_offsets ? ctx->h_off[slot] : nullptr,
-                               stride, seg_len, uint32_t(m), &k))
+      if (int rc = server_post(ctx, kind, dev_mode, in, d_init, out, h_offsets ? ctx->h_off[slot] : nullptr, stride,
+                               seg_len, uint32_t(m), &k))
         return rc;
       srv_of[slot] = k;
       note_host(ctx, ICS_K_TICK_SERVER, 16, 8);

@@ -1537,98 +1537,6 @@ __global__ __launch_bounds__(kBlock) void k_tick(uint8_t* __restrict__ bytes, Ti
   signal_done(done);
 }
 
-// ---------------------------------------------- resident tick server -----
-// A one-block kernel that stays resident between ticks and takes each tick's
-// job from a mailbox in coherent page-locked host memory (TickMailbox,
-// icsum_launch.h) instead of being launched per tick: a tick then pays no
-// launch (the ~3-5 us from the doorbell to the first wave), only the
-// mailbox poll and the payload's PCIe reads.  Every descriptor word carries
-// the job's sequence number in its high half, so one poll (wave 0: lane k
-// reads word k, lane 63 the quit word) that finds the expected number in
-// every word the job uses has read a complete descriptor, whatever order the
-// host's stores landed in.  The job runs as k_tick's body (16-lane group per
-// segment, starts / lengths from the descriptor), its results go to the
-// job's page-locked result area, and `done` takes the sequence number with a
-// system-scope release.  The server exits on the quit word, after idle_us
-// without a job, or after kSrvMaxLife of 100 MHz ticks (the host relaunches
-// it when a job finds it gone): every wave reaches an exit.
-constexpr uint64_t kSrvMaxLife = 100000000ull;  // 1 s of s_memrealtime
-
-__global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const uint8_t* __restrict__ zpad,
-                                                        uint32_t expect, uint32_t idle_us) {
-  __shared__ uint32_t s_desc[64];
-  __shared__ uint32_t s_cmd;  // 0 none yet, 1 a job, 2 exit
-  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
-  const uint32_t g = threadIdx.x >> 4, gl = threadIdx.x & 15u;
-  const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  uint64_t t_job = t0;
-  for (;;) {
-    if (wv == 0) {
-      const uint64_t word = __hip_atomic_load(&mb->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      const uint32_t pay = uint32_t(word), seq = uint32_t(word >> 32);
-      const uint32_t w0 = __builtin_amdgcn_readlane(pay, 0), s0 = __builtin_amdgcn_readlane(seq, 0);
-      const uint32_t nw = kSrvHead + 2u * ((w0 >> 8) & 0xffu);  // the words this job uses
-      const bool fresh = lane >= nw || lane == kSrvQuit || seq == expect;
-      const bool job = s0 == expect && __all(fresh);
-      const bool quit = __builtin_amdgcn_readlane(uint32_t(word | (word >> 32)), kSrvQuit) != 0;
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      const bool idle = now - t_job > uint64_t(idle_us) * 100u || now - t0 > kSrvMaxLife;
-      if (job) s_desc[lane] = pay;
-      if (lane == 0) s_cmd = quit ? 2u : job ? 1u : idle ? 2u : 0u;
-    }
-    __syncthreads();
-    const uint32_t cmd = s_cmd;
-    if (cmd == 2u) break;  // uniform
-    if (cmd == 0u) {
-      __builtin_amdgcn_s_sleep(2);
-      __syncthreads();  // wave 0 rewrites s_cmd next round
-      continue;
-    }
-    // a resident kernel gets no launch-time cache invalidation: without this
-    // system-scope acquire its loads of the reused staging slots would hit
-    // the previous job's lines still held in L1 / L2
-    // (the L2 holds such lines: without it, or with the CU's L1 alone
-    // invalidated, the tests read the previous job's bytes;
-    // profiles/r6_tick_server_inv.jsonl)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    // the job: checksum (op 0) or the fused IPv4 item (op 1, mode), n <= 16
-    // segments at [bytes + s_j, + len_j), results into the page-locked area
-    const uint32_t w0 = s_desc[0], op = w0 & 0xfu, mode = (w0 >> 4) & 0xfu, n = (w0 >> 8) & 0xffu;
-    uint8_t* bytes = reinterpret_cast<uint8_t*>(uint64_t(s_desc[1]) | (uint64_t(s_desc[2]) << 32));
-    const uint32_t* init = reinterpret_cast<const uint32_t*>(uint64_t(s_desc[3]) | (uint64_t(s_desc[4]) << 32));
-    uint8_t* res = reinterpret_cast<uint8_t*>(uint64_t(s_desc[5]) | (uint64_t(s_desc[6]) << 32));
-    const uint32_t bsh = frame_shift(bytes);
-    bytes -= bsh;
-    const bool valid = g < n;
-    const uint32_t gi = valid ? g : 0u;
-    const uint64_t s = uint64_t(s_desc[kSrvHead + 2u * gi]) + bsh;
-    const uint64_t e = valid ? s + s_desc[kSrvHead + 2u * gi + 1u] : s;
-    if (op == 0u) {
-      const uint32_t i0 = init ? init[gi] : 0u;
-      uint32_t ev = 0, od = 0;
-      seg_sums<16, 8, true, 3>(bytes, s, e, gl, ev, od);
-      const uint32_t tot = group_sum<16>(combine_roles(ev, od, uint32_t(s) & 1u));
-      if (valid && gl == 15) reinterpret_cast<uint16_t*>(res)[g] = uint16_t(fold_value(i0 + tot));
-    } else {
-      uint16_t* ip = reinterpret_cast<uint16_t*>(res);
-      ipv4_item<16, 8, true, 3>(bytes, s, e, g, valid, gl, int(mode), ip, ip + n, res + 4u * n, zpad, zlast);
-    }
-    // results out before `done` (signal_done's order): every wave's stores
-    // retired, the block's barrier, one system-scope release
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      __hip_atomic_store(&mb->done, uint64_t(expect), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    ++expect;
-    t_job = __builtin_amdgcn_s_memrealtime();
-    __syncthreads();  // s_desc / s_cmd are rewritten by the next poll
-  }
-  if (threadIdx.x == 0) __hip_atomic_store(&mb->state, uint64_t(kSrvExited), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
 // ------------------------------------------- device-side wrap (f2) -------
 // TCPOverIPv4Adapter::wrap_tcp_in_ip (tcp_over_ip.cpp:69-88) for a batch:
 // datagram i = [40 header bytes][payload], the payload already in place (laid
@@ -1826,6 +1734,125 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
     __builtin_amdgcn_wave_barrier();  // the next step rewrites sw
   }
   signal_done(done);
+}
+
+// ---------------------------------------------- resident tick server -----
+// A one-block kernel that stays resident between ticks and takes each tick's
+// job from a mailbox in coherent page-locked host memory (TickMailbox,
+// icsum_launch.h) instead of being launched per tick: a tick then pays no
+// launch (the ~3-5 us from the doorbell to the first wave), only the
+// mailbox poll and the payload's PCIe reads.  Every descriptor word carries
+// the job's sequence number in its high half, so one poll (wave 0: lane k
+// reads word k, lane 63 the quit word) that finds the expected number in
+// every word the job uses has read a complete descriptor, whatever order the
+// host's stores landed in.  The job runs as k_tick's body (16-lane group per
+// segment, starts / lengths from the descriptor), its results go to the
+// job's page-locked result area, and `done` takes the sequence number with a
+// system-scope release.  The server exits on the quit word, after idle_us
+// without a job, or after kSrvMaxLife of 100 MHz ticks (the host relaunches
+// it when a job finds it gone): every wave reaches an exit.
+constexpr uint64_t kSrvMaxLife = 100000000ull;  // 1 s of s_memrealtime
+
+__global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const uint8_t* __restrict__ zpad,
+                                                        uint32_t expect, uint32_t idle_us) {
+  __shared__ uint32_t s_desc[64];
+  __shared__ uint32_t s_cmd;  // 0 none yet, 1 a job, 2 exit
+  const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  const uint32_t g = threadIdx.x >> 4, gl = threadIdx.x & 15u;
+  const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  uint64_t t_job = t0;
+  for (;;) {
+    if (wv == 0) {
+      const uint64_t word = __hip_atomic_load(&mb->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      const uint32_t pay = uint32_t(word), seq = uint32_t(word >> 32);
+      const uint32_t w0 = __builtin_amdgcn_readlane(pay, 0), s0 = __builtin_amdgcn_readlane(seq, 0);
+      const uint32_t nj = (w0 >> 8) & 0xffu, nw = kSrvHead + 2u * nj;  // the words this job uses
+      const bool inits = (w0 >> 16) & 1u;
+      const bool used = lane < nw || (inits && lane >= kSrvInit && lane < kSrvInit + nj);
+      const bool fresh = !used || seq == expect;
+      const bool job = s0 == expect && __all(fresh);
+      const bool quit = __builtin_amdgcn_readlane(uint32_t(word | (word >> 32)), kSrvQuit) != 0;
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      const bool idle = now - t_job > uint64_t(idle_us) * 100u || now - t0 > kSrvMaxLife;
+      if (job) s_desc[lane] = pay;
+      if (lane == 0) s_cmd = quit ? 2u : job ? 1u : idle ? 2u : 0u;
+    }
+    __syncthreads();
+    const uint32_t cmd = s_cmd;
+    if (cmd == 2u) break;  // uniform
+    if (cmd == 0u) {
+      __builtin_amdgcn_s_sleep(2);
+      __syncthreads();  // wave 0 rewrites s_cmd next round
+      continue;
+    }
+    // a resident kernel gets no launch-time cache invalidation: without this
+    // system-scope acquire its loads of the reused staging slots would hit
+    // the previous job's lines still held in L1 / L2
+    // (the L2 holds such lines: without it, or with the CU's L1 alone
+    // invalidated, the tests read the previous job's bytes;
+    // profiles/r6_tick_server_inv.jsonl)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+    // the job: checksum (op 0) or the fused IPv4 item (op 1, mode), n <= 16
+    // segments at [bytes + s_j, + len_j), results into the page-locked area
+    const uint32_t w0 = s_desc[0], op = w0 & 0xfu, mode = (w0 >> 4) & 0xfu, n = (w0 >> 8) & 0xffu;
+    uint8_t* bytes = reinterpret_cast<uint8_t*>(uint64_t(s_desc[1]) | (uint64_t(s_desc[2]) << 32));
+    const uint32_t* init = reinterpret_cast<const uint32_t*>(uint64_t(s_desc[3]) | (uint64_t(s_desc[4]) << 32));
+    uint8_t* res = reinterpret_cast<uint8_t*>(uint64_t(s_desc[5]) | (uint64_t(s_desc[6]) << 32));
+    const uint32_t bsh = frame_shift(bytes);
+    bytes -= bsh;
+    const bool valid = g < n;
+    const uint32_t gi = valid ? g : 0u;
+    const uint64_t s = uint64_t(s_desc[kSrvHead + 2u * gi]) + bsh;
+    const uint64_t e = valid ? s + s_desc[kSrvHead + 2u * gi + 1u] : s;
+    // per-segment words (inits, message records) requested with the stream,
+    // unconditionally (a load under a branch is waited for at its join,
+    // ahead of the stream: one more PCIe round trip)
+    const uint32_t* const iw = init ? init : reinterpret_cast<const uint32_t*>(zpad);
+    if (op == 0u) {
+      const uint32_t i0 = (w0 >> 16) & 1u ? s_desc[kSrvInit + gi] : 0u;
+      uint32_t ev = 0, od = 0;
+      seg_sums<16, 8, true, 3>(bytes, s, e, gl, ev, od);
+      const uint32_t tot = group_sum<16>(combine_roles(ev, od, uint32_t(s) & 1u));
+      if (valid && gl == 15) reinterpret_cast<uint16_t*>(res)[g] = uint16_t(fold_value(i0 + tot));
+    } else if (op == 2u) {
+      // wrap_tcp_in_ip (tcp_over_ip.cpp:69-88) as k_tcp_wrap with its headers
+      // to an array: the payload after 40 bytes of header room (mode 0) or
+      // the segment alone (mode 1); the record (ics_tcp_msg) at `init`
+      const bool ok = valid && (mode == 1u || e - s >= 40);
+      const uint64_t p0 = ok ? (mode == 1u ? s : s + 40) : e;
+      const uint32_t* rec = iw + 7u * gi;  // 28-byte records
+      uint32_t r[7];
+#pragma unroll
+      for (int k = 0; k < 7; ++k) r[k] = rec[k];
+      uint32_t ev = 0, od = 0;
+      seg_sums<16, 8, true, 3>(bytes, p0, e, gl, ev, od);
+      const uint32_t tot = __shfl(group_sum<16>(combine_roles(ev, od, uint32_t(p0) & 1u)),
+                                  int((threadIdx.x & 63u) | 15u), 64);  // to every lane of the group
+      const u32x4 a{r[0], r[1], r[2], r[3]};
+      uint32_t w[10], ipc, tcv;
+      wrap_header(a, r[4], r[5], r[6] & 0xffffu, e - p0, tot, w, ipc, tcv);
+      uint32_t wk = w[0];
+#pragma unroll
+      for (uint32_t k = 1; k < 10; ++k) wk = gl == k ? w[k] : wk;
+      if (ok && gl < 10) reinterpret_cast<uint32_t*>(res)[10u * g + gl] = wk;
+    } else {
+      uint16_t* ip = reinterpret_cast<uint16_t*>(res);
+      ipv4_item<16, 8, true, 3>(bytes, s, e, g, valid, gl, int(mode), ip, ip + n, res + 4u * n, zpad, zlast);
+    }
+    // results out before `done` (signal_done's order): every wave's stores
+    // retired, the block's barrier, one system-scope release
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      __hip_atomic_store(&mb->done, uint64_t(expect), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    ++expect;
+    t_job = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();  // s_desc / s_cmd are rewritten by the next poll
+  }
+  if (threadIdx.x == 0) __hip_atomic_store(&mb->state, uint64_t(kSrvExited), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // --------------------------------------------------- router batch -------

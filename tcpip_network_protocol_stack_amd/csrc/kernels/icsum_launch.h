@@ -214,9 +214,11 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
 //                u8 status x n (op 1)
 //   w[kSrvHead + 2 j], w[kSrvHead + 2 j + 1] = segment j's start (relative to
 //                the bytes) and length
+//   w[kSrvInit + j] = segment j's init (op 0 with w[0] bit 16 set: the inits
+//                travel in the descriptor, not as a PCIe read of their own)
 // w[kSrvQuit] != 0: exit.  The device writes `done` (the last finished
 // sequence number) and, when it exits, `state` = kSrvExited.
-constexpr uint32_t kSrvHead = 7, kSrvQuit = 63;
+constexpr uint32_t kSrvHead = 7, kSrvInit = kSrvHead + 2 * kTickSegs, kSrvQuit = 63;
 constexpr uint64_t kSrvRunning = 1, kSrvExited = 2;
 struct alignas(256) TickMailbox {
   uint64_t w[64];
@@ -224,7 +226,7 @@ struct alignas(256) TickMailbox {
   uint64_t state;
   uint64_t pad[30];
 };
-static_assert(kSrvHead + 2 * kTickSegs <= kSrvQuit, "the descriptor fits below the quit word");
+static_assert(kSrvInit + kTickSegs <= kSrvQuit, "the descriptor fits below the quit word");
 hipError_t launch_tick_server(TickMailbox* mb, const void* zero16, uint32_t expect, uint32_t idle_us,
                               hipStream_t st);
 

@@ -412,3 +412,44 @@ def test_tick_server_idle_exit_relaunch_and_stop(orc):
             assert (eng.checksum_batch_host(buf, len(segs), offsets=off) == want).all()
             assert eng.dispatch_info()["kernel"] == "tick_server"
         # leave it resident: the engine's close (ics_destroy) stops it
+
+
+@pytest.mark.parametrize("pinned", [False, True])
+def test_tick_server_wrap_vs_oracle(srv_eng, orc, pinned):
+    """Wrap ticks on the server: ics_tcp_wrap_batch_host (headers written into
+    the datagrams) and ics_tcp_wrap_headers_host (payloads alone, headers to
+    an array) for 1..16 messages of 0..1460-byte payloads, offsets and fixed
+    stride, against the oracle's serialize(wrap_tcp_in_ip(msg)); 17 take the
+    launches."""
+    import torch
+
+    from test_gpu_wrap import _oracle_wire, _random_batch
+
+    rng = np.random.default_rng(0x5E9 + pinned)
+    for n in (1, 5, 16, 17):
+        segs, m = _random_batch(rng, n)
+        want = _oracle_wire(orc, segs, m)
+        buf, off = pack_contiguous(segs, 3)
+        h = torch.empty(buf.size, dtype=torch.uint8, pin_memory=pinned).numpy()
+        h[:] = buf
+        srv_eng.tcp_wrap_batch_host(h, m, n, offsets=off)
+        assert (srv_eng.dispatch_info()["kernel"] == "tick_server") == (n <= 16), n
+        for i, w in enumerate(want):
+            assert h[off[i]:off[i + 1]].tobytes() == w, (n, i)
+        pays = [s[40:] for s in segs]
+        pb, poff = pack_contiguous(pays, 1)
+        ph = torch.empty(pb.size, dtype=torch.uint8, pin_memory=pinned).numpy()
+        ph[:] = pb
+        hd = srv_eng.tcp_wrap_headers_host(ph, m, n, offsets=poff)
+        for i, w in enumerate(want):
+            assert hd[40 * i:40 * i + 40].tobytes() == w[:40], (n, i)
+        # fixed stride: 1040-byte datagrams
+        L = 1040
+        _, m2 = _random_batch(rng, n, fixed=L - 40)
+        body = rng.integers(0, 256, n * L, dtype=np.uint8)
+        fh = torch.empty(body.size, dtype=torch.uint8, pin_memory=pinned).numpy()
+        fh[:] = body
+        srv_eng.tcp_wrap_batch_host(fh, m2, n, stride=L, dgram_len=L)
+        for i in range(n):
+            w = _oracle_wire(orc, [b"\0" * 40 + body[i * L + 40:(i + 1) * L].tobytes()], m2[i:i + 1])[0]
+            assert fh[i * L:(i + 1) * L].tobytes() == w, (n, i, "fixed")
