@@ -74,6 +74,10 @@ class BatchEngine
     std::vector<std::optional<TCPMessage>> unwrap_packed(TCPOverIPv4Adapter& adapter, const uint8_t* bytes,
                                                          const uint64_t* offsets, size_t n);
 
+    // the resident tick server (ics_set_tick_server): a per-tick loop's calls
+    // of <= 16 datagrams without a kernel launch each; 0 turns it off
+    void set_tick_server(uint32_t idle_us);
+
     // page-locked host memory from the engine's device runtime
     void* host_alloc(size_t bytes);
     void host_free(void* p);

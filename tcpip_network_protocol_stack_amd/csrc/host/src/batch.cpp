@@ -295,6 +295,11 @@ void BatchEngine::patch_packed(uint8_t* bytes, const uint64_t* offsets, size_t n
               "ics_ipv4_tcp_batch_host");
 }
 
+void BatchEngine::set_tick_server(uint32_t idle_us)
+{
+    check(ics_set_tick_server(ctx_, idle_us), "ics_set_tick_server");
+}
+
 void* BatchEngine::host_alloc(size_t bytes)
 {
     void* p = nullptr;

@@ -553,6 +553,22 @@ int main()
         EXPECT(std::chrono::steady_clock::now() - t0 < std::chrono::seconds(2));
         close(sv[0]);
     }
+    // a per-tick loop on the resident tick server: each tick verifies a few
+    // received wires and wraps a few messages (<= 16 each: the server's
+    // jobs), every result equal to the per-object calls; then off again
+    {
+        eng.set_tick_server(5000);
+        for (int t = 0; t < 200; ++t) {
+            const size_t k = 1 + static_cast<size_t>(rng() % 16), at = static_cast<size_t>(rng() % (msgs.size() - k));
+            std::vector<std::string_view> tw(wires.begin() + at, wires.begin() + at + k);
+            const auto tst = eng.verify_raw(tw);
+            for (size_t i = 0; i < k; ++i) EXPECT(tst[i] == ICS_ST_ACCEPT);
+            const auto td = eng.wrap(A, std::span<const TCPMessage>(msgs.data() + at, k));
+            for (size_t i = 0; i < k; ++i) EXPECT(joined(serialize(td[i])) == wires[at + i]);
+            if (t % 50 == 49) std::this_thread::sleep_for(std::chrono::milliseconds(8));  // the server idles out
+        }
+        eng.set_tick_server(0);
+    }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);
     return failures ? 1 : 0;
