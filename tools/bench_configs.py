@@ -112,6 +112,9 @@ def main():
     ap.add_argument("--settle-ms", type=float, default=150.0,
                     help="untimed warm-up per row (0 for counter passes, which serialise every dispatch)")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--warm-server", type=int, default=-1,
+                    help="stack rows: a second engine with its tick server resident (idle limit in us; 0: the "
+                         "second engine without a server, the control) poked before every row")
     ap.add_argument("--wrap-device-only", action="store_true", help="wrap rows: skip the host-memory rows")
     args = ap.parse_args()
     global timed
@@ -527,11 +530,22 @@ def main():
         torch.cuda.synchronize()
         calls = args.iters * args.rounds
         rows = {}
+        poke = lambda: None  # noqa: E731
+        if args.warm_server >= 0:  # does a resident block elsewhere on the card change the idle-queue cost?
+            warm = Engine(0)
+            warm.set_tick_server(args.warm_server)
+            wbuf = torch.zeros(64, dtype=torch.uint8, pin_memory=True).numpy()
+
+            def poke():
+                warm.checksum_batch_host(wbuf, 1, stride=64, seg_len=64)
+                print(json.dumps({"warm_server_us": args.warm_server, "kernel": warm.dispatch_info()["kernel"]}),
+                      file=sys.stderr)
         entries = {verify: "ics_ipv4_tcp_batch VERIFY", wrap: "ics_tcp_wrap_batch",
                    wrap_apart: "ics_tcp_wrap_headers"}
         for name, fn, other in (("verify_alone", verify, None), ("verify_after_wrap", verify, wrap),
                                 ("wrap_alone", wrap, None), ("wrap_after_verify", wrap, verify),
                                 ("wrap_apart_alone", wrap_apart, None), ("wrap_apart_after_verify", wrap_apart, verify)):
+            poke()
             before = eng.dispatch_info()
             t, info = per_call(fn, other, calls)
             rows[name] = t
@@ -545,6 +559,7 @@ def main():
         # the same calls back to back (events around `iters` calls): no host
         # gap between a call's first event and its launch
         for name, fn in (("verify_b2b", verify), ("wrap_b2b", wrap), ("wrap_apart_b2b", wrap_apart)):
+            poke()
             t = timed(lambda i=0, f=fn: f(), args.iters)
             nbytes = int(roff[-1]) if fn is verify else int(toff[-1])
             emit(f"stack_tick_{name}", nbytes, t, n * (5 if fn is verify else 28),
@@ -571,6 +586,7 @@ def main():
 
         both = int(roff[-1]) + int(toff[-1])
         for name, fn in (("both_one_stream", tick_one), ("both_two_streams", tick_two)):
+            poke()
             t = timed(fn, args.iters)
             emit(f"stack_tick_{name}", both, t, n * 33,
                  entry="ics_ipv4_tcp_batch VERIFY + ics_tcp_wrap_headers",
