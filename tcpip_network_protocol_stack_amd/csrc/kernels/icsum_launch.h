@@ -207,9 +207,10 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
 // Resident tick server (k_tick_server): one block that stays resident and
 // takes per-tick jobs from this mailbox in coherent page-locked host memory.
 // Descriptor word k = payload (low 32 bits) | job sequence number (high 32):
-//   w[0] = op (0 checksum, 1 fused IPv4) | mode << 4 | n << 8   (n <= kTickSegs)
+//   w[0] = op (0 checksum, 1 fused IPv4, 2 wrap) | mode << 4 | n << 8
+//          (n <= kTickSegs) | inits in the descriptor << 16
 //   w[1], w[2] = the bytes' (device-visible) address, low / high half
-//   w[3], w[4] = per-segment inits (0: none; op 0)
+//   w[3], w[4] = the wrap's message records (op 2)
 //   w[5], w[6] = the result area: u16 x n values (op 0) or u16 ip, u16 tcp,
 //                u8 status x n (op 1)
 //   w[kSrvHead + 2 j], w[kSrvHead + 2 j + 1] = segment j's start (relative to

@@ -7,7 +7,7 @@ set -euo pipefail
 cd "$GRAFT_REPO_ROOT"
 O=gpurun_out/${1:-r6tick}; mkdir -p $O
 L=tcpip_network_protocol_stack_amd/libicsum.so
-export TICK_OPS=${TICK_OPS:-verify,verify_off,checksum,checksum_off} TICK_SIZES=${TICK_SIZES:-1,16} TICK_MEM=pinned TICK_CALLS=${TICK_CALLS:-300}
+export TICK_OPS=${TICK_OPS:-verify,verify_off,checksum,checksum_off} TICK_SIZES=${TICK_SIZES:-1,16} TICK_MEM=${TICK_MEM:-pinned} TICK_CALLS=${TICK_CALLS:-300}
 shift || true
 for rep in 1 2; do
   for v in "$@"; do
