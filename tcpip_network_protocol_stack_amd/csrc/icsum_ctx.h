@@ -88,9 +88,9 @@ struct ics_ctx {
   // wave (0: span_segs_for)
   int tile = -1;
   uint32_t span_segs = 0;
-  uint32_t span_blocks = 0;
+  uint32_t span_blocks = 0;  // test hook: grid cap of the tile launch (0: none), reaches its grid-stride form
   int slot_prio = 0;    // staging-slot stream priority (ICSUM_FORCE slot_prio; 0: default stream creation)
-  int tick_inline = 1;  // zero-copy ticks of <= kTickSegs offsets segments through k_tick (ICSUM_FORCE tick_inline=0: off)  // test hook: grid cap of the tile launch (0: none), reaches its grid-stride form
+  int tick_inline = 1;  // zero-copy ticks of <= kTickSegs offsets segments through k_tick (ICSUM_FORCE tick_inline=0: off)
   static constexpr uint64_t kSpanBytes = 20 << 10;  // segment bytes per span (span_segs_for)
   static constexpr uint64_t kTileMin = uint64_t(1) << 16;  // tile launches from this many segments (AUTO)
   static constexpr uint64_t kTileMinChecksum = uint64_t(1) << 17;  // ... of the plain checksum (tile_wins)
