@@ -12,7 +12,9 @@
 // Environment: TICK_OPS (comma list of verify, verify_off, checksum, checksum_off, wrap;
 // default all), TICK_SIZES (comma list of batch sizes, default 1..8192),
 // TICK_MEM (pinned | pageable, default both), TICK_CALLS (timed calls per
-// round, default 200).  Checksum calls pass per-segment inits (the NS
+// round, default 200), TICK_GAP_US (host busy time before each call, outside
+// the timed call: a loop that does other work between ticks; default 0).
+// Checksum calls pass per-segment inits (the NS
 // workload's pseudo-header sums).  bench.py's host_inclusive runs it as
 // TICK_OPS=checksum TICK_SIZES=1,16 TICK_MEM=pinned (built by build()).
 #include <dlfcn.h>
@@ -138,6 +140,7 @@ int main(int argc, char** argv) {
   std::vector<uint64_t> offs(kMaxN + 1);
   for (uint64_t i = 0; i <= kMaxN; ++i) offs[i] = i * kL;
   const int rounds = 5, calls = getenv("TICK_CALLS") ? std::max(10, atoi(getenv("TICK_CALLS"))) : 200;
+  const double gap_us = getenv("TICK_GAP_US") ? atof(getenv("TICK_GAP_US")) : 0.0;
   // every (build, op) pair of a size and memory kind is timed interleaved call
   // by call, the first pair rotating per call: each pair's calls follow every
   // other pair's equally often (blocks of calls per build or per op measured
@@ -177,6 +180,9 @@ int main(int argc, char** argv) {
             uint16_t* a = reinterpret_cast<uint16_t*>(res[j].data());
             uint16_t* b = a + n;
             uint8_t* st = reinterpret_cast<uint8_t*>(b + n);
+            if (gap_us > 0)
+              for (const auto g0 = clk::now(); std::chrono::duration<double, std::micro>(clk::now() - g0).count() < gap_us;) {
+              }
             const auto t0 = clk::now();
             if (!strcmp(op, "verify_off"))
               check(l, l.ipv4_host(l.ctx, src, offs.data(), 0, 0, n, ICS_MODE_VERIFY, a, b, st));
@@ -196,9 +202,10 @@ int main(int argc, char** argv) {
         while (first > 0 && !strcmp(vars[first - 1].op, vars[j].op)) --first;
         const bool same = res[j] == res[first];
         printf("{\"op\": \"%s\", \"mem\": \"%s\", \"n\": %llu, \"bytes\": %llu, \"lib\": \"%s\", \"p10_us\": %.2f, "
-               "\"p50_us\": %.2f, \"p90_us\": %.2f, \"same_as_first\": %s}\n",
+               "\"p50_us\": %.2f, \"p90_us\": %.2f, \"gap_us\": %.1f, \"same_as_first\": %s}\n",
                vars[j].op, mem ? "pinned" : "pageable", (unsigned long long)n, (unsigned long long)(n * kL),
-               libs[vars[j].k].path.c_str(), pct(t[j], 0.1), pct(t[j], 0.5), pct(t[j], 0.9), same ? "true" : "false");
+               libs[vars[j].k].path.c_str(), pct(t[j], 0.1), pct(t[j], 0.5), pct(t[j], 0.9), gap_us,
+               same ? "true" : "false");
         fflush(stdout);
       }
     }
