@@ -453,3 +453,48 @@ def test_tick_server_wrap_vs_oracle(srv_eng, orc, pinned):
         for i in range(n):
             w = _oracle_wire(orc, [b"\0" * 40 + body[i * L + 40:(i + 1) * L].tobytes()], m2[i:i + 1])[0]
             assert fh[i * L:(i + 1) * L].tobytes() == w, (n, i, "fixed")
+
+
+def test_tick_server_threads_and_two_contexts(orc):
+    """Three threads call one engine's served host entry points at once (the
+    context serialises its host calls: ics_ctx::mu) while a fourth drives a
+    second engine whose own server is resident beside the first; checksum
+    ticks with inits and VERIFY ticks of 1..16 segments from pageable and
+    page-locked memory, every result equal to the oracle's."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import torch
+
+    from conftest import engine_with
+    from test_gpu_parity import _random_datagrams
+
+    rng = np.random.default_rng(0x5EA)
+    jobs = []
+    for t in range(4):
+        mine = []
+        for k in range(24):
+            n = int(rng.integers(1, 17))
+            buf, off = pack_contiguous(_random_datagrams(rng, n), int(rng.integers(0, 16)))
+            h = torch.empty(buf.size, dtype=torch.uint8, pin_memory=bool(k % 2)).numpy()
+            h[:] = buf
+            init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+            w = orc.ipv4_tcp_batch(buf.copy(), n, 1, offsets=off)
+            mine.append((h, n, off, init, orc.checksum_batch(buf, n, offsets=off, init=init), w))
+        jobs.append(mine)
+    for e1 in engine_with({"tick_server": 20000}):
+        for e2 in engine_with({"tick_server": 20000}):
+            def run(t):
+                eng = e1 if t < 3 else e2
+                for rep in range(3):
+                    for h, n, off, init, want_ck, w in jobs[t]:
+                        assert (eng.checksum_batch_host(h, n, offsets=off, init=init) == want_ck).all(), (t, rep, n)
+                        ip, tcp, st = eng.ipv4_tcp_batch_host(h, n, 1, offsets=off)
+                        assert (ip == w[0]).all() and (tcp == w[1]).all() and (st == w[2]).all(), (t, rep, n)
+                return True
+
+            with ThreadPoolExecutor(4) as ex:
+                assert all(ex.map(run, range(4)))
+            assert e1.dispatch_info()["kernel"] == "tick_server"
+            assert e2.dispatch_info()["kernel"] == "tick_server"
+            e2.set_tick_server(0)
+        e1.set_tick_server(0)
