@@ -20,7 +20,10 @@
  *   - Segment addressing (used by every batch call):
  *       d_offsets != NULL : segment i = bytes[d_offsets[i], d_offsets[i+1])
  *                           (n+1 monotone uint64 offsets; starts may be odd /
- *                           unaligned — byte roles are relative to each start)
+ *                           unaligned — byte roles are relative to each start;
+ *                           the *_host calls reject decreasing h_offsets with
+ *                           ICS_ERR_INVALID, the device calls trust them and
+ *                           libicsum_debug.so reports them)
  *       d_offsets == NULL : segment i = bytes[i*stride, i*stride + seg_len)
  *   - Byte bases (d_bytes, d_dgrams, d_payloads, h_bytes, ...) may lie at ANY
  *     address, as InternetChecksum::add takes any string_view

@@ -93,10 +93,19 @@ struct Chunk {
 };
 
 // Next chunk starting at segment i0 (whose first `pos` bytes were already
-// staged as pieces) that fits the slot.
+// staged as pieces) that fits the slot.  The offsets are the caller's host
+// array: every one a chunk takes is checked monotone here (a decreasing
+// pair would reach the kernels as a segment of ~2^64 bytes), in the loop
+// that reads them anyway.
+int not_monotone(uint64_t i) {
+  return fail(ICS_ERR_INVALID, "offsets not monotone: offsets[%llu] > offsets[%llu]", (unsigned long long)i,
+              (unsigned long long)(i + 1));
+}
+
 int next_chunk(const ics_ctx* ctx, const uint64_t* offsets, uint64_t stride, uint64_t seg_len, uint64_t n,
                uint64_t i0, uint64_t pos, bool allow_pieces, uint64_t cap_n, Chunk* c) {
   const uint64_t cap_b = ctx->slot_bytes;
+  if (offsets && offsets[i0 + 1] < offsets[i0]) return not_monotone(i0);
   const uint64_t s0 = offsets ? offsets[i0] : i0 * stride;
   const uint64_t len0 = offsets ? offsets[i0 + 1] - s0 : seg_len;
   if (pos || len0 > cap_b) {  // segment i0 does not fit a slot: its next piece
@@ -117,7 +126,10 @@ int next_chunk(const ics_ctx* ctx, const uint64_t* offsets, uint64_t stride, uin
   }
   const uint64_t b0 = offsets[i0];
   uint64_t i1 = i0;
-  while (i1 < n && i1 - i0 < cap_n && offsets[i1 + 1] - b0 <= cap_b) ++i1;
+  while (i1 < n && i1 - i0 < cap_n && offsets[i1 + 1] - b0 <= cap_b) {
+    if (offsets[i1 + 1] < offsets[i1]) return not_monotone(i1);
+    ++i1;
+  }
   *c = {i0, i1, b0, offsets[i1]};
   return ICS_OK;
 }

@@ -498,3 +498,36 @@ def test_tick_server_threads_and_two_contexts(orc):
             assert e2.dispatch_info()["kernel"] == "tick_server"
             e2.set_tick_server(0)
         e1.set_tick_server(0)
+
+
+@pytest.mark.parametrize("force", [None, {"tick_server": 3000}], ids=["launched", "server"])
+def test_host_offsets_not_monotone_rejected(orc, force):
+    """A host batch whose offsets decrease anywhere — the first pair, inside
+    a per-tick batch (k_tick / the tick server), inside a DMA'd batch — is
+    ICS_ERR_INVALID ("not monotone") before any kernel reads it (a
+    decreasing pair would otherwise reach a kernel as a segment of ~2^64
+    bytes), for the checksum, fused IPv4 and wrap entries; the engine's next
+    calls are exact."""
+    from conftest import engine_with
+    from tcpip_network_protocol_stack_amd._lib import IcsumError
+    from test_gpu_parity import _random_datagrams
+    from test_gpu_wrap import _random_batch
+
+    rng = np.random.default_rng(0x0FF)
+    for eng in engine_with(force):
+        for n, bad in ((5, 0), (5, 2), (16, 15), (4000, 3000)):
+            segs = _random_datagrams(rng, n)
+            buf, off = pack_contiguous(segs, 3)
+            wsegs, m = _random_batch(rng, n)
+            wbuf, woff = pack_contiguous(wsegs, 1)
+            for o in (off, woff):
+                o[bad + 1] = o[bad] - 1  # offsets[bad] > offsets[bad + 1]
+            with pytest.raises(IcsumError, match="not monotone"):
+                eng.checksum_batch_host(buf, n, offsets=off)
+            with pytest.raises(IcsumError, match="not monotone"):
+                eng.ipv4_tcp_batch_host(buf, n, 1, offsets=off)
+            with pytest.raises(IcsumError, match="not monotone"):
+                eng.tcp_wrap_batch_host(wbuf, m, n, offsets=woff)
+            # and the engine goes on exactly
+            good, goff = pack_contiguous(segs, 3)
+            assert (eng.checksum_batch_host(good, n, offsets=goff) == orc.checksum_batch(good, n, offsets=goff)).all()
