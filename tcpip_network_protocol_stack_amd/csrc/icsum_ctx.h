@@ -221,6 +221,7 @@ struct ics_ctx {
   uint32_t srv_seq = 0;       // the last job posted
   bool srv_launched = false;  // a server was launched (its `state` word says whether it still runs)
   uint64_t n_srv_jobs = 0, n_srv_launches = 0;
+  uint32_t srv_pollers = 1;  // waves polling the mailbox, staggered (ICSUM_FORCE srv_pollers, 1..4)
 };
 
 namespace icsum::detail {

@@ -276,7 +276,7 @@ int server_launch(ics_ctx* ctx) {
   }
   mb_store(&ctx->h_mb->state, icsum::kSrvRunning);
   const uint32_t expect = uint32_t(mb_load(&ctx->h_mb->done)) + 1u;  // the oldest job not done
-  ICS_HIP(icsum::launch_tick_server(ctx->h_mb, ctx->d_zero, expect, ctx->srv_idle_us, ctx->st_srv));
+  ICS_HIP(icsum::launch_tick_server(ctx->h_mb, ctx->d_zero, expect, ctx->srv_idle_us, ctx->srv_pollers, ctx->st_srv));
   ctx->srv_launched = true;
   ++ctx->n_srv_launches;
   return ICS_OK;

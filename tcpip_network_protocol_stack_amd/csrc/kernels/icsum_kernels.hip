@@ -1754,7 +1754,7 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
 constexpr uint64_t kSrvMaxLife = 100000000ull;  // 1 s of s_memrealtime
 
 __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const uint8_t* __restrict__ zpad,
-                                                        uint32_t expect, uint32_t idle_us) {
+                                                        uint32_t expect, uint32_t idle_us, uint32_t pollers) {
   __shared__ uint32_t s_desc[64];
   __shared__ uint32_t s_cmd;  // 0 none yet, 1 a job, 2 exit
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
@@ -1762,30 +1762,43 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const u
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t t_job = t0;
+  if (threadIdx.x == 0) s_cmd = 0u;
+  __syncthreads();
   for (;;) {
-    if (wv == 0) {
-      const uint64_t word = __hip_atomic_load(&mb->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      const uint32_t pay = uint32_t(word), seq = uint32_t(word >> 32);
-      const uint32_t w0 = __builtin_amdgcn_readlane(pay, 0), s0 = __builtin_amdgcn_readlane(seq, 0);
-      const uint32_t nj = (w0 >> 8) & 0xffu, nw = kSrvHead + 2u * nj;  // the words this job uses
-      const bool inits = (w0 >> 16) & 1u;
-      const bool used = lane < nw || (inits && lane >= kSrvInit && lane < kSrvInit + nj);
-      const bool fresh = !used || seq == expect;
-      const bool job = s0 == expect && __all(fresh);
-      const bool quit = __builtin_amdgcn_readlane(uint32_t(word | (word >> 32)), kSrvQuit) != 0;
-      const uint64_t now = __builtin_amdgcn_s_memrealtime();
-      const bool idle = now - t_job > uint64_t(idle_us) * 100u || now - t0 > kSrvMaxLife;
-      if (job) s_desc[lane] = pay;
-      if (lane == 0) s_cmd = quit ? 2u : job ? 1u : idle ? 2u : 0u;
+    // waves 0 .. pollers - 1 poll, each on its own, started a fraction of a
+    // PCIe round trip apart: a job posted at a random moment is seen by the
+    // next poll to start, sooner with more pollers.  The first to see the
+    // job, the quit word or the idle limit claims s_cmd (a job claimed
+    // first wins over another wave's idle verdict); the rest stop polling.
+    if (wv < pollers) {
+      for (uint32_t k = 0; k < wv; ++k) __builtin_amdgcn_s_sleep(14);  // ~0.4 us each
+      while (__hip_atomic_load(&s_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
+        const uint64_t word = __hip_atomic_load(&mb->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint32_t pay = uint32_t(word), seq = uint32_t(word >> 32);
+        const uint32_t w0 = __builtin_amdgcn_readlane(pay, 0), s0 = __builtin_amdgcn_readlane(seq, 0);
+        const uint32_t nj = (w0 >> 8) & 0xffu, nw = kSrvHead + 2u * nj;  // the words this job uses
+        const bool inits = (w0 >> 16) & 1u;
+        const bool used = lane < nw || (inits && lane >= kSrvInit && lane < kSrvInit + nj);
+        const bool fresh = !used || seq == expect;
+        const bool job = s0 == expect && __all(fresh);
+        const bool quit = __builtin_amdgcn_readlane(uint32_t(word | (word >> 32)), kSrvQuit) != 0;
+        const uint64_t now = __builtin_amdgcn_s_memrealtime();
+        const bool idle = now - t_job > uint64_t(idle_us) * 100u || now - t0 > kSrvMaxLife;
+        if (job && !quit) s_desc[lane] = pay;  // (another poller may store the same words)
+        if (job || quit || idle) {
+          if (lane == 0) {
+            uint32_t none = 0u;
+            __hip_atomic_compare_exchange_strong(&s_cmd, &none, quit ? 2u : job ? 1u : 2u, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+          }
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
     }
     __syncthreads();
     const uint32_t cmd = s_cmd;
     if (cmd == 2u) break;  // uniform
-    if (cmd == 0u) {
-      __builtin_amdgcn_s_sleep(2);
-      __syncthreads();  // wave 0 rewrites s_cmd next round
-      continue;
-    }
     // a resident kernel gets no launch-time cache invalidation: without this
     // system-scope acquire its loads of the reused staging slots would hit
     // the previous job's lines still held in L1 / L2
@@ -1850,6 +1863,7 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const u
     }
     ++expect;
     t_job = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) s_cmd = 0u;  // every wave read it at the barrier before the done store
     __syncthreads();  // s_desc / s_cmd are rewritten by the next poll
   }
   if (threadIdx.x == 0) __hip_atomic_store(&mb->state, uint64_t(kSrvExited), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -3019,9 +3033,10 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
 }
 
 hipError_t launch_tick_server(TickMailbox* mb, const void* zero16, uint32_t expect, uint32_t idle_us,
-                              hipStream_t st) {
+                              uint32_t pollers, hipStream_t st) {
+  if (pollers < 1 || pollers > kBlock / 64) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_tick_server, dim3(1), dim3(kBlock), 0, st, mb, static_cast<const uint8_t*>(zero16), expect,
-                     idle_us);
+                     idle_us, pollers);
   return hipGetLastError();
 }
 

@@ -229,7 +229,7 @@ struct alignas(256) TickMailbox {
 };
 static_assert(kSrvInit + kTickSegs <= kSrvQuit, "the descriptor fits below the quit word");
 hipError_t launch_tick_server(TickMailbox* mb, const void* zero16, uint32_t expect, uint32_t idle_us,
-                              hipStream_t st);
+                              uint32_t pollers, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg
 // (include/icsum.h), 28 bytes.

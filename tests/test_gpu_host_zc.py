@@ -323,7 +323,8 @@ def test_tick_offsets_in_kernel_arguments(tick_eng, orc, pinned, base):
             assert (tick_eng.dispatch_info()["kernel"] == "tick") == (want_tick and n <= 16), (n, mode)
 
 
-SRV_FORCE = [{"tick_server": 3000}]  # resident; leaves after 3 ms without a call
+# resident; leaves after 3 ms without a call; srv_pollers 4: every wave polls
+SRV_FORCE = [{"tick_server": 3000}, {"tick_server": 3000, "srv_pollers": 4}]
 
 
 @pytest.fixture(scope="module", params=SRV_FORCE, ids=force_id)
