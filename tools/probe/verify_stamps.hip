@@ -6,7 +6,7 @@
 // launch the default dispatch takes: 16 datagrams per wave) alone — each call
 // after a synchronize, HIP events around it — and back to back.  For the last
 // alone call it prints the block timeline: kernel span (first start to last
-// end), when the first and the last block started, and when 50 / 90 / 99 /
+// end; span_b2b_us: the same for the last back-to-back call), when the first and the last block started, and when 50 / 90 / 99 /
 // 100 % of the blocks (and of the datagram bytes) had finished.
 //   hipcc --offload-arch=gfx950 -O3 -DICSUM_STAMPS -I../../include \
 //     -I../../tcpip_network_protocol_stack_amd/csrc/kernels verify_stamps.hip -o verify_stamps
@@ -87,6 +87,9 @@ int main(int argc, char** argv) {
     CK(hipEventElapsedTime(&ms, e0, e1));
     b2b.push_back(ms * 1000.f / 20.f);
   }
+  // the last back-to-back call's blocks: its span by the waves' own clock
+  static uint64_t stamps_b2b[1u << 16][3];
+  CK(hipMemcpyFromSymbol(stamps_b2b, HIP_SYMBOL(icsum::g_block_stamps), sizeof(stamps_b2b)));
   // the fixed cost of one launch from an idle stream, HIP events around it:
   // an empty kernel of one block and of the VERIFY launch's 4096 blocks
   std::vector<float> empty1, emptyN;
@@ -121,15 +124,20 @@ int main(int argc, char** argv) {
   std::sort(starts.begin(), starts.end());
   std::sort(ends.begin(), ends.end());
   std::sort(dur.begin(), dur.end());
+  uint64_t u0 = ~0ull, u1 = 0;
+  for (uint64_t b = 0; b < blocks; ++b) {
+    u0 = std::min(u0, stamps_b2b[b][0]);
+    u1 = std::max(u1, stamps_b2b[b][1]);
+  }
   auto q = [&](const std::vector<uint64_t>& v, double f) { return 0.01 * double(v[size_t(f * (v.size() - 1))]); };
   const double bytes = double(off[n]);
   std::printf("{\"n\": %llu, \"blocks\": %llu, \"bytes\": %.0f, \"alone_us_p50\": %.2f, \"b2b_us\": %.2f, "
-              "\"span_us\": %.2f, \"start_us\": {\"p50\": %.2f, \"p90\": %.2f, \"last\": %.2f}, "
+              "\"span_us\": %.2f, \"span_b2b_us\": %.2f, \"start_us\": {\"p50\": %.2f, \"p90\": %.2f, \"last\": %.2f}, "
               "\"end_us\": {\"first\": %.2f, \"p50\": %.2f, \"p90\": %.2f, \"p99\": %.2f, \"last\": %.2f}, "
               "\"block_us\": {\"p10\": %.2f, \"p50\": %.2f, \"p90\": %.2f, \"max\": %.2f}, \"frac_alone\": %.4f, "
               "\"frac_span\": %.4f, \"empty_launch_us\": {\"one_block\": %.2f, \"same_grid\": %.2f}}\n",
               (unsigned long long)n, (unsigned long long)blocks, bytes, alone[alone.size() / 2], b2b[2],
-              0.01 * double(t1 - t0), q(starts, 0.5), q(starts, 0.9), q(starts, 1.0), q(ends, 0.0), q(ends, 0.5),
+              0.01 * double(t1 - t0), 0.01 * double(u1 - u0), q(starts, 0.5), q(starts, 0.9), q(starts, 1.0), q(ends, 0.0), q(ends, 0.5),
               q(ends, 0.9), q(ends, 0.99), q(ends, 1.0), q(dur, 0.1), q(dur, 0.5), q(dur, 0.9), q(dur, 1.0),
               bytes / (alone[alone.size() / 2] * 1e3) / 8000.0, bytes / (0.01 * double(t1 - t0) * 1e3) / 8000.0,
               empty1[empty1.size() / 2], emptyN[emptyN.size() / 2]);
