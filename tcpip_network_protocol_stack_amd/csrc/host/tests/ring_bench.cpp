@@ -317,7 +317,11 @@ int main(int argc, char** argv)
         // datagrams: the arena's unwrap (GPU verify + host parse + gates) and
         // the engine's wrap, against the per-object path on the drop-in types
         // (parse + unwrap_tcp_in_ip, wrap_tcp_in_ip + serialize) on this core.
+        // RING_TICK_SERVER=idle_us: the same with the resident tick server on.
         icsum::BatchEngine eng(0);
+        const char* srv_env = std::getenv("RING_TICK_SERVER");
+        const uint32_t srv_idle = srv_env ? uint32_t(std::strtoul(srv_env, nullptr, 10)) : 0u;
+        if (srv_idle) eng.set_tick_server(srv_idle);
         TCPOverIPv4Adapter a, b;
         a.config_mut().source = Address{"10.1.2.3", 4321};
         a.config_mut().destination = Address{"10.9.8.7", 80};
@@ -379,9 +383,10 @@ int main(int argc, char** argv)
                     t_cpu_wrap.push_back(cw);
                 }
             }
-            std::printf("{\"mode\": \"tick\", \"datagrams\": %zu, \"iters\": %zu, \"unwrap_us\": %.2f, \"wrap_us\": %.2f, "
-                        "\"cpu_unwrap_us\": %.2f, \"cpu_wrap_us\": %.2f, \"accepted\": %zu, \"cpu_accepted\": %zu}\n",
-                        k, iters, p50(t_unwrap), p50(t_wrap), p50(t_cpu_unwrap), p50(t_cpu_wrap), ok, cpu_ok);
+            std::printf("{\"mode\": \"tick\", \"tick_server_idle_us\": %u, \"datagrams\": %zu, \"iters\": %zu, "
+                        "\"unwrap_us\": %.2f, \"wrap_us\": %.2f, \"cpu_unwrap_us\": %.2f, \"cpu_wrap_us\": %.2f, "
+                        "\"accepted\": %zu, \"cpu_accepted\": %zu}\n",
+                        srv_idle, k, iters, p50(t_unwrap), p50(t_wrap), p50(t_cpu_unwrap), p50(t_cpu_wrap), ok, cpu_ok);
             std::fflush(stdout);
             if (ok != (iters + 20) * k || cpu_ok != ok) return 2;
         }
