@@ -348,7 +348,8 @@ def host_inclusive(eng, data, init, out, n, seg, passes=3, calls=300):
             "tick_p50_cpp_server": tick_cpp_guarded(calls, "tick_server=20000"),
             "tick_cpp_note": "the same calls from C++ (tools/probe/tick_latency, dlopen of the in-tree libicsum.so, "
                              "1500-byte segments with inits, page-locked), no interpreter in the loop; _server: "
-                             "with the resident tick server (ics_set_tick_server, 20 ms idle), no launch per call"}
+                             "with the resident tick server (ics_set_tick_server, 20 ms idle; 4 blocks, 16 segments each), "
+                             "no launch per call"}
 
 
 def tick_cpp(calls, force=None):
@@ -359,7 +360,7 @@ def tick_cpp(calls, force=None):
     lib = os.path.join(ROOT, "tcpip_network_protocol_stack_amd", "libicsum.so") + (f"@{force}" if force else "")
     if not os.path.exists(exe):
         return None
-    env = dict(os.environ, TICK_OPS="checksum", TICK_SIZES="1,16", TICK_MEM="pinned", TICK_CALLS=str(calls))
+    env = dict(os.environ, TICK_OPS="checksum", TICK_SIZES="1,16,64", TICK_MEM="pinned", TICK_CALLS=str(calls))
     r = subprocess.run([exe, lib], env=env, capture_output=True, text=True, timeout=120)
     if r.returncode:
         raise RuntimeError(f"tick_latency: {r.returncode} {r.stderr.strip()[-300:]}")

@@ -282,15 +282,21 @@ int ics_tcp_wrap_headers_host(ics_ctx* ctx, const void* h_payloads, const uint64
                               uint64_t payload_len, uint64_t n, const ics_tcp_msg* h_msgs, void* h_hdrs);
 
 /* Resident tick server (not a reference interface).  idle_us > 0: the
- * zero-copy *_host calls of at most 16 segments (checksum, fused IPv4 in any
- * mode; fixed stride or offsets) are taken by a one-block kernel that stays
- * resident on the context's GPU between calls and reads each call's job from
- * a mailbox in page-locked memory — no kernel launch per call.  It leaves
- * after idle_us microseconds without a call (the next call launches it
- * again) or on ics_set_tick_server(ctx, 0) / ics_destroy.  While it is
- * resident the device is busy: hipDeviceSynchronize waits until it leaves.
- * Results are identical to the launched path.  0 (default): off. */
+ * zero-copy *_host calls of at most 16 x blocks segments (checksum, fused
+ * IPv4 in any mode, both wraps; fixed stride or offsets) are taken by a
+ * kernel of `blocks` blocks that stays resident on the context's GPU between
+ * calls and reads each call's job from mailboxes in page-locked memory (16
+ * segments per block) — no kernel launch per call.  It leaves after idle_us
+ * microseconds without a call (the next call launches it again) or on
+ * ics_set_tick_server(ctx, 0) / ics_destroy.  While it is resident the
+ * device is busy: hipDeviceSynchronize waits until it leaves.  Results are
+ * identical to the launched path.  0 (default): off. */
 int ics_set_tick_server(ics_ctx* ctx, uint32_t idle_us);
+/* The server's blocks, 1..8 (default 4: ticks of up to 64 segments).  Each
+ * resident block keeps one CU and one poll of its mailbox in flight over
+ * PCIe; a tick of at most 16 segments costs the same with any number.
+ * Takes effect at the server's next launch (a running server is stopped). */
+int ics_set_tick_server_blocks(ics_ctx* ctx, uint32_t blocks);
 
 /* ---- device memory helpers for FFI callers without an allocator -------- */
 int ics_malloc(ics_ctx* ctx, void** d_ptr, size_t bytes);

@@ -79,6 +79,7 @@ SIGNATURES = {
     "ics_sum_batch": (_int, [_p, _p, _p, _u64, _u64, _p, _p, _p, _u64, _p]),
     "ics_set_binning": (_int, [_p, _int]),
     "ics_set_tick_server": (_int, [_p, ctypes.c_uint32]),
+    "ics_set_tick_server_blocks": (_int, [_p, ctypes.c_uint32]),
     "ics_fold_batch": (_int, [_p, _p, _p, _u64, _p]),
     "ics_ipv4_tcp_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _int, _p, _p, _p, _p]),
     "ics_router_ttl_batch": (_int, [_p, _p, _p, _u64, _u64, _u64, _p, _p]),

@@ -75,8 +75,10 @@ class BatchEngine
                                                          const uint64_t* offsets, size_t n);
 
     // the resident tick server (ics_set_tick_server): a per-tick loop's calls
-    // of <= 16 datagrams without a kernel launch each; 0 turns it off
+    // of <= 16 x blocks datagrams without a kernel launch each; 0 turns it
+    // off; blocks 1..8 (ics_set_tick_server_blocks, default 4)
     void set_tick_server(uint32_t idle_us);
+    void set_tick_server_blocks(uint32_t blocks);
 
     // page-locked host memory from the engine's device runtime
     void* host_alloc(size_t bytes);

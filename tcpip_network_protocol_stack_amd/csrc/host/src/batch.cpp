@@ -300,6 +300,11 @@ void BatchEngine::set_tick_server(uint32_t idle_us)
     check(ics_set_tick_server(ctx_, idle_us), "ics_set_tick_server");
 }
 
+void BatchEngine::set_tick_server_blocks(uint32_t blocks)
+{
+    check(ics_set_tick_server_blocks(ctx_, blocks), "ics_set_tick_server_blocks");
+}
+
 void* BatchEngine::host_alloc(size_t bytes)
 {
     void* p = nullptr;

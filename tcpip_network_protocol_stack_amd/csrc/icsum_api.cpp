@@ -200,6 +200,16 @@ int ics_set_tick_server(ics_ctx* ctx, uint32_t idle_us) {
   return rc;
 }
 
+int ics_set_tick_server_blocks(ics_ctx* ctx, uint32_t blocks) {
+  if (int rc = bind(ctx)) return rc;
+  if (blocks < 1 || blocks > icsum::kSrvBlocksMax)
+    return fail(ICS_ERR_INVALID, "tick server blocks %u outside 1..%u", blocks, icsum::kSrvBlocksMax);
+  std::lock_guard<std::mutex> lock(ctx->mu);
+  const int rc = icsum::detail::server_stop(ctx);  // the next tick launches the new grid
+  ctx->srv_blocks = blocks;
+  return rc;
+}
+
 int ics_fold_batch(ics_ctx* ctx, const uint32_t* d_sum, uint16_t* d_out, uint64_t n, void* stream) {
   if (int rc = bind(ctx)) return rc;
   if (n == 0) return ICS_OK;

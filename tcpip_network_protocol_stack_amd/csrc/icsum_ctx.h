@@ -212,14 +212,16 @@ struct ics_ctx {
   size_t copy_threads = 8;
   std::unique_ptr<icsum::detail::WorkerPool> copy_pool;
   // resident tick server (ics_set_tick_server; icsum_host.cpp): zero-copy
-  // ticks of <= kTickSegs segments go to a kernel that stays resident
-  // between ticks and takes them from a mailbox in coherent page-locked
-  // memory — no launch per tick.  srv_idle_us 0: off.
+  // ticks of <= kTickSegs x srv_blocks segments go to a kernel that stays
+  // resident between ticks and takes them from mailboxes in coherent
+  // page-locked memory — no launch per tick.  srv_idle_us 0: off.
   uint32_t srv_idle_us = 0;
-  icsum::TickMailbox* h_mb = nullptr;
+  uint32_t srv_blocks = 4;  // resident blocks, one mailbox each (ics_set_tick_server_blocks; ICSUM_FORCE srv_blocks)
+  uint32_t srv_grid = 0;    // the blocks of the grid launched last
+  icsum::TickMailbox* h_mb = nullptr;  // kSrvBlocksMax mailboxes
   hipStream_t st_srv = nullptr;
-  uint32_t srv_seq = 0;       // the last job posted
-  bool srv_launched = false;  // a server was launched (its `state` word says whether it still runs)
+  uint32_t srv_seq[icsum::kSrvBlocksMax] = {};  // the last job posted to each mailbox
+  bool srv_launched = false;  // a server was launched (its `state` words say whether it still runs)
   uint64_t n_srv_jobs = 0, n_srv_launches = 0;
   uint32_t srv_pollers = 1;  // waves polling the mailbox, staggered (ICSUM_FORCE srv_pollers, 1..4)
 };

@@ -267,63 +267,105 @@ namespace {
 uint64_t mb_load(const uint64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 void mb_store(uint64_t* p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
 
+// a posted tick: its parts' sequence numbers, part p in mailbox p (parts 0: none)
+struct SrvTick {
+  uint32_t seq[icsum::kSrvBlocksMax];
+  uint32_t parts;
+};
+
+// every block of the grid launched last has left (block 0 leaves first, the
+// others within a poll of seeing its `state`): only then may a new grid
+// start, so no two blocks ever serve one mailbox
+bool server_gone(const ics_ctx* ctx) {
+  for (uint32_t b = 0; b < ctx->srv_grid; ++b)
+    if (mb_load(&ctx->h_mb[b].state) != icsum::kSrvExited) return false;
+  return true;
+}
+
 int server_launch(ics_ctx* ctx) {
   if (!ctx->h_mb) {
-    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_mb), sizeof(icsum::TickMailbox), hipHostMallocCoherent));
-    std::memset(static_cast<void*>(ctx->h_mb), 0, sizeof(icsum::TickMailbox));
+    const size_t sz = sizeof(icsum::TickMailbox) * icsum::kSrvBlocksMax;
+    ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_mb), sz, hipHostMallocCoherent));
+    std::memset(static_cast<void*>(ctx->h_mb), 0, sz);
     if (!host_pinned(ctx->h_mb).kernel) return fail(ICS_ERR_HIP, "tick server: mailbox not device-visible");
     ICS_HIP(hipStreamCreateWithFlags(&ctx->st_srv, hipStreamNonBlocking));
   }
-  mb_store(&ctx->h_mb->state, icsum::kSrvRunning);
-  const uint32_t expect = uint32_t(mb_load(&ctx->h_mb->done)) + 1u;  // the oldest job not done
-  ICS_HIP(icsum::launch_tick_server(ctx->h_mb, ctx->d_zero, expect, ctx->srv_idle_us, ctx->srv_pollers, ctx->st_srv));
+  // each block reads its mailbox's `done` at start: the oldest job not done
+  for (uint32_t b = 0; b < ctx->srv_blocks; ++b) mb_store(&ctx->h_mb[b].state, icsum::kSrvRunning);
+  ICS_HIP(icsum::launch_tick_server(ctx->h_mb, ctx->srv_blocks, ctx->d_zero, ctx->srv_idle_us, ctx->srv_pollers,
+                                    ctx->st_srv));
+  ctx->srv_grid = ctx->srv_blocks;
   ctx->srv_launched = true;
   ++ctx->n_srv_launches;
   return ICS_OK;
 }
 
-// the job's descriptor words, each stamped with its sequence number; the
-// server takes the job once every word it uses carries that number
+// (re)launch the grid when none runs; a grid part-way out is waited for
+int server_ensure(ics_ctx* ctx) {
+  if (ctx->srv_launched && mb_load(&ctx->h_mb[0].state) != icsum::kSrvExited) return ICS_OK;
+  if (ctx->srv_launched) {
+    const auto t0 = std::chrono::steady_clock::now();
+    while (!server_gone(ctx))
+      if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2))
+        return fail(ICS_ERR_HIP, "tick server: blocks still resident 2 s after block 0 left");
+  }
+  return server_launch(ctx);
+}
+
+// The tick's descriptors, sub-job b (segments [16 b, 16 b + 16) of n) into
+// mailbox b, each word stamped with that mailbox's sequence number (the
+// server takes a job once every word it uses carries the number); mailbox 0
+// last, so a tick is never seen by block 0 alone of the blocks it uses
 int server_post(ics_ctx* ctx, int op, int mode, const void* bytes, const uint32_t* init, void* res,
-                const uint64_t* rel_off, uint64_t stride, uint64_t seg_len, uint32_t n, uint32_t* seq) {
-  if (!ctx->srv_launched || mb_load(&ctx->h_mb->state) == icsum::kSrvExited)
-    if (int rc = server_launch(ctx)) return rc;
-  const uint32_t k = ++ctx->srv_seq;
-  const uint64_t stamp = uint64_t(k) << 32;
-  uint64_t* w = ctx->h_mb->w;
-  auto put = [&](uint32_t i, uint64_t v32) { __atomic_store_n(&w[i], stamp | (v32 & 0xffffffffull), __ATOMIC_RELAXED); };
+                const uint64_t* rel_off, uint64_t stride, uint64_t seg_len, uint32_t n, SrvTick* tick) {
+  if (int rc = server_ensure(ctx)) return rc;
+  const uint32_t parts = (n + icsum::kTickSegs - 1) / icsum::kTickSegs;
   // w[3..4]: the wrap's message records (device-visible); the checksum's
   // inits (the caller's host array) travel as words below, never as an address
   const uint64_t b = reinterpret_cast<uintptr_t>(bytes), ini = op == 2 ? reinterpret_cast<uintptr_t>(init) : 0,
                  r = reinterpret_cast<uintptr_t>(res);
-  for (uint32_t j = 0; j < n; ++j) {
-    const uint64_t s0 = rel_off ? rel_off[j] : j * stride;
-    put(icsum::kSrvHead + 2 * j, s0);
-    put(icsum::kSrvHead + 2 * j + 1, rel_off ? rel_off[j + 1] - s0 : seg_len);
-  }
   const bool inits = op == 0 && init;  // checksum inits: in the descriptor itself
-  if (inits)
-    for (uint32_t j = 0; j < n; ++j) put(icsum::kSrvInit + j, init[j]);
-  put(1, b);
-  put(2, b >> 32);
-  put(3, ini);
-  put(4, ini >> 32);
-  put(5, r);
-  put(6, r >> 32);
-  put(0, uint64_t(op) | (uint64_t(mode) << 4) | (uint64_t(n) << 8) | (uint64_t(inits) << 16));
+  for (uint32_t p = parts; p-- > 0;) {
+    const uint32_t k = ++ctx->srv_seq[p];
+    const uint64_t stamp = uint64_t(k) << 32;
+    uint64_t* w = ctx->h_mb[p].w;
+    auto put = [&](uint32_t i, uint64_t v32) {
+      __atomic_store_n(&w[i], stamp | (v32 & 0xffffffffull), __ATOMIC_RELAXED);
+    };
+    const uint32_t j0 = p * icsum::kTickSegs, m = std::min(n - j0, icsum::kTickSegs);
+    for (uint32_t j = 0; j < m; ++j) {
+      const uint64_t s0 = rel_off ? rel_off[j0 + j] : (j0 + j) * stride;
+      put(icsum::kSrvHead + 2 * j, s0);
+      put(icsum::kSrvHead + 2 * j + 1, rel_off ? rel_off[j0 + j + 1] - s0 : seg_len);
+    }
+    if (inits)
+      for (uint32_t j = 0; j < m; ++j) put(icsum::kSrvInit + j, init[j0 + j]);
+    put(1, b);
+    put(2, b >> 32);
+    put(3, ini);
+    put(4, ini >> 32);
+    put(5, r);
+    put(6, r >> 32);
+    put(icsum::kSrvPart, j0 | (uint64_t(n) << 8));
+    put(0, uint64_t(op) | (uint64_t(mode) << 4) | (uint64_t(m) << 8) | (uint64_t(inits) << 16));
+    tick->seq[p] = k;
+  }
+  tick->parts = parts;
   ++ctx->n_srv_jobs;
-  *seq = k;
   return ICS_OK;
 }
 
-// spin until the server reports job k done; a server that idled out (or hit
-// its lifetime) before taking the job is launched again, and it takes it
-int server_wait(ics_ctx* ctx, uint32_t k) {
+// spin until the server reports every part of the tick done; a server that
+// idled out (or hit its lifetime) before taking them is launched again, and
+// it takes them
+int server_wait(ics_ctx* ctx, const SrvTick& tick) {
   const auto t0 = std::chrono::steady_clock::now();
+  uint32_t p = 0;
   for (uint32_t i = 1;; ++i) {
-    if (int32_t(uint32_t(mb_load(&ctx->h_mb->done)) - k) >= 0) return ICS_OK;
+    while (p < tick.parts && int32_t(uint32_t(mb_load(&ctx->h_mb[p].done)) - tick.seq[p]) >= 0) ++p;
+    if (p == tick.parts) return ICS_OK;
     if ((i & 255) == 0) {
-      if (mb_load(&ctx->h_mb->state) == icsum::kSrvExited)
+      if (mb_load(&ctx->h_mb[0].state) == icsum::kSrvExited && server_gone(ctx))
         if (int rc = server_launch(ctx)) return rc;
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(2)) {
         (void)server_stop(ctx);
@@ -376,13 +418,13 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
   Chunk pending[ics_ctx::kMaxSlots];
   bool busy[ics_ctx::kMaxSlots] = {};
   uint64_t flag_of[ics_ctx::kMaxSlots] = {};  // zero-copy chunk: its completion word's value (0: event)
-  uint32_t srv_of[ics_ctx::kMaxSlots] = {};   // a tick-server job: its sequence number (0: none)
+  SrvTick srv_of[ics_ctx::kMaxSlots] = {};    // a tick-server job: its parts' sequence numbers (parts 0: none)
   uint32_t piece_sum = 0;  // running sum of the long segment whose pieces are in flight
   auto retire = [&](int k) -> int {
     if (!busy[k]) return ICS_OK;
-    if (srv_of[k]) {
-      const uint32_t job = srv_of[k];
-      srv_of[k] = 0;
+    if (srv_of[k].parts) {
+      const SrvTick job = srv_of[k];
+      srv_of[k].parts = 0;
       if (int rc = server_wait(ctx, job)) return rc;
     } else if (flag_of[k]) {
       if (int rc = wait_flag(ctx, k, flag_of[k])) return rc;
@@ -499,7 +541,8 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
     // a zero-copy tick of a few segments with offsets: the offsets travel in
     // the kernel arguments (k_tick), not as a dependent PCIe read
     const bool tick = zc && h_offsets && kind != 2 && m <= icsum::kTickSegs && ctx->tick_inline;
-    const bool srv = zc && m <= icsum::kTickSegs && ctx->srv_idle_us && (h_offsets || nb < (1u << 31));
+    const bool srv =
+        zc && m <= icsum::kTickSegs * ctx->srv_blocks && ctx->srv_idle_us && (h_offsets || nb < (1u << 31));
     if (srv) {  // the resident tick server takes it: no launch
       const uint32_t* d_init = nullptr;  // checksum: the inits; wrap: the message records
       void* out = res;
@@ -512,11 +555,9 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
         out = ctx->h_hdr[slot];
         dev_mode = mode;  // 1: payload only (headers apart)
       }
-      uint32_t k = 0;
       if (int rc = server_post(ctx, kind, dev_mode, in, d_init, out, h_offsets ? ctx->h_off[slot] : nullptr, stride,
-                               seg_len, uint32_t(m), &k))
+                               seg_len, uint32_t(m), &srv_of[slot]))
         return rc;
-      srv_of[slot] = k;
       note_host(ctx, ICS_K_TICK_SERVER, 16, 8);
     } else if (tick) {
       const uint32_t* d_init = nullptr;

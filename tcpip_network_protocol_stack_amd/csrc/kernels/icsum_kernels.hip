@@ -1751,17 +1751,32 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
 // system-scope release.  The server exits on the quit word, after idle_us
 // without a job, or after kSrvMaxLife of 100 MHz ticks (the host relaunches
 // it when a job finds it gone): every wave reaches an exit.
+// Several blocks (ics_ctx::srv_blocks): block b serves mailbox b, with its
+// own sequence numbers; a tick of n > 16 segments is split over mailboxes
+// 0 .. ceil(n / 16) - 1 (w[kSrvPart]: the sub-job's first segment and the
+// tick's n place its results), and every tick has a part in mailbox 0.  Block
+// 0 alone decides to leave (quit word, idle, lifetime) and says so in its
+// `state`; blocks b > 0 poll that word in place of the quit word and leave
+// once they see it, so the grid leaves as a whole and the host relaunches
+// only a grid that has fully left (no two blocks ever serve one mailbox).
 constexpr uint64_t kSrvMaxLife = 100000000ull;  // 1 s of s_memrealtime
 
-__global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const uint8_t* __restrict__ zpad,
-                                                        uint32_t expect, uint32_t idle_us, uint32_t pollers) {
+__global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mbs, const uint8_t* __restrict__ zpad,
+                                                        uint32_t idle_us, uint32_t pollers) {
   __shared__ uint32_t s_desc[64];
   __shared__ uint32_t s_cmd;  // 0 none yet, 1 a job, 2 exit
+  TickMailbox* const mb = mbs + blockIdx.x;
+  const bool lead = blockIdx.x == 0;
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t g = threadIdx.x >> 4, gl = threadIdx.x & 15u;
   const uint32_t* const zlast = reinterpret_cast<const uint32_t*>(zpad) + 7;
   const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
   uint64_t t_job = t0;
+  // the oldest job of this mailbox not done (the grid before this one has
+  // left: its last `done` store is final)
+  uint32_t expect = uint32_t(__hip_atomic_load(&mb->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) + 1u;
+  // lane 63's poll word: the quit word (block 0) or block 0's state
+  const uint64_t* const w63 = lead ? &mb->w[kSrvQuit] : &mbs[0].state;
   if (threadIdx.x == 0) s_cmd = 0u;
   __syncthreads();
   for (;;) {
@@ -1773,17 +1788,21 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const u
     if (wv < pollers) {
       for (uint32_t k = 0; k < wv; ++k) __builtin_amdgcn_s_sleep(14);  // ~0.4 us each
       while (__hip_atomic_load(&s_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
-        const uint64_t word = __hip_atomic_load(&mb->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const uint64_t word =
+            __hip_atomic_load(lane == kSrvQuit ? w63 : &mb->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t pay = uint32_t(word), seq = uint32_t(word >> 32);
         const uint32_t w0 = __builtin_amdgcn_readlane(pay, 0), s0 = __builtin_amdgcn_readlane(seq, 0);
         const uint32_t nj = (w0 >> 8) & 0xffu, nw = kSrvHead + 2u * nj;  // the words this job uses
         const bool inits = (w0 >> 16) & 1u;
-        const bool used = lane < nw || (inits && lane >= kSrvInit && lane < kSrvInit + nj);
+        const bool used = lane < nw || lane == kSrvPart || (inits && lane >= kSrvInit && lane < kSrvInit + nj);
         const bool fresh = !used || seq == expect;
         const bool job = s0 == expect && __all(fresh);
-        const bool quit = __builtin_amdgcn_readlane(uint32_t(word | (word >> 32)), kSrvQuit) != 0;
+        const uint64_t q = __builtin_amdgcn_readlane(uint32_t(word | (word >> 32)), kSrvQuit);
+        const bool quit = lead ? q != 0 : q == kSrvExited;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
-        const bool idle = now - t_job > uint64_t(idle_us) * 100u || now - t0 > kSrvMaxLife;
+        // blocks b > 0 leave with block 0 (their lifetime bound only a backstop)
+        const bool idle = lead ? now - t_job > uint64_t(idle_us) * 100u || now - t0 > kSrvMaxLife
+                               : now - t0 > 2 * kSrvMaxLife;
         if (job && !quit) s_desc[lane] = pay;  // (another poller may store the same words)
         if (job || quit || idle) {
           if (lane == 0) {
@@ -1809,6 +1828,8 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const u
     // the job: checksum (op 0) or the fused IPv4 item (op 1, mode), n <= 16
     // segments at [bytes + s_j, + len_j), results into the page-locked area
     const uint32_t w0 = s_desc[0], op = w0 & 0xfu, mode = (w0 >> 4) & 0xfu, n = (w0 >> 8) & 0xffu;
+    // the sub-job's segments are the tick's [first, first + n) of nt
+    const uint32_t first = s_desc[kSrvPart] & 0xffu, nt = (s_desc[kSrvPart] >> 8) & 0xffu;
     uint8_t* bytes = reinterpret_cast<uint8_t*>(uint64_t(s_desc[1]) | (uint64_t(s_desc[2]) << 32));
     const uint32_t* init = reinterpret_cast<const uint32_t*>(uint64_t(s_desc[3]) | (uint64_t(s_desc[4]) << 32));
     uint8_t* res = reinterpret_cast<uint8_t*>(uint64_t(s_desc[5]) | (uint64_t(s_desc[6]) << 32));
@@ -1827,14 +1848,14 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const u
       uint32_t ev = 0, od = 0;
       seg_sums<16, 8, true, 3>(bytes, s, e, gl, ev, od);
       const uint32_t tot = group_sum<16>(combine_roles(ev, od, uint32_t(s) & 1u));
-      if (valid && gl == 15) reinterpret_cast<uint16_t*>(res)[g] = uint16_t(fold_value(i0 + tot));
+      if (valid && gl == 15) reinterpret_cast<uint16_t*>(res)[first + g] = uint16_t(fold_value(i0 + tot));
     } else if (op == 2u) {
       // wrap_tcp_in_ip (tcp_over_ip.cpp:69-88) as k_tcp_wrap with its headers
       // to an array: the payload after 40 bytes of header room (mode 0) or
       // the segment alone (mode 1); the record (ics_tcp_msg) at `init`
       const bool ok = valid && (mode == 1u || e - s >= 40);
       const uint64_t p0 = ok ? (mode == 1u ? s : s + 40) : e;
-      const uint32_t* rec = iw + 7u * gi;  // 28-byte records
+      const uint32_t* rec = iw + 7u * (first + gi);  // 28-byte records
       uint32_t r[7];
 #pragma unroll
       for (int k = 0; k < 7; ++k) r[k] = rec[k];
@@ -1848,10 +1869,11 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mb, const u
       uint32_t wk = w[0];
 #pragma unroll
       for (uint32_t k = 1; k < 10; ++k) wk = gl == k ? w[k] : wk;
-      if (ok && gl < 10) reinterpret_cast<uint32_t*>(res)[10u * g + gl] = wk;
+      if (ok && gl < 10) reinterpret_cast<uint32_t*>(res)[10u * (first + g) + gl] = wk;
     } else {
       uint16_t* ip = reinterpret_cast<uint16_t*>(res);
-      ipv4_item<16, 8, true, 3>(bytes, s, e, g, valid, gl, int(mode), ip, ip + n, res + 4u * n, zpad, zlast);
+      ipv4_item<16, 8, true, 3>(bytes, s, e, g, valid, gl, int(mode), ip + first, ip + nt + first,
+                                res + 4u * nt + first, zpad, zlast);
     }
     // results out before `done` (signal_done's order): every wave's stores
     // retired, the block's barrier, one system-scope release
@@ -3032,10 +3054,10 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
   return hipGetLastError();
 }
 
-hipError_t launch_tick_server(TickMailbox* mb, const void* zero16, uint32_t expect, uint32_t idle_us,
+hipError_t launch_tick_server(TickMailbox* mbs, uint32_t blocks, const void* zero16, uint32_t idle_us,
                               uint32_t pollers, hipStream_t st) {
-  if (pollers < 1 || pollers > kBlock / 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_tick_server, dim3(1), dim3(kBlock), 0, st, mb, static_cast<const uint8_t*>(zero16), expect,
+  if (pollers < 1 || pollers > kBlock / 64 || blocks < 1 || blocks > kSrvBlocksMax) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_tick_server, dim3(blocks), dim3(kBlock), 0, st, mbs, static_cast<const uint8_t*>(zero16),
                      idle_us, pollers);
   return hipGetLastError();
 }

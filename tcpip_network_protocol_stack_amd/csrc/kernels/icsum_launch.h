@@ -204,11 +204,15 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
                        uint16_t* out, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
                        const void* zero16, const Done& done, hipStream_t st);
 
-// Resident tick server (k_tick_server): one block that stays resident and
-// takes per-tick jobs from this mailbox in coherent page-locked host memory.
+// Resident tick server (k_tick_server): 1..kSrvBlocksMax blocks that stay
+// resident, block b taking per-tick jobs from mailbox b of an array in
+// coherent page-locked host memory (a tick of n segments: sub-jobs of <= 16
+// in mailboxes 0 .. ceil(n / 16) - 1, each with its own sequence numbers).
 // Descriptor word k = payload (low 32 bits) | job sequence number (high 32):
 //   w[0] = op (0 checksum, 1 fused IPv4, 2 wrap) | mode << 4 | n << 8
-//          (n <= kTickSegs) | inits in the descriptor << 16
+//          (the sub-job's n <= kTickSegs) | inits in the descriptor << 16
+//   w[kSrvPart] = the sub-job's first segment in the tick | the tick's n << 8
+//          (results: value first + j of the tick's result arrays)
 //   w[1], w[2] = the bytes' (device-visible) address, low / high half
 //   w[3], w[4] = the wrap's message records (op 2)
 //   w[5], w[6] = the result area: u16 x n values (op 0) or u16 ip, u16 tcp,
@@ -217,9 +221,12 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
 //                the bytes) and length
 //   w[kSrvInit + j] = segment j's init (op 0 with w[0] bit 16 set: the inits
 //                travel in the descriptor, not as a PCIe read of their own)
-// w[kSrvQuit] != 0: exit.  The device writes `done` (the last finished
-// sequence number) and, when it exits, `state` = kSrvExited.
-constexpr uint32_t kSrvHead = 7, kSrvInit = kSrvHead + 2 * kTickSegs, kSrvQuit = 63;
+// Mailbox 0's w[kSrvQuit] != 0: exit.  Block b writes mailbox b's `done` (the
+// last finished sequence number) and, when it exits, `state` = kSrvExited;
+// blocks b > 0 leave once mailbox 0's `state` says block 0 has.
+constexpr uint32_t kSrvHead = 7, kSrvInit = kSrvHead + 2 * kTickSegs, kSrvPart = kSrvInit + kTickSegs,
+                   kSrvQuit = 63;
+constexpr uint32_t kSrvBlocksMax = 8;  // ticks of up to 128 segments
 constexpr uint64_t kSrvRunning = 1, kSrvExited = 2;
 struct alignas(256) TickMailbox {
   uint64_t w[64];
@@ -227,8 +234,8 @@ struct alignas(256) TickMailbox {
   uint64_t state;
   uint64_t pad[30];
 };
-static_assert(kSrvInit + kTickSegs <= kSrvQuit, "the descriptor fits below the quit word");
-hipError_t launch_tick_server(TickMailbox* mb, const void* zero16, uint32_t expect, uint32_t idle_us,
+static_assert(kSrvPart < kSrvQuit, "the descriptor fits below the quit word");
+hipError_t launch_tick_server(TickMailbox* mbs, uint32_t blocks, const void* zero16, uint32_t idle_us,
                               uint32_t pollers, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg

@@ -74,9 +74,14 @@ class Engine:
 
     def set_tick_server(self, idle_us):
         """ics_set_tick_server: idle_us > 0 keeps a resident kernel that takes
-        the zero-copy *_host calls of <= 16 segments without a launch (it
-        leaves after idle_us without a call); 0 stops it."""
+        the zero-copy *_host calls of <= 16 x blocks segments without a launch
+        (it leaves after idle_us without a call); 0 stops it."""
         self._check(self.lib.ics_set_tick_server(self.ctx, int(idle_us)))
+
+    def set_tick_server_blocks(self, blocks):
+        """ics_set_tick_server_blocks: the resident server's blocks, 1..8
+        (default 4), 16 segments per block."""
+        self._check(self.lib.ics_set_tick_server_blocks(self.ctx, int(blocks)))
 
     def dispatch_info(self):
         """ics_dispatch_info: {'plan_hits', 'plan_misses', 'plan_requests',
