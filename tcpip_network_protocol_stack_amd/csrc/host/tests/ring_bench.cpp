@@ -322,6 +322,9 @@ int main(int argc, char** argv)
         const char* srv_env = std::getenv("RING_TICK_SERVER");
         const uint32_t srv_idle = srv_env ? uint32_t(std::strtoul(srv_env, nullptr, 10)) : 0u;
         if (srv_idle) eng.set_tick_server(srv_idle);
+        // RING_TICK_SERVER_BLOCKS=1..8: the server's blocks (default 4: 64 datagrams)
+        if (const char* blk = std::getenv("RING_TICK_SERVER_BLOCKS"))
+            eng.set_tick_server_blocks(uint32_t(std::strtoul(blk, nullptr, 10)));
         TCPOverIPv4Adapter a, b;
         a.config_mut().source = Address{"10.1.2.3", 4321};
         a.config_mut().destination = Address{"10.9.8.7", 80};
