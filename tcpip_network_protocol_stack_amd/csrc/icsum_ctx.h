@@ -89,8 +89,6 @@ struct ics_ctx {
   int tile = -1;
   uint32_t span_segs = 0;
   uint32_t span_blocks = 0;  // test hook: grid cap of the tile launch (0: none), reaches its grid-stride form
-  int tile_piece = 0;           // tile launches: 0 k_span (window loop), 1 k_piece (one-shot pieces)
-  uint32_t piece_bytes = 6144;  // k_piece: segment bytes per span (span_segs_for)
   int slot_prio = 0;    // staging-slot stream priority (ICSUM_FORCE slot_prio; 0: default stream creation)
   int tick_inline = 1;  // zero-copy ticks of <= kTickSegs offsets segments through k_tick (ICSUM_FORCE tick_inline=0: off)
   static constexpr uint64_t kSpanBytes = 20 << 10;  // segment bytes per span (span_segs_for)

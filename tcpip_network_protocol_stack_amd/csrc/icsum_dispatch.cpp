@@ -28,9 +28,8 @@ static_assert(icsum::kBvDense64 == ICS_BV_DENSE64 && icsum::kBvTiny == ICS_BV_TI
 // 265.9 — flat from about 16 to 40 KiB per span.
 uint32_t span_segs_for(const ics_ctx* ctx, uint32_t avg) {
   if (ctx->span_segs) return ctx->span_segs;
-  const uint64_t target = ctx->tile_piece ? ctx->piece_bytes : ics_ctx::kSpanBytes;
-  if (avg == 0) return ctx->tile_piece ? uint32_t(std::clamp<uint64_t>(target / 1024, 1, 63)) : 63;
-  return uint32_t(std::clamp<uint64_t>(target / avg, 1, 63));
+  if (avg == 0) return 63;
+  return uint32_t(std::clamp<uint64_t>(ics_ctx::kSpanBytes / avg, 1, 63));
 }
 
 bool wrap_two_pass(const ics_ctx* ctx, bool headers_apart, uint64_t n) {
@@ -234,7 +233,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
   }
   if (sp.offsets && ctx->tile == 1) {  // test hook: the tile launch on every offsets batch
     const uint32_t S = span_segs_for(ctx, 0);
-    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st, ctx->span_blocks, ctx->tile_piece != 0));
+    ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st, ctx->span_blocks));
     note(ctx, ICS_K_TILE, {int(S), ICS_TILE_CHECKSUM, true, 0, 1});
     return ICS_OK;
   }
@@ -291,7 +290,7 @@ int checksum_device(ics_ctx* ctx, const icsum::SegSpec& sp, const uint32_t* d_in
     const bool mix8 = hit && hit_plan != icsum::kPlanWholeBatchSmall && short_mix(mix);
     if (hit && !mix8 && hit_plan != icsum::kPlanWholeBatchSmall && tile_wins(ctx, mix, sp.n, false)) {
       const uint32_t S = span_segs_for(ctx, mix.avg);
-      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st, ctx->span_blocks, ctx->tile_piece != 0));
+      ICS_HIP(icsum::launch_tile_checksum(sp, d_init, d_odd, d_out, out_kind, S, st, ctx->span_blocks));
       note(ctx, ICS_K_TILE, {int(S), ICS_TILE_CHECKSUM, true, 0, 1}, int(hit_plan));
       return replan(ctx, sp, lps, req, st);
     }
@@ -396,7 +395,7 @@ int ipv4_device(ics_ctx* ctx, const icsum::SegSpec& sp, int mode, uint16_t* d_ip
   }
   if (d_offsets && (ctx->tile == 1 || tile)) {  // the test hook, or the cached mix favours the tile launch
     const uint32_t S = span_segs_for(ctx, span_avg);
-    ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, S, st, ctx->span_blocks, ctx->tile_piece != 0));
+    ICS_HIP(icsum::launch_tile_ipv4(sp, mode, d_ip_ck, d_tcp_ck, d_status, S, st, ctx->span_blocks));
     note(ctx, ICS_K_TILE, {int(S), ICS_TILE_IPV4, true, 0, 1}, plan_used);
     return replan(ctx, sp, 64, req, st);
   }
@@ -481,7 +480,7 @@ int wrap_device(ics_ctx* ctx, const icsum::SegSpec& sp, const ics_tcp_msg* d_msg
   if (sp.offsets && (ctx->tile == 1 || tile_pick)) {  // the wrap (in place or headers apart) as a tile launch
     const uint32_t S = span_segs_for(ctx, plan >= 0 ? mix.avg : 0u);
     ICS_HIP(icsum::launch_tile_wrap(sp, reinterpret_cast<const icsum::TcpMsg*>(d_msgs), hdr_out, d_ip_ck, d_tcp_ck,
-                                    S, st, ctx->span_blocks, ctx->tile_piece != 0));
+                                    S, st, ctx->span_blocks));
     note(ctx, ICS_K_TILE, {int(S), hdr_out ? ICS_TILE_WRAP_APART : ICS_TILE_WRAP, true, 0, 1}, plan);
     return replan(ctx, sp, 64, req, st);
   }
@@ -629,9 +628,6 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "tick_server" && v >= 0 && v <= 10000000) ctx->srv_idle_us = uint32_t(v);
     else if (k == "srv_pollers" && v >= 1 && v <= 4) ctx->srv_pollers = uint32_t(v);
     else if (k == "srv_blocks" && v >= 1 && v <= int64_t(icsum::kSrvBlocksMax)) ctx->srv_blocks = uint32_t(v);
-    else if (k == "tile_piece" && (v == 0 || v == 1)) ctx->tile_piece = int(v);
-    else if (k == "piece_k" && (v == 7 || v == 12)) icsum::set_piece_k(uint32_t(v));
-    else if (k == "piece_bytes" && v >= 256 && v <= (1 << 20)) ctx->piece_bytes = uint32_t(v);
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);

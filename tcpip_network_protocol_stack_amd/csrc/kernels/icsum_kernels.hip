@@ -2438,203 +2438,6 @@ __global__ __launch_bounds__(kBlock) void k_span(uint8_t* __restrict__ bytes, co
   }
 }
 
-// ------------------------------------- one-shot span pieces (round 6) -----
-// k_piece: the spans of k_span (wave w owns segments [S w, S w + m)), their
-// bytes streamed with k_checksum's footprint instead of a window loop: the
-// span's byte range [off[i0] & ~127, off[i0 + m]) is cut into four
-// line-anchored pieces, one per 16-lane group, each lane issuing up to
-// kPieceK dwordx4 global loads at once (chunk 16 u + l of its piece), so a
-// short span is one round of loads per wave, like a one-shot k_checksum wave
-// (the footprint that streams at 88-90 % of 8 TB/s where a wave's sequential
-// windows reach 84-87 %, profiles/r5_probe_footprint.jsonl,
-// r5_probe_stream_*.jsonl).  A span longer than 4 x 112 chunks takes passes of
-// 4 x 112.  Each lane's chunk sums are scanned per group (DPP row scans per
-// load slot), the groups' totals added in span order, and every chunk's
-// prefix F written to the wave's LDS table (8 B per chunk).  Each point's own
-// chunk is loaded by its lane before the stream with the default policy (the
-// primed boundary lines of k_checksum: a neighbouring group's load of the
-// same line then hits L2), so F(point) = table[chunk] + the point's chunk
-// masked below it, and segment t's sums are F(A_{t+1}) - F(B_t) as in
-// k_span (span_outputs).
-// K: loads per lane per pass (7: 112 chunks = 1792 B per group, 7 KiB per
-// wave pass; 12: 3 KiB per group, 12 KiB per wave pass)
-
-// inclusive scan over each row of 16 lanes (a 16-lane group)
-__device__ __forceinline__ uint32_t row_prefix_incl(uint32_t x) {
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x111, 0xF, 0xF, false);  // row_shr:1
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x112, 0xF, 0xF, false);  // row_shr:2
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x114, 0xF, 0xF, false);  // row_shr:4
-  x += __builtin_amdgcn_update_dpp(0u, x, 0x118, 0xF, 0xF, false);  // row_shr:8
-  return x;
-}
-
-__device__ __forceinline__ uint32_t row_last(uint32_t x) {
-  return __builtin_amdgcn_update_dpp(0u, x, 0x15F, 0xF, 0xF, false);  // row_newbcast:15
-}
-
-__device__ __forceinline__ uint32_t chunk_word(const u32x4& v, uint32_t k) {
-  return k == 0 ? v.x : k == 1 ? v.y : k == 2 ? v.z : v.w;
-}
-
-template <int OP, int OUT, int kPieceK>
-__global__ __launch_bounds__(kBlock) void k_piece(uint8_t* __restrict__ bytes, const uint64_t* __restrict__ off,
-                                                  uint64_t n, uint32_t S, TileArgs a, uint32_t remap,
-                                                  const u32x4* __restrict__ zero16) {
-  constexpr uint32_t kPieceGroupChunks = 16u * uint32_t(kPieceK);  // chunks per group per pass
-  constexpr uint32_t kPieceTab = 4u * kPieceGroupChunks;           // chunks per wave pass
-  constexpr bool TWO = OP == kTileIpv4 || OP == kTileWrap;  // a second point per lane: lo_t
-  constexpr uint32_t kWaves = kBlock / 64;
-  __shared__ uint32_t s_tab[kWaves][kPieceTab][2];  // per pass: every chunk's prefix; then the wraps' header stage
-  const uint32_t lane = threadIdx.x & 63u, gq = lane >> 4, gl = lane & 15u;
-  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const uint32_t bsh = frame_shift(bytes);  // the kernel's frame (icsum_device.h)
-  bytes -= bsh;
-  const uint64_t nspans = (n + S - 1) / S;
-  const uint64_t span = uint64_t(block_order(remap)) * kWaves + wv;
-  if (span >= nspans) return;  // wave-uniform; no block barrier anywhere
-  const uint64_t i0 = span * S;
-  const uint32_t m = uint32_t(n - i0 < S ? n - i0 : S);
-  const bool valid = lane < m;
-  const uint64_t i = i0 + (valid ? lane : 0u);
-  // point A (one load per lane) and the span's range (two scalar loads)
-  const uint64_t x = off[i0 + (lane <= m ? lane : m)] + bsh;
-  const uint64_t first = off[i0] + bsh, tend = off[i0 + m] + bsh;
-  uint32_t w0 = 0, w1 = 0;
-  if constexpr (OP == kTileSum) {
-    w0 = a.init[i * a.init_step];
-    w1 = a.odd[i * a.odd_step];
-  }
-  const uint64_t a0c = (first >> 7) << 3;  // the line holding the first byte, in chunks
-  const uint64_t nch = tend > (a0c << 4) ? ((tend + 15) >> 4) - a0c : 0;
-  const uint64_t passes = nch <= kPieceTab ? 1 : (nch + kPieceTab - 1) / kPieceTab;
-  // chunks per group per pass: a short span split evenly over the four
-  // groups (line multiples), a long one in blocks of 16 K
-  const uint32_t Bc = passes > 1 ? kPieceGroupChunks : uint32_t(((nch + 3) / 4 + 7) & ~uint64_t(7));
-  const u32x4* const cb = reinterpret_cast<const u32x4*>(bytes) + a0c;
-  [[maybe_unused]] const uint8_t* const env_lo = bytes + (a0c << 4);
-  [[maybe_unused]] const uint8_t* const env_hi = env_lo + (nch << 4);
-  u32x4 v[kPieceK];
-  auto load_pass = [&](uint64_t p) {
-    const uint64_t pbase = p * 4u * Bc;
-#pragma unroll
-    for (int u = 0; u < kPieceK; ++u) {
-      const uint32_t r = 16u * uint32_t(u) + gl;
-      const uint64_t c = pbase + uint64_t(gq) * Bc + r;
-      const bool ok = r < Bc && c < nch;
-      if (ok) ICS_CHECK16(cb + c, env_lo, env_hi);
-      v[u] = __builtin_nontemporal_load(ok ? cb + c : zero16);
-    }
-  };
-  // the first pass's stream goes out on the scalar range alone, before
-  // anything that waits for the vector offsets load (the points' chunks
-  // below are requested behind it and hit the lines it brings in)
-  load_pass(0);
-  __builtin_amdgcn_sched_barrier(0);
-  // the point's own chunk (its bytes below the point enter F)
-  const uint64_t e = shfl_down64(x);
-#ifdef ICSUM_BOUNDS_CHECK
-  if (valid && e < x) bounds_fail(kBoundsOffsets, i);
-#endif
-  const bool hdr = OP == kTileIpv4 && valid && e - x >= 20;
-  const uint64_t pc = lane <= m ? (x >> 4) - a0c : ~uint64_t(0);
-  const bool has_a = pc < nch;
-  if (has_a) ICS_CHECK16(cb + pc, env_lo, env_hi);
-  const u32x4 pa = *(has_a ? cb + pc : zero16);
-  // point B where it needs no loaded byte: the in-place wrap's payload start
-  uint64_t lo = x;
-  if constexpr (OP == kTileWrap) lo = valid && e - x >= 40 ? x + 40 : e;
-  uint64_t qc = TWO ? (lo >> 4) - a0c : pc;
-  u32x4 pb = pa;
-  if constexpr (OP == kTileWrap) {
-    const bool load_b = valid && qc != pc && qc < nch;
-    if (load_b) ICS_CHECK16(cb + qc, env_lo, env_hi);
-    pb = *(load_b ? cb + qc : zero16);
-    if (!(valid && qc < nch)) pb = u32x4{0u, 0u, 0u, 0u};
-    else if (qc == pc) pb = pa;
-  }
-  uint32_t ce = 0, co = 0;  // the span's sums before the current pass
-  uint32_t fe = 0, fo = 0, ge = 0, go = 0;
-  uint32_t* const tab = &s_tab[wv][0][0];
-  for (uint64_t p = 0; p < passes; ++p) {  // wave-uniform
-    const uint64_t pbase = p * 4u * Bc;
-    if (p > 0) load_pass(p);
-    if constexpr (OP == kTileIpv4) {
-      if (p == 0) {
-        // point B = start + 4 IHL (options skipped, ipv4_header.cpp:50): the
-        // header's first byte is in the point's own chunk
-        const uint32_t xb = uint32_t(x) & 15u;
-        const uint32_t b0 = (chunk_word(pa, xb >> 2) >> (8u * (xb & 3u))) & 0xffu;
-        uint64_t o = 4u * (b0 & 0x0fu);
-        if (o < 20) o = 20;
-        if (hdr && o > e - x) o = e - x;
-        lo = hdr ? x + o : e;
-        qc = (lo >> 4) - a0c;
-        const bool load_b = valid && qc != pc && qc < nch;
-        if (load_b) ICS_CHECK16(cb + qc, env_lo, env_hi);
-        const u32x4 t = *(load_b ? cb + qc : zero16);
-        pb = !(valid && qc < nch) ? u32x4{0u, 0u, 0u, 0u} : (qc == pc ? pa : t);
-      }
-    }
-    // per-chunk sums, scanned per group in chunk order (r = 16 u + l); the
-    // table takes each chunk's prefix within its group as soon as it is
-    // known (the groups' bases are added when a point reads it)
-    uint32_t re = 0, ro = 0;  // the group's running total (row-uniform)
-#pragma unroll
-    for (int u = 0; u < kPieceK; ++u) {
-      uint32_t ev = 0, od = 0;
-      acc_chunk(v[u], ev, od);
-      const uint32_t ie = row_prefix_incl(ev), io = row_prefix_incl(od);
-      const uint32_t r = 16u * uint32_t(u) + gl;
-      if (r < Bc) {
-        tab[2u * (gq * Bc + r)] = re + ie - ev;
-        tab[2u * (gq * Bc + r) + 1u] = ro + io - od;
-      }
-      re += row_last(ie);
-      ro += row_last(io);
-    }
-    // the four groups' totals in span order (scalars)
-    const uint32_t g0e = __builtin_amdgcn_readlane(re, 0), g1e = __builtin_amdgcn_readlane(re, 16),
-                   g2e = __builtin_amdgcn_readlane(re, 32), g3e = __builtin_amdgcn_readlane(re, 48);
-    const uint32_t g0o = __builtin_amdgcn_readlane(ro, 0), g1o = __builtin_amdgcn_readlane(ro, 16),
-                   g2o = __builtin_amdgcn_readlane(ro, 32), g3o = __builtin_amdgcn_readlane(ro, 48);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // F at the points whose chunk this pass covered: the span's sums before
-    // the chunk's group + the table's prefix + the chunk's bytes below the point
-    auto table_F = [&](uint64_t c, uint32_t b, const u32x4& chunk, uint32_t& fe_, uint32_t& fo_) {
-      const uint32_t k = uint32_t(c - pbase);
-      const uint32_t g = (k >= Bc) + (k >= 2u * Bc) + (k >= 3u * Bc);
-      fe_ = ce + (g > 0 ? g0e : 0u) + (g > 1 ? g1e : 0u) + (g > 2 ? g2e : 0u) + tab[2u * k];
-      fo_ = co + (g > 0 ? g0o : 0u) + (g > 1 ? g1o : 0u) + (g > 2 ? g2o : 0u) + tab[2u * k + 1u];
-      acc_chunk(chunk & byte_range_mask(0u, b), fe_, fo_);
-    };
-    const uint64_t pend = pbase + 4u * Bc;
-    if (pc >= pbase && pc < pend && pc < nch) table_F(pc, uint32_t(x) & 15u, pa, fe, fo);
-    if constexpr (TWO) {
-      if (valid && qc >= pbase && qc < pend && qc < nch) table_F(qc, uint32_t(lo) & 15u, pb, ge, go);
-    }
-    ce += g0e + g1e + g2e + g3e;
-    co += g0o + g1o + g2o + g3o;
-    __builtin_amdgcn_wave_barrier();  // the next pass rewrites the table
-  }
-  // a point at the aligned end of the last chunk: every byte is below it
-  if (lane <= m && pc >= nch) {
-    fe = ce;
-    fo = co;
-  }
-  if constexpr (TWO) {
-    if (valid && qc >= nch) {
-      ge = ce;
-      go = co;
-    }
-  } else {
-    ge = fe;
-    go = fo;
-  }
-  span_outputs<OP, OUT>(bytes, a, lane, valid, i, i0, m, x, e, lo, hdr, fe, fo, ge, go, w0, w1, tab);
-}
-
 // ------------------------------------------------- workload spec ---------
 constexpr uint64_t kGolden = 0x9E3779B97F4A7C15ull;
 
@@ -2847,7 +2650,6 @@ inline uint32_t blocks_for(uint64_t groups, uint32_t groups_per_block, uint32_t 
   return uint32_t(b < cap ? b : cap);
 }
 
-uint32_t g_piece_k = 7;  // k_piece loads per lane per pass (7 or 12; ICSUM_FORCE piece_k, process-wide like xcd_remap)
 uint32_t g_xcd_remap = 10;  // log2 of the XCD run length of block_order (1024 blocks); 0: hardware order
 
 inline SegSrc src_of(const SegSpec& sp) {
@@ -2964,23 +2766,13 @@ hipError_t launch_wrap_t(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_ou
 
 // k_span: one wave per S segments, four independent waves per block
 template <int OP, int OUT>
-hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, uint32_t S, hipStream_t st, uint32_t max_blocks,
-                         bool piece) {
+hipError_t launch_span_t(const SegSpec& sp, const TileArgs& a, uint32_t S, hipStream_t st, uint32_t max_blocks) {
   if (!sp.offsets || sp.list || sp.n == 0 || S == 0 || S > kSpanSegs) return hipErrorInvalidValue;
   const uint64_t waves = (sp.n + S - 1) / S;
   const uint64_t blocks = (waves + kBlock / 64 - 1) / (kBlock / 64);
   const uint64_t cap = max_blocks && max_blocks < kMaxGridBlocks ? max_blocks : kMaxGridBlocks;
   uint8_t* const bytes = const_cast<uint8_t*>(sp.bytes);
   const u32x4* const z = static_cast<const u32x4*>(sp.zero16);
-  if (piece && blocks <= cap) {  // one-shot span pieces (k_piece); a grid-stride batch takes k_span
-    if (g_piece_k == 12)
-      hipLaunchKernelGGL((k_piece<OP, OUT, 12>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, bytes, sp.offsets, sp.n,
-                         S, a, g_xcd_remap, z);
-    else
-      hipLaunchKernelGGL((k_piece<OP, OUT, 7>), dim3(uint32_t(blocks)), dim3(kBlock), 0, st, bytes, sp.offsets, sp.n,
-                         S, a, g_xcd_remap, z);
-    return hipGetLastError();
-  }
   if (blocks > cap)  // more spans than one grid: grid-stride
     hipLaunchKernelGGL((k_span<OP, OUT, true>), dim3(uint32_t(cap)), dim3(kBlock), 0, st, bytes,
                        sp.offsets, sp.n, S, a, g_xcd_remap, z);
@@ -3144,7 +2936,6 @@ hipError_t launch_checksum_bins(const SegSpec& sp, const uint32_t* init, const u
 }
 
 void set_xcd_remap(uint32_t run_log2) { g_xcd_remap = run_log2 < 31 ? run_log2 : 31; }
-void set_piece_k(uint32_t k) { g_piece_k = k == 12 ? 12u : 7u; }
 
 bool bounds_checked_build() {
 #ifdef ICSUM_BOUNDS_CHECK
@@ -3272,36 +3063,36 @@ hipError_t launch_tick_server(TickMailbox* mbs, uint32_t blocks, const void* zer
 }
 
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t S, hipStream_t st, uint32_t max_blocks, bool piece) {
+                                uint32_t S, hipStream_t st, uint32_t max_blocks) {
   TileArgs a{};
   a.init = init ? init : static_cast<const uint32_t*>(sp.zero16);
   a.odd = odd ? odd : static_cast<const uint8_t*>(sp.zero16);
   a.init_step = init ? 1u : 0u;
   a.odd_step = odd ? 1u : 0u;
   a.out = out;
-  return out_kind == 0 ? launch_span_t<kTileSum, 0>(sp, a, S, st, max_blocks, piece)
-                       : launch_span_t<kTileSum, 1>(sp, a, S, st, max_blocks, piece);
+  return out_kind == 0 ? launch_span_t<kTileSum, 0>(sp, a, S, st, max_blocks)
+                       : launch_span_t<kTileSum, 1>(sp, a, S, st, max_blocks);
 }
 
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                            uint32_t S, hipStream_t st, uint32_t max_blocks, bool piece) {
+                            uint32_t S, hipStream_t st, uint32_t max_blocks) {
   TileArgs a{};
   a.mode = mode;
   a.ip_ck = ip_ck;
   a.tcp_ck = tcp_ck;
   a.status = status;
-  return launch_span_t<kTileIpv4, 0>(sp, a, S, st, max_blocks, piece);
+  return launch_span_t<kTileIpv4, 0>(sp, a, S, st, max_blocks);
 }
 
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t S, hipStream_t st, uint32_t max_blocks, bool piece) {
+                            uint16_t* tcp_ck, uint32_t S, hipStream_t st, uint32_t max_blocks) {
   TileArgs a{};
   a.msgs = msgs;
   a.hdr_out = hdr_out;
   a.ip_ck = ip_ck;
   a.tcp_ck = tcp_ck;
-  return hdr_out ? launch_span_t<kTileWrapApart, 0>(sp, a, S, st, max_blocks, piece)
-                 : launch_span_t<kTileWrap, 0>(sp, a, S, st, max_blocks, piece);
+  return hdr_out ? launch_span_t<kTileWrapApart, 0>(sp, a, S, st, max_blocks)
+                 : launch_span_t<kTileWrap, 0>(sp, a, S, st, max_blocks);
 }
 
 uint64_t batchv_blocks(int cls, uint64_t n) {

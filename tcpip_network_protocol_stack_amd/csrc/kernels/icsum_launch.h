@@ -163,8 +163,6 @@ hipError_t launch_ipv4_batchv(const BvDgram* b, int k, int cls, int mode, const 
 
 // XCD-aware block order of k_checksum / k_ipv4_tcp launches (process-wide)
 void set_xcd_remap(uint32_t run_log2);
-// k_piece's loads per lane per pass (7 or 12; process-wide, a dev knob)
-void set_piece_k(uint32_t k);
 hipError_t launch_fold(const uint32_t* sum, uint16_t* out, uint64_t n, hipStream_t st);
 hipError_t launch_ipv4_tcp(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck,
                            uint8_t* status, Geometry g, uint32_t max_blocks, hipStream_t st);
@@ -187,13 +185,11 @@ hipError_t launch_router_hdrs(const SegSpec& sp, uint32_t* hdr_out, uint8_t* sta
 // (mode as launch_ipv4_tcp) and the in-place wrap (as launch_tcp_wrap in place).
 // max_blocks (test hook ICSUM_FORCE span_blocks; 0: none): a grid of more
 // blocks runs the grid-stride instantiation with that many, as batches of
-// more spans than 2^24 blocks hold do.  piece: the spans as one-shot pieces
-// (k_piece, four 16-lane groups per wave loading the span at once) instead
-// of k_span's window loop; a grid-stride launch always takes k_span.
+// more spans than 2^24 blocks hold do.
 hipError_t launch_tile_checksum(const SegSpec& sp, const uint32_t* init, const uint8_t* odd, void* out, int out_kind,
-                                uint32_t S, hipStream_t st, uint32_t max_blocks = 0, bool piece = false);
+                                uint32_t S, hipStream_t st, uint32_t max_blocks = 0);
 hipError_t launch_tile_ipv4(const SegSpec& sp, int mode, uint16_t* ip_ck, uint16_t* tcp_ck, uint8_t* status,
-                            uint32_t S, hipStream_t st, uint32_t max_blocks = 0, bool piece = false);
+                            uint32_t S, hipStream_t st, uint32_t max_blocks = 0);
 
 // Per-tick zero-copy host calls (k_tick): at most kTickSegs segments of an
 // offsets batch in one block, the n + 1 offsets (relative to `bytes`) copied
@@ -263,7 +259,7 @@ hipError_t launch_tcp_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_
 // the wrap as a tile launch: in place (hdr_out null) or, with hdr_out, the
 // payload-only batch of ics_tcp_wrap_headers with its headers to hdr_out
 hipError_t launch_tile_wrap(const SegSpec& sp, const TcpMsg* msgs, uint32_t* hdr_out, uint16_t* ip_ck,
-                            uint16_t* tcp_ck, uint32_t S, hipStream_t st, uint32_t max_blocks = 0, bool piece = false);
+                            uint16_t* tcp_ck, uint32_t S, hipStream_t st, uint32_t max_blocks = 0);
 // pass 2 of the two-pass wrap alone (k_tcp_hdr): headers from the records and
 // the payload sums pass 1 left in `sums` (roles from each payload's start)
 hipError_t launch_tcp_hdr(const SegSpec& sp, const TcpMsg* msgs, const uint32_t* sums, uint32_t* hdr_out,

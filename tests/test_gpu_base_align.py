@@ -46,13 +46,11 @@ CSUM_FORCE = [None, {"lps": 16, "unroll": 8, "mode": 3}, {"lps": 64, "unroll": 8
               {"lps": 8, "unroll": 8, "mode": 3}, {"lps": 4, "unroll": 2, "mode": 2, "segs": 2},
               {"lps": 1, "unroll": 4, "mode": 4}, {"twoclass": 16}, {"twoclass": 32},
               {"bin": 1, "bin_plan": 1}, {"bin": 1, "bin_plan": 0}, {"bin": 1, "bin_plan": 2},
-              {"bin": 1, "bin_plan": 3}, {"tile": 1}, {"tile": 1, "span_segs": 7}, {"tile": 1, "tile_piece": 1},
-              {"tile": 1, "tile_piece": 1, "span_segs": 9}]
+              {"bin": 1, "bin_plan": 3}, {"tile": 1}, {"tile": 1, "span_segs": 7}]
 IPV4_FORCE = [None, {"lps": 16, "unroll": 8, "mode": 3}, {"lps": 4, "unroll": 1, "mode": 2},
               {"lps": 1, "unroll": 4, "mode": 0}, {"twoclass": 16}, {"twoclass": 32}, {"tile": 1},
-              {"tile": 1, "span_segs": 1}, {"tile": 1, "tile_piece": 1}, {"tile": 1, "tile_piece": 1, "span_segs": 1}]
-WRAP_FORCE = [None, {"wrap_passes": 1}, {"wrap_passes": 2}, {"tile": 1}, {"tile": 1, "span_segs": 7},
-              {"tile": 1, "tile_piece": 1}, {"tile": 1, "tile_piece": 1, "span_segs": 3}]
+              {"tile": 1, "span_segs": 1}]
+WRAP_FORCE = [None, {"wrap_passes": 1}, {"wrap_passes": 2}, {"tile": 1}, {"tile": 1, "span_segs": 7}]
 # fixed-stride batches never take the offsets-only launches (two-class, binned, tile)
 CSUM_FIXED_FORCE = [f for f in CSUM_FORCE if not f or not ({"tile", "twoclass", "bin"} & set(f))]
 IPV4_FIXED_FORCE = [f for f in IPV4_FORCE if not f or not ({"tile", "twoclass"} & set(f))]

@@ -28,11 +28,7 @@ pytestmark = pytest.mark.gpu
 # blocks by the span_blocks hook, so each wave runs many spans in turn and
 # reuses its LDS windows and register sets across them
 TILE_FORCE = [{"tile": 1}, {"tile": 1, "span_segs": 1}, {"tile": 1, "span_segs": 7},
-              {"tile": 1, "span_segs": 1, "span_blocks": 3}, {"tile": 1, "span_segs": 7, "span_blocks": 5},
-              # the same spans as one-shot pieces (k_piece): the plan's span
-              # size, one and seven segments, 63 (long spans: several passes)
-              {"tile": 1, "tile_piece": 1}, {"tile": 1, "tile_piece": 1, "span_segs": 1},
-              {"tile": 1, "tile_piece": 1, "span_segs": 7}, {"tile": 1, "tile_piece": 1, "span_segs": 63}]
+              {"tile": 1, "span_segs": 1, "span_blocks": 3}, {"tile": 1, "span_segs": 7, "span_blocks": 5}]
 
 
 @pytest.fixture(scope="module", params=TILE_FORCE, ids=force_id)

@@ -83,9 +83,6 @@ VARIANTS = {
     **{f"S{k}": {"tile": 1, "span_segs": k} for k in range(1, 64)},
     # the span launch as a persistent grid of G blocks (grid-stride over the spans)
     **{f"G{g}": {"span_blocks": g} for g in (768, 1024, 1280, 1536, 2048, 4096)},
-    "piece": {"tile": 1, "tile_piece": 1},  # the tile launch as one-shot pieces (k_piece, round 6)
-    **{f"P{k}": {"tile": 1, "tile_piece": 1, "piece_bytes": k} for k in (1024, 2048, 3072, 4096, 6144, 8192, 12288)},
-    **{f"K12P{k}": {"tile": 1, "tile_piece": 1, "piece_k": 12, "piece_bytes": k} for k in (8192, 12288, 16384, 20480)},
 }
 
 
