@@ -81,6 +81,8 @@ VARIANTS = {
     "span": {"tile": 1},         # the tile launch, k_span (span size: the plan's, or 63)
     "per_segment": {"tile": 0},  # the per-segment / two-class launches
     **{f"S{k}": {"tile": 1, "span_segs": k} for k in range(1, 64)},
+    # one per-segment launch of a forced lane-group geometry (g<lanes>x<loads per lane>)
+    **{f"g{l}x{u}": {"tile": 0, "lps": l, "unroll": u, "mode": 3} for l, u in ((8, 8), (16, 4), (16, 8), (32, 8))},
     # the span launch as a persistent grid of G blocks (grid-stride over the spans)
     **{f"G{g}": {"span_blocks": g} for g in (768, 1024, 1280, 1536, 2048, 4096)},
 }
