@@ -554,12 +554,15 @@ int main()
         close(sv[0]);
     }
     // a per-tick loop on the resident tick server: each tick verifies a few
-    // received wires and wraps a few messages (<= 16 each: the server's
-    // jobs), every result equal to the per-object calls; then off again
+    // received wires and wraps a few messages (the server's jobs: <= 64 on
+    // its default 4 blocks, then <= 128 on 8), every result equal to the
+    // per-object calls; then off again
     {
         eng.set_tick_server(5000);
-        for (int t = 0; t < 200; ++t) {
-            const size_t k = 1 + static_cast<size_t>(rng() % 16), at = static_cast<size_t>(rng() % (msgs.size() - k));
+        for (int t = 0; t < 300; ++t) {
+            if (t == 200) eng.set_tick_server_blocks(8);
+            const size_t most = t < 200 ? 64 : 128;
+            const size_t k = 1 + static_cast<size_t>(rng() % most), at = static_cast<size_t>(rng() % (msgs.size() - k));
             std::vector<std::string_view> tw(wires.begin() + at, wires.begin() + at + k);
             const auto tst = eng.verify_raw(tw);
             for (size_t i = 0; i < k; ++i) EXPECT(tst[i] == ICS_ST_ACCEPT);
@@ -568,6 +571,7 @@ int main()
             if (t % 50 == 49) std::this_thread::sleep_for(std::chrono::milliseconds(8));  // the server idles out
         }
         eng.set_tick_server(0);
+        eng.set_tick_server_blocks(4);
     }
     std::printf("%s: %zu checksums, %zu wraps, %zu unwraps (%zu accepted)\n", failures ? "FAILED" : "OK",
                 segs.size(), msgs.size(), rx.size(), accepted);

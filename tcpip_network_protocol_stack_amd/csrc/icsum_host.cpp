@@ -314,8 +314,10 @@ int server_ensure(ics_ctx* ctx) {
 
 // The tick's descriptors, sub-job b (segments [16 b, 16 b + 16) of n) into
 // mailbox b, each word stamped with that mailbox's sequence number (the
-// server takes a job once every word it uses carries the number); mailbox 0
-// last, so a tick is never seen by block 0 alone of the blocks it uses
+// server takes a job once every word it uses carries the number).  Mailbox 0
+// goes last: when block 0 takes its part (restarting the idle clock that
+// decides the grid's exit) the other parts are already posted.  A part the
+// grid left without taking is taken by the relaunched grid (server_wait).
 int server_post(ics_ctx* ctx, int op, int mode, const void* bytes, const uint32_t* init, void* res,
                 const uint64_t* rel_off, uint64_t stride, uint64_t seg_len, uint32_t n, SrvTick* tick) {
   if (int rc = server_ensure(ctx)) return rc;
