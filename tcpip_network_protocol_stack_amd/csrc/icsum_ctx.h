@@ -218,7 +218,16 @@ struct ics_ctx {
   uint32_t srv_idle_us = 0;
   uint32_t srv_blocks = 4;  // resident blocks, one mailbox each (ics_set_tick_server_blocks; ICSUM_FORCE srv_blocks)
   uint32_t srv_grid = 0;    // the blocks of the grid launched last
-  icsum::TickMailbox* h_mb = nullptr;  // kSrvBlocksMax mailboxes
+  icsum::TickMailbox* h_mb = nullptr;  // kSrvBlocksMax done / state words (page-locked)
+  // kSrvBlocksMax x kSrvWords descriptor words: page-locked, or with srv_vram
+  // uncached device memory the host writes through the PCIe BAR (then each
+  // tick's bytes are copied into d_srv_stage too: the server reads nothing
+  // over PCIe; ICSUM_FORCE srv_vram)
+  uint64_t* srv_words = nullptr;
+  int srv_vram = 0;
+  bool srv_words_vram = false;
+  static constexpr size_t kSrvStageBytes = size_t(256) << 10;  // per slot: a tick's bytes + records
+  uint8_t* d_srv_stage[kMaxSlots] = {};
   hipStream_t st_srv = nullptr;
   uint32_t srv_seq[icsum::kSrvBlocksMax] = {};  // the last job posted to each mailbox
   bool srv_launched = false;  // a server was launched (its `state` words say whether it still runs)

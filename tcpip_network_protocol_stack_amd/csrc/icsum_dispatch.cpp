@@ -628,6 +628,7 @@ int apply_force(ics_ctx* ctx, const char* spec) {
     else if (k == "tick_server" && v >= 0 && v <= 10000000) ctx->srv_idle_us = uint32_t(v);
     else if (k == "srv_pollers" && v >= 1 && v <= 4) ctx->srv_pollers = uint32_t(v);
     else if (k == "srv_blocks" && v >= 1 && v <= int64_t(icsum::kSrvBlocksMax)) ctx->srv_blocks = uint32_t(v);
+    else if (k == "srv_vram" && (v == 0 || v == 1)) ctx->srv_vram = int(v);
     else if (k == "twoclass_remap" && v >= 0 && v <= 30) ctx->twoclass_remap = uint32_t(v);
     else if (k == "twoclass_lds" && v >= 0 && v <= 65536) ctx->twoclass_lds = uint32_t(v);
     else if (k == "zero_copy_max" && v >= 0) ctx->zero_copy_max = uint64_t(v);

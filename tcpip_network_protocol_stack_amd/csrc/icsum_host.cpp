@@ -235,6 +235,12 @@ void free_staging(ics_ctx* ctx) {
   ctx->st_srv = nullptr;
   if (ctx->h_mb) (void)hipHostFree(ctx->h_mb);
   ctx->h_mb = nullptr;
+  if (ctx->srv_words) (void)(ctx->srv_words_vram ? hipFree(ctx->srv_words) : hipHostFree(ctx->srv_words));
+  ctx->srv_words = nullptr;
+  for (int k = 0; k < ics_ctx::kMaxSlots; ++k) {
+    if (ctx->d_srv_stage[k]) (void)hipFree(ctx->d_srv_stage[k]);
+    ctx->d_srv_stage[k] = nullptr;
+  }
   for (int k = 0; k < ics_ctx::kMaxSlots; ++k) {
     if (ctx->st[k]) (void)hipStreamSynchronize(ctx->st[k]);
     if (ctx->h_in[k]) (void)hipHostFree(ctx->h_in[k]);
@@ -266,6 +272,12 @@ namespace {
 
 uint64_t mb_load(const uint64_t* p) { return __atomic_load_n(p, __ATOMIC_ACQUIRE); }
 void mb_store(uint64_t* p, uint64_t v) { __atomic_store_n(p, v, __ATOMIC_RELEASE); }
+// stores into device memory through the BAR sit in the CPU's write-combining
+// buffers until flushed: without this the server saw some jobs only after
+// milliseconds, or not within 1 s (profiles/r6_probe_vram_mailbox*.jsonl)
+void bar_flush(const ics_ctx* ctx) {
+  if (ctx->srv_words_vram) __builtin_ia32_sfence();
+}
 
 // a posted tick: its parts' sequence numbers, part p in mailbox p (parts 0: none)
 struct SrvTick {
@@ -288,12 +300,27 @@ int server_launch(ics_ctx* ctx) {
     ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->h_mb), sz, hipHostMallocCoherent));
     std::memset(static_cast<void*>(ctx->h_mb), 0, sz);
     if (!host_pinned(ctx->h_mb).kernel) return fail(ICS_ERR_HIP, "tick server: mailbox not device-visible");
+    const size_t wsz = sizeof(uint64_t) * icsum::kSrvWords * icsum::kSrvBlocksMax;
+    if (ctx->srv_vram) {
+      ICS_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->srv_words), wsz, hipDeviceMallocUncached));
+      ctx->srv_words_vram = true;
+      ICS_HIP(hipMemset(ctx->srv_words, 0, wsz));
+      for (int k = 0; k < ics_ctx::kMaxSlots; ++k)
+        ICS_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->d_srv_stage[k]), ics_ctx::kSrvStageBytes,
+                                      hipDeviceMallocUncached));
+    } else {
+      ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->srv_words), wsz, hipHostMallocCoherent));
+      std::memset(ctx->srv_words, 0, wsz);
+    }
     ICS_HIP(hipStreamCreateWithFlags(&ctx->st_srv, hipStreamNonBlocking));
   }
-  // each block reads its mailbox's `done` at start: the oldest job not done
+  // each block reads its mailbox's `done` at start: the oldest job not done;
+  // the exit word block 0 set when the last grid left goes back to 0
+  mb_store(&ctx->srv_words[icsum::kSrvExit], 0);
+  bar_flush(ctx);
   for (uint32_t b = 0; b < ctx->srv_blocks; ++b) mb_store(&ctx->h_mb[b].state, icsum::kSrvRunning);
-  ICS_HIP(icsum::launch_tick_server(ctx->h_mb, ctx->srv_blocks, ctx->d_zero, ctx->srv_idle_us, ctx->srv_pollers,
-                                    ctx->st_srv));
+  ICS_HIP(icsum::launch_tick_server(ctx->srv_words, ctx->h_mb, ctx->srv_blocks, ctx->d_zero, ctx->srv_idle_us,
+                                    ctx->srv_pollers, ctx->st_srv));
   ctx->srv_grid = ctx->srv_blocks;
   ctx->srv_launched = true;
   ++ctx->n_srv_launches;
@@ -330,7 +357,7 @@ int server_post(ics_ctx* ctx, int op, int mode, const void* bytes, const uint32_
   for (uint32_t p = parts; p-- > 0;) {
     const uint32_t k = ++ctx->srv_seq[p];
     const uint64_t stamp = uint64_t(k) << 32;
-    uint64_t* w = ctx->h_mb[p].w;
+    uint64_t* w = ctx->srv_words + icsum::kSrvWords * p;
     auto put = [&](uint32_t i, uint64_t v32) {
       __atomic_store_n(&w[i], stamp | (v32 & 0xffffffffull), __ATOMIC_RELAXED);
     };
@@ -352,6 +379,7 @@ int server_post(ics_ctx* ctx, int op, int mode, const void* bytes, const uint32_
     put(0, uint64_t(op) | (uint64_t(mode) << 4) | (uint64_t(m) << 8) | (uint64_t(inits) << 16));
     tick->seq[p] = k;
   }
+  bar_flush(ctx);
   tick->parts = parts;
   ++ctx->n_srv_jobs;
   return ICS_OK;
@@ -382,9 +410,11 @@ int server_wait(ics_ctx* ctx, const SrvTick& tick) {
 
 int server_stop(ics_ctx* ctx) {
   if (!ctx->h_mb || !ctx->srv_launched) return ICS_OK;
-  mb_store(&ctx->h_mb->w[icsum::kSrvQuit], 1);
+  mb_store(&ctx->srv_words[icsum::kSrvQuit], 1);
+  bar_flush(ctx);
   const hipError_t e = hipStreamSynchronize(ctx->st_srv);  // the server exits on the quit word
-  mb_store(&ctx->h_mb->w[icsum::kSrvQuit], 0);
+  mb_store(&ctx->srv_words[icsum::kSrvQuit], 0);
+  bar_flush(ctx);
   ctx->srv_launched = false;
   if (e != hipSuccess) return fail(ICS_ERR_HIP, "tick server: %s", hipGetErrorString(e));
   return ICS_OK;
@@ -546,19 +576,31 @@ int run_pipeline(ics_ctx* ctx, int kind, void* h_bytes, const uint64_t* h_offset
     const bool srv =
         zc && m <= icsum::kTickSegs * ctx->srv_blocks && ctx->srv_idle_us && (h_offsets || nb < (1u << 31));
     if (srv) {  // the resident tick server takes it: no launch
+      if (int rc = server_ensure(ctx)) return rc;
       const uint32_t* d_init = nullptr;  // checksum: the inits; wrap: the message records
       void* out = res;
       int dev_mode = mode == ICS_MODE_PATCH ? ICS_MODE_COMPUTE : mode;  // PATCH: fields written at retire
+      const void* bytes_in = in;
+      // srv_vram: the tick's bytes (and the wrap's records) written into
+      // device memory through the BAR, so the server reads nothing over PCIe
+      const uint64_t rec_at = (nb + 15) & ~uint64_t(15);
+      const bool stage = ctx->srv_words_vram && rec_at + m * sizeof(ics_tcp_msg) <= ics_ctx::kSrvStageBytes;
+      if (stage) {
+        std::memcpy(ctx->d_srv_stage[slot], in, nb);
+        bytes_in = ctx->d_srv_stage[slot];
+      }
       if (kind == 0 && h_init) {
         d_init = h_init + c.i0;  // copied into the descriptor (server_post)
       } else if (kind == 2) {
-        std::memcpy(ctx->h_msg[slot], h_msgs + c.i0, m * sizeof(ics_tcp_msg));
-        d_init = reinterpret_cast<const uint32_t*>(ctx->h_msg[slot]);
+        uint8_t* recs = stage ? ctx->d_srv_stage[slot] + rec_at : ctx->h_msg[slot];
+        std::memcpy(recs, h_msgs + c.i0, m * sizeof(ics_tcp_msg));
+        d_init = reinterpret_cast<const uint32_t*>(recs);
         out = ctx->h_hdr[slot];
         dev_mode = mode;  // 1: payload only (headers apart)
       }
-      if (int rc = server_post(ctx, kind, dev_mode, in, d_init, out, h_offsets ? ctx->h_off[slot] : nullptr, stride,
-                               seg_len, uint32_t(m), &srv_of[slot]))
+      if (stage) bar_flush(ctx);  // the staged bytes land before any descriptor word
+      if (int rc = server_post(ctx, kind, dev_mode, bytes_in, d_init, out, h_offsets ? ctx->h_off[slot] : nullptr,
+                               stride, seg_len, uint32_t(m), &srv_of[slot]))
         return rc;
       note_host(ctx, ICS_K_TICK_SERVER, 16, 8);
     } else if (tick) {

@@ -1761,11 +1761,13 @@ __global__ __launch_bounds__(kBlock) void k_tcp_hdr(uint8_t* __restrict__ dg,
 // only a grid that has fully left (no two blocks ever serve one mailbox).
 constexpr uint64_t kSrvMaxLife = 100000000ull;  // 1 s of s_memrealtime
 
-__global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mbs, const uint8_t* __restrict__ zpad,
-                                                        uint32_t idle_us, uint32_t pollers) {
+__global__ __launch_bounds__(kBlock) void k_tick_server(uint64_t* words, TickMailbox* mbs,
+                                                        const uint8_t* __restrict__ zpad, uint32_t idle_us,
+                                                        uint32_t pollers) {
   __shared__ uint32_t s_desc[64];
   __shared__ uint32_t s_cmd;  // 0 none yet, 1 a job, 2 exit
   TickMailbox* const mb = mbs + blockIdx.x;
+  const uint64_t* const mw = words + kSrvWords * blockIdx.x;  // this block's descriptor words
   const bool lead = blockIdx.x == 0;
   const uint32_t wv = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   const uint32_t g = threadIdx.x >> 4, gl = threadIdx.x & 15u;
@@ -1775,8 +1777,8 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mbs, const 
   // the oldest job of this mailbox not done (the grid before this one has
   // left: its last `done` store is final)
   uint32_t expect = uint32_t(__hip_atomic_load(&mb->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) + 1u;
-  // lane 63's poll word: the quit word (block 0) or block 0's state
-  const uint64_t* const w63 = lead ? &mb->w[kSrvQuit] : &mbs[0].state;
+  // lane 63's poll word: the quit word (block 0) or block 0's exit word
+  const uint64_t* const w63 = lead ? &words[kSrvQuit] : &words[kSrvExit];
   if (threadIdx.x == 0) s_cmd = 0u;
   __syncthreads();
   for (;;) {
@@ -1789,7 +1791,7 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mbs, const 
       for (uint32_t k = 0; k < wv; ++k) __builtin_amdgcn_s_sleep(14);  // ~0.4 us each
       while (__hip_atomic_load(&s_cmd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == 0u) {
         const uint64_t word =
-            __hip_atomic_load(lane == kSrvQuit ? w63 : &mb->w[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            __hip_atomic_load(lane == kSrvQuit ? w63 : &mw[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         const uint32_t pay = uint32_t(word), seq = uint32_t(word >> 32);
         const uint32_t w0 = __builtin_amdgcn_readlane(pay, 0), s0 = __builtin_amdgcn_readlane(seq, 0);
         const uint32_t nj = (w0 >> 8) & 0xffu, nw = kSrvHead + 2u * nj;  // the words this job uses
@@ -1798,7 +1800,7 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mbs, const 
         const bool fresh = !used || seq == expect;
         const bool job = s0 == expect && __all(fresh);
         const uint64_t q = __builtin_amdgcn_readlane(uint32_t(word | (word >> 32)), kSrvQuit);
-        const bool quit = lead ? q != 0 : q == kSrvExited;
+        const bool quit = q != 0;
         const uint64_t now = __builtin_amdgcn_s_memrealtime();
         // blocks b > 0 leave with block 0 (their lifetime bound only a backstop)
         const bool idle = lead ? now - t_job > uint64_t(idle_us) * 100u || now - t0 > kSrvMaxLife
@@ -1888,7 +1890,10 @@ __global__ __launch_bounds__(kBlock) void k_tick_server(TickMailbox* mbs, const 
     if (threadIdx.x == 0) s_cmd = 0u;  // every wave read it at the barrier before the done store
     __syncthreads();  // s_desc / s_cmd are rewritten by the next poll
   }
-  if (threadIdx.x == 0) __hip_atomic_store(&mb->state, uint64_t(kSrvExited), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (threadIdx.x == 0) {
+    if (lead) __hip_atomic_store(&words[kSrvExit], uint64_t(1), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&mb->state, uint64_t(kSrvExited), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // --------------------------------------------------- router batch -------
@@ -3054,11 +3059,11 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
   return hipGetLastError();
 }
 
-hipError_t launch_tick_server(TickMailbox* mbs, uint32_t blocks, const void* zero16, uint32_t idle_us,
-                              uint32_t pollers, hipStream_t st) {
+hipError_t launch_tick_server(uint64_t* words, TickMailbox* mbs, uint32_t blocks, const void* zero16,
+                              uint32_t idle_us, uint32_t pollers, hipStream_t st) {
   if (pollers < 1 || pollers > kBlock / 64 || blocks < 1 || blocks > kSrvBlocksMax) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(k_tick_server, dim3(blocks), dim3(kBlock), 0, st, mbs, static_cast<const uint8_t*>(zero16),
-                     idle_us, pollers);
+  hipLaunchKernelGGL(k_tick_server, dim3(blocks), dim3(kBlock), 0, st, words, mbs,
+                     static_cast<const uint8_t*>(zero16), idle_us, pollers);
   return hipGetLastError();
 }
 

@@ -221,22 +221,25 @@ hipError_t launch_tick(const uint8_t* bytes, const uint64_t* offsets, uint32_t n
 //                the bytes) and length
 //   w[kSrvInit + j] = segment j's init (op 0 with w[0] bit 16 set: the inits
 //                travel in the descriptor, not as a PCIe read of their own)
-// Mailbox 0's w[kSrvQuit] != 0: exit.  Block b writes mailbox b's `done` (the
-// last finished sequence number) and, when it exits, `state` = kSrvExited;
-// blocks b > 0 leave once mailbox 0's `state` says block 0 has.
+// Mailbox b = 64 descriptor words at words + 64 b (page-locked host memory,
+// or with srv_vram uncached device memory the host writes through the BAR)
+// and a TickMailbox in page-locked memory.  Mailbox 0's w[kSrvQuit] != 0:
+// exit; block 0 sets w[kSrvExit] when it leaves and blocks b > 0 leave on
+// seeing it.  Block b writes mailbox b's `done` (the last finished sequence
+// number) and, when it exits, `state` = kSrvExited.
 constexpr uint32_t kSrvHead = 7, kSrvInit = kSrvHead + 2 * kTickSegs, kSrvPart = kSrvInit + kTickSegs,
-                   kSrvQuit = 63;
+                   kSrvExit = 62, kSrvQuit = 63;
 constexpr uint32_t kSrvBlocksMax = 8;  // ticks of up to 128 segments
+constexpr uint32_t kSrvWords = 64;     // descriptor words per mailbox
 constexpr uint64_t kSrvRunning = 1, kSrvExited = 2;
-struct alignas(256) TickMailbox {
-  uint64_t w[64];
+struct alignas(128) TickMailbox {
   uint64_t done;
   uint64_t state;
-  uint64_t pad[30];
+  uint64_t pad[14];
 };
-static_assert(kSrvPart < kSrvQuit, "the descriptor fits below the quit word");
-hipError_t launch_tick_server(TickMailbox* mbs, uint32_t blocks, const void* zero16, uint32_t idle_us,
-                              uint32_t pollers, hipStream_t st);
+static_assert(kSrvPart < kSrvExit, "the descriptor fits below the exit and quit words");
+hipError_t launch_tick_server(uint64_t* words, TickMailbox* mbs, uint32_t blocks, const void* zero16,
+                              uint32_t idle_us, uint32_t pollers, hipStream_t st);
 
 // Fields of one TCP message for the device-side wrap; layout of ics_tcp_msg
 // (include/icsum.h), 28 bytes.

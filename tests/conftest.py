@@ -34,7 +34,7 @@ def engine_with(force=None, debug=False):
     `force` ({key: value}: lps, unroll, mode, segs, bin, bin_min, bin_plan,
     bin_blocks, last_bin_lps, last_bin_blocks, dense_segs, twoclass,
     wrap_passes, xcd_remap, zero_copy_max, tile, span_segs, span_blocks,
-    tick_inline, tick_server, srv_pollers, srv_blocks, slot_prio, poison_ticket —
+    tick_inline, tick_server, srv_pollers, srv_blocks, srv_vram, slot_prio, poison_ticket —
     INTEGRATION.md §6), read once at
     ics_create."""
     import torch

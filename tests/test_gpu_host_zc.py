@@ -326,7 +326,9 @@ def test_tick_offsets_in_kernel_arguments(tick_eng, orc, pinned, base):
 # resident; leaves after 3 ms without a call; srv_pollers 4: every wave
 # polls; srv_blocks 4: four resident blocks, ticks of up to 64 segments
 SRV_FORCE = [{"tick_server": 3000, "srv_blocks": 1}, {"tick_server": 3000, "srv_blocks": 1, "srv_pollers": 4},
-             {"tick_server": 3000, "srv_blocks": 4}, {"tick_server": 3000, "srv_blocks": 8}]
+             {"tick_server": 3000, "srv_blocks": 4}, {"tick_server": 3000, "srv_blocks": 8},
+             # descriptors and the tick's bytes in device memory the host writes through the BAR
+             {"tick_server": 3000, "srv_blocks": 4, "srv_vram": 1}, {"tick_server": 3000, "srv_blocks": 1, "srv_vram": 1}]
 
 
 @pytest.fixture(scope="module", params=SRV_FORCE, ids=force_id)
@@ -392,8 +394,8 @@ def test_tick_server_vs_oracle(srv_eng, orc, pinned, base):
             assert (fh == hb).all(), (n, mode, base, "fixed")
 
 
-@pytest.mark.parametrize("blocks", [1, 4, 8])
-def test_tick_server_idle_exit_relaunch_and_stop(orc, blocks):
+@pytest.mark.parametrize("blocks,vram", [(1, 0), (4, 0), (8, 0), (4, 1)])
+def test_tick_server_idle_exit_relaunch_and_stop(orc, blocks, vram):
     """The server leaves after its idle time and the next call launches it
     again (exact results across many exits; with four blocks the grid
     leaves as a whole and ticks of 1..64 segments alternate); ics_set_tick_server(0) stops it
@@ -410,7 +412,7 @@ def test_tick_server_idle_exit_relaunch_and_stop(orc, blocks):
     big = [rng.integers(0, 256, int(x), dtype=np.uint8).tobytes() for x in rng.integers(0, 1500, 16 * blocks)]
     bbuf, boff = pack_contiguous(big, 7)
     bwant = orc.checksum_batch(bbuf, len(big), offsets=boff)
-    for eng in engine_with({"tick_server": 500, "srv_blocks": blocks}):  # 0.5 ms idle: it leaves between most calls
+    for eng in engine_with({"tick_server": 500, "srv_blocks": blocks, "srv_vram": vram}):  # 0.5 ms idle: leaves between most calls
         for i in range(40):
             got = eng.checksum_batch_host(buf, len(segs), offsets=off)
             assert (got == want).all(), i

@@ -116,9 +116,14 @@ int run(const char* name, int box_vram, int pay_vram, uint32_t plen) {
     const auto t0 = std::chrono::steady_clock::now();
     std::memcpy(src, &k, 4);  // a different payload every job: a stale read shows in the sum
     std::memcpy(payload, src, plen);
+    __builtin_ia32_sfence();  // the payload lands before the sequence word
     std::atomic_thread_fence(std::memory_order_seq_cst);
     const double cus = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
     __atomic_store_n(&box->seq, k, __ATOMIC_RELEASE);
+    // a store to BAR-mapped VRAM can sit in the CPU's write-combining buffer
+    // until something flushes it: without this fence the first runs saw
+    // 1 s timeouts and a 10 ms p99 (profiles/r6_probe_vram_mailbox*.jsonl)
+    __builtin_ia32_sfence();
     while (__atomic_load_n(&res->seq, __ATOMIC_ACQUIRE) < k) {
       if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(1)) {  // the job never arrived
         __atomic_store_n(&box->quit, 1, __ATOMIC_RELEASE);
