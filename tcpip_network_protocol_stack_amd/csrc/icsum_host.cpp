@@ -304,7 +304,10 @@ int server_launch(ics_ctx* ctx) {
     if (ctx->srv_vram) {
       ICS_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->srv_words), wsz, hipDeviceMallocUncached));
       ctx->srv_words_vram = true;
-      ICS_HIP(hipMemset(ctx->srv_words, 0, wsz));
+      // zeroed by the host through the BAR like every later store (a device
+      // memset could land after the first descriptor words)
+      std::memset(ctx->srv_words, 0, wsz);
+      bar_flush(ctx);
       for (int k = 0; k < ics_ctx::kMaxSlots; ++k)
         ICS_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->d_srv_stage[k]), ics_ctx::kSrvStageBytes,
                                       hipDeviceMallocUncached));
