@@ -346,10 +346,12 @@ def host_inclusive(eng, data, init, out, n, seg, passes=3, calls=300):
             "tick_p50": tick, "tick_note": f"{seg}-byte segments, {calls} ctypes calls, preallocated outputs, buffer addresses taken once",
             "tick_p50_cpp": tick_cpp_guarded(calls),
             "tick_p50_cpp_server": tick_cpp_guarded(calls, "tick_server=20000"),
+            "tick_p50_cpp_server_vram": tick_cpp_guarded(calls, "tick_server=20000,srv_vram=1"),
             "tick_cpp_note": "the same calls from C++ (tools/probe/tick_latency, dlopen of the in-tree libicsum.so, "
                              "1500-byte segments with inits, page-locked), no interpreter in the loop; _server: "
                              "with the resident tick server (ics_set_tick_server, 20 ms idle; 4 blocks, 16 segments each), "
-                             "no launch per call"}
+                             "no launch per call; _server_vram: the same with its descriptors and each tick's bytes "
+                             "written into device memory through the BAR (ICSUM_FORCE srv_vram, opt-in)"}
 
 
 def tick_cpp(calls, force=None):
