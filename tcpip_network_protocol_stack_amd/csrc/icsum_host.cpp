@@ -237,6 +237,7 @@ void free_staging(ics_ctx* ctx) {
   ctx->h_mb = nullptr;
   if (ctx->srv_words) (void)(ctx->srv_words_vram ? hipFree(ctx->srv_words) : hipHostFree(ctx->srv_words));
   ctx->srv_words = nullptr;
+  ctx->srv_words_vram = false;
   for (int k = 0; k < ics_ctx::kMaxSlots; ++k) {
     if (ctx->d_srv_stage[k]) (void)hipFree(ctx->d_srv_stage[k]);
     ctx->d_srv_stage[k] = nullptr;
@@ -302,16 +303,29 @@ int server_launch(ics_ctx* ctx) {
     if (!host_pinned(ctx->h_mb).kernel) return fail(ICS_ERR_HIP, "tick server: mailbox not device-visible");
     const size_t wsz = sizeof(uint64_t) * icsum::kSrvWords * icsum::kSrvBlocksMax;
     if (ctx->srv_vram) {
-      ICS_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->srv_words), wsz, hipDeviceMallocUncached));
-      ctx->srv_words_vram = true;
-      // zeroed by the host through the BAR like every later store (a device
-      // memset could land after the first descriptor words)
-      std::memset(ctx->srv_words, 0, wsz);
-      bar_flush(ctx);
-      for (int k = 0; k < ics_ctx::kMaxSlots; ++k)
-        ICS_HIP(hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->d_srv_stage[k]), ics_ctx::kSrvStageBytes,
-                                      hipDeviceMallocUncached));
-    } else {
+      // every piece or none: a failed allocation falls back to page-locked words
+      bool ok = hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->srv_words), wsz, hipDeviceMallocUncached) ==
+                hipSuccess;
+      for (int k = 0; ok && k < ics_ctx::kMaxSlots; ++k)
+        ok = hipExtMallocWithFlags(reinterpret_cast<void**>(&ctx->d_srv_stage[k]), ics_ctx::kSrvStageBytes,
+                                   hipDeviceMallocUncached) == hipSuccess;
+      if (!ok) {
+        (void)hipGetLastError();
+        if (ctx->srv_words) (void)hipFree(ctx->srv_words);
+        ctx->srv_words = nullptr;
+        for (int k = 0; k < ics_ctx::kMaxSlots; ++k) {
+          if (ctx->d_srv_stage[k]) (void)hipFree(ctx->d_srv_stage[k]);
+          ctx->d_srv_stage[k] = nullptr;
+        }
+      } else {
+        ctx->srv_words_vram = true;
+        // zeroed by the host through the BAR like every later store (a
+        // device memset could land after the first descriptor words)
+        std::memset(ctx->srv_words, 0, wsz);
+        bar_flush(ctx);
+      }
+    }
+    if (!ctx->srv_words) {
       ICS_HIP(hipHostMalloc(reinterpret_cast<void**>(&ctx->srv_words), wsz, hipHostMallocCoherent));
       std::memset(ctx->srv_words, 0, wsz);
     }
